@@ -1,0 +1,179 @@
+/*
+ * redcliff_hip.h -- C-ABI of libredcliff_hip.so, the MI355X (gfx950) implementation of the
+ * REDCLIFF-S cMLP factor-model fitting hot path.
+ *
+ * The reference (carlson-lab/redcliff-s-hypothesizing-dynamic-causal-graphs) is pure
+ * Python/PyTorch: it has no FFI of its own.  Each entry point below replaces one piece
+ * of the reference's Python hot path (citations relative to the reference tree); the
+ * Python host package binds them with ctypes.
+ *
+ * Conventions
+ *  - All pointers are device pointers owned by the caller (PyTorch caching allocator).
+ *    Nothing here allocates or frees device memory; scratch is a caller-supplied
+ *    workspace of redcliff_workspace_bytes() bytes.
+ *  - Every call is stream-ordered on the given hipStream_t (passed as void*) and does
+ *    not synchronise the host.  Calls are stateless and re-entrant.
+ *  - Return value: 0 on success, a negative argument-validation code, or a positive
+ *    hipError_t.  redcliff_last_error() returns a thread-local message.
+ *  - R "replicas" (independent fits with identical shapes, e.g. grid-search points)
+ *    may be packed into one call; every per-replica buffer has an explicit stride.
+ *  - fp32 throughout (the reference calls .float() on every model,
+ *    general_utils/model_utils.py:392,417).
+ */
+#ifndef REDCLIFF_HIP_H
+#define REDCLIFF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define REDCLIFF_ABI_VERSION 1
+
+/* error codes (negative) */
+#define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
+#define REDCLIFF_ELIMIT (-2)  /* dimension outside what the kernels support     */
+#define REDCLIFF_EWORKSPACE (-3)
+
+/* step flags: which parts of one batch_update run (...withStateSmoothing.py:741-881) */
+#define RC_BN_TRAIN      (1 << 0)  /* embedder BatchNorm in train mode (batch statistics)        */
+#define RC_LOSS_FORECAST (1 << 1)  /* forecast MSE term (:629)                                   */
+#define RC_LOSS_FACTOR   (1 << 2)  /* supervised factor-score MSE (:633-663)                     */
+#define RC_LOSS_FWL1     (1 << 3)  /* factor-weight L1 (:666)                                    */
+#define RC_LOSS_ADJ      (1 << 4)  /* lag-weighted adjacency L1 of conditional GC (:696-715)     */
+#define RC_STEP_A        (1 << 5)  /* Adam step on the embedder (optimizerA)                     */
+#define RC_STEP_B        (1 << 6)  /* Adam step on the factors  (optimizerB)                     */
+#define RC_VALUES        (1 << 7)  /* compute loss values (validate_training, :1650-1790)        */
+#define RC_CONFUSION     (1 << 8)  /* accumulate the factor-score confusion matrix (:786-803)    */
+#define RC_STORE_OUTPUTS (1 << 9)  /* run the factor forward even without a loss (model.forward)  */
+#define RC_REFRESH_SUPPORTS (1 << 10) /* recompute the DGCNN Chebyshev supports before the step  */
+
+/* Shapes shared by every call. */
+typedef struct RedcliffDims {
+  int32_t R;      /* replicas packed in one launch                                   */
+  int32_t Bmax;   /* largest batch the workspace is sized for                         */
+  int32_t T;      /* recorded time steps per window in the dataset buffer             */
+  int32_t p;      /* channels (num_chans)                                            */
+  int32_t L;      /* gen_lag: factor Conv1d kernel width                             */
+  int32_t K;      /* num_factors                                                     */
+  int32_t h;      /* factor hidden width (gen_hidden == [h])                          */
+  int32_t F;      /* embed_lag == DGCNN num_features_per_node                        */
+  int32_t n;      /* DGCNN Chebyshev layers                                          */
+  int32_t H;      /* DGCNN hidden channels per node                                   */
+  int32_t M1;     /* DGCNN fc1 width (64 in torcheeg)                                */
+  int32_t nsup;   /* num_supervised_factors                                          */
+  int32_t use_sigmoid;   /* use_sigmoid_restriction                                  */
+  float sigmoid_ecc;     /* sigmoid_eccentricity_coeff                               */
+} RedcliffDims;
+
+/* torch.optim.Adam hyper-parameters of one parameter group.  Doubles are what torch's
+ * Python side computes the bias corrections with; the fp32 copies are the scalars torch
+ * applies element-wise (_single_tensor_adam / _multi_tensor_adam). */
+typedef struct RedcliffAdamHyper {
+  double lr, beta1, beta2;
+  float eps, weight_decay;
+  float beta2_f;            /* (float)beta2                                  */
+  float one_minus_beta1_f;  /* (float)(1 - beta1): lerp weight               */
+  float one_minus_beta2_f;  /* (float)(1 - beta2): addcmul value             */
+  float pad_;
+} RedcliffAdamHyper;
+
+/* Per-replica hyper-parameters, stored as a device array of R entries. */
+typedef struct RedcliffReplicaHyper {
+  float c_forecast, c_factor, c_cos, c_fwl1, c_smooth, c_adj; /* coeff_dict          */
+  double bn_eps, bn_momentum;                                 /* BatchNorm1d         */
+  RedcliffAdamHyper A;                                        /* optimizerA: embedder */
+  RedcliffAdamHyper B;                                        /* optimizerB: factors  */
+} RedcliffReplicaHyper;
+
+/* Packed parameter layouts (floats, per replica):
+ *  embedder (DGCNN): A[p][p] | gcW[n][F][H] | bn_w[F] | bn_b[F] | fc1W[M1][p*H] | fc1b[M1]
+ *                    | fc2W[K][M1] | fc2b[K]
+ *  factors:          W0[K][p][h][p][L] | b0[K][p][h] | W1[K][p][h] | b1[K][p]
+ * (W0[k][j] is the Conv1d(p,h,L) weight of network j of factor k, models/cmlp.py:19.) */
+
+typedef struct RedcliffStepArgs {
+  RedcliffDims d;
+  int32_t B;            /* windows in this batch (<= Bmax)                          */
+  int32_t flags;        /* RC_* bitmask                                             */
+  int32_t n_bn_updates; /* BatchNorm running-stat updates this step (3 in train phases) */
+  int32_t tA, tB;       /* Adam step numbers (1-based) used for bias correction      */
+  /* data: X[N][T][p] windows, labels[N][K] (already selected time index)            */
+  const float* X; int64_t x_rstride; int64_t row0;
+  const float* labels; int64_t lab_rstride;
+  const double* bn_stats; int64_t bn_stats_rstride; /* [2][F] batch mean / biased var */
+  /* parameters and Adam state                                                      */
+  float* emb; float* emb_m; float* emb_v; int64_t emb_stride;
+  float* fac; float* fac_m; float* fac_v; int64_t fac_stride;
+  float* bn_rm; float* bn_rv;                      /* [R][F]                           */
+  const RedcliffReplicaHyper* hyper;               /* device [R]                       */
+  void* ws; size_t ws_bytes;                       /* workspace                        */
+  double* acc;        /* [R][8] validation accumulators (may be NULL without RC_VALUES) */
+  int32_t* confusion; /* [R][nsup][nsup] (may be NULL without RC_CONFUSION)              */
+} RedcliffStepArgs;
+
+int redcliff_abi_version(void);
+const char* redcliff_last_error(void);
+
+/* Workspace bytes for one launch of R replicas (all kernels share one layout). */
+size_t redcliff_workspace_bytes(const RedcliffDims* d);
+size_t redcliff_emb_param_count(const RedcliffDims* d);
+size_t redcliff_fac_param_count(const RedcliffDims* d);
+
+/* BatchNorm batch statistics of the embedder window X[row][Lmax-F:Lmax] for n_batches
+ * consecutive batches of size B (last one may be ragged; N total windows).
+ * stats[r][batch][2][F] (mean, biased variance).  Replaces the statistics half of
+ * torch.nn.BatchNorm1d.forward in train mode (torcheeg DGCNN.BN1, models/dgcnn.py:37). */
+int redcliff_bn_batch_stats(const RedcliffDims* d, const float* X, int64_t x_rstride, int64_t N, int32_t B,
+                            double* stats, int64_t stats_rstride, void* stream);
+
+/* normalize_A + Chebyshev supports [I, L, L^2, ...] of the DGCNN adjacency into the
+ * workspace (torcheeg normalize_A / generate_cheby_adj).  Must run after any change
+ * of the embedder parameters made outside redcliff_train_step. */
+int redcliff_dgcnn_supports(const RedcliffDims* d, const float* emb, int64_t emb_stride, void* ws, void* stream);
+
+/* One REDCLIFF-S batch_update (...withStateSmoothing.py:734-933) for the published
+ * configuration: DGCNN embedder, conditional_factor_fixed_embedder GC, factor weights
+ * applied after simulation, num_sims == 1.  With RC_VALUES and no RC_STEP_* it is the
+ * per-batch body of validate_training.  Launches the fused kernel chain on `stream`. */
+int redcliff_train_step(const RedcliffStepArgs* a, void* stream);
+
+/* nsteps consecutive batch_updates of one epoch without returning to the host:
+ * step i uses rows[i] / sizes[i] (host arrays) as row0 / B, bn_stats advanced by
+ * i*bn_stats_step doubles, and Adam step numbers a->tA + i (a->tB + i) when the
+ * corresponding RC_STEP_* flag is set.  RC_REFRESH_SUPPORTS applies to the first step. */
+int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_t* rows, const int32_t* sizes,
+                         int32_t bn_stats_step, void* stream);
+
+/* Offsets (floats, per replica) of the workspace regions: T R f1 w a y G G0 dwp dAadj dWi dS dgb S
+ * dZ amat lossp xsim gfc total.  Returns the number of offsets available.  The host reads
+ * w (raw embedder output), y (per-factor predictions), xsim (mixed forecast), G / G0
+ * (group norms) back from a step run with RC_STORE_OUTPUTS. */
+int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out);
+
+/* Stand-alone forward of K cMLPs (models/cmlp.py:90-101) on B windows Xwin[r][B][L][p]
+ * (x_rstride floats between replicas).  Per replica (ws_rstride floats) the workspace
+ * receives a[K][p][B][h] | y[B][K][p] | G[K][p][p][L] | G0[K][p][p]; y is the prediction
+ * of network j of factor k for window b. */
+int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride, const float* fac,
+                            int64_t fac_stride, float* ws, int64_t ws_rstride, void* stream);
+
+/* G[r][k][j][c][t] = ||W0[k][j][:, c, t]||_2, G0[r][k][j][c] = ||W0[k][j][:, c, :]||_F (models/cmlp.py:147-167) */
+int redcliff_gc_norms(const RedcliffDims* d, const float* fac, int64_t fac_stride, float* G, float* G0, void* stream);
+/* In-place proximal step on layer-0 weights, penalty 0=GL 1=GSGL 2=H (models/cmlp.py:117-144). */
+int redcliff_prox(const RedcliffDims* d, float* fac, int64_t fac_stride, float lam, float lr, int32_t penalty,
+                  void* stream);
+
+/* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
+ * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()
+ * synchronises them and returns per-kernel totals (ids 0..5: supports, emb_fwd, fac_fwd,
+ * fac_bwd, emb_bwd, emb_final).  Returns the number of kernel ids. */
+int redcliff_kernel_timing(int32_t enable);
+int redcliff_kernel_times(double* total_ms, int64_t* counts, int32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REDCLIFF_HIP_H */

@@ -1,0 +1,81 @@
+// rc_aux.hip -- cMLP group norms (GC extraction) and proximal steps on gfx950.
+//
+// Reference: models/cmlp.py:147-167 (cMLP.GC: ||W0[:, c, t]|| over hidden units, or over
+// hidden units and lags) and models/cmlp.py:117-144 (perform_prox_update_on_GC_weights:
+// GL / GSGL / H shrinkage with threshold lr*lam).  One workgroup per (factor, network).
+#include "rc_common.h"
+
+namespace {
+
+__global__ __launch_bounds__(RC_BLOCK) void k_gc_norms(RedcliffDims d, const float* fac, int64_t fs, FacOff fo,
+                                                       float* G, float* G0) {
+  const int r = blockIdx.y, kj = blockIdx.x;
+  const int p = d.p, h = d.h, L = d.L, Q = p * L;
+  const float* W = fac + r * fs + fo.W0 + (int64_t)kj * h * Q;
+  float* Gr = G + ((int64_t)r * d.K * p + kj) * Q;
+  float* G0r = G0 + ((int64_t)r * d.K * p + kj) * p;
+  for (int e = threadIdx.x; e < Q; e += RC_BLOCK) {
+    float s = 0.f;
+    for (int u = 0; u < h; ++u) s += W[(int64_t)u * Q + e] * W[(int64_t)u * Q + e];
+    Gr[e] = sqrtf(s);
+  }
+  for (int cc = threadIdx.x; cc < p; cc += RC_BLOCK) {
+    float s = 0.f;
+    for (int u = 0; u < h; ++u)
+      for (int t = 0; t < L; ++t) s += W[(int64_t)u * Q + cc * L + t] * W[(int64_t)u * Q + cc * L + t];
+    G0r[cc] = sqrtf(s);
+  }
+}
+
+// W <- W / max(norm, thr) * max(norm - thr, 0) on the groups of one input channel.
+__global__ __launch_bounds__(RC_BLOCK) void k_prox(RedcliffDims d, float* fac, int64_t fs, FacOff fo, float lam,
+                                                   float lr, int penalty) {
+  const int r = blockIdx.y, kj = blockIdx.x;
+  const int p = d.p, h = d.h, L = d.L, Q = p * L;
+  float* W = fac + r * fs + fo.W0 + (int64_t)kj * h * Q;
+  const float thr = lr * lam;
+  // one thread per input channel c (p <= 64): the groups never straddle channels
+  const int cc = threadIdx.x;
+  if (cc >= p) return;
+  auto shrink = [&](int t0, int t1) {
+    float s = 0.f;
+    for (int u = 0; u < h; ++u)
+      for (int t = t0; t < t1; ++t) s += W[(int64_t)u * Q + cc * L + t] * W[(int64_t)u * Q + cc * L + t];
+    const float nrm = sqrtf(s);
+    const float den = fmaxf(nrm, thr), num = fmaxf(nrm - thr, 0.f);
+    for (int u = 0; u < h; ++u)
+      for (int t = t0; t < t1; ++t) {
+        const int64_t i = (int64_t)u * Q + cc * L + t;
+        W[i] = (W[i] / den) * num;
+      }
+  };
+  if (penalty == 0) {  // GL: one group per input channel (norm over hidden units and lags)
+    shrink(0, L);
+  } else if (penalty == 1) {  // GSGL: per (channel, lag) groups, then per channel
+    for (int t = 0; t < L; ++t) shrink(t, t + 1);
+    shrink(0, L);
+  } else {  // H: nested prefixes of the lag axis, lowest index = most lagged (cmlp.py:138-141)
+    for (int i = 0; i < L; ++i) shrink(0, i + 1);
+  }
+}
+
+}  // namespace
+
+extern "C" int redcliff_gc_norms(const RedcliffDims* d, const float* fac, int64_t fac_stride, float* G, float* G0,
+                                 void* stream) {
+  if (!d || !fac || !G || !G0) { rc_set_error("gc_norms: null argument"); return REDCLIFF_EINVAL; }
+  if (d->p > 64 || d->h > 4096) { rc_set_error("gc_norms: p > 64"); return REDCLIFF_ELIMIT; }
+  hipLaunchKernelGGL(k_gc_norms, dim3(d->K * d->p, d->R), dim3(RC_BLOCK), 0, (hipStream_t)stream, *d, fac,
+                     fac_stride, rc_fac_off(*d), G, G0);
+  return rc_check(hipGetLastError(), "k_gc_norms");
+}
+
+extern "C" int redcliff_prox(const RedcliffDims* d, float* fac, int64_t fac_stride, float lam, float lr,
+                             int32_t penalty, void* stream) {
+  if (!d || !fac) { rc_set_error("prox: null argument"); return REDCLIFF_EINVAL; }
+  if (penalty < 0 || penalty > 2) { rc_set_error("unsupported penalty %d", penalty); return REDCLIFF_EINVAL; }
+  if (d->p > RC_BLOCK) { rc_set_error("prox: p > %d", RC_BLOCK); return REDCLIFF_ELIMIT; }
+  hipLaunchKernelGGL(k_prox, dim3(d->K * d->p, d->R), dim3(RC_BLOCK), 0, (hipStream_t)stream, *d, fac, fac_stride,
+                     rc_fac_off(*d), lam, lr, penalty);
+  return rc_check(hipGetLastError(), "k_prox");
+}

@@ -1,0 +1,243 @@
+// rc_capi.hip -- extern "C" entry points of libredcliff_hip.so (see include/redcliff_hip.h).
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "rc_common.h"
+
+// ---- optional per-kernel HIP-event timing (bench / profiling only) -------------------------
+namespace {
+enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_N };
+struct TimedLaunch {
+  int id;
+  hipEvent_t a, b;
+};
+bool g_timing = false;
+std::vector<TimedLaunch> g_launches;
+
+template <class F>
+int timed(int id, hipStream_t s, F&& launch) {
+  if (!g_timing) return launch();
+  TimedLaunch t{id, nullptr, nullptr};
+  int e = rc_check(hipEventCreate(&t.a), "hipEventCreate");
+  if (!e) e = rc_check(hipEventCreate(&t.b), "hipEventCreate");
+  if (!e) e = rc_check(hipEventRecord(t.a, s), "hipEventRecord");
+  if (e) return e;
+  e = launch();
+  const int e2 = rc_check(hipEventRecord(t.b, s), "hipEventRecord");
+  g_launches.push_back(t);
+  return e ? e : e2;
+}
+}  // namespace
+
+static thread_local char g_err[512] = "";
+
+void rc_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int rc_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  rc_set_error("%s: %s", what, hipGetErrorString(e));
+  return (int)e;
+}
+
+size_t rc_emb_bwd_lds(const RedcliffDims& d);
+
+// Shape limits of the kernels (LDS tiles, register-blocked accumulators).
+static int check_dims(const RedcliffDims* d) {
+  if (!d) { rc_set_error("null dims"); return REDCLIFF_EINVAL; }
+  if (d->R < 1 || d->Bmax < 1 || d->p < 1 || d->L < 1 || d->K < 1 || d->h < 1 || d->F < 1 || d->n < 1 || d->H < 1 ||
+      d->M1 < 1 || d->nsup < 0 || d->nsup > d->K || d->T < 1) {
+    rc_set_error("invalid dims (R=%d Bmax=%d p=%d L=%d K=%d h=%d F=%d n=%d H=%d M1=%d nsup=%d T=%d)", d->R, d->Bmax,
+                 d->p, d->L, d->K, d->h, d->F, d->n, d->H, d->M1, d->nsup, d->T);
+    return REDCLIFF_EINVAL;
+  }
+  const int Lmax = rc_lmax(*d);
+  if (d->T < Lmax) { rc_set_error("T=%d shorter than max(gen_lag, embed_lag)=%d", d->T, Lmax); return REDCLIFF_EINVAL; }
+  if (d->p > 64 || d->K > 16 || d->h > 128 || d->F > 64 || d->n > 4 || d->M1 > 64 || d->Bmax > 512 ||
+      d->p * d->H > 32 * RC_BLOCK || d->M1 * d->H > 32 * RC_BLOCK || d->F * d->H > 32 * RC_BLOCK || d->L > 64) {
+    rc_set_error("dims outside kernel limits (p<=64 K<=16 h<=128 F<=64 n<=4 M1<=64 Bmax<=512 p*H,M1*H,F*H<=8192)");
+    return REDCLIFF_ELIMIT;
+  }
+  if (d->F < d->L) {
+    rc_set_error("fused path needs embed_lag >= gen_lag (forward and GC embedder windows coincide)");
+    return REDCLIFF_ELIMIT;
+  }
+  if (rc_emb_bwd_lds(*d) > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
+    rc_set_error("embedder backward LDS budget exceeded for Bmax*K=%d", d->Bmax * d->K);
+    return REDCLIFF_ELIMIT;
+  }
+  return 0;
+}
+
+extern "C" {
+
+int redcliff_abi_version(void) { return REDCLIFF_ABI_VERSION; }
+
+const char* redcliff_last_error(void) { return g_err; }
+
+size_t redcliff_workspace_bytes(const RedcliffDims* d) {
+  if (check_dims(d) != 0) return 0;
+  return sizeof(float) * (size_t)rc_ws_off(*d).total * (size_t)d->R;
+}
+
+size_t redcliff_emb_param_count(const RedcliffDims* d) { return d ? (size_t)rc_emb_off(*d).total : 0; }
+size_t redcliff_fac_param_count(const RedcliffDims* d) { return d ? (size_t)rc_fac_off(*d).total : 0; }
+
+// Offsets (floats, per replica) of the workspace regions the host reads back:
+// out[0..] = T R f1 w a y G G0 dwp dAadj dWi dS dgb S dZ amat lossp xsim gfc total
+int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out) {
+  if (check_dims(d) != 0) return REDCLIFF_EINVAL;
+  const WsOff o = rc_ws_off(*d);
+  const int64_t v[] = {o.T, o.R, o.f1, o.w, o.a, o.y, o.G, o.G0, o.dwp, o.dAadj, o.dWi, o.dS, o.dgb, o.S, o.dZ,
+                       o.amat, o.lossp, o.xsim, o.gfc, o.total};
+  const int nv = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n_out && i < nv; ++i) out[i] = v[i];
+  return nv;
+}
+
+int redcliff_bn_batch_stats(const RedcliffDims* d, const float* X, int64_t x_rstride, int64_t N, int32_t B,
+                            double* stats, int64_t stats_rstride, void* stream) {
+  int e = check_dims(d);
+  if (e) return e;
+  if (!X || !stats || N < 1 || B < 1) { rc_set_error("bn_batch_stats: bad arguments"); return REDCLIFF_EINVAL; }
+  return rc_launch_bn_stats(*d, X, x_rstride, N, B, stats, stats_rstride, (hipStream_t)stream);
+}
+
+int redcliff_dgcnn_supports(const RedcliffDims* d, const float* emb, int64_t emb_stride, void* ws, void* stream) {
+  int e = check_dims(d);
+  if (e) return e;
+  const WsOff wo = rc_ws_off(*d);
+  return rc_launch_supports(*d, emb, emb_stride, (float*)ws, wo.total, rc_emb_off(*d), wo, (hipStream_t)stream);
+}
+
+static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
+  int e = check_dims(&a->d);
+  if (e) return e;
+  const RedcliffDims& d = a->d;
+  if (a->B < 1 || a->B > d.Bmax) { rc_set_error("batch %d outside [1, Bmax=%d]", a->B, d.Bmax); return REDCLIFF_EINVAL; }
+  if (!a->X || !a->emb || !a->fac || !a->hyper || !a->ws || !a->bn_rm || !a->bn_rv) {
+    rc_set_error("null buffer in step arguments");
+    return REDCLIFF_EINVAL;
+  }
+  const WsOff wo = rc_ws_off(d);
+  if (a->ws_bytes < sizeof(float) * (size_t)wo.total * (size_t)d.R) {
+    rc_set_error("workspace too small: %zu < %zu", a->ws_bytes, sizeof(float) * (size_t)wo.total * (size_t)d.R);
+    return REDCLIFF_EWORKSPACE;
+  }
+  if ((a->flags & (RC_LOSS_FORECAST | RC_VALUES)) && d.T < rc_lmax(d) + 1) {
+    rc_set_error("forecast loss needs T > max(gen_lag, embed_lag)");
+    return REDCLIFF_EINVAL;
+  }
+  if ((a->flags & RC_BN_TRAIN) && !a->bn_stats) { rc_set_error("train-mode BatchNorm needs bn_stats"); return REDCLIFF_EINVAL; }
+  if ((a->flags & (RC_LOSS_FACTOR | RC_CONFUSION)) && d.nsup > 0 && !a->labels) {
+    rc_set_error("factor-score loss needs labels");
+    return REDCLIFF_EINVAL;
+  }
+  if ((a->flags & RC_VALUES) && !a->acc) { rc_set_error("RC_VALUES needs acc"); return REDCLIFF_EINVAL; }
+  if ((a->flags & RC_CONFUSION) && d.nsup > 0 && !a->confusion) { rc_set_error("RC_CONFUSION needs confusion"); return REDCLIFF_EINVAL; }
+  if ((a->flags & (RC_STEP_A | RC_STEP_B)) && (!a->emb_m || !a->emb_v || !a->fac_m || !a->fac_v)) {
+    rc_set_error("optimizer state missing");
+    return REDCLIFF_EINVAL;
+  }
+  memset(&c, 0, sizeof(c));
+  c.d = d;
+  c.B = a->B;
+  c.Lmax = rc_lmax(d);
+  c.Ls = rc_ls(d);
+  c.flags = a->flags;
+  c.nbn = a->n_bn_updates;
+  c.tA = a->tA;
+  c.tB = a->tB;
+  c.X = a->X; c.xr = a->x_rstride; c.row0 = a->row0;
+  c.lab = a->labels; c.labr = a->lab_rstride;
+  c.bns = a->bn_stats; c.bnsr = a->bn_stats_rstride;
+  c.emb = a->emb; c.embM = a->emb_m; c.embV = a->emb_v; c.es = a->emb_stride;
+  c.fac = a->fac; c.facM = a->fac_m; c.facV = a->fac_v; c.fs = a->fac_stride;
+  c.rm = a->bn_rm; c.rv = a->bn_rv;
+  c.hyp = a->hyper;
+  c.ws = (float*)a->ws; c.wss = wo.total;
+  c.acc = a->acc;
+  c.conf = a->confusion;
+  c.eo = rc_emb_off(d);
+  c.fo = rc_fac_off(d);
+  c.wo = wo;
+  return 0;
+}
+
+int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
+  if (!a) { rc_set_error("null step arguments"); return REDCLIFF_EINVAL; }
+  StepCtx c;
+  int e = make_ctx(a, c);
+  if (e) return e;
+  hipStream_t s = (hipStream_t)stream;
+  const int fl = a->flags;
+  const bool emb_grad = fl & RC_STEP_A;
+  const bool fac = (fl & (RC_STEP_B | RC_VALUES | RC_STORE_OUTPUTS)) || (emb_grad && (fl & (RC_LOSS_FORECAST | RC_LOSS_ADJ)));
+  if (fl & RC_REFRESH_SUPPORTS) {
+    if ((e = timed(KT_SUPPORTS, s, [&] { return rc_launch_supports(c.d, c.emb, c.es, c.ws, c.wss, c.eo, c.wo, s); })))
+      return e;
+  }
+  if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd(c, s); }))) return e;
+  if (fac) {
+    if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd(c, s); }))) return e;
+    if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
+  }
+  if (emb_grad) {
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
+  } else if (fl & (RC_VALUES | RC_CONFUSION)) {
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
+  }
+  if (emb_grad || c.nbn > 0) {
+    if ((e = timed(KT_EMB_FINAL, s, [&] { return rc_launch_emb_final(c, s); }))) return e;
+  }
+  return 0;
+}
+
+int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_t* rows, const int32_t* sizes,
+                         int32_t bn_stats_step, void* stream) {
+  if (!a || nsteps < 0 || (nsteps > 0 && (!rows || !sizes))) { rc_set_error("train_steps: bad arguments"); return REDCLIFF_EINVAL; }
+  RedcliffStepArgs s = *a;
+  for (int32_t i = 0; i < nsteps; ++i) {
+    s.row0 = rows[i];
+    s.B = sizes[i];
+    s.flags = (i == 0) ? a->flags : (a->flags & ~RC_REFRESH_SUPPORTS);
+    s.tA = a->tA + ((a->flags & RC_STEP_A) ? i : 0);
+    s.tB = a->tB + ((a->flags & RC_STEP_B) ? i : 0);
+    if (a->bn_stats) s.bn_stats = a->bn_stats + (int64_t)i * bn_stats_step;
+    const int e = redcliff_train_step(&s, stream);
+    if (e) return e;
+  }
+  return 0;
+}
+
+// Per-kernel timing: while enabled every launch of redcliff_train_step is bracketed by
+// HIP events on its stream.  redcliff_kernel_times() waits for the recorded events,
+// adds the elapsed milliseconds per kernel (ids: supports, emb_fwd, fac_fwd, fac_bwd,
+// emb_bwd, emb_final) into total_ms[]/counts[] and clears the record.
+int redcliff_kernel_timing(int32_t enable) {
+  g_timing = enable != 0;
+  return 0;
+}
+
+int redcliff_kernel_times(double* total_ms, int64_t* counts, int32_t n) {
+  for (int i = 0; i < n; ++i) { total_ms[i] = 0.0; counts[i] = 0; }
+  int err = 0;
+  for (auto& t : g_launches) {
+    float ms = 0.f;
+    if (!err) err = rc_check(hipEventSynchronize(t.b), "kernel_times");
+    if (!err) err = rc_check(hipEventElapsedTime(&ms, t.a, t.b), "kernel_times");
+    if (!err && t.id < n) { total_ms[t.id] += ms; counts[t.id] += 1; }
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  g_launches.clear();
+  return err ? err : KT_N;
+}
+
+}  // extern "C"

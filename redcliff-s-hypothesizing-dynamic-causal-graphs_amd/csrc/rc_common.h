@@ -1,0 +1,216 @@
+// rc_common.h -- shared layout / context definitions for the REDCLIFF-S gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "redcliff_hip.h"
+
+#define RC_BLOCK 256
+#define RC_LDS_LIMIT_FLOATS 16384  // 64 KiB of dynamic LDS per workgroup
+
+// Offsets (in floats) inside one replica's packed embedder parameters.
+struct EmbOff {
+  int64_t A, gcW, bnw, bnb, fc1W, fc1b, fc2W, fc2b, total;
+};
+// Offsets inside one replica's packed factor parameters.
+struct FacOff {
+  int64_t W0, b0, W1, b1, total;
+};
+// Offsets (in floats) inside one replica's workspace slice.
+struct WsOff {
+  int64_t T;      // [Bmax][n][p][F]   Chebyshev-filtered embedder inputs S_i x
+  int64_t R;      // [Bmax][p][H]      relu(graph-conv) activations
+  int64_t f1;     // [Bmax][M1]        fc1 pre-activation
+  int64_t w;      // [Bmax][K]         raw embedder output (pre-sigmoid)
+  int64_t a;      // [K][p][Bmax][h]   factor hidden activations (reused for dz)
+  int64_t y;      // [Bmax][K][p]      per-factor predictions
+  int64_t G;      // [K][p][p][L]      lagged group norms of W0
+  int64_t G0;     // [K][p][p]         lag-free group norms of W0
+  int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
+  int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
+  int64_t dWi;    // [p][n][F][H]      graph-conv weight gradient partials (per node)
+  int64_t dS;     // [n][p][p]         gradient wrt Chebyshev supports
+  int64_t dgb;    // [p][2][F]         BatchNorm affine gradient partials (per node)
+  int64_t S;      // [n][p][p]         supports (S_0 = I)
+  int64_t dZ;     // [p][Bmax][H]      graph-conv output gradient per node
+  int64_t amat;   // [8][p][p]         scratch for the adjacency backward
+  int64_t lossp;  // [p + K*p + 8]     per-batch loss partials
+  int64_t xsim;   // [Bmax][p]         mixed forecast
+  int64_t gfc;    // [K*M1 + K + M1]   fc2W / fc2b / fc1b gradients (applied in the final kernel)
+  int64_t total;
+};
+
+__host__ __device__ inline int rc_lmax(const RedcliffDims& d) { return d.L > d.F ? d.L : d.F; }
+__host__ __device__ inline int rc_ls(const RedcliffDims& d) { return d.L < d.F ? d.L : d.F; }
+
+inline EmbOff rc_emb_off(const RedcliffDims& d) {
+  EmbOff o;
+  int64_t x = 0;
+  o.A = x; x += (int64_t)d.p * d.p;
+  o.gcW = x; x += (int64_t)d.n * d.F * d.H;
+  o.bnw = x; x += d.F;
+  o.bnb = x; x += d.F;
+  o.fc1W = x; x += (int64_t)d.M1 * d.p * d.H;
+  o.fc1b = x; x += d.M1;
+  o.fc2W = x; x += (int64_t)d.K * d.M1;
+  o.fc2b = x; x += d.K;
+  o.total = x;
+  return o;
+}
+
+inline FacOff rc_fac_off(const RedcliffDims& d) {
+  FacOff o;
+  int64_t x = 0;
+  int64_t kp = (int64_t)d.K * d.p;
+  o.W0 = x; x += kp * d.h * d.p * d.L;
+  o.b0 = x; x += kp * d.h;
+  o.W1 = x; x += kp * d.h;
+  o.b1 = x; x += kp;
+  o.total = x;
+  return o;
+}
+
+inline int64_t rc_align64(int64_t x) { return (x + 63) & ~(int64_t)63; }
+
+inline WsOff rc_ws_off(const RedcliffDims& d) {
+  WsOff o;
+  int64_t x = 0;
+  const int64_t B = d.Bmax, p = d.p, K = d.K;
+  o.T = x; x = rc_align64(x + B * d.n * p * d.F);
+  o.R = x; x = rc_align64(x + B * p * d.H);
+  o.f1 = x; x = rc_align64(x + B * d.M1);
+  o.w = x; x = rc_align64(x + B * K);
+  o.a = x; x = rc_align64(x + K * p * B * d.h);
+  o.y = x; x = rc_align64(x + B * K * p);
+  o.G = x; x = rc_align64(x + K * p * p * d.L);
+  o.G0 = x; x = rc_align64(x + K * p * p);
+  o.dwp = x; x = rc_align64(x + p * B * K);
+  o.dAadj = x; x = rc_align64(x + K * p * p);
+  o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);
+  o.dS = x; x = rc_align64(x + d.n * p * p);
+  o.dgb = x; x = rc_align64(x + p * 2 * d.F);
+  o.S = x; x = rc_align64(x + d.n * p * p);
+  o.dZ = x; x = rc_align64(x + p * B * d.H);
+  o.amat = x; x = rc_align64(x + 8 * p * p);
+  o.lossp = x; x = rc_align64(x + p + K * p + 8);
+  o.xsim = x; x = rc_align64(x + B * p);
+  o.gfc = x; x = rc_align64(x + K * d.M1 + K + d.M1);
+  o.total = x;
+  return o;
+}
+
+// Slots of the per-batch loss partials (after the p + K*p per-network entries).
+#define LP_FACTOR 0
+#define LP_FWL1 1
+#define LP_COS 2
+#define LP_SMOOTH 3
+// Validation accumulator slots (coefficient-normalised, validate_training :1704-1729).
+#define ACC_FORECAST 0
+#define ACC_FACTOR 1
+#define ACC_COS 2
+#define ACC_FWL1 3
+#define ACC_SMOOTH 4
+#define ACC_ADJ 5
+#define ACC_COMBO 6
+#define ACC_BATCHES 7
+
+// Everything a step kernel needs, passed by value.
+struct StepCtx {
+  RedcliffDims d;
+  int B, Lmax, Ls, flags, nbn;
+  int tA, tB;  // Adam step numbers (1-based)
+  const float* X; int64_t xr; int64_t row0;
+  const float* lab; int64_t labr;
+  const double* bns; int64_t bnsr;
+  float *emb, *embM, *embV; int64_t es;
+  float *fac, *facM, *facV; int64_t fs;
+  float *rm, *rv;
+  const RedcliffReplicaHyper* hyp;
+  float* ws; int64_t wss;
+  double* acc;
+  int* conf;
+  EmbOff eo;
+  FacOff fo;
+  WsOff wo;
+};
+
+// ---------------------------------------------------------------------------------------------
+// device helpers
+__device__ inline float rc_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum; every thread gets the result.  `red` must hold >= RC_BLOCK/64 floats.
+__device__ inline float rc_block_sum(float v, float* red) {
+  v = rc_wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+__device__ inline double rc_block_sum_d(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+__device__ inline float rc_sign(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
+__device__ inline float rc_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
+
+// Bias-correction scalars of step t, computed the way torch's Python side does (doubles),
+// then rounded to the fp32 values the element-wise kernels apply.
+struct RcAdamScalars {
+  float neg_step, bc2s, eps, wd, b2, omb1, omb2;
+};
+__device__ inline RcAdamScalars rc_adam_scalars(const RedcliffAdamHyper& h, int t) {
+  RcAdamScalars s;
+  const double bc1 = 1.0 - pow(h.beta1, (double)t);
+  const double bc2 = 1.0 - pow(h.beta2, (double)t);
+  s.neg_step = (float)(-(h.lr / bc1));
+  s.bc2s = (float)sqrt(bc2);
+  s.eps = h.eps;
+  s.wd = h.weight_decay;
+  s.b2 = h.beta2_f;
+  s.omb1 = h.one_minus_beta1_f;
+  s.omb2 = h.one_minus_beta2_f;
+  return s;
+}
+
+// torch.optim.Adam (_single_tensor_adam, coupled L2 weight decay) for one element:
+//   g += wd*p; m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+//   p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1)
+__device__ inline void rc_adam(float& p, float& m, float& v, float g, const RcAdamScalars& s) {
+  if (s.wd != 0.f) g = g + p * s.wd;
+  m = m + s.omb1 * (g - m);
+  v = v * s.b2 + (s.omb2 * g) * g;
+  const float denom = sqrtf(v) / s.bc2s + s.eps;
+  p = p + s.neg_step * (m / denom);
+}
+
+// Shared host-side helpers (defined in rc_capi.hip).
+void rc_set_error(const char* fmt, ...);
+int rc_check(hipError_t e, const char* what);
+
+// Launchers implemented in the kernel translation units.
+int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s);
+int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s);
+int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
+int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
+int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
+int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,
+                       WsOff wo, hipStream_t s);
+int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,
+                       hipStream_t s);

@@ -1,0 +1,782 @@
+// rc_embed.hip -- DGCNN factor-score embedder on gfx950: forward, backward, optimizer
+// finalisation, Chebyshev supports and BatchNorm batch statistics.
+//
+// Reference: models/redcliff_factor_score_embedders.py:335-392 (DGCNN_Embedder),
+// models/dgcnn.py:15-64 (DGCNN_Model) and the torcheeg 1.1.3 DGCNN it wraps
+// (restated in oracle/torcheeg_dgcnn.py):
+//   x_bn = BN1(x)                      BatchNorm1d over F features, stats over (B, p)
+//   L    = D^-1/2 relu(A) D^-1/2       normalize_A
+//   Z_b  = sum_i (S_i x_bn_b) W_i      S = [I, L, L^2, ...]  (Chebynet)
+//   w_b  = fc2(relu(fc1(vec(relu(Z_b)))))
+// One batch_update runs the embedder 3x on the same window (forward + two GC calls,
+// ...withStateSmoothing.py:844-856); the math is identical, so it is evaluated once,
+// the three upstream gradients are summed, and the BatchNorm running statistics are
+// advanced n_bn_updates (=3) times.
+#include "rc_common.h"
+
+namespace {
+
+// BatchNorm scale/shift exactly as torch's CPU kernel forms them
+// (batch_norm_cpu_collect_linear_and_constant_terms): y = x*alpha + beta.
+__device__ void bn_affine(const StepCtx& c, int r, const float* E, float* alpha, float* beta, float* mean_out,
+                          float* inv_out) {
+  const RedcliffDims& d = c.d;
+  const bool train = c.flags & RC_BN_TRAIN;
+  for (int f = threadIdx.x; f < d.F; f += blockDim.x) {
+    float mean, inv;
+    if (train) {
+      const double* st = c.bns + r * c.bnsr;
+      mean = (float)st[f];
+      inv = (float)(1.0 / sqrt(st[d.F + f] + c.hyp[r].bn_eps));
+    } else {
+      mean = c.rm[r * d.F + f];
+      inv = 1.0f / sqrtf(c.rv[r * d.F + f] + (float)c.hyp[r].bn_eps);
+    }
+    const float a = inv * E[c.eo.bnw + f];
+    alpha[f] = a;
+    beta[f] = E[c.eo.bnb + f] - mean * a;
+    if (mean_out) mean_out[f] = mean;
+    if (inv_out) inv_out[f] = inv;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: embedder forward.  grid (ceil(B/SB), R); one workgroup handles SB windows.
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y;
+  const int b0 = blockIdx.x * SB;
+  const int nb = min(SB, c.B - b0);
+  if (nb <= 0) return;
+  const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
+  const int pF = p * F, pH = p * H;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr;
+  const int tid = threadIdx.x;
+
+  extern __shared__ float sm[];
+  float* xs = sm;              // [SB][p][F]
+  float* Ti = xs + SB * pF;    // [p][F]
+  float* Rl = Ti + pF;         // [SB][p*H]
+  float* f1l = Rl + SB * pH;   // [SB][M1]
+  float* alpha = f1l + SB * M1;
+  float* beta = alpha + F;
+
+  bn_affine(c, r, E, alpha, beta, nullptr, nullptr);
+  __syncthreads();
+  for (int e = tid; e < nb * pF; e += RC_BLOCK) {
+    const int s = e / pF, rem = e - s * pF, ch = rem / F, f = rem - ch * F;
+    const int64_t row = c.row0 + b0 + s;
+    const float x = X[(row * d.T + (c.Lmax - F + f)) * p + ch];
+    xs[e] = x * alpha[f] + beta[f];
+  }
+  __syncthreads();
+
+  const float* S = ws + c.wo.S;
+  const float* gw = E + c.eo.gcW;
+  const int NZ = (pH + RC_BLOCK - 1) / RC_BLOCK;  // <= 32 (checked on the host)
+  for (int s = 0; s < nb; ++s) {
+    float z[32];
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) z[kk] = 0.f;
+    for (int i = 0; i < n; ++i) {
+      for (int e = tid; e < pF; e += RC_BLOCK) {
+        const int ch = e / F, f = e - ch * F;
+        float v;
+        if (i == 0) {
+          v = xs[s * pF + e];
+        } else {
+          v = 0.f;
+          const float* Srow = S + ((int64_t)i * p + ch) * p;
+          for (int cc = 0; cc < p; ++cc) v += Srow[cc] * xs[s * pF + cc * F + f];
+        }
+        Ti[e] = v;
+        ws[c.wo.T + ((int64_t)(b0 + s) * n + i) * pF + e] = v;
+      }
+      __syncthreads();
+      const float* Wi = gw + (int64_t)i * F * H;
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) {
+        const int e = tid + kk * RC_BLOCK;
+        if (kk < NZ && e < pH) {
+          const int ch = e / H, hh = e - ch * H;
+          float acc = z[kk];
+          const float* trow = Ti + ch * F;
+          for (int f = 0; f < F; ++f) acc += trow[f] * Wi[f * H + hh];
+          z[kk] = acc;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (kk < NZ && e < pH) {
+        const float v = fmaxf(z[kk], 0.f);
+        Rl[s * pH + e] = v;
+        ws[c.wo.R + (int64_t)(b0 + s) * pH + e] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  // fc1: one wave per output row, lanes split the p*H contraction (coalesced weight rows)
+  const float* W1 = E + c.eo.fc1W;
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int m = wv; m < M1; m += RC_BLOCK / 64) {
+    float acc[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) acc[s] = 0.f;
+    const float* wr = W1 + (int64_t)m * pH;
+    for (int q = lane; q < pH; q += 64) {
+      const float wq = wr[q];
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+        if (s < nb) acc[s] += wq * Rl[s * pH + q];
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < nb) {
+        const float t = rc_wave_sum(acc[s]) + E[c.eo.fc1b + m];
+        if (lane == 0) {
+          f1l[s * M1 + m] = t;
+          ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = t;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < nb * K; e += RC_BLOCK) {
+    const int s = e / K, k = e - s * K;
+    const float* w2 = E + c.eo.fc2W + (int64_t)k * M1;
+    float acc = 0.f;
+    for (int m = 0; m < M1; ++m) acc += w2[m] * fmaxf(f1l[s * M1 + m], 0.f);
+    ws[c.wo.w + (int64_t)(b0 + s) * K + k] = acc + E[c.eo.fc2b + k];
+  }
+}
+
+// dL/d(raw embedder output) for every window of the batch, into LDS dr[B][K].
+// Sums the factor-side gradient (per-channel partials from the factor kernel) with the
+// supervised-score MSE and factor-weight L1 terms, through the optional sigmoid.
+__device__ void build_draw(const StepCtx& c, int r, float* dr) {
+  const RedcliffDims& d = c.d;
+  const int K = d.K, B = c.B, nsup = d.nsup;
+  const float* ws = c.ws + r * c.wss;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
+  const bool sig = d.use_sigmoid;
+  const float ecc = d.sigmoid_ecc;
+  const int ncol = nsup > 0 ? nsup : K;  // columns of factor_scores[0] (state_label_preds)
+  for (int e = threadIdx.x; e < B * K; e += blockDim.x) {
+    const int b = e / K, k = e - b * K;
+    const float raw = ws[c.wo.w + (int64_t)b * K + k];
+    const float weff = sig ? rc_sigmoid(ecc * raw) : raw;
+    float gw = 0.f;
+    if (fac_grad)
+      for (int j = 0; j < d.p; ++j) gw += ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k];
+    float graw = sig ? gw * ecc * weff * (1.f - weff) : gw;
+    if (k < ncol) {
+      // score used by the factor MSE and the L1: class logits when supervised, else w
+      const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
+      float gsl = 0.f;
+      if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) {
+        const float y = c.lab[r * c.labr + (c.row0 + b) * K + k];
+        gsl += hy.c_factor * (2.f / (float)(B * nsup)) * (sl - y);
+      }
+      if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
+      if (nsup > 0)
+        graw += sig ? gsl * sl * (1.f - sl) : gsl;
+      else
+        graw += sig ? gsl * ecc * weff * (1.f - weff) : gsl;
+    }
+    dr[e] = graw;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3 head: fc2 / fc1-bias gradients, loss values, confusion matrix.  (blockIdx.x == p)
+__device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
+  const RedcliffDims& d = c.d;
+  const int K = d.K, M1 = d.M1, B = c.B, p = d.p, nsup = d.nsup;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const int tid = threadIdx.x;
+  float* dr = sm;
+  float* red = dr + ((d.Bmax * K + 1) & ~1);  // even offset: doubles follow
+  if (c.flags & RC_STEP_A) {
+    build_draw(c, r, dr);
+    __syncthreads();
+    const float* f1 = ws + c.wo.f1;
+    float* gfc = ws + c.wo.gfc;
+    for (int e = tid; e < K * M1 + K + M1; e += RC_BLOCK) {
+      float g = 0.f;
+      if (e < K * M1) {
+        const int k = e / M1, m = e - k * M1;
+        for (int b = 0; b < B; ++b) g += dr[b * K + k] * fmaxf(f1[(int64_t)b * M1 + m], 0.f);
+      } else if (e < K * M1 + K) {
+        const int k = e - K * M1;
+        for (int b = 0; b < B; ++b) g += dr[b * K + k];
+      } else {
+        const int m = e - K * M1 - K;
+        for (int b = 0; b < B; ++b) {
+          if (f1[(int64_t)b * M1 + m] > 0.f) {
+            float t = 0.f;
+            for (int k = 0; k < K; ++k) t += dr[b * K + k] * E[c.eo.fc2W + (int64_t)k * M1 + m];
+            g += t;
+          }
+        }
+      }
+      gfc[e] = g;
+    }
+  }
+  if (!(c.flags & (RC_VALUES | RC_CONFUSION))) return;
+  __syncthreads();
+  const bool sig = d.use_sigmoid;
+  const float ecc = d.sigmoid_ecc;
+  const float* wraw = ws + c.wo.w;
+  const int ncol = nsup > 0 ? nsup : K;
+  double* dred = reinterpret_cast<double*>(red + 8);
+  if (c.flags & RC_VALUES) {
+    // supervised MSE and factor-weight L1 (values)
+    double fsum = 0.0, l1 = 0.0;
+    for (int e = tid; e < B * K; e += RC_BLOCK) {
+      const int b = e / K, k = e - b * K;
+      if (k >= ncol) continue;
+      const float raw = wraw[(int64_t)b * K + k];
+      const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : (sig ? rc_sigmoid(ecc * raw) : raw);
+      l1 += fabsf(sl);
+      if (nsup > 0) {
+        const float y = c.lab[r * c.labr + (c.row0 + b) * K + k];
+        fsum += (double)(sl - y) * (double)(sl - y);
+      }
+    }
+    fsum = rc_block_sum_d(fsum, dred);
+    l1 = rc_block_sum_d(l1, dred);
+    // cosine similarity of the lag-free conditional GC estimates (metrics.py:342-381):
+    // v_bk[r][c] = w_bk * G0[k][r][c] + A[c][r] - I[r][c]; value only (detached).
+    double cs = 0.0;
+    const int npair = K * (K - 1) / 2;
+    const float* G0 = ws + c.wo.G0;
+    const float* A = E + c.eo.A;
+    for (int e = tid; e < B * npair; e += RC_BLOCK) {
+      const int b = e / npair;
+      int q = e - b * npair, k1 = 0;
+      while (q >= K - 1 - k1) { q -= K - 1 - k1; ++k1; }
+      const int k2 = k1 + 1 + q;
+      const float r1 = wraw[(int64_t)b * K + k1], r2 = wraw[(int64_t)b * K + k2];
+      const float w1 = sig ? rc_sigmoid(ecc * r1) : r1, w2 = sig ? rc_sigmoid(ecc * r2) : r2;
+      float dot = 0.f, n1 = 0.f, n2 = 0.f;
+      for (int rr = 0; rr < p; ++rr)
+        for (int cc = 0; cc < p; ++cc) {
+          const float at = A[cc * p + rr];
+          const float eye = (rr == cc ? 1.f : 0.f);
+          const float v1 = (w1 * G0[((int64_t)k1 * p + rr) * p + cc] + at) - eye;
+          const float v2 = (w2 * G0[((int64_t)k2 * p + rr) * p + cc] + at) - eye;
+          dot += v1 * v2;
+          n1 += v1 * v1;
+          n2 += v2 * v2;
+        }
+      const float eps2 = 1e-16f;
+      cs += (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
+    }
+    cs = (K > 1) ? rc_block_sum_d(cs, dred) : 0.0;
+    if (tid == 0) {
+      const float* lp = ws + c.wo.lossp;
+      double fore = 0.0;
+      for (int j = 0; j < p; ++j) fore += (double)lp[j] / (double)B;
+      fore *= hy.c_forecast;
+      double adj = 0.0;
+      for (int e = 0; e < K * p; ++e) adj += lp[p + e];
+      const double factor = nsup > 0 ? hy.c_factor * fsum / (double)(B * nsup) : 0.0;
+      const double fwl1 = hy.c_fwl1 * (l1 - 1.0);
+      const double cosv = hy.c_cos * cs;
+      const double smooth = 0.0;  // num_sims == 1
+      const double combo = fore + factor + fwl1 + smooth + adj + (K > 1 ? cosv : 0.0);
+      double* acc = c.acc + r * 8;
+      acc[ACC_FORECAST] += hy.c_forecast > 0.f ? fore / hy.c_forecast : fore;
+      acc[ACC_FACTOR] += hy.c_factor > 0.f ? factor / hy.c_factor : factor;
+      acc[ACC_COS] += (K > 1) ? (hy.c_cos > 0.f ? cosv / hy.c_cos : cosv) : 0.0;
+      acc[ACC_FWL1] += hy.c_fwl1 > 0.f ? fwl1 / hy.c_fwl1 : fwl1;
+      acc[ACC_SMOOTH] += 0.0;
+      acc[ACC_ADJ] += hy.c_adj > 0.f ? adj / hy.c_adj : adj;
+      acc[ACC_COMBO] += combo;
+      acc[ACC_BATCHES] += 1.0;
+    }
+  }
+  if ((c.flags & RC_CONFUSION) && nsup > 0 && tid == 0) {
+    // np.argmax (first maximum) of state_label_preds[0] and of the labels (:801-803)
+    int* conf = c.conf + (int64_t)r * nsup * nsup;
+    for (int b = 0; b < B; ++b) {
+      int pred = 0, lab = 0;
+      float best = 0.f, bestl = 0.f;
+      for (int k = 0; k < nsup; ++k) {
+        const float raw = wraw[(int64_t)b * K + k];
+        const float sl = sig ? rc_sigmoid(raw) : raw;
+        const float y = c.lab[r * c.labr + (c.row0 + b) * K + k];
+        if (k == 0 || sl > best) { best = sl; pred = k; }
+        if (k == 0 || y > bestl) { bestl = y; lab = k; }
+      }
+      conf[lab * nsup + pred] += 1;
+    }
+  }
+}
+
+// K3 node workgroup c: fc1 columns of node c (gradient + Adam), graph-conv output
+// gradient dZ, per-node partials of dW_i, dS_i row c and BatchNorm affine gradients.
+#define EMB_CH 16
+__device__ void emb_bwd_node(const StepCtx& c, int r, int node, float* sm) {
+  const RedcliffDims& d = c.d;
+  const int K = d.K, M1 = d.M1, B = c.B, p = d.p, H = d.H, F = d.F, n = d.n;
+  const int pH = p * H, pF = p * F;
+  float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const int tid = threadIdx.x;
+  float* dr = sm;                 // [B][K]
+  float* Fs = dr + B * K;         // [M1][H]   fc1 columns of this node
+  float* df1c = Fs + M1 * H;      // [CH][M1]
+  float* Rc = df1c + EMB_CH * M1; // [CH][H]
+  float* dZc = Rc + EMB_CH * H;   // [CH][H]
+
+  build_draw(c, r, dr);
+  for (int e = tid; e < M1 * H; e += RC_BLOCK) {
+    const int m = e / H, hh = e - m * H;
+    Fs[e] = E[c.eo.fc1W + (int64_t)m * pH + node * H + hh];
+  }
+  __syncthreads();
+  const float* f1 = ws + c.wo.f1;
+  const float* Rg = ws + c.wo.R;
+  float* dZg = ws + c.wo.dZ + (int64_t)node * d.Bmax * H;
+  const int NE = (M1 * H + RC_BLOCK - 1) / RC_BLOCK;  // <= 32
+  float acc[32];
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) acc[kk] = 0.f;
+  for (int bc = 0; bc < B; bc += EMB_CH) {
+    const int nbc = min(EMB_CH, B - bc);
+    for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
+      const int s = e / M1, m = e - s * M1, b = bc + s;
+      float g = 0.f;
+      if (f1[(int64_t)b * M1 + m] > 0.f)
+        for (int k = 0; k < K; ++k) g += dr[b * K + k] * E[c.eo.fc2W + (int64_t)k * M1 + m];
+      df1c[e] = g;
+    }
+    for (int e = tid; e < nbc * H; e += RC_BLOCK) {
+      const int s = e / H, hh = e - s * H;
+      Rc[e] = Rg[(int64_t)(bc + s) * pH + node * H + hh];
+    }
+    __syncthreads();
+    for (int e = tid; e < nbc * H; e += RC_BLOCK) {
+      const int s = e / H, hh = e - s * H;
+      float g = 0.f;
+      for (int m = 0; m < M1; ++m) g += Fs[m * H + hh] * df1c[s * M1 + m];
+      const float v = Rc[e] > 0.f ? g : 0.f;
+      dZc[e] = v;
+      dZg[(int64_t)(bc + s) * H + hh] = v;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (kk < NE && e < M1 * H) {
+        const int m = e / H, hh = e - m * H;
+        float a = acc[kk];
+        for (int s = 0; s < nbc; ++s) a += df1c[s * M1 + m] * Rc[s * H + hh];
+        acc[kk] = a;
+      }
+    }
+    __syncthreads();
+  }
+  // Adam on this node's fc1 columns (no other workgroup reads them in this kernel)
+  {
+    const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
+    float* P = E + c.eo.fc1W;
+    float* Mm = c.embM + r * c.es + c.eo.fc1W;
+    float* V = c.embV + r * c.es + c.eo.fc1W;
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (kk < NE && e < M1 * H) {
+        const int m = e / H, hh = e - m * H;
+        const int64_t idx = (int64_t)m * pH + node * H + hh;
+        float pp = P[idx], mm = Mm[idx], vv = V[idx];
+        rc_adam(pp, mm, vv, acc[kk], as);
+        P[idx] = pp; Mm[idx] = mm; V[idx] = vv;
+      }
+    }
+  }
+  __syncthreads();
+
+  // dW_i partial of this node: sum_b T_i,b[node][f] * dZ_b[node][h]
+  const float* Tg = ws + c.wo.T;
+  float* Tc = df1c;  // reuse: [CH][F] (F <= M1 checked on host)
+  const int NW = (F * H + RC_BLOCK - 1) / RC_BLOCK;  // <= 32
+  for (int i = 0; i < n; ++i) {
+    float a2[32];
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) a2[kk] = 0.f;
+    for (int bc = 0; bc < B; bc += EMB_CH) {
+      const int nbc = min(EMB_CH, B - bc);
+      for (int e = tid; e < nbc * F; e += RC_BLOCK) {
+        const int s = e / F, f = e - s * F;
+        Tc[e] = Tg[((int64_t)(bc + s) * n + i) * pF + node * F + f];
+      }
+      for (int e = tid; e < nbc * H; e += RC_BLOCK) dZc[e] = dZg[(int64_t)bc * H + e];
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) {
+        const int e = tid + kk * RC_BLOCK;
+        if (kk < NW && e < F * H) {
+          const int f = e / H, hh = e - f * H;
+          float a = a2[kk];
+          for (int s = 0; s < nbc; ++s) a += Tc[s * F + f] * dZc[s * H + hh];
+          a2[kk] = a;
+        }
+      }
+      __syncthreads();
+    }
+    float* out = ws + c.wo.dWi + (((int64_t)node * n + i) * F) * H;
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (kk < NW && e < F * H) out[e] = a2[kk];
+    }
+  }
+  __syncthreads();
+
+  // per window: dT_i[f] = sum_h dZ[h] W_i[f][h]; dS_i[node][c'] += dT_i . x_bn[c'];
+  // BN affine partials dgamma_f += sum_i dT_i[f] (S_i xhat)[node][f], dbeta_f += sum_i dT_i[f] rowsum(S_i)[node]
+  float* xh = sm + B * K;          // [p][F]   (reuses Fs)
+  float* dTl = xh + pF;            // [n][F]
+  float* Srow = dTl + n * F;       // [n][p]
+  float* alpha = Srow + n * p;     // [F]
+  float* beta = alpha + F;         // [F]
+  float* mean = beta + F;          // [F]
+  float* inv = mean + F;           // [F]
+  float* rs = inv + F;             // [n]
+  bn_affine(c, r, E, alpha, beta, mean, inv);
+  const float* S = ws + c.wo.S;
+  for (int e = tid; e < n * p; e += RC_BLOCK) {
+    const int i = e / p, cc = e - i * p;
+    Srow[e] = S[((int64_t)i * p + node) * p + cc];
+  }
+  __syncthreads();
+  if (tid < n) {
+    float t = 0.f;
+    for (int cc = 0; cc < p; ++cc) t += Srow[tid * p + cc];
+    rs[tid] = t;
+  }
+  const float* X = c.X + r * c.xr;
+  const float* gw = E + c.eo.gcW;
+  float dSacc = 0.f, dgam = 0.f, dbet = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const int64_t row = c.row0 + b;
+    for (int e = tid; e < pF; e += RC_BLOCK) {
+      const int cc = e / F, f = e - cc * F;
+      xh[e] = (X[(row * d.T + (c.Lmax - F + f)) * p + cc] - mean[f]) * inv[f];
+    }
+    if (tid < n * F) {
+      const int i = tid / F, f = tid - i * F;
+      const float* dz = dZg + (int64_t)b * H;
+      const float* wr = gw + ((int64_t)i * F + f) * H;
+      float t = 0.f;
+      for (int hh = 0; hh < H; ++hh) t += dz[hh] * wr[hh];
+      dTl[tid] = t;
+    }
+    __syncthreads();
+    if (tid < (n - 1) * p) {
+      const int i = 1 + tid / p, cp = tid - (i - 1) * p;
+      const float* X0 = X + (row * d.T + (c.Lmax - F)) * p + cp;
+      float t = 0.f;
+      for (int f = 0; f < F; ++f) t += dTl[i * F + f] * (X0[(int64_t)f * p] * alpha[f] + beta[f]);
+      dSacc += t;
+    }
+    if (tid < F) {
+      const int f = tid;
+      for (int i = 0; i < n; ++i) {
+        float u = 0.f;
+        if (i == 0) {
+          u = xh[node * F + f];
+        } else {
+          for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * xh[cc * F + f];
+        }
+        dgam += dTl[i * F + f] * u;
+        dbet += dTl[i * F + f] * rs[i];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < (n - 1) * p) {
+    const int i = 1 + tid / p, cp = tid - (i - 1) * p;
+    ws[c.wo.dS + ((int64_t)i * p + node) * p + cp] = dSacc;
+  }
+  if (tid < F) {
+    ws[c.wo.dgb + ((int64_t)node * 2 + 0) * F + tid] = dgam;
+    ws[c.wo.dgb + ((int64_t)node * 2 + 1) * F + tid] = dbet;
+  }
+}
+
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int head_only) {
+  extern __shared__ float sm[];
+  const int r = blockIdx.y;
+  if (head_only || (int)blockIdx.x == c.d.p)
+    emb_bwd_head(c, r, sm);
+  else
+    emb_bwd_node(c, r, blockIdx.x, sm);
+}
+
+// Supports of normalize_A(A) into S[n][p][p] (S_0 = I, S_1 = L, S_i = S_{i-1} L).
+__device__ void dev_supports(const float* A, float* S, float* dinv, int p, int n) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < p; i += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < p; ++j) s += fmaxf(A[i * p + j], 0.f);
+    dinv[i] = 1.f / sqrtf(s + 1e-10f);
+  }
+  __syncthreads();
+  for (int e = tid; e < p * p; e += blockDim.x) {
+    const int i = e / p, j = e - i * p;
+    S[e] = (i == j) ? 1.f : 0.f;
+    if (n > 1) S[p * p + e] = (dinv[i] * fmaxf(A[e], 0.f)) * dinv[j];
+  }
+  __syncthreads();
+  for (int l = 2; l < n; ++l) {
+    const float* prev = S + (int64_t)(l - 1) * p * p;
+    const float* Lm = S + (int64_t)p * p;
+    float* out = S + (int64_t)l * p * p;
+    for (int e = tid; e < p * p; e += blockDim.x) {
+      const int i = e / p, j = e - i * p;
+      float t = 0.f;
+      for (int k = 0; k < p; ++k) t += prev[i * p + k] * Lm[k * p + j];
+      out[e] = t;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const float* emb, int64_t es, float* ws,
+                                                       int64_t wss, EmbOff eo, WsOff wo) {
+  const int r = blockIdx.x;
+  __shared__ float dinv[64];
+  dev_supports(emb + r * es + eo.A, ws + r * wss + wo.S, dinv, d.p, d.n);
+}
+
+// ------------------------------------------------------------------------------------------
+// K4: embedder optimizer finalisation.  Workgroups [0, nw) apply Adam to W_i, fc2, fc1 bias,
+// BN affine (reducing per-node partials in fixed order); workgroup nw handles the
+// adjacency A (Chebyshev + normalize_A backward, adjacency-L1 gradient), the BN running
+// statistics and recomputes the supports for the next step.
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y;
+  const int p = d.p, n = d.n, F = d.F, H = d.H, K = d.K, M1 = d.M1;
+  float* E = c.emb + r * c.es;
+  float* Mm = c.embM + r * c.es;
+  float* V = c.embV + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const bool stepA = c.flags & RC_STEP_A;
+  const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
+  const int nFH = n * F * H, nfc = K * M1 + K + M1;
+  const int total = nFH + nfc + 2 * F;
+  if ((int)blockIdx.x < nw) {
+    if (!stepA) return;
+    const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
+    if (e >= total) return;
+    float g = 0.f;
+    int64_t idx;
+    if (e < nFH) {
+      for (int cc = 0; cc < p; ++cc) g += ws[c.wo.dWi + (int64_t)cc * nFH + e];
+      idx = c.eo.gcW + e;
+    } else if (e < nFH + nfc) {
+      const int q = e - nFH;
+      g = ws[c.wo.gfc + q];
+      if (q < K * M1) idx = c.eo.fc2W + q;
+      else if (q < K * M1 + K) idx = c.eo.fc2b + (q - K * M1);
+      else idx = c.eo.fc1b + (q - K * M1 - K);
+    } else {
+      const int q = e - nFH - nfc;
+      const int which = q / F, f = q - which * F;  // 0: gamma, 1: beta
+      for (int cc = 0; cc < p; ++cc) g += ws[c.wo.dgb + ((int64_t)cc * 2 + which) * F + f];
+      idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
+    }
+    float pp = E[idx], mm = Mm[idx], vv = V[idx];
+    rc_adam(pp, mm, vv, g, as);
+    E[idx] = pp; Mm[idx] = mm; V[idx] = vv;
+    return;
+  }
+  // ---- adjacency workgroup
+  const int tid = threadIdx.x;
+  __shared__ float dinv[64], dsum[64], dd[64];
+  const int pp2 = p * p;
+  float* Ar = ws + c.wo.amat;           // relu(A)
+  float* dL = Ar + pp2;
+  float* dSw = dL + pp2;                // working copies of dS_1..dS_{n-1}
+  const float* S = ws + c.wo.S;         // pre-update supports (S_1 = L)
+  if (stepA) {
+    float* A = E + c.eo.A;
+    for (int e = tid; e < pp2; e += RC_BLOCK) {
+      Ar[e] = fmaxf(A[e], 0.f);
+      dL[e] = 0.f;
+    }
+    for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) dSw[e] = ws[c.wo.dS + pp2 + e];
+    __syncthreads();
+    for (int i = tid; i < p; i += RC_BLOCK) {
+      float s = 0.f;
+      for (int j = 0; j < p; ++j) s += Ar[i * p + j];
+      dsum[i] = s;
+      dinv[i] = 1.f / sqrtf(s + 1e-10f);
+    }
+    __syncthreads();
+    // back through S_l = S_{l-1} L, l = n-1 .. 2
+    for (int l = n - 1; l >= 2; --l) {
+      const float* dSl = dSw + (int64_t)(l - 1) * pp2;
+      float* dSprev = dSw + (int64_t)(l - 2) * pp2;
+      const float* Sprev = S + (int64_t)(l - 1) * pp2;
+      const float* Lm = S + pp2;
+      for (int e = tid; e < pp2; e += RC_BLOCK) {
+        const int a = e / p, b = e - a * p;
+        float t1 = 0.f, t2 = 0.f;
+        for (int k = 0; k < p; ++k) {
+          t1 += dSl[a * p + k] * Lm[b * p + k];     // (dS_l L^T)[a][b]
+          t2 += Sprev[k * p + a] * dSl[k * p + b];  // (S_{l-1}^T dS_l)[a][b]
+        }
+        dSprev[e] += t1;
+        dL[e] += t2;
+      }
+      __syncthreads();
+    }
+    if (n >= 2) {
+      for (int e = tid; e < pp2; e += RC_BLOCK) dL[e] += dSw[e];
+      __syncthreads();
+    }
+    // normalize_A backward: L[i][j] = dinv_i relu(A)[i][j] dinv_j, dinv_i = (sum_j relu(A)[i][j] + 1e-10)^-1/2
+    for (int i = tid; i < p; i += RC_BLOCK) {
+      float g = 0.f;
+      for (int j = 0; j < p; ++j) g += dL[i * p + j] * Ar[i * p + j] * dinv[j] + dL[j * p + i] * dinv[j] * Ar[j * p + i];
+      // d(dinv)/d(sum) = -1/2 (sum + 1e-10)^-3/2
+      dd[i] = g * (-0.5f) * dinv[i] * dinv[i] * dinv[i];
+    }
+    __syncthreads();
+    const RedcliffReplicaHyper& hy = c.hyp[r];
+    (void)hy;
+    for (int e = tid; e < pp2; e += RC_BLOCK) {
+      const int i = e / p, j = e - i * p;
+      float g = (A[e] > 0.f) ? (dL[e] * dinv[i] * dinv[j] + dd[i]) : 0.f;
+      if (c.flags & RC_LOSS_ADJ)
+        for (int k = 0; k < K; ++k) g += ws[c.wo.dAadj + (int64_t)k * pp2 + e];
+      float pv = A[e], mv = Mm[c.eo.A + e], vv = V[c.eo.A + e];
+      rc_adam(pv, mv, vv, g, as);
+      A[e] = pv; Mm[c.eo.A + e] = mv; V[c.eo.A + e] = vv;
+    }
+    __syncthreads();
+    dev_supports(A, ws + c.wo.S, dinv, p, n);
+  }
+  // BatchNorm running statistics (torch: double math, momentum*stat + (1-momentum)*running)
+  if (c.nbn > 0 && tid < F) {
+    const double* st = c.bns + r * c.bnsr;
+    const double mom = c.hyp[r].bn_momentum;
+    const double N = (double)c.B * p;
+    const double mean = st[tid], var_u = st[F + tid] * N / (N - 1.0);
+    float rm = c.rm[r * F + tid], rv = c.rv[r * F + tid];
+    for (int t = 0; t < c.nbn; ++t) {
+      rm = (float)(mom * mean + (1.0 - mom) * (double)rm);
+      rv = (float)(mom * var_u + (1.0 - mom) * (double)rv);
+    }
+    c.rm[r * F + tid] = rm;
+    c.rv[r * F + tid] = rv;
+  }
+}
+
+// BatchNorm batch statistics for consecutive batches.  grid (nbatch, R).
+__global__ __launch_bounds__(RC_BLOCK) void k_bn_stats(RedcliffDims d, const float* X, int64_t xr, int64_t N,
+                                                       int B, double* st, int64_t str) {
+  const int r = blockIdx.y, bi = blockIdx.x;
+  const int64_t b0 = (int64_t)bi * B;
+  const int nb = (int)((N - b0) < B ? (N - b0) : B);
+  const int p = d.p, F = d.F;
+  const int Lmax = rc_lmax(d);
+  const float* Xr = X + r * xr;
+  __shared__ double red[8];
+  const int cnt = nb * p;
+  for (int f = 0; f < F; ++f) {
+    double s = 0.0;
+    for (int e = threadIdx.x; e < cnt; e += RC_BLOCK) {
+      const int b = e / p, cc = e - b * p;
+      s += Xr[((b0 + b) * d.T + (Lmax - F + f)) * p + cc];
+    }
+    const double mean = rc_block_sum_d(s, red) / (double)cnt;
+    double q = 0.0;
+    for (int e = threadIdx.x; e < cnt; e += RC_BLOCK) {
+      const int b = e / p, cc = e - b * p;
+      const double v = Xr[((b0 + b) * d.T + (Lmax - F + f)) * p + cc] - mean;
+      q += v * v;
+    }
+    const double var = rc_block_sum_d(q, red) / (double)cnt;
+    if (threadIdx.x == 0) {
+      double* o = st + r * str + (int64_t)bi * 2 * F;
+      o[f] = mean;
+      o[F + f] = var;
+    }
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+static int emb_fwd_sb(const RedcliffDims& d) {
+  const int pF = d.p * d.F, pH = d.p * d.H;
+  int sb = (RC_LDS_LIMIT_FLOATS - pF - 2 * d.F) / (pF + pH + d.M1);
+  if (sb > 16) sb = 16;
+  return sb;
+}
+
+int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int SB = emb_fwd_sb(d);
+  if (SB < 1) { rc_set_error("embedder forward: p*F + p*H too large for LDS"); return REDCLIFF_ELIMIT; }
+  const size_t lds = sizeof(float) * ((size_t)SB * d.p * d.F + d.p * d.F + (size_t)SB * d.p * d.H + SB * d.M1 + 2 * d.F);
+  dim3 grid((c.B + SB - 1) / SB, d.R);
+  hipLaunchKernelGGL(k_emb_fwd, grid, dim3(RC_BLOCK), lds, s, c, SB);
+  return rc_check(hipGetLastError(), "k_emb_fwd");
+}
+
+size_t rc_emb_bwd_lds(const RedcliffDims& d) {
+  const size_t head = (size_t)d.Bmax * d.K + 2 + 8 + 16;
+  const size_t node1 = (size_t)d.Bmax * d.K + (size_t)d.M1 * d.H + EMB_CH * d.M1 + 2 * EMB_CH * d.H;
+  const size_t node3 = (size_t)d.Bmax * d.K + d.p * d.F + d.n * d.F + d.n * d.p + 4 * d.F + d.n;
+  size_t m = head > node1 ? head : node1;
+  m = m > node3 ? m : node3;
+  return m * sizeof(float);
+}
+
+int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
+  const RedcliffDims& d = c.d;
+  const size_t lds = rc_emb_bwd_lds(d);
+  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  if (node_wgs)
+    hipLaunchKernelGGL(k_emb_bwd, dim3(d.p + 1, d.R), dim3(RC_BLOCK), lds, s, c, 0);
+  else
+    hipLaunchKernelGGL(k_emb_bwd, dim3(1, d.R), dim3(RC_BLOCK), lds, s, c, 1);
+  return rc_check(hipGetLastError(), "k_emb_bwd");
+}
+
+int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F;
+  const int nw = (total + RC_BLOCK - 1) / RC_BLOCK;
+  hipLaunchKernelGGL(k_emb_final, dim3(nw + 1, d.R), dim3(RC_BLOCK), 0, s, c, nw);
+  return rc_check(hipGetLastError(), "k_emb_final");
+}
+
+int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,
+                       WsOff wo, hipStream_t s) {
+  hipLaunchKernelGGL(k_supports, dim3(d.R), dim3(RC_BLOCK), 0, s, d, emb, es, ws, wss, eo, wo);
+  return rc_check(hipGetLastError(), "k_supports");
+}
+
+int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,
+                       hipStream_t s) {
+  const int nbatch = (int)((N + B - 1) / B);
+  hipLaunchKernelGGL(k_bn_stats, dim3(nbatch, d.R), dim3(RC_BLOCK), 0, s, d, X, xr, N, B, st, str);
+  return rc_check(hipGetLastError(), "k_bn_stats");
+}

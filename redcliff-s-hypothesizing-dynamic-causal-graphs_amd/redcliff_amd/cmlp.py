@@ -1,0 +1,58 @@
+"""cMLP factor networks (models/cmlp.py) backed by the gfx950 kernels.
+
+Parameter tree and initialisation order are the reference's (``networks.{j}.layers.{i}``;
+Conv1d(p, h, L) default init, then ``xavier_uniform_``, then the 1x1 Conv1d,
+models/cmlp.py:13-27) so seeded models are bit-identical.  ``forward``, ``GC`` and
+``perform_prox_update_on_GC_weights`` run on the GPU through libredcliff_hip.so
+(redcliff_factor_forward / redcliff_gc_norms / redcliff_prox); there is no CPU path.
+"""
+import torch
+import torch.nn as nn
+
+from . import kernels
+
+
+class MLP(nn.Module):
+    def __init__(self, num_series, lag, hidden):
+        super().__init__()
+        self.activation = torch.nn.ReLU()
+        self.lag = lag
+        widths = list(hidden) + [1]
+        first = nn.Conv1d(num_series, widths[0], lag)
+        nn.init.xavier_uniform_(first.weight)
+        self.layers = nn.ModuleList([first] + [nn.Conv1d(a, b, 1) for a, b in zip(widths[:-1], widths[1:])])
+
+    def forward(self, X):
+        # one network == a cMLP with a single channel output; route through the grouped kernel
+        return kernels.single_network_forward(self, X)
+
+
+class cMLP(nn.Module):
+    def __init__(self, num_chans, lag, hidden, wavelet_level=None, save_path=None):
+        super().__init__()
+        if wavelet_level is not None:
+            raise NotImplementedError("wavelet_level != None (wavelet-decomposed inputs) is outside the MI355X path")
+        self.num_chans = num_chans
+        self.wavelet_level = None
+        self.wavelet_mask = None
+        self.lag = lag
+        self.hidden = list(hidden)
+        self.num_series = num_chans
+        self.activation = torch.nn.ReLU()
+        self.networks = nn.ModuleList([MLP(self.num_series, lag, hidden) for _ in range(self.num_series)])
+
+    def forward(self, X):
+        """X (batch, T, p) -> (batch, T - lag + 1, p) (models/cmlp.py:90-101)."""
+        return kernels.cmlp_forward([self], X)[0]
+
+    def perform_prox_update_on_GC_weights(self, lam, lr, penalty):
+        """In-place GL / GSGL / H proximal step on layer-0 weights (models/cmlp.py:117-144)."""
+        kernels.cmlp_prox([self], lam, lr, penalty)
+
+    def GC(self, threshold=True, ignore_lag=True, combine_wavelet_representations=False, rank_wavelets=False):
+        """Group norms of layer-0 weights: (p, p) or (p, p, lag) (models/cmlp.py:147-203)."""
+        if rank_wavelets:
+            raise NotImplementedError("rank_wavelets needs wavelet_level != None")
+        G, G0 = kernels.cmlp_gc_norms([self])
+        out = G0[0] if ignore_lag else G[0]
+        return (out > 0).int() if threshold else out

@@ -1,0 +1,427 @@
+"""Device state of a REDCLIFF-S fit and the fused gfx950 training step.
+
+``FitEngine`` owns, per model:
+  * the packed parameter buffers (embedder group A, factor group B).  Every nn.Parameter
+    of the model is re-pointed to a view of these buffers, so ``state_dict()``, the
+    user's optimizers and the kernels all see the same memory;
+  * the Adam moments of optimizerA / optimizerB, also exposed to the torch optimizers as
+    views (``optimizer.state[p]['exp_avg']`` ...), with a shared step counter;
+  * the workspace of the kernel chain and the device-resident copy of the training set
+    (the reference re-reads and re-unpickles its data for every item,
+    data/synthetic_datasets.py:135-244; here the windows are uploaded once).
+
+One ``batch_update`` of the reference (models/redcliff_s_cmlp_withStateSmoothing.py:734-933)
+is one ``redcliff_train_step`` call; an epoch is one ``redcliff_train_steps`` call.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .dgcnn import M1
+from .kernels import factor_views, ptr
+
+
+# ----------------------------------------------------------------------------- phases
+def phase_of_epoch(model, epoch_num):
+    """...withStateSmoothing.py:741-759 -> list of update kinds run in this batch_update."""
+    mode = model.training_mode
+    if epoch_num <= model.num_pretrain_epochs - 1:
+        kinds = []
+        if "pretrain_embedder" in mode:
+            kinds.append("pretrain_embedder")
+        if "pretrain_factor" in mode:
+            kinds.append("pretrain_factor")
+        return kinds
+    if "acclimate_factors" in mode and epoch_num <= model.num_pretrain_epochs + model.num_acclimation_epochs - 1:
+        return ["acclimate"]
+    if "combined" in mode:
+        return ["combined"]
+    if "post_train_factor" in mode:
+        return ["post_train"]
+    raise NotImplementedError()
+
+
+def flags_for(kind, nsup):
+    """Loss terms / optimizer steps of one update kind (compute_loss flags, :718-729)."""
+    conf = nat.CONFUSION if nsup > 0 else 0
+    if kind == "pretrain_embedder":  # embedder_pretrain_loss: factor + fw_l1 (+ smoothing); optimizerA
+        return nat.BN_TRAIN | nat.LOSS_FACTOR | nat.LOSS_FWL1 | nat.STEP_A | conf, 3
+    if kind in ("pretrain_factor", "acclimate", "post_train"):  # factor_pretrain_loss; embedder eval; optimizerB
+        return nat.LOSS_FORECAST | nat.LOSS_FWL1 | nat.LOSS_ADJ | nat.STEP_B, 0
+    if kind == "combined":
+        return (nat.BN_TRAIN | nat.LOSS_FORECAST | nat.LOSS_FACTOR | nat.LOSS_FWL1 | nat.LOSS_ADJ | nat.STEP_A |
+                nat.STEP_B | conf), 3
+    raise ValueError(kind)
+
+
+def select_labels(Y, K, Lmax):
+    """Label matrix (B, K) that compute_loss compares against (:635-661)."""
+    Y = Y.to(torch.float32)
+    if Y.dim() == 3:
+        lab = Y[:, :, Lmax] if Y.size(2) > Lmax else Y[:, :, 0]
+    elif Y.dim() == 2:
+        lab = Y
+    else:
+        raise NotImplementedError("Cannot handle ground-truth labels with Y.size() == " + str(tuple(Y.size())))
+    if lab.size(1) < K:
+        lab = torch.cat([lab, torch.zeros(lab.size(0), K - lab.size(1), dtype=lab.dtype, device=lab.device)], 1)
+    return lab[:, :K].contiguous()
+
+
+# ----------------------------------------------------------------------------- engine
+class FitEngine:
+    def __init__(self, model):
+        self.model = model
+        emb = model.factor_score_embedder
+        self.dgcnn = emb.dgcnn.dgcnn
+        self.p = model.num_series
+        self.L = model.gen_lag
+        self.K = model.num_factors_nK
+        self.nsup = model.num_supervised_factors
+        self.h = model.gen_hidden[0]
+        self.F = self.dgcnn.in_channels
+        self.n = self.dgcnn.num_layers
+        self.H = self.dgcnn.hid_channels
+        self.Lmax = max(model.gen_lag, model.embed_lag)
+        self.device = self.dgcnn.A.device
+        self.sig = bool(emb.use_sigmoid_restriction)
+        self.ecc = float(emb.sigmoid_eccentricity_coeff or 0.0)
+        self._emb_layout()
+        PA = self.eo["total"]
+        PB = self.fo["total"]
+        dev = self.device
+        self.emb = torch.empty(PA, device=dev, dtype=torch.float32)
+        self.fac = torch.empty(PB, device=dev, dtype=torch.float32)
+        self.bn = torch.empty(2, self.F, device=dev, dtype=torch.float32)
+        self.acc = torch.zeros(8, device=dev, dtype=torch.float64)
+        self.conf = torch.zeros(max(self.nsup, 1) ** 2, device=dev, dtype=torch.int32)
+        self.opt = {"A": None, "B": None}  # bound optimizer state per group
+        self.ws = None
+        self.ws_dims = None
+        self.hyper_key = None
+        self.hyper_dev = None
+        self.supports_fresh = False
+        self.dataset_cache = {}
+        self.bind()
+
+    # ------------------------------------------------------------------ layout / binding
+    def _emb_layout(self):
+        p, n, F, H, K = self.p, self.n, self.F, self.H, self.K
+        o = {"A": 0}
+        o["gcW"] = o["A"] + p * p
+        o["bnw"] = o["gcW"] + n * F * H
+        o["bnb"] = o["bnw"] + F
+        o["fc1W"] = o["bnb"] + F
+        o["fc1b"] = o["fc1W"] + M1 * p * H
+        o["fc2W"] = o["fc1b"] + M1
+        o["fc2b"] = o["fc2W"] + K * M1
+        o["total"] = o["fc2b"] + K
+        self.eo = o
+        kp = K * self.p
+        fo = {"W0": 0}
+        fo["b0"] = fo["W0"] + kp * self.h * self.p * self.L
+        fo["W1"] = fo["b0"] + kp * self.h
+        fo["b1"] = fo["W1"] + kp * self.h
+        fo["total"] = fo["b1"] + kp
+        self.fo = fo
+
+    def _emb_pairs(self):
+        g, o, E = self.dgcnn, self.eo, self.emb
+        p, n, F, H, K = self.p, self.n, self.F, self.H, self.K
+        pairs = [(g.A, E[o["A"]:o["A"] + p * p].view(p, p))]
+        for i in range(n):
+            pairs.append((g.layer1.gc1[i].weight, E[o["gcW"] + i * F * H:o["gcW"] + (i + 1) * F * H].view(F, H)))
+        pairs += [(g.BN1.weight, E[o["bnw"]:o["bnw"] + F]), (g.BN1.bias, E[o["bnb"]:o["bnb"] + F]),
+                  (g.fc1.linear.weight, E[o["fc1W"]:o["fc1W"] + M1 * p * H].view(M1, p * H)),
+                  (g.fc1.linear.bias, E[o["fc1b"]:o["fc1b"] + M1]),
+                  (g.fc2.linear.weight, E[o["fc2W"]:o["fc2W"] + K * M1].view(K, M1)),
+                  (g.fc2.linear.bias, E[o["fc2b"]:o["fc2b"] + K])]
+        return pairs
+
+    def _fac_pairs(self):
+        return factor_views(self.fac, list(self.model.factors), self.p, self.h, self.L)
+
+    def bind(self):
+        """Copy current parameter values into the packed buffers and alias the parameters."""
+        with torch.no_grad():
+            self.pairs = self._emb_pairs() + self._fac_pairs()
+            for prm, view in self.pairs:
+                view.copy_(prm.detach())
+                prm.data = view
+            bnm = self.dgcnn.BN1
+            self.bn[0].copy_(bnm.running_mean)
+            self.bn[1].copy_(bnm.running_var)
+            bnm.running_mean = self.bn[0]
+            bnm.running_var = self.bn[1]
+        self.bound_ptrs = [prm.data_ptr() for prm, _ in self.pairs]
+        self.supports_fresh = False
+
+    def ensure_bound(self):
+        cur = [prm.data_ptr() for prm, _ in self.pairs]
+        bn = self.dgcnn.BN1
+        if (cur != self.bound_ptrs or bn.running_mean.data_ptr() != self.bn[0].data_ptr()
+                or bn.running_var.data_ptr() != self.bn[1].data_ptr()):
+            self.bind()
+            for g in ("A", "B"):
+                if self.opt[g] is not None:
+                    self._attach_state(g)
+
+    def invalidate(self):
+        """Parameters were modified in place from outside: supports must be recomputed."""
+        self.supports_fresh = False
+
+    # ------------------------------------------------------------------ optimizers
+    def _group_params(self, g):
+        n_emb = 1 + self.n + 6
+        pr = [prm for prm, _ in self.pairs]
+        return pr[:n_emb] if g == "A" else pr[n_emb:]
+
+    def _attach_state(self, g):
+        st = self.opt[g]
+        opt = st["opt"]
+        mflat, vflat = st["m"], st["v"]
+        base = self.emb if g == "A" else self.fac
+        for prm in self._group_params(g):
+            off = (prm.data_ptr() - base.data_ptr()) // 4
+            n = prm.numel()
+            opt.state[prm] = {"step": st["step"], "exp_avg": mflat[off:off + n].view_as(prm),
+                              "exp_avg_sq": vflat[off:off + n].view_as(prm)}
+
+    def bind_optimizer(self, g, opt):
+        st = self.opt[g]
+        if st is not None and st["opt"] is opt:
+            return st
+        if not isinstance(opt, torch.optim.Adam):
+            raise NotImplementedError("the fused step implements torch.optim.Adam (model_utils.py:747-762)")
+        if len(opt.param_groups) != 1:
+            raise NotImplementedError("one parameter group per optimizer expected")
+        grp = opt.param_groups[0]
+        if grp.get("amsgrad") or grp.get("maximize") or grp.get("decoupled_weight_decay", False):
+            raise NotImplementedError("amsgrad / maximize / decoupled weight decay are not used by REDCLIFF-S")
+        mine = set(id(x) for x in self._group_params(g))
+        theirs = set(id(x) for x in grp["params"])
+        if mine != theirs:
+            raise ValueError("optimizer%s must own exactly model.gen_model[%d].parameters()" % (g, 0 if g == "A" else 1))
+        base = self.emb if g == "A" else self.fac
+        m = torch.zeros_like(base)
+        v = torch.zeros_like(base)
+        step = 0
+        for prm in self._group_params(g):
+            s = opt.state.get(prm)
+            if s and "exp_avg" in s:  # resume from a torch-stepped optimizer
+                off = (prm.data_ptr() - base.data_ptr()) // 4
+                m[off:off + prm.numel()] = s["exp_avg"].reshape(-1)
+                v[off:off + prm.numel()] = s["exp_avg_sq"].reshape(-1)
+                step = int(float(s["step"]))
+        st = {"opt": opt, "m": m, "v": v, "t": step, "step": torch.tensor(float(step), dtype=torch.float32)}
+        self.opt[g] = st
+        self._attach_state(g)
+        return st
+
+    def _sync_steps(self):
+        for g in ("A", "B"):
+            st = self.opt[g]
+            if st is not None:
+                st["step"].fill_(float(st["t"]))
+
+    # ------------------------------------------------------------------ hyper-parameters
+    def _hyper(self):
+        m = self.model
+        bnm = self.dgcnn.BN1
+        gA = self.opt["A"]["opt"].param_groups[0] if self.opt["A"] else None
+        gB = self.opt["B"]["opt"].param_groups[0] if self.opt["B"] else None
+
+        def adam(gr):
+            if gr is None:
+                return (0.0, (0.9, 0.999), 1e-8, 0.0)
+            return (float(gr["lr"]), tuple(float(b) for b in gr["betas"]), float(gr["eps"]), float(gr["weight_decay"]))
+
+        key = (m.FORECAST_COEFF, m.FACTOR_SCORE_COEFF, m.FACTOR_COS_SIM_COEFF, m.FACTOR_WEIGHT_L1_COEFF,
+               getattr(m, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF", 0.0), m.ADJ_L1_REG_COEFF, float(bnm.eps),
+               float(bnm.momentum if bnm.momentum is not None else 0.1), adam(gA), adam(gB))
+        if key != self.hyper_key:
+            h = nat.ReplicaHyper()
+            (h.c_forecast, h.c_factor, h.c_cos, h.c_fwl1, h.c_smooth, h.c_adj) = [float(x) for x in key[:6]]
+            h.bn_eps, h.bn_momentum = key[6], key[7]
+            h.A = nat.adam_hyper(key[8][0], key[8][1], key[8][2], key[8][3])
+            h.B = nat.adam_hyper(key[9][0], key[9][1], key[9][2], key[9][3])
+            raw = np.frombuffer(bytes(h), dtype=np.uint8).copy()
+            self.hyper_dev = torch.from_numpy(raw).to(self.device)
+            self.hyper_key = key
+        return self.hyper_dev
+
+    # ------------------------------------------------------------------ workspace
+    def dims(self, Bmax, T):
+        return nat.Dims(R=1, Bmax=int(Bmax), T=int(T), p=self.p, L=self.L, K=self.K, h=self.h, F=self.F, n=self.n,
+                        H=self.H, M1=M1, nsup=self.nsup, use_sigmoid=int(self.sig), sigmoid_ecc=self.ecc)
+
+    def workspace(self, Bmax, T):
+        Bmax = max(int(Bmax), 1)
+        if self.ws_dims is not None and self.ws_dims[0] >= Bmax:
+            d = self.dims(self.ws_dims[0], T)
+        else:
+            d = self.dims(Bmax, T)
+            nbytes = nat.lib().redcliff_workspace_bytes(ctypes.byref(d))
+            if nbytes == 0:
+                nat.check(-1, "workspace_bytes")
+            self.ws = torch.zeros(nbytes // 4, device=self.device, dtype=torch.float32)
+            self.ws_dims = (Bmax,)
+            self.ws_off = nat.workspace_layout(d)
+            self.supports_fresh = False
+        return d
+
+    # ------------------------------------------------------------------ data
+    def bn_stats(self, d, X, N, B):
+        nb = (N + B - 1) // B
+        st = torch.empty(nb, 2, self.F, device=self.device, dtype=torch.float64)
+        nat.check(nat.lib().redcliff_bn_batch_stats(ctypes.byref(d), ptr(X), 0, int(N), int(B), ptr(st), 0,
+                                                    _stream()), "bn_batch_stats")
+        return st
+
+    def stage(self, X, Y):
+        """One host batch -> device tensors (X (B,T,p), labels (B,K), BN batch stats)."""
+        X = X.to(self.device, torch.float32).contiguous()
+        B, T, p = X.shape
+        if p != self.p:
+            raise ValueError("expected %d channels, got %d" % (self.p, p))
+        lab = select_labels(Y.to(self.device), self.K, self.Lmax) if Y is not None else None
+        d = self.workspace(B, T)
+        st = self.bn_stats(d, X, B, B)
+        return X, lab, st, d
+
+    def cache_dataset(self, loader):
+        """Upload an iterable of (X, Y) batches once; later epochs replay the same order
+        (the reference DataLoader has no shuffling: data/synthetic_datasets.py:272-276)."""
+        key = id(loader)
+        if key in self.dataset_cache:
+            return self.dataset_cache[key]
+        xs, ys, sizes = [], [], []
+        for X, Y in loader:
+            xs.append(X.to(torch.float32))
+            ys.append(select_labels(Y, self.K, self.Lmax) if Y is not None else torch.zeros(X.shape[0], self.K))
+            sizes.append(int(X.shape[0]))
+        Xall = torch.cat(xs, 0).to(self.device).contiguous()
+        lab = torch.cat(ys, 0).to(self.device, torch.float32).contiguous()
+        rows = np.cumsum([0] + sizes[:-1]).astype(np.int64)
+        d = self.workspace(max(sizes), Xall.shape[1])
+        stats = [self.bn_stats(d, Xall[r:r + s], s, s) for r, s in zip(rows, sizes)]
+        ds = {"X": Xall, "lab": lab, "rows": rows, "sizes": np.asarray(sizes, dtype=np.int32),
+              "stats": torch.cat(stats, 0).contiguous(), "T": int(Xall.shape[1]), "Bmax": max(sizes),
+              "len": len(sizes), "loader": loader}
+        self.dataset_cache[key] = ds
+        return ds
+
+    # ------------------------------------------------------------------ step launch
+    def _args(self, d, flags, nbn, X, lab, stats):
+        a = nat.StepArgs()
+        a.d = d
+        a.flags = flags | (0 if self.supports_fresh else nat.REFRESH_SUPPORTS)
+        a.n_bn_updates = nbn
+        stA, stB = self.opt["A"], self.opt["B"]
+        a.tA = (stA["t"] + 1) if stA else 1
+        a.tB = (stB["t"] + 1) if stB else 1
+        a.X = X.data_ptr()
+        a.labels = lab.data_ptr() if lab is not None else None
+        a.bn_stats = stats.data_ptr() if stats is not None else None
+        a.emb, a.emb_stride = self.emb.data_ptr(), self.emb.numel()
+        a.fac, a.fac_stride = self.fac.data_ptr(), self.fac.numel()
+        if stA:
+            a.emb_m, a.emb_v = stA["m"].data_ptr(), stA["v"].data_ptr()
+        else:
+            a.emb_m = a.emb_v = self.emb.data_ptr()
+        if stB:
+            a.fac_m, a.fac_v = stB["m"].data_ptr(), stB["v"].data_ptr()
+        else:
+            a.fac_m = a.fac_v = self.fac.data_ptr()
+        a.bn_rm, a.bn_rv = self.bn[0].data_ptr(), self.bn[1].data_ptr()
+        a.hyper = self._hyper().data_ptr()
+        a.ws, a.ws_bytes = self.ws.data_ptr(), self.ws.numel() * 4
+        a.acc = self.acc.data_ptr()
+        a.confusion = self.conf.data_ptr()
+        return a
+
+    def _after(self, flags, nbn, nsteps):
+        self.supports_fresh = True
+        if flags & nat.STEP_A:
+            self.opt["A"]["t"] += nsteps
+        if flags & nat.STEP_B:
+            self.opt["B"]["t"] += nsteps
+        if nbn:
+            self.dgcnn.BN1.num_batches_tracked.add_(nbn * nsteps)
+        self._sync_steps()
+
+    def run_steps(self, kinds, X, lab, stats, d, rows, sizes, oA, oB):
+        """Run the update kinds of one phase over consecutive batches (rows/sizes)."""
+        self.ensure_bound()
+        for kind in kinds:
+            flags, nbn = flags_for(kind, self.nsup)
+            if flags & nat.STEP_A:
+                self.bind_optimizer("A", oA)
+            if flags & nat.STEP_B:
+                self.bind_optimizer("B", oB)
+            if not (flags & nat.BN_TRAIN):
+                stats_p = None
+            else:
+                stats_p = stats
+            a = self._args(d, flags, nbn, X, lab, stats_p)
+            rows_a = np.ascontiguousarray(rows, dtype=np.int64)
+            sizes_a = np.ascontiguousarray(sizes, dtype=np.int32)
+            nat.check(nat.lib().redcliff_train_steps(ctypes.byref(a), len(rows_a), rows_a.ctypes.data_as(ctypes.c_void_p),
+                                                     sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * self.F, _stream()),
+                      "train_steps")
+            self._after(flags, nbn, len(rows_a))
+
+    def run_values(self, X, lab, d, rows, sizes, train_bn=False, stats=None, confusion=True):
+        """validate_training body over consecutive batches; returns (acc[8], confusion)."""
+        self.ensure_bound()
+        self.acc.zero_()
+        self.conf.zero_()
+        flags = nat.VALUES | (nat.CONFUSION if (confusion and self.nsup > 0) else 0)
+        if train_bn:
+            flags |= nat.BN_TRAIN
+        a = self._args(d, flags, 0, X, lab, stats if train_bn else None)
+        rows_a = np.ascontiguousarray(rows, dtype=np.int64)
+        sizes_a = np.ascontiguousarray(sizes, dtype=np.int32)
+        nat.check(nat.lib().redcliff_train_steps(ctypes.byref(a), len(rows_a), rows_a.ctypes.data_as(ctypes.c_void_p),
+                                                 sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * self.F, _stream()),
+                  "validate")
+        self.supports_fresh = True
+        return self.acc.cpu().numpy(), self.conf.cpu().numpy().reshape(max(self.nsup, 1), max(self.nsup, 1))
+
+    def forward_outputs(self, X, train_bn, bn_updates):
+        """Embedder + factors + mixing on windows X (B, T>=Lmax, p): returns w_raw, y, xsim."""
+        self.ensure_bound()
+        X = X.to(self.device, torch.float32).contiguous()
+        B, T, _ = X.shape
+        d = self.workspace(B, T)
+        stats = self.bn_stats(d, X, B, B) if train_bn else None
+        flags = nat.STORE_OUTPUTS | (nat.BN_TRAIN if train_bn else 0)
+        a = self._args(d, flags, bn_updates if train_bn else 0, X, None, stats)
+        a.B = B
+        a.row0 = 0
+        nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "forward")
+        self.supports_fresh = True
+        if train_bn and bn_updates:
+            self.dgcnn.BN1.num_batches_tracked.add_(bn_updates)
+        o = self.ws_off
+        w = self.ws[o["w"]:o["w"] + B * self.K].view(B, self.K).clone()
+        y = self.ws[o["y"]:o["y"] + B * self.K * self.p].view(B, self.K, self.p).clone()
+        xs = self.ws[o["xsim"]:o["xsim"] + B * self.p].view(B, self.p).clone()
+        return w, y, xs
+
+    def gc_norms(self):
+        """(G (K,p,p,L), G0 (K,p,p)) of the current factor weights."""
+        self.ensure_bound()
+        d = nat.Dims(R=1, Bmax=1, T=self.L, p=self.p, L=self.L, K=self.K, h=self.h, F=self.L, n=1, H=1, M1=1,
+                     nsup=0, use_sigmoid=0, sigmoid_ecc=0.0)
+        G = torch.empty(self.K, self.p, self.p, self.L, device=self.device, dtype=torch.float32)
+        G0 = torch.empty(self.K, self.p, self.p, device=self.device, dtype=torch.float32)
+        nat.check(nat.lib().redcliff_gc_norms(ctypes.byref(d), ptr(self.fac), self.fac.numel(), ptr(G), ptr(G0),
+                                              _stream()), "gc_norms")
+        return G, G0
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

@@ -1,0 +1,396 @@
+"""REDCLIFF_S_CMLP_withStateSmoothing on MI355X -- drop-in for
+models/redcliff_s_cmlp_withStateSmoothing.py (the class every published run uses).
+
+Same constructor signature, parameter tree (state_dict keys), seeded initialisation,
+``forward`` / ``GC`` / ``compute_loss`` / ``batch_update`` / ``validate_training`` /
+``fit`` / ``save_checkpoint`` call contracts.  The numerical work of a training step
+runs in the fused gfx950 kernel chain of libredcliff_hip.so (redcliff_amd.engine):
+the embedder, the K x p factor networks, the conditional-GC penalties, the backward
+pass and both Adam updates.  There is no CPU / eager fallback: on a host without the
+HIP library or without a GPU the compute methods raise.
+
+Scope of the fused path: DGCNN embedder, one hidden factor
+layer, num_sims == 1, factor weights applied after simulation, embed_lag >= gen_lag,
+primary GC mode conditional_factor_fixed_embedder -- the published configuration.
+Other combinations are accepted by the constructor (checkpoint compatibility) and raise
+NotImplementedError when trained.
+"""
+import math
+import weakref
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as nat
+from . import metrics as M
+from .cmlp import cMLP
+from .engine import FitEngine, phase_of_epoch, select_labels
+from .redcliff_factor_score_embedders import (DGCNN_Embedder, MLPClassifierForMultipleObjectives,
+                                              MLPClassifierForSingleObjective, cEmbedder)
+
+TRAINING_MODES = [
+    "pretrain_embedder_then_acclimate_factors_then_combined",
+    "pretrain_embedder_then_post_train_factor_withComboCosSimL1FreezeByEpoch",
+    "pretrain_embedder_then_post_train_factor_withComboCosSimL1FreezeByBatch",
+    "pretrain_embedder_then_post_train_factor_withL1FreezeByEpoch",
+    "pretrain_embedder_then_post_train_factor_withL1FreezeByBatch",
+    "pretrain_embedder_then_post_train_factor",
+    "pretrain_embedder_and_pretrain_factor_then_combined",
+    "pretrain_embedder_then_combined",
+    "pretrain_factor_then_combined",
+    "combined",
+]
+POSSIBLE_GC_EST_MODES = [
+    "fixed_factor_exclusive", "raw_embedder", "conditional_factor_exclusive", "fixed_embedder_exclusive",
+    "conditional_embedder_exclusive", "fixed_factor_fixed_embedder", "conditional_factor_fixed_embedder",
+    "fixed_factor_conditional_embedder", "conditional_factor_conditional_embedder",
+]
+
+
+class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
+    _WITH_SMOOTHING = True
+
+    def __init__(self, num_chans, gen_lag, gen_hidden, embed_lag, embed_hidden_sizes, num_in_timesteps,
+                 num_out_timesteps, num_factors, num_supervised_factors, coeff_dict, use_sigmoid_restriction,
+                 factor_score_embedder_type, factor_score_embedder_args, primary_gc_est_mode, forward_pass_mode,
+                 num_sims=1, wavelet_level=None, save_path=None,
+                 training_mode="pretrain_embedder_and_pretrain_factor_then_combined", num_pretrain_epochs=0,
+                 num_acclimation_epochs=0, STATE_SCORE_SMOOTHING_EPSILON=0.0001):
+        super().__init__()
+        if wavelet_level is not None:
+            raise NotImplementedError("wavelet_level != None (wavelet-decomposed inputs) is outside the MI355X path")
+        self.MAX_NUM_SAMPS_FOR_GC_VIS = 5
+        self.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING = 40
+        self.STATE_SCORE_SMOOTHING_EPSILON = STATE_SCORE_SMOOTHING_EPSILON
+        self.num_chans = num_chans
+        self.num_series = num_chans
+        self.gen_lag = gen_lag
+        self.gen_hidden = gen_hidden
+        self.num_gen_hiddens = len(gen_hidden)
+        self.embed_lag = embed_lag
+        self.embed_hidden_sizes = embed_hidden_sizes
+        self.num_in_timesteps = num_in_timesteps
+        self.num_out_timesteps = num_out_timesteps
+        self.num_factors_nK = num_factors
+        self.num_supervised_factors = num_supervised_factors
+        self.coeff_dict = coeff_dict
+        self.FORECAST_COEFF = coeff_dict["FORECAST_COEFF"]
+        self.FACTOR_SCORE_COEFF = coeff_dict["FACTOR_SCORE_COEFF"]
+        self.FACTOR_COS_SIM_COEFF = coeff_dict["FACTOR_COS_SIM_COEFF"]
+        self.FACTOR_WEIGHT_L1_COEFF = coeff_dict["FACTOR_WEIGHT_L1_COEFF"]
+        if self._WITH_SMOOTHING:
+            self.FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF = coeff_dict["FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF"]
+        self.ADJ_L1_REG_COEFF = coeff_dict["ADJ_L1_REG_COEFF"]
+        self.DAGNESS_REG_COEFF = coeff_dict["DAGNESS_REG_COEFF"]
+        self.DAGNESS_LAG_COEFF = coeff_dict["DAGNESS_LAG_COEFF"]
+        self.DAGNESS_NODE_COEFF = coeff_dict["DAGNESS_NODE_COEFF"]
+        self.num_sims = num_sims
+        self.wavelet_level = wavelet_level
+        assert training_mode in TRAINING_MODES
+        self.training_mode = training_mode
+        assert (num_pretrain_epochs > 0) if "pretrain" in training_mode else (num_pretrain_epochs == 0)
+        assert (num_acclimation_epochs > 0) if "acclimate" in training_mode else (num_acclimation_epochs == 0)
+        self.num_pretrain_epochs = num_pretrain_epochs
+        self.num_acclimation_epochs = num_acclimation_epochs
+        assert forward_pass_mode in ["apply_factor_weights_at_each_sim_step", "apply_factor_weights_after_sim_completion"]
+        self.forward_pass_mode = forward_pass_mode
+        self.supervised_loss_fn = nn.MSELoss(reduction="mean")
+        self.use_sigmoid_restriction = use_sigmoid_restriction
+        assert factor_score_embedder_type in ["cEmbedder", "DGCNN", "Vanilla_Embedder"]
+        self.CAUSAL_EMBEDDER_TYPES = ["cEmbedder", "DGCNN"]
+        self.factor_score_embedder_type = factor_score_embedder_type
+        self.factor_score_embedder_args = factor_score_embedder_args
+        self.POSSIBLE_GC_EST_MODES = list(POSSIBLE_GC_EST_MODES)
+        assert primary_gc_est_mode in POSSIBLE_GC_EST_MODES
+        self.primary_gc_est_mode = primary_gc_est_mode
+        args = [a[1] for a in factor_score_embedder_args]
+        # construction order (embedder first, then factors) fixes the RNG stream (:111-144)
+        if factor_score_embedder_type == "cEmbedder":
+            self.factor_score_embedder = cEmbedder(num_chans, num_supervised_factors, num_factors,
+                                                   use_sigmoid_restriction, *args, wavelet_level, save_path)
+        elif factor_score_embedder_type == "DGCNN":
+            assert primary_gc_est_mode != "conditional_embedder_exclusive"
+            assert len(factor_score_embedder_args) == 4
+            self.factor_score_embedder = DGCNN_Embedder(num_chans, 1, *args, use_sigmoid_restriction, num_factors,
+                                                        num_supervised_factors)
+        else:
+            if num_supervised_factors > 0:
+                self.factor_score_embedder = MLPClassifierForMultipleObjectives(
+                    self.num_series, embed_lag, num_factors, num_supervised_factors, embed_hidden_sizes,
+                    use_sigmoid_restriction)
+            else:
+                self.factor_score_embedder = MLPClassifierForSingleObjective(
+                    self.num_series, embed_lag, num_factors, embed_hidden_sizes, use_sigmoid_restriction)
+        self.factors = nn.ModuleList([cMLP(num_chans, gen_lag, gen_hidden, wavelet_level=wavelet_level,
+                                           save_path=save_path) for _ in range(num_factors)])
+        self.gen_model = nn.ModuleList([self.factor_score_embedder, self.factors])
+        self._engine = None
+
+    # ------------------------------------------------------------------ plumbing
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_engine"] = None
+        return st
+
+    @property
+    def Lmax(self):
+        return max(self.gen_lag, self.embed_lag)
+
+    def fused_supported(self):
+        return (self.factor_score_embedder_type == "DGCNN" and self.num_sims == 1 and self.num_gen_hiddens == 1
+                and self.forward_pass_mode == "apply_factor_weights_after_sim_completion"
+                and self.embed_lag >= self.gen_lag
+                and self.primary_gc_est_mode == "conditional_factor_fixed_embedder")
+
+    def engine(self):
+        if not self.fused_supported():
+            raise NotImplementedError(
+                "the gfx950 fused path covers the published REDCLIFF-S configuration (DGCNN embedder, num_sims=1, "
+                "gen_hidden of length 1, weights applied after simulation, embed_lag >= gen_lag, "
+                "conditional_factor_fixed_embedder); got embedder=%s num_sims=%d mode=%s gc=%s" % (
+                    self.factor_score_embedder_type, self.num_sims, self.forward_pass_mode, self.primary_gc_est_mode))
+        A = self.factor_score_embedder.dgcnn.dgcnn.A
+        if not A.is_cuda:
+            raise RuntimeError("REDCLIFF-S on MI355X: move the model to the GPU first (model.cuda()); "
+                               "there is no CPU path")
+        nat.lib()
+        if self._engine is None or self._engine.device != A.device:
+            self._engine = FitEngine(self)
+        self.factor_score_embedder.owner = weakref.ref(self)
+        return self._engine
+
+    # ------------------------------------------------------------------ forward
+    def _labels_from_w(self, w_raw):
+        emb = self.factor_score_embedder
+        nsup = self.num_supervised_factors
+        w = torch.sigmoid(emb.sigmoid_eccentricity_coeff * w_raw) if emb.use_sigmoid_restriction else w_raw
+        if nsup > 0:
+            logits = w_raw[:, :nsup]
+            if emb.use_sigmoid_restriction:
+                logits = torch.sigmoid(logits)
+        else:
+            logits = None
+        return w, logits
+
+    def _embed_windows(self, Xw, use_final_activation=True):
+        """DGCNN_Embedder.forward on time-major windows Xw (B, F, p)."""
+        eng = self.engine()
+        B, F, p = Xw.shape
+        pad = self.Lmax - F
+        if pad > 0:
+            Xw = torch.cat([torch.zeros(B, pad, p, device=Xw.device, dtype=Xw.dtype), Xw], 1)
+        train = self.factor_score_embedder.training
+        w_raw, _, _ = eng.forward_outputs(Xw, train_bn=train, bn_updates=1)
+        w, logits = self._labels_from_w(w_raw)
+        if logits is not None and not use_final_activation and self.factor_score_embedder.use_sigmoid_restriction:
+            logits = w_raw[:, :self.num_supervised_factors]
+        return w, logits
+
+    def forward(self, X, factor_weightings=None):
+        """X (B, T, p) -> (x_sim (B, S, p), [per-factor predictions], [w], [state labels] * S)
+        (...withStateSmoothing.py:326-412).  Uses the last embed_lag / gen_lag steps of X."""
+        if factor_weightings is not None:
+            raise NotImplementedError("externally supplied factor_weightings are not supported on the fused path")
+        eng = self.engine()
+        X = X.to(eng.device, torch.float32)
+        if X.shape[1] < self.Lmax:
+            raise ValueError("forward needs at least max(gen_lag, embed_lag) time steps")
+        Xw = X[:, X.shape[1] - self.Lmax:, :].contiguous()
+        train = self.factor_score_embedder.training
+        w_raw, y, xs = eng.forward_outputs(Xw, train_bn=train, bn_updates=1)
+        w, logits = self._labels_from_w(w_raw)
+        if logits is None:
+            logits = w
+        preds = [y[:, k, :].unsqueeze(1) for k in range(self.num_factors_nK)]
+        return xs.unsqueeze(1), preds, [w], [logits for _ in range(self.num_sims)]
+
+    # ------------------------------------------------------------------ GC
+    def _factor_gcs(self, threshold, ignore_lag):
+        G, G0 = self.engine().gc_norms()
+        ests = [G0[k].view(self.num_series, self.num_series, 1) if ignore_lag else G[k]
+                for k in range(self.num_factors_nK)]
+        return [(e > 0).int() for e in ests] if threshold else ests
+
+    def _embedder_gc(self, threshold, combine):
+        G = self.factor_score_embedder.GC(threshold=threshold, combine_node_feature_edges=combine)
+        return G.view(self.num_series, self.num_series, 1)
+
+    def GC(self, gc_est_mode, X=None, threshold=True, ignore_lag=True, combine_wavelet_representations=False,
+           rank_wavelets=False):
+        """The nine GC estimate modes of ...withStateSmoothing.py:415-620 (DGCNN embedder)."""
+        if rank_wavelets:
+            raise NotImplementedError("rank_wavelets needs wavelet_level != None")
+        if self.factor_score_embedder_type != "DGCNN":
+            raise NotImplementedError("GC on the fused path is implemented for the DGCNN embedder")
+        ls = min(self.gen_lag, self.embed_lag)
+        comb = combine_wavelet_representations
+        if gc_est_mode == "fixed_factor_exclusive":
+            return [self._factor_gcs(threshold, ignore_lag)]
+        if gc_est_mode in ("raw_embedder", "fixed_embedder_exclusive"):
+            return [[self._embedder_gc(threshold, comb)]]
+        if gc_est_mode in ("conditional_embedder_exclusive", "fixed_factor_conditional_embedder",
+                           "conditional_factor_conditional_embedder"):
+            raise ValueError("conditional_embedder_exclusive is not supported for model with DGCNN factor score "
+                             "embedder type")
+        if gc_est_mode == "fixed_factor_fixed_embedder":
+            fg = self._factor_gcs(threshold, ignore_lag)
+            eg = self._embedder_gc(threshold, comb)
+            if not ignore_lag:
+                return [[g[:, :, -ls:] + eg[:, :, -ls:] for g in fg]]
+            return [[g + eg for g in fg]]
+        if gc_est_mode in ("conditional_factor_exclusive", "conditional_factor_fixed_embedder"):
+            w, _ = self.factor_score_embedder(torch.transpose(X[:, -self.embed_lag:, :], 1, 2))
+            fg = self._factor_gcs(threshold, ignore_lag)
+            out = [[w[b, k] * fg[k] for k in range(w.size(1))] for b in range(w.size(0))]
+            if gc_est_mode == "conditional_factor_exclusive":
+                return out
+            eg = self._embedder_gc(threshold, comb)
+            for b in range(X.size(0)):
+                for k in range(self.num_factors_nK):
+                    out[b][k] = out[b][k] + eg if ignore_lag else out[b][k][:, :, -ls:] + eg[:, :, -ls:]
+            return out
+        raise ValueError("GC EST MODE == " + str(gc_est_mode) + " IS NOT SUPPORTED")
+
+    # ------------------------------------------------------------------ loss (values)
+    @torch.no_grad()
+    def compute_loss(self, conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
+                     node_dag_scale=0.1, embedder_pretrain_loss=False, factor_pretrain_loss=False):
+        """Loss terms of ...withStateSmoothing.py:624-731 as values.  Gradients of the
+        training objective are produced by the fused step (batch_update), not by autograd."""
+        gc = self.GC(gc_est_mode, X=conditioning_X, threshold=False, ignore_lag=True)
+        gc_lagged = self.GC(gc_est_mode, X=conditioning_X, threshold=False, ignore_lag=False)
+        dev = preds.device
+        forecast = self.FORECAST_COEFF * sum(self.supervised_loss_fn(preds[:, :, i], targets[:, :, i])
+                                             for i in range(self.num_series))
+        factor = torch.zeros(1, device=dev)
+        nsup = self.num_supervised_factors
+        if factor_scores is not None and factor_scores[0] is not None and nsup > 0:
+            lab = select_labels(factor_labels.to(dev), factor_labels.size(1), self.Lmax)
+            yhat = sum(factor_scores) / (1. * len(factor_scores)) if not (
+                factor_labels.dim() == 3 and factor_labels.size(2) > self.Lmax) else factor_scores[0]
+            factor = factor + self.FACTOR_SCORE_COEFF * self.supervised_loss_fn(yhat[:, :nsup], lab[:, :nsup])
+        fw_l1 = self.FACTOR_WEIGHT_L1_COEFF * (torch.norm(factor_scores[0], 1) - 1.)
+        smooth = torch.zeros(1, device=dev)
+        cos_pen, adj = None, None
+        logw = [math.log(i + 2.) for i in range(gc_lagged[0][0].size(2))]
+        for b in range(len(gc)):
+            if len(gc[b]) > 1:
+                eye = torch.eye(self.num_series, device=dev).view(self.num_series, self.num_series, 1)
+                vs = [(g - eye).flatten() for g in gc[b]]
+                tot = 0.
+                for i in range(len(vs)):
+                    for j in range(i + 1, len(vs)):
+                        tot += float(torch.nn.functional.cosine_similarity(vs[i].view(1, -1), vs[j].view(1, -1)))
+                v = self.FACTOR_COS_SIM_COEFF * tot
+                cos_pen = v if cos_pen is None else cos_pen + v
+            for G in gc_lagged[b]:
+                v = self.ADJ_L1_REG_COEFF * sum(lw * torch.sum(torch.abs(G[:, :, i])) for i, lw in enumerate(logw))
+                adj = v if adj is None else adj + v
+        cos_t = None if cos_pen is None else torch.tensor(cos_pen, device=dev)
+        if embedder_pretrain_loss:
+            combo = factor + fw_l1 + smooth
+        elif factor_pretrain_loss:
+            combo = forecast + fw_l1 + smooth + adj + (cos_t if cos_t is not None else 0.)
+        else:
+            combo = forecast + factor + fw_l1 + smooth + adj + (cos_t if cos_t is not None else 0.)
+        terms = [forecast, factor, cos_t, fw_l1]
+        if self._WITH_SMOOTHING:
+            terms.append(smooth * getattr(self, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF", 0.0))
+        return combo, terms + [adj, None]
+
+    def resume_training_from_checkpoint(self, training_meta_data_path):
+        """...withStateSmoothing.py:209-251: histories of a previous run; fit() resumes at best_it+1.
+        (Optimizer state is not checkpointed, as in the reference.)"""
+        import pickle
+        with open(training_meta_data_path, "rb") as f:
+            meta = pickle.load(f)  # a file written by this package's (or the reference's) save_checkpoint
+        self.chkpt_epoch = meta["epoch"]
+        for k, v in meta.items():
+            setattr(self, "chkpt_" + k, v)
+
+    # ------------------------------------------------------------------ training step
+    def batch_update(self, epoch_num, batch_num, X, Y, optimizerA, optimizerB, output_length, best_model=None,
+                     training_status_of_each_factor=None, running_factor_score_confusion_matrix=None):
+        """One REDCLIFF-S update on a host or device batch (...withStateSmoothing.py:734-933)."""
+        if "FreezeByBatch" in self.training_mode:
+            raise NotImplementedError("FreezeByBatch training modes are not on the fused path")
+        if output_length != 1:
+            raise NotImplementedError("output_length must be 1 (num_sims * output_length target steps)")
+        eng = self.engine()
+        kinds = phase_of_epoch(self, epoch_num)
+        Xd, lab, st, d = eng.stage(X, Y)
+        if running_factor_score_confusion_matrix is not None:
+            eng.conf.zero_()
+        eng.run_steps(kinds, Xd, lab, st, d, [0], [Xd.shape[0]], optimizerA, optimizerB)
+        self._set_module_modes(kinds[-1] if kinds else None)
+        if running_factor_score_confusion_matrix is not None and self.num_supervised_factors > 0:
+            n = self.num_supervised_factors
+            running_factor_score_confusion_matrix += eng.conf.cpu().numpy().reshape(n, n)
+        return best_model, running_factor_score_confusion_matrix
+
+    def _set_module_modes(self, kind):
+        if kind in ("pretrain_embedder", "combined"):
+            self.factor_score_embedder.train()
+        elif kind in ("pretrain_factor", "acclimate", "post_train"):
+            self.factor_score_embedder.eval()
+            for f in self.factors:
+                f.train()
+
+    # ------------------------------------------------------------------ validation
+    def validate_training(self, X_val, output_length, num_series, factor_score_val_acc_history=None,
+                          factor_score_val_tpr_history=None, factor_score_val_tnr_history=None,
+                          factor_score_val_fpr_history=None, factor_score_val_fnr_history=None):
+        """...withStateSmoothing.py:1650-1790: coefficient-normalised loss terms averaged over batches."""
+        eng = self.engine()
+        self.factor_score_embedder.eval()
+        for f in self.factors:
+            f.eval()
+        ds = eng.cache_dataset(X_val)
+        d = eng.workspace(ds["Bmax"], ds["T"])
+        acc, conf = eng.run_values(ds["X"], ds["lab"], d, ds["rows"], ds["sizes"])
+        nb = float(ds["len"])
+        vals = [acc[nat_i] / nb for nat_i in range(7)]
+        forecast, factor, cos, fwl1, smooth, adj, combo = vals
+        out = [forecast, factor, cos, fwl1]
+        if self._WITH_SMOOTHING:
+            out.append(smooth)
+        out += [adj, 0.0, 0.0, 0.0, combo]
+        if self.num_supervised_factors > 0:
+            TPR, TNR, FPR, FNR, ACC = _confusion_rates(conf)
+            factor_score_val_acc_history.append(ACC)
+            factor_score_val_tpr_history.append(TPR)
+            factor_score_val_tnr_history.append(TNR)
+            factor_score_val_fpr_history.append(FPR)
+            factor_score_val_fnr_history.append(FNR)
+            out += [factor_score_val_acc_history, factor_score_val_tpr_history, factor_score_val_tnr_history,
+                    factor_score_val_fpr_history, factor_score_val_fnr_history]
+        return tuple(out)
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, save_dir, X_train, optimizerA, optimizerB, input_length, output_length, num_sim_steps, max_iter,
+            X_val, lookback=5, check_every=50, verbose=1, GC=None, deltaConEps=0.1, in_degree_coeff=1.,
+            out_degree_coeff=1., prior_factors_path=None, cost_criteria="CosineSimilarity",
+            unsupervised_start_index=0, max_factor_prior_batches=10, stopping_criteria_forecast_coeff=1.,
+            stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., save_plots=False):
+        """Epoch loop of ...withStateSmoothing.py:1175-1647 with the batches resident on the GPU."""
+        from .fit_loop import run_fit
+        return run_fit(self, save_dir, X_train, optimizerA, optimizerB, output_length, max_iter, X_val, lookback,
+                       check_every, verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path,
+                       stopping_criteria_forecast_coeff, stopping_criteria_factor_coeff,
+                       stopping_criteria_cosSim_coeff, save_plots)
+
+    def save_checkpoint(self, save_dir, it, best_model, *histories, **kw):
+        """final_best_model.bin + training_meta_data_and_hyper_parameters.pkl (:936-990)."""
+        from .fit_loop import save_checkpoint
+        return save_checkpoint(self, save_dir, it, best_model, *histories, **kw)
+
+
+def _confusion_rates(cm):
+    cm = np.asarray(cm, dtype=np.float64)
+    TP = np.diag(cm)
+    FP = cm.sum(axis=0) - TP
+    FN = cm.sum(axis=1) - TP
+    TN = cm.sum() - (FP + FN + TP)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return TP / (TP + FN), TN / (TN + FP), FP / (FP + TN), FN / (TP + FN), (TP + TN) / (TP + FP + FN + TN)

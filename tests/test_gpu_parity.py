@@ -1,0 +1,259 @@
+"""GPU parity of the fused gfx950 REDCLIFF-S path against the reference's golden vectors
+and against the CPU oracle on the same seeded inputs.
+
+Tolerance (north star): losses / GC tensors within 1e-4 relative in fp32; parameters
+after N Adam steps within rtol 1e-4 (atol 2e-6 for near-zero entries, set by fp32
+re-association of batch reductions); thresholded graphs / F1 identical.
+All compute goes through libredcliff_hip.so (the tests fail if it is not loaded).
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_close, batches, ctor_args, load, state
+
+pytestmark = pytest.mark.gpu
+
+FUSED_SCENARIOS = ["dgcnn_c1", "dgcnn_d4ic", "dgcnn_partial_sigmoid", "dgcnn_unsup", "dgcnn_base", "dgcnn_feql"]
+RTOL, ATOL = 1e-4, 2e-6
+
+
+def build(meta, device="cuda"):
+    import redcliff_amd
+    args, kw = ctor_args(meta)
+    torch.manual_seed(meta["seed"])
+    cls = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing if meta["smoothing_class"] else redcliff_amd.REDCLIFF_S_CMLP
+    return cls(*args, **kw).float().to(device)
+
+
+def make_opts(m, lrA, lrB):
+    oA = torch.optim.Adam(m.gen_model[0].parameters(), lr=lrA, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    oB = torch.optim.Adam(m.gen_model[1].parameters(), lr=lrB, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    return oA, oB
+
+
+def compare_state(tag, model, want, rtol=RTOL, atol=ATOL):
+    got = dict((k, v.detach().cpu().numpy()) for k, v in model.state_dict().items() if not k.startswith("gen_model."))
+    assert set(got) == set(want)
+    for k in want:
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(want[k]), tag + k
+            continue
+        scale = max(1.0, float(np.abs(want[k]).max()))
+        assert_close("%s/%s" % (tag, k), got[k], want[k], rtol, atol * scale)
+
+
+def test_native_library_is_the_compute_path():
+    from redcliff_amd import _native as nat
+    L = nat.lib()
+    assert L is not None
+    import os
+    maps = open("/proc/self/maps").read()
+    assert os.path.basename(nat.LIB_PATH) in maps
+
+
+@pytest.mark.parametrize("name", FUSED_SCENARIOS)
+def test_batch_update_schedule_matches_reference(name):
+    d, meta = load(name)
+    m = build(meta)
+    oA, oB = make_opts(m, meta["lrA"], meta["lrB"])
+    bs = batches(d, meta)
+    step = 0
+    for epoch in meta["epochs"]:
+        for bi, (Xb, Yb) in enumerate(bs):
+            m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+            step += 1
+            compare_state("step%d" % step, m, state(d, "step%d" % step))
+    hist = [[] for _ in range(5)] if meta["nsup"] > 0 else []
+    vals = m.validate_training(bs, 1, meta["p"], *hist)
+    names = ["forecast", "factor", "cos", "fw_l1", "smooth", "adj", "dag_reg", "dag_lag", "dag_node", "combo"]
+    if not meta["smoothing_class"]:
+        names = ["forecast", "factor", "cos", "fw_l1", "adj", "dag_reg", "dag_lag", "dag_node", "combo"]
+    for n_, v in zip(names, vals):
+        assert_close("val/" + n_, v, d["val/" + n_], 1e-4, 1e-6)
+
+
+@pytest.mark.parametrize("name", FUSED_SCENARIOS)
+def test_forward_and_gc_match_reference(name):
+    from oracle.redcliff_oracle import OracleREDCLIFF
+    d, meta = load(name)
+    m = build(meta)
+    m.eval()
+    args, kw = ctor_args(meta)
+    torch.manual_seed(meta["seed"])
+    oracle = OracleREDCLIFF(*args, with_smoothing=meta["smoothing_class"], **kw)
+    oracle.eval()
+    Xb, Yb = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    X = Xb[:, :Lm, :].cuda()
+    with torch.no_grad():
+        x_sim, fpreds, fws, labels = m(X)
+    assert_close("x_sim", x_sim.cpu().numpy(), d["eval/x_sim"], RTOL, 1e-5)
+    assert_close("w", fws[0].cpu().numpy(), d["eval/w"], RTOL, 1e-5)
+    assert_close("labels0", labels[0].cpu().numpy(), d["eval/labels0"], RTOL, 1e-5)
+    for k, fp in enumerate(fpreds):
+        assert_close("fpred%d" % k, fp.cpu().numpy(), d["eval/fpred%d" % k], RTOL, 1e-5)
+    for key in [k for k in d.files if k.startswith("eval/gc/")]:
+        _, _, mode, ign, comb = key.split("/")
+        gcs = m.GC(mode, X=X, threshold=False, ignore_lag=ign == "ign1", combine_wavelet_representations=comb == "comb1")
+        arr = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in gcs])
+        assert_close(key, arr, d[key], RTOL, 1e-5)
+        # threshold=True thresholds each factor / embedder graph before weighting (cmlp.py:201-202)
+        thr = m.GC(mode, X=X, threshold=True, ignore_lag=ign == "ign1", combine_wavelet_representations=comb == "comb1")
+        tarr = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in thr])
+        with torch.no_grad():
+            othr = oracle.GC(mode, X=Xb[:, :Lm, :], threshold=True, ignore_lag=ign == "ign1",
+                             combine_wavelet_representations=comb == "comb1")
+        oarr = np.stack([np.stack([g.numpy() for g in row]) for row in othr])
+        assert_close(key + "/thresholded", tarr, oarr, RTOL, 1e-5)
+
+
+def test_train_mode_forward_updates_bn_like_reference():
+    d, meta = load("dgcnn_c1")
+    m = build(meta)
+    m.train()
+    Xb, _ = batches(d, meta)[0]
+    with torch.no_grad():
+        x_sim, _, fws, _ = m(Xb[:, :max(meta["L"], meta["F"]), :].cuda())
+    assert_close("train x_sim", x_sim.cpu().numpy(), d["train_fwd/x_sim"], RTOL, 1e-5)
+    assert_close("train w", fws[0].cpu().numpy(), d["train_fwd/w"], RTOL, 1e-5)
+    assert int(m.factor_score_embedder.dgcnn.dgcnn.BN1.num_batches_tracked) == 1
+
+
+def test_cmlp_gc_prox_forward_match_reference():
+    import redcliff_amd
+    d, _ = load("cmlp_prox")
+    torch.manual_seed(3)
+    net = redcliff_amd.cMLP(5, 4, [6]).cuda()
+    for ign in (0, 1):
+        assert_close("gc", net.GC(threshold=False, ignore_lag=bool(ign)).cpu().numpy(), d["gc/ign%d" % ign], 1e-5, 1e-6)
+        np.testing.assert_array_equal(net.GC(threshold=True, ignore_lag=bool(ign)).cpu().numpy(), d["gct/ign%d" % ign])
+    with torch.no_grad():
+        y = net(torch.from_numpy(d["fwd/X"]).cuda())
+    assert_close("fwd", y.cpu().numpy(), d["fwd/Y"], 1e-5, 1e-6)
+    for pen in ("GL", "GSGL", "H"):
+        n2 = copy.deepcopy(net)
+        n2.perform_prox_update_on_GC_weights(0.9, 0.5, pen)
+        want = state(d, "prox_" + pen)
+        for k, v in n2.state_dict().items():
+            assert_close("prox_%s/%s" % (pen, k), v.cpu().numpy(), want[k], 1e-5, 1e-6)
+
+
+# --------------------------------------------------------------------------- vs the oracle at real sizes
+CONFIGS = {
+    # C1 north-star ratio config: p=10, L=5, K=4, h=25, DGCNN F=16 / 3 layers / 100 hidden, B=128
+    "C1K4": dict(p=10, L=5, K=4, nsup=4, h=25, F=16, n=3, H=100, B=128, T=100, label_T=100),
+    # C2 D4IC-shaped: p=10, L=4, K=4, h=100, F=20, 2 layers, 30 hidden, labels (N, K, 1), T=21
+    "C2": dict(p=10, L=4, K=4, nsup=4, h=100, F=20, n=2, H=30, B=128, T=21, label_T=1),
+    # C4 TST-shaped: p=12, L=4, K=9 (3 supervised), h=25, F=16, 3 layers, 100 hidden, T=150
+    "C4": dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, B=128, T=150, label_T=150),
+}
+
+
+def oracle_and_hip(cfg, seed=0):
+    from oracle.redcliff_oracle import OracleREDCLIFF, reference_coeffs
+    import redcliff_amd
+    coeff = reference_coeffs(cfg["K"], cfg["p"])
+    eargs = [("num_features_per_node", cfg["F"]), ("num_graph_conv_layers", cfg["n"]),
+             ("num_hidden_nodes", cfg["H"]), ("sigmoid_eccentricity_coeff", 10.0)]
+    args = (cfg["p"], cfg["L"], [cfg["h"]], cfg["F"], [0], cfg["L"], 1, cfg["K"], cfg["nsup"], coeff, False, "DGCNN",
+            eargs, "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion")
+    kw = dict(num_sims=1, training_mode="pretrain_embedder_then_acclimate_factors_then_combined",
+              num_pretrain_epochs=1, num_acclimation_epochs=1)
+    torch.manual_seed(seed)
+    o = OracleREDCLIFF(*args, **kw)
+    torch.manual_seed(seed)
+    m = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(*args, **kw).cuda()
+    return o, m
+
+
+def synth(cfg, N, seed):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(N, cfg["T"], cfg["p"]).astype(np.float32)
+    for t in range(2, cfg["T"]):
+        X[:, t] += 0.4 * X[:, t - 1] - 0.2 * X[:, t - 2]
+    X /= X.std()
+    if cfg["label_T"] == 1:
+        Y = np.zeros((N, cfg["K"], 1), np.float32)
+        Y[np.arange(N), rng.randint(0, cfg["K"], N), 0] = 10.0
+    else:
+        Y = np.zeros((N, cfg["K"], cfg["label_T"]), np.float32)
+        Y[np.arange(N), rng.randint(0, cfg["K"], N), :] = 1.0
+    return torch.from_numpy(X), torch.from_numpy(Y)
+
+
+@pytest.mark.parametrize("cname", list(CONFIGS))
+def test_published_configs_three_phases_vs_oracle(cname):
+    cfg = CONFIGS[cname]
+    o, m = oracle_and_hip(cfg)
+    X, Y = synth(cfg, 2 * cfg["B"] + 40, seed=5)
+    B = cfg["B"]
+    bs = [(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)]
+    from oracle.redcliff_oracle import make_optimizers
+    oA, oB = make_optimizers(o, 5e-4, 1e-4, 1e-4, 5e-4, 1e-4, 1e-4)
+    hA, hB = make_optimizers(m, 5e-4, 1e-4, 1e-4, 5e-4, 1e-4, 1e-4)
+    for epoch in (0, 1, 2):
+        for bi, (Xb, Yb) in enumerate(bs):
+            o.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+            m.batch_update(epoch, bi, Xb, Yb, hA, hB, 1)
+    want = dict((k, v.detach().numpy()) for k, v in o.state_dict().items() if not k.startswith("gen_model."))
+    compare_state(cname, m, want, rtol=2e-4, atol=5e-6)
+    # losses / GC estimates on held-out windows
+    Xv, Yv = synth(cfg, 64, seed=9)
+    ov = o.validate([(Xv, Yv)])
+    hist = [[] for _ in range(5)]
+    hv = m.validate_training([(Xv, Yv)], 1, cfg["p"], *hist)
+    for i, k in enumerate(["forecast", "factor", "cos", "fw_l1", "smooth", "adj"]):
+        assert_close("val/" + k, hv[i], ov[k], 1e-4, 1e-6)
+    o.eval()
+    m.eval()
+    Lm = max(cfg["L"], cfg["F"])
+    with torch.no_grad():
+        go = o.GC("conditional_factor_fixed_embedder", X=Xv[:40, :Lm], threshold=False, ignore_lag=False)
+        gm = m.GC("conditional_factor_fixed_embedder", X=Xv[:40, :Lm].cuda(), threshold=False, ignore_lag=False)
+    a = np.stack([np.stack([g.numpy() for g in row]) for row in go])
+    b = np.stack([np.stack([g.cpu().numpy() for g in row]) for row in gm])
+    assert_close("GC", b, a, 1e-4, 1e-5)
+    np.testing.assert_array_equal(b > 0, a > 0)
+
+
+def test_fit_trace_matches_reference():
+    import redcliff_amd
+    d, meta = load("fit_trace")
+    args = (meta["p"], meta["L"], [meta["h"]], meta["F"], [0], meta["L"], 1, meta["K"], meta["nsup"], meta["coeff"],
+            False, "DGCNN", [("num_features_per_node", meta["F"]), ("num_graph_conv_layers", meta["n"]),
+                             ("num_hidden_nodes", meta["H"]), ("sigmoid_eccentricity_coeff", 10.0)],
+            meta["gc_mode"], meta["fwd_mode"])
+    torch.manual_seed(meta["seed"])
+    m = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(*args, num_sims=1, training_mode=meta["training_mode"],
+                                                        num_pretrain_epochs=meta["pre"],
+                                                        num_acclimation_epochs=meta["acc"]).cuda()
+    B = meta["B"]
+    X, Y, Xv, Yv = [torch.from_numpy(d[k]) for k in ("X", "Y", "Xv", "Yv")]
+    train = [(X[i:i + B], Y[i:i + B]) for i in range(0, len(X), B)]
+    val = [(Xv[i:i + B], Yv[i:i + B]) for i in range(0, len(Xv), B)]
+    true_gc = [d["true_gc%d" % k] for k in range(meta["K"])]
+    oA, oB = make_opts(m, 5e-4, 5e-4)
+    m.fit(None, train, oA, oB, meta["L"], 1, 1, meta["max_iter"], val, lookback=1, check_every=1, verbose=0,
+          GC=true_gc, stopping_criteria_forecast_coeff=10., stopping_criteria_factor_coeff=100.,
+          stopping_criteria_cosSim_coeff=1.)
+    h = m.fit_history
+    for k in ("avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
+              "avg_adj_penalty", "avg_combo_loss"):
+        assert_close(k, np.asarray(h[k]), d["hist/" + k], 1e-4, 1e-6)
+    assert h["best_it"] == int(d["hist/best_it"])
+    for sf in range(meta["K"]):
+        np.testing.assert_allclose(h["f1score_histories"][0.0][sf], d["hist/f1_%d" % sf], rtol=0, atol=1e-6)
+    compare_state("final", m, state(d, "final"), rtol=2e-4, atol=5e-6)
+    m.eval()
+    with torch.no_grad():
+        gcs = m.GC(meta["gc_mode"], X=val[0][0][:, :max(meta["L"], meta["F"])].cuda(), threshold=False,
+                   ignore_lag=False, combine_wavelet_representations=True)
+    arr = np.stack([np.stack([g.cpu().numpy() for g in row]) for row in gcs])
+    assert_close("final_gc", arr, d["final_gc"], 1e-4, 1e-5)
+    from redcliff_amd.metrics import get_f1_score
+    f1 = np.asarray([[get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), true_gc[k].sum(axis=2))
+                      for k, g in enumerate(row)] for row in arr])
+    np.testing.assert_array_equal(f1, d["f1"])

@@ -1,0 +1,65 @@
+"""CPU tests of the host-side mirror: parameter trees / seeded init against the reference's
+golden vectors, the phase schedule, label selection, and loud failure without a GPU."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import SCENARIOS, ctor_args, load, state
+from oracle.redcliff_oracle import OracleREDCLIFF
+
+
+def build(meta):
+    import redcliff_amd
+    args, kw = ctor_args(meta)
+    torch.manual_seed(meta["seed"])
+    cls = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing if meta["smoothing_class"] else redcliff_amd.REDCLIFF_S_CMLP
+    return cls(*args, **kw).float()
+
+
+@pytest.mark.parametrize("name", [s for s in SCENARIOS])
+def test_seeded_init_matches_reference(name):
+    d, meta = load(name)
+    m = build(meta)
+    want = state(d, "init")
+    got = dict((k, v) for k, v in m.state_dict().items() if not k.startswith("gen_model."))
+    assert set(got) == set(want)
+    for k in want:
+        np.testing.assert_array_equal(got[k].numpy(), want[k], err_msg=k)
+
+
+def test_phase_schedule_matches_oracle():
+    from redcliff_amd.engine import phase_of_epoch
+    d, meta = load("dgcnn_c1")
+    args, kw = ctor_args(meta)
+    for mode, pre, acc in [("pretrain_embedder_then_acclimate_factors_then_combined", 2, 3),
+                           ("pretrain_embedder_then_combined", 2, 0), ("combined", 0, 0),
+                           ("pretrain_embedder_and_pretrain_factor_then_combined", 1, 0),
+                           ("pretrain_embedder_then_post_train_factor", 2, 0)]:
+        kw2 = dict(kw, training_mode=mode, num_pretrain_epochs=pre, num_acclimation_epochs=acc)
+        torch.manual_seed(0)
+        o = OracleREDCLIFF(*args, **kw2)
+        torch.manual_seed(0)
+        m = build(dict(meta, training_mode=mode, pre=pre, acc=acc))
+        for ep in range(8):
+            want = list(o.phase(ep))
+            want = [w for w in want if w is not None]
+            assert phase_of_epoch(m, ep) == want, (mode, ep)
+
+
+def test_label_selection_rules():
+    from redcliff_amd.engine import select_labels
+    Y = torch.arange(2 * 3 * 10, dtype=torch.float32).view(2, 3, 10)
+    assert torch.equal(select_labels(Y, 3, 5), Y[:, :, 5])        # T_y > Lmax: label at Lmax (:637)
+    Y1 = Y[:, :, :1]
+    assert torch.equal(select_labels(Y1, 3, 5), Y1[:, :, 0])      # D4IC: (N, K, 1)
+    Y2 = Y[:, :, 0]
+    assert torch.equal(select_labels(Y2, 3, 5), Y2)               # 2-D labels
+    assert select_labels(Y2[:, :2], 3, 5).shape == (2, 3)          # fewer label columns than factors
+
+
+def test_compute_without_gpu_fails_loudly():
+    d, meta = load("dgcnn_c1")
+    m = build(meta)
+    X = torch.from_numpy(d["X"][:4])
+    with pytest.raises(RuntimeError, match="GPU"):
+        m(X[:, :5])
