@@ -147,16 +147,18 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream);
 int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_t* rows, const int32_t* sizes,
                          int32_t bn_stats_step, void* stream);
 
-/* Offsets (floats, per replica) of the workspace regions: T R f1 w a y G G0 dwp dAadj dWi dS dgb S
- * dZ amat lossp xsim gfc total.  Returns the number of offsets available.  The host reads
- * w (raw embedder output), y (per-factor predictions), xsim (mixed forecast), G / G0
- * (group norms) back from a step run with RC_STORE_OUTPUTS. */
+/* Offsets (floats, per replica) of the workspace regions: T R f1 w a y G G0 w1 dwp dAadj dWi dS
+ * dgb S dZ amat lossp xsim gfc total.  Returns the number of offsets available.  The host reads
+ * w (raw embedder output), y (per-factor predictions as nU = ceil(h/16) partial sums
+ * y[nU][Bmax][K][p] over 16-unit hidden chunks), xsim (mixed forecast), G / G0 (group norms)
+ * back from a step run with RC_STORE_OUTPUTS. */
 int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out);
 
 /* Stand-alone forward of K cMLPs (models/cmlp.py:90-101) on B windows Xwin[r][B][L][p]
  * (x_rstride floats between replicas).  Per replica (ws_rstride floats) the workspace
- * receives a[K][p][B][h] | y[B][K][p] | G[K][p][p][L] | G0[K][p][p]; y is the prediction
- * of network j of factor k for window b. */
+ * receives a[K][p][B][h] | y[nU][B][K][p] | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h];
+ * sum_u y[u][b][k][j] (nU = ceil(h/16) hidden-chunk partials, output bias in chunk 0) is
+ * the prediction of network j of factor k for window b. */
 int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride, const float* fac,
                             int64_t fac_stride, float* ws, int64_t ws_rstride, void* stream);
 

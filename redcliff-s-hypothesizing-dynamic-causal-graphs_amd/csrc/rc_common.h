@@ -22,14 +22,15 @@ struct WsOff {
   int64_t f1;     // [Bmax][M1]        fc1 pre-activation
   int64_t w;      // [Bmax][K]         raw embedder output (pre-sigmoid)
   int64_t a;      // [K][p][Bmax][h]   factor hidden activations (reused for dz)
-  int64_t y;      // [Bmax][K][p]      per-factor predictions
+  int64_t y;      // [nU][Bmax][K][p]  per-factor predictions, partial over 16-unit hidden chunks
   int64_t G;      // [K][p][p][L]      lagged group norms of W0
   int64_t G0;     // [K][p][p]         lag-free group norms of W0
+  int64_t w1;     // [K][p][h]         pre-update snapshot of the factor output weights
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
   int64_t dWi;    // [p][n][F][H]      graph-conv weight gradient partials (per node)
-  int64_t dS;     // [n][p][p]         gradient wrt Chebyshev supports
-  int64_t dgb;    // [p][2][F]         BatchNorm affine gradient partials (per node)
+  int64_t dS;     // [p][nch][n][p]    gradient wrt Chebyshev supports (row c, partial per column chunk)
+  int64_t dgb;    // [p][nch][2][F]    BatchNorm affine gradient partials (per node and chunk)
   int64_t S;      // [n][p][p]         supports (S_0 = I)
   int64_t dZ;     // [p][Bmax][H]      graph-conv output gradient per node
   int64_t amat;   // [8][p][p]         scratch for the adjacency backward
@@ -69,6 +70,13 @@ inline FacOff rc_fac_off(const RedcliffDims& d) {
   return o;
 }
 
+// graph-conv hidden columns per embedder-backward workgroup
+#define EMB_HC 16
+__host__ __device__ inline int rc_nchunk(const RedcliffDims& d) { return (d.H + EMB_HC - 1) / EMB_HC; }
+// factor hidden units per factor-kernel workgroup
+#define FAC_UC 16
+__host__ __device__ inline int rc_nuchunk(const RedcliffDims& d) { return (d.h + FAC_UC - 1) / FAC_UC; }
+
 inline int64_t rc_align64(int64_t x) { return (x + 63) & ~(int64_t)63; }
 
 inline WsOff rc_ws_off(const RedcliffDims& d) {
@@ -80,14 +88,15 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.f1 = x; x = rc_align64(x + B * d.M1);
   o.w = x; x = rc_align64(x + B * K);
   o.a = x; x = rc_align64(x + K * p * B * d.h);
-  o.y = x; x = rc_align64(x + B * K * p);
+  o.y = x; x = rc_align64(x + (int64_t)rc_nuchunk(d) * B * K * p);
   o.G = x; x = rc_align64(x + K * p * p * d.L);
   o.G0 = x; x = rc_align64(x + K * p * p);
+  o.w1 = x; x = rc_align64(x + K * p * d.h);
   o.dwp = x; x = rc_align64(x + p * B * K);
   o.dAadj = x; x = rc_align64(x + K * p * p);
   o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);
-  o.dS = x; x = rc_align64(x + d.n * p * p);
-  o.dgb = x; x = rc_align64(x + p * 2 * d.F);
+  o.dS = x; x = rc_align64(x + p * rc_nchunk(d) * d.n * p);
+  o.dgb = x; x = rc_align64(x + p * rc_nchunk(d) * 2 * d.F);
   o.S = x; x = rc_align64(x + d.n * p * p);
   o.dZ = x; x = rc_align64(x + p * B * d.H);
   o.amat = x; x = rc_align64(x + 8 * p * p);

@@ -41,102 +41,100 @@ __device__ void bn_affine(const StepCtx& c, int r, const float* E, float* alpha,
 }
 
 // ------------------------------------------------------------------------------------------
-// K1: embedder forward.  grid (ceil(B/SB), R); one workgroup handles SB windows.
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB) {
+// K1: embedder forward.  grid (ceil(B/SB), R); one workgroup handles SB windows with the
+// supports S_i and (when they fit) the graph-conv weights W_i staged in LDS.
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_lds) {
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y;
   const int b0 = blockIdx.x * SB;
   const int nb = min(SB, c.B - b0);
   if (nb <= 0) return;
   const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
-  const int pF = p * F, pH = p * H;
+  const int pF = p * F, pH = p * H, nFH = n * F * H;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
   const int tid = threadIdx.x;
 
   extern __shared__ float sm[];
-  float* xs = sm;              // [SB][p][F]
-  float* Ti = xs + SB * pF;    // [p][F]
-  float* Rl = Ti + pF;         // [SB][p*H]
-  float* f1l = Rl + SB * pH;   // [SB][M1]
+  float* xs = sm;                      // [SB][p][F]   x_bn
+  float* Sl = xs + SB * pF;            // [n][p][p]
+  float* Wl = Sl + n * p * p;          // [n][F][H]    (w_lds)
+  float* Tl = Wl + (w_lds ? nFH : 0);  // [SB][n][p][F]
+  float* Rl = Tl + SB * n * pF;        // [SB][p*H]
+  float* f1l = Rl + SB * pH;           // [SB][M1]
   float* alpha = f1l + SB * M1;
   float* beta = alpha + F;
 
   bn_affine(c, r, E, alpha, beta, nullptr, nullptr);
-  __syncthreads();
-  for (int e = tid; e < nb * pF; e += RC_BLOCK) {
-    const int s = e / pF, rem = e - s * pF, ch = rem / F, f = rem - ch * F;
-    const int64_t row = c.row0 + b0 + s;
-    const float x = X[(row * d.T + (c.Lmax - F + f)) * p + ch];
-    xs[e] = x * alpha[f] + beta[f];
-  }
-  __syncthreads();
-
   const float* S = ws + c.wo.S;
+  for (int e = tid; e < n * p * p; e += RC_BLOCK) Sl[e] = S[e];
   const float* gw = E + c.eo.gcW;
-  const int NZ = (pH + RC_BLOCK - 1) / RC_BLOCK;  // <= 32 (checked on the host)
-  for (int s = 0; s < nb; ++s) {
-    float z[32];
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) z[kk] = 0.f;
-    for (int i = 0; i < n; ++i) {
-      for (int e = tid; e < pF; e += RC_BLOCK) {
-        const int ch = e / F, f = e - ch * F;
-        float v;
-        if (i == 0) {
-          v = xs[s * pF + e];
-        } else {
-          v = 0.f;
-          const float* Srow = S + ((int64_t)i * p + ch) * p;
-          for (int cc = 0; cc < p; ++cc) v += Srow[cc] * xs[s * pF + cc * F + f];
-        }
-        Ti[e] = v;
-        ws[c.wo.T + ((int64_t)(b0 + s) * n + i) * pF + e] = v;
-      }
-      __syncthreads();
-      const float* Wi = gw + (int64_t)i * F * H;
-#pragma unroll
-      for (int kk = 0; kk < 32; ++kk) {
-        const int e = tid + kk * RC_BLOCK;
-        if (kk < NZ && e < pH) {
-          const int ch = e / H, hh = e - ch * H;
-          float acc = z[kk];
-          const float* trow = Ti + ch * F;
-          for (int f = 0; f < F; ++f) acc += trow[f] * Wi[f * H + hh];
-          z[kk] = acc;
-        }
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) {
-      const int e = tid + kk * RC_BLOCK;
-      if (kk < NZ && e < pH) {
-        const float v = fmaxf(z[kk], 0.f);
-        Rl[s * pH + e] = v;
-        ws[c.wo.R + (int64_t)(b0 + s) * pH + e] = v;
-      }
-    }
+  if (w_lds)
+    for (int e = tid; e < nFH; e += RC_BLOCK) Wl[e] = gw[e];
+  const float* Wsrc = w_lds ? Wl : gw;
+  __syncthreads();
+  // window rows are contiguous in the channel index: read (s, f, ch), store x_bn[s][ch][f]
+  for (int e = tid; e < nb * pF; e += RC_BLOCK) {
+    const int s = e / pF, rem = e - s * pF, f = rem / p, ch = rem - f * p;
+    const float x = X[(c.row0 + b0 + s) * d.T * p + (int64_t)(c.Lmax - F + f) * p + ch];
+    xs[s * pF + ch * F + f] = x * alpha[f] + beta[f];
   }
   __syncthreads();
-
-  // fc1: one wave per output row, lanes split the p*H contraction (coalesced weight rows)
+  // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x))
+  for (int e = tid; e < nb * n * pF; e += RC_BLOCK) {
+    const int s = e / (n * pF), rem = e - s * n * pF, i = rem / pF, q = rem - i * pF, ch = q / F, f = q - ch * F;
+    float v;
+    if (i == 0) {
+      v = xs[s * pF + q];
+    } else {
+      v = 0.f;
+      const float* Srow = Sl + (i * p + ch) * p;
+      const float* xc = xs + s * pF + f;
+      for (int cc = 0; cc < p; ++cc) v += Srow[cc] * xc[cc * F];
+    }
+    Tl[e] = v;
+    ws[c.wo.T + (int64_t)(b0 + s) * n * pF + rem] = v;
+  }
+  __syncthreads();
+  // Z = sum_i T_i W_i ; R = relu(Z)
+  for (int e = tid; e < nb * pH; e += RC_BLOCK) {
+    const int s = e / pH, rem = e - s * pH, ch = rem / H, hh = rem - ch * H;
+    float acc = 0.f;
+    for (int i = 0; i < n; ++i) {
+      const float* trow = Tl + (s * n + i) * pF + ch * F;
+      const float* wc = Wsrc + i * F * H + hh;
+      for (int f = 0; f < F; ++f) acc += trow[f] * wc[f * H];
+    }
+    const float v = fmaxf(acc, 0.f);
+    Rl[e] = v;
+    ws[c.wo.R + (int64_t)(b0 + s) * pH + rem] = v;
+  }
+  __syncthreads();
+  // fc1: one wave per output row; lanes split the p*H contraction (coalesced rows, 4 loads in flight)
   const float* W1 = E + c.eo.fc1W;
   const int lane = tid & 63, wv = tid >> 6;
   for (int m = wv; m < M1; m += RC_BLOCK / 64) {
-    float acc[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) acc[s] = 0.f;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
     const float* wr = W1 + (int64_t)m * pH;
-    for (int q = lane; q < pH; q += 64) {
-      const float wq = wr[q];
+    int q = lane;
+    for (; q + 192 < pH; q += 256) {
+      const float w0 = wr[q], w1 = wr[q + 64], w2 = wr[q + 128], w3 = wr[q + 192];
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
-        if (s < nb) acc[s] += wq * Rl[s * pH + q];
+      for (int s = 0; s < 4; ++s)
+        if (s < nb) {
+          const float* rr = Rl + s * pH + q;
+          acc[s] += w0 * rr[0] + w1 * rr[64] + w2 * rr[128] + w3 * rr[192];
+        }
+    }
+    for (; q < pH; q += 64) {
+      const float w0 = wr[q];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        if (s < nb) acc[s] += w0 * Rl[s * pH + q];
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
+    for (int s = 0; s < 4; ++s) {
       if (s < nb) {
         const float t = rc_wave_sum(acc[s]) + E[c.eo.fc1b + m];
         if (lane == 0) {
@@ -206,29 +204,50 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
   float* dr = sm;
   float* red = dr + ((d.Bmax * K + 1) & ~1);  // even offset: doubles follow
   if (c.flags & RC_STEP_A) {
+    // dfc2W[k][m] = sum_b dr[b][k] relu(f1[b][m]); dfc2b[k] = sum_b dr[b][k];
+    // dfc1b[m] = sum_b [f1[b][m] > 0] sum_k dr[b][k] fc2W[k][m]      (f1 staged BCH rows at a time)
     build_draw(c, r, dr);
-    __syncthreads();
+    float* fc2s = red + 64;                  // [K][M1]
+    float* f1c = fc2s + K * M1;              // [BCH][M1]
+    const int BCH = 64;
+    for (int e = tid; e < K * M1; e += RC_BLOCK) fc2s[e] = E[c.eo.fc2W + e];
     const float* f1 = ws + c.wo.f1;
     float* gfc = ws + c.wo.gfc;
-    for (int e = tid; e < K * M1 + K + M1; e += RC_BLOCK) {
-      float g = 0.f;
-      if (e < K * M1) {
-        const int k = e / M1, m = e - k * M1;
-        for (int b = 0; b < B; ++b) g += dr[b * K + k] * fmaxf(f1[(int64_t)b * M1 + m], 0.f);
-      } else if (e < K * M1 + K) {
-        const int k = e - K * M1;
-        for (int b = 0; b < B; ++b) g += dr[b * K + k];
-      } else {
-        const int m = e - K * M1 - K;
-        for (int b = 0; b < B; ++b) {
-          if (f1[(int64_t)b * M1 + m] > 0.f) {
-            float t = 0.f;
-            for (int k = 0; k < K; ++k) t += dr[b * K + k] * E[c.eo.fc2W + (int64_t)k * M1 + m];
-            g += t;
+    const int nout = K * M1 + K + M1;
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // nout <= 16*64 + 16 + 64 < 5*256
+    for (int bc = 0; bc < B; bc += BCH) {
+      const int nbc = min(BCH, B - bc);
+      __syncthreads();
+      for (int e = tid; e < nbc * M1; e += RC_BLOCK) f1c[e] = f1[(int64_t)bc * M1 + e];
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        const int e = tid + kk * RC_BLOCK;
+        if (e >= nout) continue;
+        float g = acc[kk];
+        if (e < K * M1) {
+          const int k = e / M1, m = e - k * M1;
+          for (int s = 0; s < nbc; ++s) g += dr[(bc + s) * K + k] * fmaxf(f1c[s * M1 + m], 0.f);
+        } else if (e < K * M1 + K) {
+          const int k = e - K * M1;
+          for (int s = 0; s < nbc; ++s) g += dr[(bc + s) * K + k];
+        } else {
+          const int m = e - K * M1 - K;
+          for (int s = 0; s < nbc; ++s) {
+            if (f1c[s * M1 + m] > 0.f) {
+              float t = 0.f;
+              for (int k = 0; k < K; ++k) t += dr[(bc + s) * K + k] * fc2s[k * M1 + m];
+              g += t;
+            }
           }
         }
+        acc[kk] = g;
       }
-      gfc[e] = g;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (e < nout) gfc[e] = acc[kk];
     }
   }
   if (!(c.flags & (RC_VALUES | RC_CONFUSION))) return;
@@ -323,137 +342,50 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
   }
 }
 
-// K3 node workgroup c: fc1 columns of node c (gradient + Adam), graph-conv output
-// gradient dZ, per-node partials of dW_i, dS_i row c and BatchNorm affine gradients.
-#define EMB_CH 16
-__device__ void emb_bwd_node(const StepCtx& c, int r, int node, float* sm) {
+// K3 node/column-chunk workgroup (node c, hidden columns [h0, h0+HC)): fc1 columns of the
+// chunk (gradient + Adam), graph-conv output gradient dZ, partials of dW_i (over c),
+// dS_i[c][:] and the BatchNorm affine gradients (over c and chunk).  Everything the
+// chunk touches is staged in LDS, BC windows at a time.
+__device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, float* sm) {
   const RedcliffDims& d = c.d;
   const int K = d.K, M1 = d.M1, B = c.B, p = d.p, H = d.H, F = d.F, n = d.n;
-  const int pH = p * H, pF = p * F;
+  const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC;
+  const int h0 = ch * HC, hc = min(HC, H - h0);
+  const int nch = rc_nchunk(d);
   float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr;
   const int tid = threadIdx.x;
-  float* dr = sm;                 // [B][K]
-  float* Fs = dr + B * K;         // [M1][H]   fc1 columns of this node
-  float* df1c = Fs + M1 * H;      // [CH][M1]
-  float* Rc = df1c + EMB_CH * M1; // [CH][H]
-  float* dZc = Rc + EMB_CH * H;   // [CH][H]
+
+  float* dr = sm;                        // [Bmax][K]
+  float* fc2s = dr + d.Bmax * K;         // [K][M1]
+  float* FW = fc2s + K * M1;             // [M1][HC]  fc1 columns of the chunk
+  float* WiC = FW + M1 * HC;             // [n][F][HC]
+  float* Srow = WiC + nF * HC;           // [n][p]    row `node` of each support
+  float* rs = Srow + n * p;              // [n]       row sums
+  float* alpha = rs + 4;                 // [F]
+  float* beta = alpha + F;               // [F]
+  float* mean = beta + F;                // [F]
+  float* inv = mean + F;                 // [F]
+  float* red = inv + F;                  // [RC_BLOCK]
+  float* df1c = red + RC_BLOCK;          // [BC][M1]
+  float* Rc = df1c + BC * M1;            // [BC][HC]
+  float* dZc = Rc + BC * HC;             // [BC][HC]
+  float* Tc = dZc + BC * HC;             // [BC][n][F]   T_i row `node`
+  float* dTc = Tc + BC * nF;             // [BC][n][F]
+  float* xc = dTc + BC * nF;             // [BC][p][F]   raw window
 
   build_draw(c, r, dr);
-  for (int e = tid; e < M1 * H; e += RC_BLOCK) {
-    const int m = e / H, hh = e - m * H;
-    Fs[e] = E[c.eo.fc1W + (int64_t)m * pH + node * H + hh];
-  }
-  __syncthreads();
-  const float* f1 = ws + c.wo.f1;
-  const float* Rg = ws + c.wo.R;
-  float* dZg = ws + c.wo.dZ + (int64_t)node * d.Bmax * H;
-  const int NE = (M1 * H + RC_BLOCK - 1) / RC_BLOCK;  // <= 32
-  float acc[32];
-#pragma unroll
-  for (int kk = 0; kk < 32; ++kk) acc[kk] = 0.f;
-  for (int bc = 0; bc < B; bc += EMB_CH) {
-    const int nbc = min(EMB_CH, B - bc);
-    for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
-      const int s = e / M1, m = e - s * M1, b = bc + s;
-      float g = 0.f;
-      if (f1[(int64_t)b * M1 + m] > 0.f)
-        for (int k = 0; k < K; ++k) g += dr[b * K + k] * E[c.eo.fc2W + (int64_t)k * M1 + m];
-      df1c[e] = g;
-    }
-    for (int e = tid; e < nbc * H; e += RC_BLOCK) {
-      const int s = e / H, hh = e - s * H;
-      Rc[e] = Rg[(int64_t)(bc + s) * pH + node * H + hh];
-    }
-    __syncthreads();
-    for (int e = tid; e < nbc * H; e += RC_BLOCK) {
-      const int s = e / H, hh = e - s * H;
-      float g = 0.f;
-      for (int m = 0; m < M1; ++m) g += Fs[m * H + hh] * df1c[s * M1 + m];
-      const float v = Rc[e] > 0.f ? g : 0.f;
-      dZc[e] = v;
-      dZg[(int64_t)(bc + s) * H + hh] = v;
-    }
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) {
-      const int e = tid + kk * RC_BLOCK;
-      if (kk < NE && e < M1 * H) {
-        const int m = e / H, hh = e - m * H;
-        float a = acc[kk];
-        for (int s = 0; s < nbc; ++s) a += df1c[s * M1 + m] * Rc[s * H + hh];
-        acc[kk] = a;
-      }
-    }
-    __syncthreads();
-  }
-  // Adam on this node's fc1 columns (no other workgroup reads them in this kernel)
-  {
-    const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
-    float* P = E + c.eo.fc1W;
-    float* Mm = c.embM + r * c.es + c.eo.fc1W;
-    float* V = c.embV + r * c.es + c.eo.fc1W;
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) {
-      const int e = tid + kk * RC_BLOCK;
-      if (kk < NE && e < M1 * H) {
-        const int m = e / H, hh = e - m * H;
-        const int64_t idx = (int64_t)m * pH + node * H + hh;
-        float pp = P[idx], mm = Mm[idx], vv = V[idx];
-        rc_adam(pp, mm, vv, acc[kk], as);
-        P[idx] = pp; Mm[idx] = mm; V[idx] = vv;
-      }
-    }
-  }
-  __syncthreads();
-
-  // dW_i partial of this node: sum_b T_i,b[node][f] * dZ_b[node][h]
-  const float* Tg = ws + c.wo.T;
-  float* Tc = df1c;  // reuse: [CH][F] (F <= M1 checked on host)
-  const int NW = (F * H + RC_BLOCK - 1) / RC_BLOCK;  // <= 32
-  for (int i = 0; i < n; ++i) {
-    float a2[32];
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) a2[kk] = 0.f;
-    for (int bc = 0; bc < B; bc += EMB_CH) {
-      const int nbc = min(EMB_CH, B - bc);
-      for (int e = tid; e < nbc * F; e += RC_BLOCK) {
-        const int s = e / F, f = e - s * F;
-        Tc[e] = Tg[((int64_t)(bc + s) * n + i) * pF + node * F + f];
-      }
-      for (int e = tid; e < nbc * H; e += RC_BLOCK) dZc[e] = dZg[(int64_t)bc * H + e];
-      __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < 32; ++kk) {
-        const int e = tid + kk * RC_BLOCK;
-        if (kk < NW && e < F * H) {
-          const int f = e / H, hh = e - f * H;
-          float a = a2[kk];
-          for (int s = 0; s < nbc; ++s) a += Tc[s * F + f] * dZc[s * H + hh];
-          a2[kk] = a;
-        }
-      }
-      __syncthreads();
-    }
-    float* out = ws + c.wo.dWi + (((int64_t)node * n + i) * F) * H;
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) {
-      const int e = tid + kk * RC_BLOCK;
-      if (kk < NW && e < F * H) out[e] = a2[kk];
-    }
-  }
-  __syncthreads();
-
-  // per window: dT_i[f] = sum_h dZ[h] W_i[f][h]; dS_i[node][c'] += dT_i . x_bn[c'];
-  // BN affine partials dgamma_f += sum_i dT_i[f] (S_i xhat)[node][f], dbeta_f += sum_i dT_i[f] rowsum(S_i)[node]
-  float* xh = sm + B * K;          // [p][F]   (reuses Fs)
-  float* dTl = xh + pF;            // [n][F]
-  float* Srow = dTl + n * F;       // [n][p]
-  float* alpha = Srow + n * p;     // [F]
-  float* beta = alpha + F;         // [F]
-  float* mean = beta + F;          // [F]
-  float* inv = mean + F;           // [F]
-  float* rs = inv + F;             // [n]
   bn_affine(c, r, E, alpha, beta, mean, inv);
+  for (int e = tid; e < K * M1; e += RC_BLOCK) fc2s[e] = E[c.eo.fc2W + e];
+  for (int e = tid; e < M1 * HC; e += RC_BLOCK) {
+    const int m = e / HC, hh = e - m * HC;
+    FW[e] = hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;
+  }
+  for (int e = tid; e < nF * HC; e += RC_BLOCK) {
+    const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
+    WiC[e] = hh < hc ? E[c.eo.gcW + ((int64_t)i * F + f) * H + h0 + hh] : 0.f;
+  }
   const float* S = ws + c.wo.S;
   for (int e = tid; e < n * p; e += RC_BLOCK) {
     const int i = e / p, cc = e - i * p;
@@ -465,63 +397,150 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, float* sm) {
     for (int cc = 0; cc < p; ++cc) t += Srow[tid * p + cc];
     rs[tid] = t;
   }
-  const float* X = c.X + r * c.xr;
-  const float* gw = E + c.eo.gcW;
-  float dSacc = 0.f, dgam = 0.f, dbet = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const int64_t row = c.row0 + b;
-    for (int e = tid; e < pF; e += RC_BLOCK) {
-      const int cc = e / F, f = e - cc * F;
-      xh[e] = (X[(row * d.T + (c.Lmax - F + f)) * p + cc] - mean[f]) * inv[f];
+  // accumulators: dfc1W chunk (M1*HC <= 1024 -> 4 / thread), dW_i chunk (n*F*HC <= 4096 -> 16 / thread)
+  float afc[4] = {0.f, 0.f, 0.f, 0.f};
+  float awi[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) awi[k] = 0.f;
+  // dS_i[node][c'] (i >= 1) and BN partials, reduced at the end through LDS
+  const int nS = (n - 1) * p;
+  float aS = 0.f, aG = 0.f, aB = 0.f;
+  const float* f1 = ws + c.wo.f1;
+  const float* Rg = ws + c.wo.R;
+  const float* Tg = ws + c.wo.T;
+  for (int bc = 0; bc < B; bc += BC) {
+    const int nbc = min(BC, B - bc);
+    for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
+      const int s = e / M1, m = e - s * M1, b = bc + s;
+      float g = 0.f;
+      if (f1[(int64_t)b * M1 + m] > 0.f)
+        for (int k = 0; k < K; ++k) g += dr[b * K + k] * fc2s[k * M1 + m];
+      df1c[e] = g;
     }
-    if (tid < n * F) {
-      const int i = tid / F, f = tid - i * F;
-      const float* dz = dZg + (int64_t)b * H;
-      const float* wr = gw + ((int64_t)i * F + f) * H;
-      float t = 0.f;
-      for (int hh = 0; hh < H; ++hh) t += dz[hh] * wr[hh];
-      dTl[tid] = t;
+    for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
+      const int s = e / HC, hh = e - s * HC;
+      Rc[e] = hh < hc ? Rg[(int64_t)(bc + s) * pH + node * H + h0 + hh] : 0.f;
+    }
+    for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
+      const int s = e / nF, rem = e - s * nF, i = rem / F, f = rem - i * F;
+      Tc[e] = Tg[(int64_t)(bc + s) * n * pF + i * pF + node * F + f];
+    }
+    for (int e = tid; e < nbc * pF; e += RC_BLOCK) {
+      const int s = e / pF, rem = e - s * pF, f = rem / p, cc = rem - f * p;
+      xc[s * pF + cc * F + f] = X[(c.row0 + bc + s) * d.T * p + (int64_t)(c.Lmax - F + f) * p + cc];
     }
     __syncthreads();
-    if (tid < (n - 1) * p) {
-      const int i = 1 + tid / p, cp = tid - (i - 1) * p;
-      const float* X0 = X + (row * d.T + (c.Lmax - F)) * p + cp;
+    for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
+      const int s = e / HC, hh = e - s * HC;
+      float g = 0.f;
+      for (int m = 0; m < M1; ++m) g += df1c[s * M1 + m] * FW[m * HC + hh];
+      dZc[e] = Rc[e] > 0.f ? g : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (e < M1 * HC) {
+        const int m = e / HC, hh = e - m * HC;
+        float a = afc[k];
+        for (int s = 0; s < nbc; ++s) a += df1c[s * M1 + m] * Rc[s * HC + hh];
+        afc[k] = a;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (e < nF * HC) {
+        const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
+        float a = awi[k];
+        for (int s = 0; s < nbc; ++s) a += Tc[s * nF + i * F + f] * dZc[s * HC + hh];
+        awi[k] = a;
+      }
+    }
+    for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
+      const int s = e / nF, rem = e - s * nF;
+      const float* wr = WiC + rem * HC;
+      const float* dz = dZc + s * HC;
       float t = 0.f;
-      for (int f = 0; f < F; ++f) t += dTl[i * F + f] * (X0[(int64_t)f * p] * alpha[f] + beta[f]);
-      dSacc += t;
+      for (int hh = 0; hh < HC; ++hh) t += dz[hh] * wr[hh];
+      dTc[e] = t;
+    }
+    __syncthreads();
+    if (tid < nS) {
+      const int i = 1 + tid / p, cp = tid - (i - 1) * p;
+      float t = 0.f;
+      for (int s = 0; s < nbc; ++s) {
+        const float* dt = dTc + s * nF + i * F;
+        const float* xr = xc + s * pF + cp * F;
+        for (int f = 0; f < F; ++f) t += dt[f] * (xr[f] * alpha[f] + beta[f]);
+      }
+      aS += t;
     }
     if (tid < F) {
       const int f = tid;
-      for (int i = 0; i < n; ++i) {
-        float u = 0.f;
-        if (i == 0) {
-          u = xh[node * F + f];
-        } else {
-          for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * xh[cc * F + f];
+      for (int s = 0; s < nbc; ++s) {
+        for (int i = 0; i < n; ++i) {
+          float u;
+          if (i == 0) {
+            u = (xc[s * pF + node * F + f] - mean[f]) * inv[f];
+          } else {
+            u = 0.f;
+            for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xc[s * pF + cc * F + f] - mean[f]) * inv[f]);
+          }
+          const float dt = dTc[s * nF + i * F + f];
+          aG += dt * u;
+          aB += dt * rs[i];
         }
-        dgam += dTl[i * F + f] * u;
-        dbet += dTl[i * F + f] * rs[i];
       }
     }
     __syncthreads();
   }
-  if (tid < (n - 1) * p) {
-    const int i = 1 + tid / p, cp = tid - (i - 1) * p;
-    ws[c.wo.dS + ((int64_t)i * p + node) * p + cp] = dSacc;
+  // fc1 columns of this chunk: Adam (no other workgroup reads them in this kernel)
+  if (c.flags & RC_STEP_A) {
+    const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
+    float* P = E + c.eo.fc1W;
+    float* Mm = c.embM + r * c.es + c.eo.fc1W;
+    float* V = c.embV + r * c.es + c.eo.fc1W;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (e < M1 * HC) {
+        const int m = e / HC, hh = e - m * HC;
+        if (hh < hc) {
+          const int64_t idx = (int64_t)m * pH + node * H + h0 + hh;
+          float pp = P[idx], mm = Mm[idx], vv = V[idx];
+          rc_adam(pp, mm, vv, afc[k], as);
+          P[idx] = pp; Mm[idx] = mm; V[idx] = vv;
+        }
+      }
+    }
   }
+  float* dWi = ws + c.wo.dWi + (int64_t)node * n * F * H;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * RC_BLOCK;
+    if (e < nF * HC) {
+      const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
+      if (hh < hc) dWi[((int64_t)i * F + f) * H + h0 + hh] = awi[k];
+    }
+  }
+  const int64_t part = (int64_t)node * nch + ch;
+  if (tid < nS) ws[c.wo.dS + part * n * p + p + tid] = aS;  // layout [part][n][p], rows i >= 1
   if (tid < F) {
-    ws[c.wo.dgb + ((int64_t)node * 2 + 0) * F + tid] = dgam;
-    ws[c.wo.dgb + ((int64_t)node * 2 + 1) * F + tid] = dbet;
+    ws[c.wo.dgb + (part * 2 + 0) * F + tid] = aG;
+    ws[c.wo.dgb + (part * 2 + 1) * F + tid] = aB;
   }
 }
 
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int head_only) {
+// grid (p * nchunk + 1, R): workgroups [0, p*nchunk) are node/column chunks, the last one is the head.
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int head_only, int BC) {
   extern __shared__ float sm[];
   const int r = blockIdx.y;
-  if (head_only || (int)blockIdx.x == c.d.p)
+  const int nch = rc_nchunk(c.d);
+  if (head_only || (int)blockIdx.x == c.d.p * nch)
     emb_bwd_head(c, r, sm);
   else
-    emb_bwd_node(c, r, blockIdx.x, sm);
+    emb_bwd_node(c, r, blockIdx.x / nch, blockIdx.x % nch, BC, sm);
 }
 
 // Supports of normalize_A(A) into S[n][p][p] (S_0 = I, S_1 = L, S_i = S_{i-1} L).
@@ -595,7 +614,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     } else {
       const int q = e - nFH - nfc;
       const int which = q / F, f = q - which * F;  // 0: gamma, 1: beta
-      for (int cc = 0; cc < p; ++cc) g += ws[c.wo.dgb + ((int64_t)cc * 2 + which) * F + f];
+      const int nparts = p * rc_nchunk(d);
+      for (int pt = 0; pt < nparts; ++pt) g += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
       idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
     }
     float pp = E[idx], mm = Mm[idx], vv = V[idx];
@@ -617,7 +637,15 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       Ar[e] = fmaxf(A[e], 0.f);
       dL[e] = 0.f;
     }
-    for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) dSw[e] = ws[c.wo.dS + pp2 + e];
+    {  // dS_i[c][c'] = sum over column chunks of node c's partials (layout [c][chunk][n][p])
+      const int nch = rc_nchunk(d);
+      for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) {
+        const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
+        float t = 0.f;
+        for (int chk = 0; chk < nch; ++chk) t += ws[c.wo.dS + (((int64_t)cc * nch + chk) * n + i) * p + cp];
+        dSw[e] = t;
+      }
+    }
     __syncthreads();
     for (int i = tid; i < p; i += RC_BLOCK) {
       float s = 0.f;
@@ -723,40 +751,51 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bn_stats(RedcliffDims d, const flo
 
 // ------------------------------------------------------------------------------------------
 // host launchers
-static int emb_fwd_sb(const RedcliffDims& d) {
-  const int pF = d.p * d.F, pH = d.p * d.H;
-  int sb = (RC_LDS_LIMIT_FLOATS - pF - 2 * d.F) / (pF + pH + d.M1);
-  if (sb > 16) sb = 16;
-  return sb;
+static size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
+  const size_t pF = (size_t)d.p * d.F, pH = (size_t)d.p * d.H;
+  return SB * pF + (size_t)d.n * d.p * d.p + (w_lds ? (size_t)d.n * d.F * d.H : 0) + SB * d.n * pF + SB * pH +
+         (size_t)SB * d.M1 + 2 * d.F;
 }
 
 int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
-  const int SB = emb_fwd_sb(d);
-  if (SB < 1) { rc_set_error("embedder forward: p*F + p*H too large for LDS"); return REDCLIFF_ELIMIT; }
-  const size_t lds = sizeof(float) * ((size_t)SB * d.p * d.F + d.p * d.F + (size_t)SB * d.p * d.H + SB * d.M1 + 2 * d.F);
+  int SB = 4, w_lds = 1;
+  while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) --SB;
+  if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) w_lds = 0;
+  if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  const size_t lds = sizeof(float) * emb_fwd_floats(d, SB, w_lds);
   dim3 grid((c.B + SB - 1) / SB, d.R);
-  hipLaunchKernelGGL(k_emb_fwd, grid, dim3(RC_BLOCK), lds, s, c, SB);
+  hipLaunchKernelGGL(k_emb_fwd, grid, dim3(RC_BLOCK), lds, s, c, SB, w_lds);
   return rc_check(hipGetLastError(), "k_emb_fwd");
 }
 
+static size_t emb_bwd_node_floats(const RedcliffDims& d, int BC) {
+  const size_t nF = (size_t)d.n * d.F;
+  return (size_t)d.Bmax * d.K + (size_t)d.K * d.M1 + (size_t)d.M1 * EMB_HC + nF * EMB_HC + (size_t)d.n * d.p + 4 +
+         4 * d.F + RC_BLOCK + (size_t)BC * (d.M1 + 2 * EMB_HC + 2 * nF + (size_t)d.p * d.F);
+}
+
+static int emb_bwd_bc(const RedcliffDims& d) {
+  int BC = 32;
+  while (BC > 1 && emb_bwd_node_floats(d, BC) > RC_LDS_LIMIT_FLOATS) BC >>= 1;
+  return BC;
+}
+
 size_t rc_emb_bwd_lds(const RedcliffDims& d) {
-  const size_t head = (size_t)d.Bmax * d.K + 2 + 8 + 16;
-  const size_t node1 = (size_t)d.Bmax * d.K + (size_t)d.M1 * d.H + EMB_CH * d.M1 + 2 * EMB_CH * d.H;
-  const size_t node3 = (size_t)d.Bmax * d.K + d.p * d.F + d.n * d.F + d.n * d.p + 4 * d.F + d.n;
-  size_t m = head > node1 ? head : node1;
-  m = m > node3 ? m : node3;
-  return m * sizeof(float);
+  const size_t head = (size_t)d.Bmax * d.K + 2 + 64 + (size_t)d.K * d.M1 + 64 * (size_t)d.M1;
+  const size_t node = emb_bwd_node_floats(d, emb_bwd_bc(d));
+  return (head > node ? head : node) * sizeof(float);
 }
 
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   const RedcliffDims& d = c.d;
   const size_t lds = rc_emb_bwd_lds(d);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  const int BC = emb_bwd_bc(d);
   if (node_wgs)
-    hipLaunchKernelGGL(k_emb_bwd, dim3(d.p + 1, d.R), dim3(RC_BLOCK), lds, s, c, 0);
+    hipLaunchKernelGGL(k_emb_bwd, dim3(d.p * rc_nchunk(d) + 1, d.R), dim3(RC_BLOCK), lds, s, c, 0, BC);
   else
-    hipLaunchKernelGGL(k_emb_bwd, dim3(1, d.R), dim3(RC_BLOCK), lds, s, c, 1);
+    hipLaunchKernelGGL(k_emb_bwd, dim3(1, d.R), dim3(RC_BLOCK), lds, s, c, 1, BC);
   return rc_check(hipGetLastError(), "k_emb_bwd");
 }
 

@@ -29,108 +29,109 @@ __device__ inline float xwin(const StepCtx& c, const float* X, int b, int q) {
 }
 
 // ------------------------------------------------------------------------------------------
-// K2a: forward of every (factor, channel) network.  grid (K*p, R).
-template <int TN>
+// K2a: forward of every (factor, channel) network, FAC_UC hidden units per workgroup.
+// grid (K*p*nU, R).  Writes relu activations a[kj][b][u], the partial output
+// ypart[uc][b][k][j] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk 0), and (chunk 0)
+// the lagged / lag-free group norms G, G0 of the network's layer-0 weights.
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd(StepCtx c) {
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, kj = blockIdx.x;
+  const int nU = rc_nuchunk(d);
+  const int r = blockIdx.y, kj = blockIdx.x / nU, uc = blockIdx.x - kj * nU;
   const int p = d.p, h = d.h, K = d.K;
   const int k = kj / p, j = kj - k * p;
   const int Q = p * d.L;
-  const int HP = 16 * TN;
+  const int u0 = uc * FAC_UC;
   const float* P = c.fac + r * c.fs;
   const float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
   const float* b0 = P + c.fo.b0 + (int64_t)kj * h;
   const float* W1 = P + c.fo.W1 + (int64_t)kj * h;
-  const float b1 = P[c.fo.b1 + kj];
+  const float b1 = uc == 0 ? P[c.fo.b1 + kj] : 0.f;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
   const int tid = threadIdx.x, tb = tid >> 4, tu = tid & 15;
+  const int u = u0 + tu;
 
   __shared__ float Xs[FK_BT * (FK_QT + 1)];
-  __shared__ float Ws[16 * TN * (FK_QT + 1)];
+  __shared__ float Ws[FAC_UC * (FK_QT + 1)];
 
   for (int bc = 0; bc < c.B; bc += FK_BT) {
-    float acc[8][TN];
+    float acc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) acc[i][jj] = 0.f;
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
     for (int q0 = 0; q0 < Q; q0 += FK_QT) {
       for (int e = tid; e < FK_BT * FK_QT; e += RC_BLOCK) {
         const int bb = e / FK_QT, qq = e - bb * FK_QT;
         const int b = bc + bb, q = q0 + qq;
         Xs[bb * (FK_QT + 1) + qq] = (b < c.B && q < Q) ? xwin(c, X, b, q) : 0.f;
       }
-      for (int e = tid; e < HP * FK_QT; e += RC_BLOCK) {
-        const int u = e / FK_QT, qq = e - u * FK_QT;
+      for (int e = tid; e < FAC_UC * FK_QT; e += RC_BLOCK) {
+        const int uu = e / FK_QT, qq = e - uu * FK_QT;
         const int q = q0 + qq;
-        Ws[u * (FK_QT + 1) + qq] = (u < h && q < Q) ? W0[(int64_t)u * Q + q] : 0.f;
+        Ws[uu * (FK_QT + 1) + qq] = (u0 + uu < h && q < Q) ? W0[(int64_t)(u0 + uu) * Q + q] : 0.f;
       }
       __syncthreads();
-#pragma unroll 4
+#pragma unroll 8
       for (int qq = 0; qq < FK_QT; ++qq) {
-        float xv[8], wv[TN];
+        const float wv = Ws[tu * (FK_QT + 1) + qq];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) xv[i] = Xs[(tb + 16 * i) * (FK_QT + 1) + qq];
-#pragma unroll
-        for (int jj = 0; jj < TN; ++jj) wv[jj] = Ws[(tu + 16 * jj) * (FK_QT + 1) + qq];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int jj = 0; jj < TN; ++jj) acc[i][jj] += xv[i] * wv[jj];
+        for (int i = 0; i < 8; ++i) acc[i] += Xs[(tb + 16 * i) * (FK_QT + 1) + qq] * wv;
       }
       __syncthreads();
     }
+    const float bu = u < h ? b0[u] : 0.f, w1 = u < h ? W1[u] : 0.f;
+    if (bc == 0 && tb == 0 && u < h) ws[c.wo.w1 + (int64_t)kj * h + u] = w1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int b = bc + tb + 16 * i;
       float ys = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < TN; ++jj) {
-        const int u = tu + 16 * jj;
-        if (u < h) {
-          const float a = fmaxf(acc[i][jj] + b0[u], 0.f);
-          if (b < c.B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
-          ys += W1[u] * a;
-        }
+      if (u < h) {
+        const float a = fmaxf(acc[i] + bu, 0.f);
+        if (b < c.B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+        ys = w1 * a;
       }
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);
-      if (tu == 0 && b < c.B) ws[c.wo.y + ((int64_t)b * K + k) * p + j] = ys + b1;
+      if (tu == 0 && b < c.B) ws[c.wo.y + (((int64_t)uc * d.Bmax + b) * K + k) * p + j] = ys + b1;
     }
   }
-  // group norms of this network's layer-0 weights (GC, models/cmlp.py:162-166)
+  if (uc != 0) return;
+  // group norms of this network's layer-0 weights (GC, models/cmlp.py:162-166), pre-update
+  __shared__ float Gsq[64 * 64];
   for (int e = tid; e < Q; e += RC_BLOCK) {
-    float s = 0.f;
-    for (int u = 0; u < h; ++u) {
-      const float w = W0[(int64_t)u * Q + e];
-      s += w * w;
+    float sq = 0.f;
+    for (int uu = 0; uu < h; ++uu) {
+      const float w = W0[(int64_t)uu * Q + e];
+      sq += w * w;
     }
-    ws[c.wo.G + (int64_t)kj * Q + e] = sqrtf(s);
+    Gsq[e] = sq;
+    ws[c.wo.G + (int64_t)kj * Q + e] = sqrtf(sq);
   }
+  __syncthreads();
   for (int cc = tid; cc < p; cc += RC_BLOCK) {
-    float s = 0.f;
-    for (int u = 0; u < h; ++u)
-      for (int t = 0; t < d.L; ++t) {
-        const float w = W0[(int64_t)u * Q + cc * d.L + t];
-        s += w * w;
-      }
-    ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(s);
+    float sq = 0.f;
+    for (int t = 0; t < d.L; ++t) sq += Gsq[cc * d.L + t];
+    ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// K2b: mixing, forecast loss, adjacency L1, backward and Adam of every network.
-// grid (K*p, R).
-template <int TN>
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
+// K2b: mixing, forecast loss, adjacency L1, backward and Adam.  grid (K*p*nU*nQ, R):
+// workgroup (network kj, hidden chunk uc, dW0 column tile qc).  The cheap per-window work
+// (x_sim, residual, dL/dy, adjacency-L1 signs) is recomputed by every workgroup of a network;
+// its outputs (dL/dw partials, loss values, dL/dA) are written by the (uc, qc) = (0, 0) one.
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ) {
+  // nUl x nQ workgroups per network (1 x 1 when there is no factor update)
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, kj = blockIdx.x;
+  const int nU = rc_nuchunk(d);
+  const int r = blockIdx.y;
+  const int kj = blockIdx.x / (nUl * nQ);
+  const int rem0 = blockIdx.x - kj * nUl * nQ;
+  const int uc = rem0 / nQ, qc = rem0 - uc * nQ;
+  const bool lead = (uc == 0 && qc == 0);
   const int p = d.p, h = d.h, K = d.K, L = d.L;
   const int k = kj / p, j = kj - k * p;
   const int Q = p * L;
-  const int HP = 16 * TN;
+  const int u0 = uc * FAC_UC, q0 = qc * FB_QT;
   float* P = c.fac + r * c.fs;
   float* PM = c.facM + r * c.fs;
   float* PV = c.facV + r * c.fs;
@@ -162,11 +163,13 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
   float fsum = 0.f;
   for (int b = tid; b < B; b += RC_BLOCK) {
     const float* wr = ws + c.wo.w + (int64_t)b * K;
-    const float* yr = ws + c.wo.y + (int64_t)b * K * p;
-    float xs = 0.f;
+    float xs = 0.f, yk = 0.f;
     for (int kk = 0; kk < K; ++kk) {
+      float yv = 0.f;
+      for (int q = 0; q < nU; ++q) yv += ws[c.wo.y + (((int64_t)q * d.Bmax + b) * K + kk) * p + j];
       const float we = sig ? rc_sigmoid(ecc * wr[kk]) : wr[kk];
-      xs = (kk == 0) ? we * yr[kk * p + j] : xs + we * yr[kk * p + j];
+      xs = (kk == 0) ? we * yv : xs + we * yv;
+      if (kk == k) yk = yv;
     }
     // the target X[:, Lmax] exists only when a loss is requested (forward() passes X[:, :Lmax])
     const float res = (c.flags & (RC_LOSS_FORECAST | RC_VALUES)) ? xs - X[((c.row0 + b) * d.T + c.Lmax) * p + j] : 0.f;
@@ -174,19 +177,19 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
     const float g = gscale * res;
     wk[b] = wb;
     dyl[b] = g * wb;
-    if (fgrad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = g * yr[k * p + j];
-    if (k == 0) {
+    if (lead && fgrad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = g * yk;
+    if (lead && k == 0) {
       fsum += res * res;
       ws[c.wo.xsim + (int64_t)b * p + j] = xs;
     }
   }
-  if (values && k == 0) {
+  if (values && lead && k == 0) {
     const float t = rc_block_sum(fsum, red);
     if (tid == 0) ws[c.wo.lossp + j] = t;
   }
 
   // ---- part 2: adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j]
-  const bool adj_on = adj_grad || values;
+  const bool adj_on = adj_grad || (values && lead);
   const int Ls = c.Ls;
   if (adj_on) {
     for (int e = tid; e < Q; e += RC_BLOCK) {
@@ -196,23 +199,25 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
     for (int cc = tid; cc < p; cc += RC_BLOCK) Acol[cc] = E[c.eo.A + cc * p + j];
     for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
     __syncthreads();
-    float vsum = 0.f;
-    for (int b = tid; b < B; b += RC_BLOCK) {
-      const float wb = wk[b];
-      float t = 0.f, v = 0.f;
-      for (int cc = 0; cc < p; ++cc)
-        for (int i = 0; i < Ls; ++i) {
-          const float g = Gs[cc * L + (L - Ls + i)];
-          const float val = wb * g + Acol[cc];
-          t += lwt[i] * rc_sign(val) * g;
-          v += lwt[i] * fabsf(val);
-        }
-      if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] += hy.c_adj * t;
-      vsum += v;
-    }
-    if (values) {
-      const float t = rc_block_sum(vsum, red);
-      if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * t;
+    if (lead) {
+      float vsum = 0.f;
+      for (int b = tid; b < B; b += RC_BLOCK) {
+        const float wb = wk[b];
+        float t = 0.f, v = 0.f;
+        for (int cc = 0; cc < p; ++cc)
+          for (int i = 0; i < Ls; ++i) {
+            const float g = Gs[cc * L + (L - Ls + i)];
+            const float val = wb * g + Acol[cc];
+            t += lwt[i] * rc_sign(val) * g;
+            v += lwt[i] * fabsf(val);
+          }
+        if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] += hy.c_adj * t;
+        vsum += v;
+      }
+      if (values) {
+        const float t = rc_block_sum(vsum, red);
+        if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * t;
+      }
     }
     if (adj_grad) {
       for (int e = tid; e < p * Ls; e += RC_BLOCK) {
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
         dAp[e] = hy.c_adj * lwt[i] * s1;
       }
       __syncthreads();
-      if (c.flags & RC_STEP_A) {
+      if (lead && (c.flags & RC_STEP_A)) {
         for (int cc = tid; cc < p; cc += RC_BLOCK) {
           float s = 0.f;
           for (int i = 0; i < Ls; ++i) s += dAp[cc * Ls + i];
@@ -241,75 +246,93 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
   if (!(c.flags & RC_STEP_B)) return;
   __syncthreads();
 
-  // ---- part 3a: output layer and ReLU backward (dz overwrites the stored activations)
-  float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
-  float* W1 = P + c.fo.W1 + (int64_t)kj * h;
-  float dW1u = 0.f, db0u = 0.f;
-  if (tid < h) {
-    const float w1 = W1[tid];
-    for (int b = 0; b < B; ++b) {
-      const float av = aw[(int64_t)b * h + tid];
-      dW1u += dyl[b] * av;
-      const float dz = av > 0.f ? dyl[b] * w1 : 0.f;
-      db0u += dz;
-      aw[(int64_t)b * h + tid] = dz;
-    }
-  }
-  float db1 = 0.f;
-  for (int b = tid; b < B; b += RC_BLOCK) db1 += dyl[b];
-  db1 = rc_block_sum(db1, red);  // includes a __syncthreads: dz visible to the workgroup
-
-  // ---- part 3b: dW0 = dz^T Xw (+ adjacency-L1 term through the group norms) and Adam
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
+  const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
+  const float* W1 = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by K2a
+  // ---- part 3a (column tile 0): output-layer / bias gradients of the chunk's hidden units
+  if (qc == 0) {
+    const int uu = tid & 15, part = tid >> 4;  // 16 slices of the batch per hidden unit
+    const int u = u0 + uu;
+    float dW1u = 0.f, db0u = 0.f;
+    if (u < h) {
+      const float w1 = W1[u];
+      for (int b = part; b < B; b += 16) {
+        const float av = aw[(int64_t)b * h + u];
+        dW1u += dyl[b] * av;
+        db0u += av > 0.f ? dyl[b] * w1 : 0.f;
+      }
+    }
+    float* rA = tiles;              // [16][16]
+    float* rB = tiles + 256;
+    rA[tid] = dW1u;
+    rB[tid] = db0u;
+    float db1 = 0.f;
+    if (uc == 0)
+      for (int b = tid; b < B; b += RC_BLOCK) db1 += dyl[b];
+    db1 = rc_block_sum(db1, red);
+    if (tid < 16 && u0 + tid < h) {
+      float g1 = 0.f, g0 = 0.f;
+      for (int s = 0; s < 16; ++s) {
+        g1 += rA[s * 16 + tid];
+        g0 += rB[s * 16 + tid];
+      }
+      const int64_t ib = c.fo.b0 + (int64_t)kj * h + u0 + tid;
+      const int64_t iw = c.fo.W1 + (int64_t)kj * h + u0 + tid;
+      rc_adam(P[ib], PM[ib], PV[ib], g0, as);
+      rc_adam(P[iw], PM[iw], PV[iw], g1, as);
+    }
+    if (uc == 0 && tid == 0) {
+      const int64_t i1 = c.fo.b1 + kj;
+      rc_adam(P[i1], PM[i1], PV[i1], db1, as);
+    }
+    __syncthreads();
+  }
+
+  // ---- part 3b: dW0 tile = dz^T Xw (+ adjacency-L1 term through the group norms) and Adam
   float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
   float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
   float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
-  float* dZs = tiles;                         // [FB_BT][HP+1]
-  float* Xs = dZs + FB_BT * (HP + 1);         // [FB_BT][FB_QT+1]
+  float* dZs = tiles + 512;                  // [FB_BT][FAC_UC+1]
+  float* Xs = dZs + FB_BT * (FAC_UC + 1);    // [FB_BT][FB_QT+1]
+  float* w1s = Xs + FB_BT * (FB_QT + 1);     // [FAC_UC]
+  if (tid < FAC_UC) w1s[tid] = (u0 + tid < h) ? W1[u0 + tid] : 0.f;
   const int tq = tid & 15, tu = tid >> 4;
-  for (int q0 = 0; q0 < Q; q0 += FB_QT) {
-    float acc[TN][4];
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[i][jj] = 0.f;
-    for (int bb0 = 0; bb0 < B; bb0 += FB_BT) {
-      for (int e = tid; e < FB_BT * HP; e += RC_BLOCK) {
-        const int bb = e / HP, u = e - bb * HP;
-        const int b = bb0 + bb;
-        dZs[bb * (HP + 1) + u] = (b < B && u < h) ? aw[(int64_t)b * h + u] : 0.f;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int bb0 = 0; bb0 < B; bb0 += FB_BT) {
+    __syncthreads();
+    for (int e = tid; e < FB_BT * FAC_UC; e += RC_BLOCK) {
+      const int bb = e / FAC_UC, uu = e - bb * FAC_UC;
+      const int b = bb0 + bb, u = u0 + uu;
+      float dz = 0.f;
+      if (b < B && u < h) {
+        const float av = aw[(int64_t)b * h + u];
+        dz = av > 0.f ? dyl[b] * w1s[uu] : 0.f;
       }
-      for (int e = tid; e < FB_BT * FB_QT; e += RC_BLOCK) {
-        const int bb = e / FB_QT, qq = e - bb * FB_QT;
-        const int b = bb0 + bb, q = q0 + qq;
-        Xs[bb * (FB_QT + 1) + qq] = (b < B && q < Q) ? xwin(c, X, b, q) : 0.f;
-      }
-      __syncthreads();
-#pragma unroll 4
-      for (int bb = 0; bb < FB_BT; ++bb) {
-        float zv[TN], xv[4];
-#pragma unroll
-        for (int i = 0; i < TN; ++i) zv[i] = dZs[bb * (HP + 1) + tu + 16 * i];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) xv[jj] = Xs[bb * (FB_QT + 1) + tq + 16 * jj];
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc[i][jj] += zv[i] * xv[jj];
-      }
-      __syncthreads();
+      dZs[bb * (FAC_UC + 1) + uu] = dz;
     }
+    for (int e = tid; e < FB_BT * FB_QT; e += RC_BLOCK) {
+      const int bb = e / FB_QT, qq = e - bb * FB_QT;
+      const int b = bb0 + bb, q = q0 + qq;
+      Xs[bb * (FB_QT + 1) + qq] = (b < B && q < Q) ? xwin(c, X, b, q) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int bb = 0; bb < FB_BT; ++bb) {
+      const float zv = dZs[bb * (FAC_UC + 1) + tu];
 #pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int u = tu + 16 * i;
-      if (u >= h) continue;
+      for (int jj = 0; jj < 4; ++jj) acc[jj] += zv * Xs[bb * (FB_QT + 1) + tq + 16 * jj];
+    }
+  }
+  {
+    const int u = u0 + tu;
+    if (u < h) {
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int q = q0 + tq + 16 * jj;
         if (q >= Q) continue;
         const int64_t idx = (int64_t)u * Q + q;
         float pw = W0[idx];
-        float g = acc[i][jj];
+        float g = acc[jj];
         if (adj_grad && Gs[q] > 0.f) g += dGs[q] * (pw / Gs[q]);
         float mm = M0[idx], vv = V0[idx];
         rc_adam(pw, mm, vv, g, as);
@@ -317,61 +340,37 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c) {
       }
     }
   }
-  // ---- part 3c: biases and the output layer
-  if (tid < h) {
-    const int64_t ib = c.fo.b0 + (int64_t)kj * h + tid;
-    rc_adam(P[ib], PM[ib], PV[ib], db0u, as);
-    const int64_t iw = c.fo.W1 + (int64_t)kj * h + tid;
-    rc_adam(P[iw], PM[iw], PV[iw], dW1u, as);
-  }
-  if (tid == 0) {
-    const int64_t i1 = c.fo.b1 + kj;
-    rc_adam(P[i1], PM[i1], PV[i1], db1, as);
-  }
 }
 
-template <int TN>
-int launch_fwd_t(const StepCtx& c, hipStream_t s) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fac_fwd<TN>), dim3(c.d.K * c.d.p, c.d.R), dim3(RC_BLOCK), 0, s, c);
-  return rc_check(hipGetLastError(), "k_fac_fwd");
-}
-
-template <int TN>
-int launch_bwd_t(const StepCtx& c, hipStream_t s) {
-  const RedcliffDims& d = c.d;
+int fac_bwd_lds_floats(const RedcliffDims& d, int Ls) {
   const int Q = d.p * d.L;
-  const size_t lds = sizeof(float) * (2 * (size_t)d.Bmax + 2 * Q + d.p + d.L + 16 + (size_t)d.p * c.Ls +
-                                      FB_BT * (16 * TN + 1) + FB_BT * (FB_QT + 1));
-  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_fac_bwd<TN>), dim3(d.K * d.p, d.R), dim3(RC_BLOCK), lds, s, c);
-  return rc_check(hipGetLastError(), "k_fac_bwd");
+  return 2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + 512 + FB_BT * (FAC_UC + 1) + FB_BT * (FB_QT + 1) + FAC_UC;
 }
 
 }  // namespace
 
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s) {
-  const int h = c.d.h;
-  if (h <= 16) return launch_fwd_t<1>(c, s);
-  if (h <= 32) return launch_fwd_t<2>(c, s);
-  if (h <= 64) return launch_fwd_t<4>(c, s);
-  if (h <= 128) return launch_fwd_t<8>(c, s);
-  rc_set_error("factor hidden width %d > 128", h);
-  return REDCLIFF_ELIMIT;
+  const RedcliffDims& d = c.d;
+  if (d.h > 128 || d.p * d.L > 4096) { rc_set_error("factor forward: h <= 128 and p*L <= 4096 required"); return REDCLIFF_ELIMIT; }
+  hipLaunchKernelGGL(k_fac_fwd, dim3(d.K * d.p * rc_nuchunk(d), d.R), dim3(RC_BLOCK), 0, s, c);
+  return rc_check(hipGetLastError(), "k_fac_fwd");
 }
 
 int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
-  const int h = c.d.h;
-  if (h <= 16) return launch_bwd_t<1>(c, s);
-  if (h <= 32) return launch_bwd_t<2>(c, s);
-  if (h <= 64) return launch_bwd_t<4>(c, s);
-  if (h <= 128) return launch_bwd_t<8>(c, s);
-  rc_set_error("factor hidden width %d > 128", h);
-  return REDCLIFF_ELIMIT;
+  const RedcliffDims& d = c.d;
+  const int Q = d.p * d.L;
+  const int nQ = (c.flags & RC_STEP_B) ? (Q + FB_QT - 1) / FB_QT : 1;
+  const size_t lds = sizeof(float) * (size_t)fac_bwd_lds_floats(d, c.Ls);
+  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  // without a factor update only the lead workgroup of each network has work
+  const int nUl = (c.flags & RC_STEP_B) ? rc_nuchunk(d) : 1;
+  hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, d.R), dim3(RC_BLOCK), lds, s, c, nUl, nQ);
+  return rc_check(hipGetLastError(), "k_fac_bwd");
 }
 
 // Stand-alone forward of K cMLPs on B windows Xwin[B][L][p] (cMLP.forward, models/cmlp.py:90-101,
 // and the per-factor predictions of REDCLIFF forward).  Per replica the workspace holds
-// a[K][p][B][h] | y[B][K][p] | G[K][p][p][L] | G0[K][p][p].
+// a[K][p][B][h] | y[nU][B][K][p] (partials over hidden chunks) | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h].
 extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride,
                                        const float* fac, int64_t fac_stride, float* ws, int64_t ws_rstride,
                                        void* stream) {
@@ -395,7 +394,8 @@ extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const f
   const int64_t kp = (int64_t)d->K * d->p;
   c.wo.a = 0;
   c.wo.y = kp * B * d->h;
-  c.wo.G = c.wo.y + (int64_t)B * kp;
+  c.wo.G = c.wo.y + (int64_t)rc_nuchunk(*d) * B * kp;
   c.wo.G0 = c.wo.G + kp * d->p * d->L;
+  c.wo.w1 = c.wo.G0 + kp * d->p;
   return rc_launch_fac_fwd(c, (hipStream_t)stream);
 }

@@ -407,7 +407,8 @@ class FitEngine:
             self.dgcnn.BN1.num_batches_tracked.add_(bn_updates)
         o = self.ws_off
         w = self.ws[o["w"]:o["w"] + B * self.K].view(B, self.K).clone()
-        y = self.ws[o["y"]:o["y"] + B * self.K * self.p].view(B, self.K, self.p).clone()
+        nU = (self.h + 15) // 16  # the forward kernel leaves per-hidden-chunk partials
+        y = self.ws[o["y"]:o["y"] + nU * d.Bmax * self.K * self.p].view(nU, d.Bmax, self.K, self.p)[:, :B].sum(0)
         xs = self.ws[o["xsim"]:o["xsim"] + B * self.p].view(B, self.p).clone()
         return w, y, xs
 

@@ -109,14 +109,15 @@ def factor_forward_packed(flat, K, p, h, L, Xwin):
     for b0 in range(0, B, chunk):
         nb = min(chunk, B - b0)
         kp = K * p
-        ws_floats = kp * nb * h + nb * kp + kp * p * L + kp * p
+        nU = (h + 15) // 16  # hidden-unit chunks of the forward kernel (FAC_UC)
+        ws_floats = kp * nb * h + nU * nb * kp + kp * p * L + kp * p + kp * h
         ws = torch.empty(ws_floats, device=Xwin.device, dtype=torch.float32)
         dims = factor_dims(K, p, L, h, Bmax=nb)
         xw = Xwin[b0:b0 + nb].contiguous()
         nat.check(nat.lib().redcliff_factor_forward(ctypes.byref(dims), nb, ptr(xw), 0, ptr(flat), 0, ptr(ws),
                                                     ws_floats, current_stream()), "factor_forward")
         off = kp * nb * h
-        out[b0:b0 + nb] = ws[off:off + nb * kp].view(nb, K, p)
+        out[b0:b0 + nb] = ws[off:off + nU * nb * kp].view(nU, nb, K, p).sum(0)
     return out
 
 
