@@ -26,6 +26,7 @@ struct WsOff {
   int64_t G;      // [K][p][p][L]      lagged group norms of W0
   int64_t G0;     // [K][p][p]         lag-free group norms of W0
   int64_t w1;     // [K][p][h]         pre-update snapshot of the factor output weights
+  int64_t gq;     // [nU][K][p][p*L]   squared layer-0 group norms, partial over hidden chunks
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
   int64_t dWi;    // [p][n][F][H]      graph-conv weight gradient partials (per node)
@@ -92,6 +93,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.G = x; x = rc_align64(x + K * p * p * d.L);
   o.G0 = x; x = rc_align64(x + K * p * p);
   o.w1 = x; x = rc_align64(x + K * p * d.h);
+  o.gq = x; x = rc_align64(x + (int64_t)rc_nuchunk(d) * K * p * p * d.L);
   o.dwp = x; x = rc_align64(x + p * B * K);
   o.dAadj = x; x = rc_align64(x + K * p * p);
   o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);

@@ -12,6 +12,8 @@
 // ...withStateSmoothing.py:844-856); the math is identical, so it is evaluated once,
 // the three upstream gradients are summed, and the BatchNorm running statistics are
 // advanced n_bn_updates (=3) times.
+#include <cstdlib>
+
 #include "rc_common.h"
 
 namespace {
@@ -111,36 +113,38 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_l
     ws[c.wo.R + (int64_t)(b0 + s) * pH + rem] = v;
   }
   __syncthreads();
-  // fc1: one wave per output row; lanes split the p*H contraction (coalesced rows, 4 loads in flight)
+  // fc1: wave wv owns rows [wv*RW, wv*RW+RW) (RW <= 16); lanes split the p*H contraction.
+  // All RW weight loads of a column step are issued together (one HBM/L2 latency per step).
   const float* W1 = E + c.eo.fc1W;
   const int lane = tid & 63, wv = tid >> 6;
-  for (int m = wv; m < M1; m += RC_BLOCK / 64) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* wr = W1 + (int64_t)m * pH;
-    int q = lane;
-    for (; q + 192 < pH; q += 256) {
-      const float w0 = wr[q], w1 = wr[q + 64], w2 = wr[q + 128], w3 = wr[q + 192];
+  const int RW = (M1 + 3) / 4, m0 = wv * RW;
+  float acc[16][4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (s < nb) {
-          const float* rr = Rl + s * pH + q;
-          acc[s] += w0 * rr[0] + w1 * rr[64] + w2 * rr[128] + w3 * rr[192];
-        }
-    }
-    for (; q < pH; q += 64) {
-      const float w0 = wr[q];
+  for (int j = 0; j < 16; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        if (s < nb) acc[s] += w0 * Rl[s * pH + q];
-    }
+    for (int s = 0; s < 4; ++s) acc[j][s] = 0.f;
+  for (int q = lane; q < pH; q += 64) {
+    float w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = (j < RW && m0 + j < M1) ? W1[(int64_t)(m0 + j) * pH + q] : 0.f;
+    float rv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[j][s] += w[j] * rv[s];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int m = m0 + j;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      if (s < nb) {
-        const float t = rc_wave_sum(acc[s]) + E[c.eo.fc1b + m];
-        if (lane == 0) {
-          f1l[s * M1 + m] = t;
-          ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = t;
-        }
+      const float t = rc_wave_sum(acc[j][s]);
+      if (j < RW && m < M1 && s < nb && lane == 0) {
+        const float v = t + E[c.eo.fc1b + m];
+        f1l[s * M1 + m] = v;
+        ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = v;
       }
     }
   }
@@ -404,6 +408,8 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, 
   for (int k = 0; k < 16; ++k) awi[k] = 0.f;
   // dS_i[node][c'] (i >= 1) and BN partials, reduced at the end through LDS
   const int nS = (n - 1) * p;
+  const int nslS = nS > 0 ? RC_BLOCK / nS : 0, oS = nS > 0 ? tid % nS : 0, slS = nS > 0 ? tid / nS : 1;
+  const int nslF = RC_BLOCK / F, oF = tid % F, slF = tid / F;
   float aS = 0.f, aG = 0.f, aB = 0.f;
   const float* f1 = ws + c.wo.f1;
   const float* Rg = ws + c.wo.R;
@@ -466,26 +472,30 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, 
       dTc[e] = t;
     }
     __syncthreads();
-    if (tid < nS) {
-      const int i = 1 + tid / p, cp = tid - (i - 1) * p;
+    // dS_i[node][c'] (i >= 1): output oS, windows split over nslS thread slices
+    if (slS < nslS) {
+      const int i = 1 + oS / p, cp = oS - (i - 1) * p;
       float t = 0.f;
-      for (int s = 0; s < nbc; ++s) {
+      for (int s = slS; s < nbc; s += nslS) {
         const float* dt = dTc + s * nF + i * F;
         const float* xr = xc + s * pF + cp * F;
         for (int f = 0; f < F; ++f) t += dt[f] * (xr[f] * alpha[f] + beta[f]);
       }
       aS += t;
     }
-    if (tid < F) {
-      const int f = tid;
-      for (int s = 0; s < nbc; ++s) {
+    // BatchNorm affine gradients of feature oF, windows split over nslF thread slices
+    if (slF < nslF) {
+      const int f = oF;
+      const float mu = mean[f], iv = inv[f];
+      for (int s = slF; s < nbc; s += nslF) {
+        const float* xs_ = xc + s * pF + f;
         for (int i = 0; i < n; ++i) {
           float u;
           if (i == 0) {
-            u = (xc[s * pF + node * F + f] - mean[f]) * inv[f];
+            u = (xs_[node * F] - mu) * iv;
           } else {
             u = 0.f;
-            for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xc[s * pF + cc * F + f] - mean[f]) * inv[f]);
+            for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xs_[cc * F] - mu) * iv);
           }
           const float dt = dTc[s * nF + i * F + f];
           aG += dt * u;
@@ -494,6 +504,31 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, 
       }
     }
     __syncthreads();
+  }
+  // reduce the thread slices in fixed order
+  const int64_t part = (int64_t)node * nch + ch;
+  red[tid] = (slS < nslS) ? aS : 0.f;
+  __syncthreads();
+  if (tid < nS) {
+    float t = 0.f;
+    for (int q = 0; q < nslS; ++q) t += red[q * nS + tid];
+    ws[c.wo.dS + part * n * p + p + tid] = t;  // layout [part][n][p], rows i >= 1
+  }
+  __syncthreads();
+  red[tid] = (slF < nslF) ? aG : 0.f;
+  __syncthreads();
+  if (tid < F) {
+    float t = 0.f;
+    for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
+    ws[c.wo.dgb + (part * 2 + 0) * F + tid] = t;
+  }
+  __syncthreads();
+  red[tid] = (slF < nslF) ? aB : 0.f;
+  __syncthreads();
+  if (tid < F) {
+    float t = 0.f;
+    for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
+    ws[c.wo.dgb + (part * 2 + 1) * F + tid] = t;
   }
   // fc1 columns of this chunk: Adam (no other workgroup reads them in this kernel)
   if (c.flags & RC_STEP_A) {
@@ -523,12 +558,6 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, 
       const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
       if (hh < hc) dWi[((int64_t)i * F + f) * H + h0 + hh] = awi[k];
     }
-  }
-  const int64_t part = (int64_t)node * nch + ch;
-  if (tid < nS) ws[c.wo.dS + part * n * p + p + tid] = aS;  // layout [part][n][p], rows i >= 1
-  if (tid < F) {
-    ws[c.wo.dgb + (part * 2 + 0) * F + tid] = aG;
-    ws[c.wo.dgb + (part * 2 + 1) * F + tid] = aB;
   }
 }
 
@@ -759,7 +788,12 @@ static size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
 
 int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
-  int SB = 4, w_lds = 1;
+  static const int sb_env = [] {
+    const char* v = getenv("REDCLIFF_EMB_SB");  // tuning knob: windows per forward workgroup
+    const int x = v ? atoi(v) : 0;
+    return (x >= 1 && x <= 4) ? x : 0;
+  }();
+  int SB = sb_env ? sb_env : 2, w_lds = 1;
   while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) --SB;
   if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) w_lds = 0;
   if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }

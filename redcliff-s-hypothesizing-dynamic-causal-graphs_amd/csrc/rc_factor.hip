@@ -31,8 +31,8 @@ __device__ inline float xwin(const StepCtx& c, const float* X, int b, int q) {
 // ------------------------------------------------------------------------------------------
 // K2a: forward of every (factor, channel) network, FAC_UC hidden units per workgroup.
 // grid (K*p*nU, R).  Writes relu activations a[kj][b][u], the partial output
-// ypart[uc][b][k][j] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk 0), and (chunk 0)
-// the lagged / lag-free group norms G, G0 of the network's layer-0 weights.
+// ypart[uc][b][k][j] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk 0), the chunk's
+// squared layer-0 group norms gq[uc][kj][q] and a snapshot of W1 for the backward.
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd(StepCtx c) {
   const RedcliffDims& d = c.d;
   const int nU = rc_nuchunk(d);
@@ -70,6 +70,15 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd(StepCtx c) {
         Ws[uu * (FK_QT + 1) + qq] = (u0 + uu < h && q < Q) ? W0[(int64_t)(u0 + uu) * Q + q] : 0.f;
       }
       __syncthreads();
+      if (bc == 0 && tid < FK_QT && q0 + tid < Q) {
+        // squared group norms of the chunk's 16 units (GC, models/cmlp.py:162-166), pre-update
+        float sq = 0.f;
+        for (int uu = 0; uu < FAC_UC; ++uu) {
+          const float w = Ws[uu * (FK_QT + 1) + tid];
+          sq += w * w;
+        }
+        ws[c.wo.gq + ((int64_t)uc * K * p + kj) * Q + q0 + tid] = sq;
+      }
 #pragma unroll 8
       for (int qq = 0; qq < FK_QT; ++qq) {
         const float wv = Ws[tu * (FK_QT + 1) + qq];
@@ -93,24 +102,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd(StepCtx c) {
       for (int o = 8; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);
       if (tu == 0 && b < c.B) ws[c.wo.y + (((int64_t)uc * d.Bmax + b) * K + k) * p + j] = ys + b1;
     }
-  }
-  if (uc != 0) return;
-  // group norms of this network's layer-0 weights (GC, models/cmlp.py:162-166), pre-update
-  __shared__ float Gsq[64 * 64];
-  for (int e = tid; e < Q; e += RC_BLOCK) {
-    float sq = 0.f;
-    for (int uu = 0; uu < h; ++uu) {
-      const float w = W0[(int64_t)uu * Q + e];
-      sq += w * w;
-    }
-    Gsq[e] = sq;
-    ws[c.wo.G + (int64_t)kj * Q + e] = sqrtf(sq);
-  }
-  __syncthreads();
-  for (int cc = tid; cc < p; cc += RC_BLOCK) {
-    float sq = 0.f;
-    for (int t = 0; t < d.L; ++t) sq += Gsq[cc * d.L + t];
-    ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
   }
 }
 
@@ -188,14 +179,30 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
     if (tid == 0) ws[c.wo.lossp + j] = t;
   }
 
-  // ---- part 2: adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j]
+  // ---- group norms G[kj][c][t] = sqrt(sum over hidden chunks), G0[kj][c] (cmlp.py:147-167)
   const bool adj_on = adj_grad || (values && lead);
   const int Ls = c.Ls;
-  if (adj_on) {
+  if (adj_on || lead) {
     for (int e = tid; e < Q; e += RC_BLOCK) {
-      Gs[e] = ws[c.wo.G + (int64_t)kj * Q + e];
-      dGs[e] = 0.f;
+      float sq = 0.f;
+      for (int q = 0; q < nU; ++q) sq += ws[c.wo.gq + ((int64_t)q * K * p + kj) * Q + e];
+      dGs[e] = sq;
+      const float g = sqrtf(sq);
+      Gs[e] = g;
+      if (lead) ws[c.wo.G + (int64_t)kj * Q + e] = g;
     }
+    __syncthreads();
+    if (lead)
+      for (int cc = tid; cc < p; cc += RC_BLOCK) {
+        float sq = 0.f;
+        for (int t = 0; t < L; ++t) sq += dGs[cc * L + t];
+        ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
+      }
+    __syncthreads();
+  }
+  // ---- part 2: adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j]
+  if (adj_on) {
+    for (int e = tid; e < Q; e += RC_BLOCK) dGs[e] = 0.f;
     for (int cc = tid; cc < p; cc += RC_BLOCK) Acol[cc] = E[c.eo.A + cc * p + j];
     for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
     __syncthreads();
@@ -370,7 +377,8 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
 
 // Stand-alone forward of K cMLPs on B windows Xwin[B][L][p] (cMLP.forward, models/cmlp.py:90-101,
 // and the per-factor predictions of REDCLIFF forward).  Per replica the workspace holds
-// a[K][p][B][h] | y[nU][B][K][p] (partials over hidden chunks) | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h].
+// a[K][p][B][h] | y[nU][B][K][p] (partials over hidden chunks) | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h]
+// | gq[nU][K][p][p*L].  G / G0 are left unset (use redcliff_gc_norms).
 extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride,
                                        const float* fac, int64_t fac_stride, float* ws, int64_t ws_rstride,
                                        void* stream) {
@@ -397,5 +405,6 @@ extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const f
   c.wo.G = c.wo.y + (int64_t)rc_nuchunk(*d) * B * kp;
   c.wo.G0 = c.wo.G + kp * d->p * d->L;
   c.wo.w1 = c.wo.G0 + kp * d->p;
+  c.wo.gq = c.wo.w1 + kp * d->h;
   return rc_launch_fac_fwd(c, (hipStream_t)stream);
 }

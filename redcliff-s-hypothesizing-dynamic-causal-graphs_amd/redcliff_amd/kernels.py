@@ -110,7 +110,7 @@ def factor_forward_packed(flat, K, p, h, L, Xwin):
         nb = min(chunk, B - b0)
         kp = K * p
         nU = (h + 15) // 16  # hidden-unit chunks of the forward kernel (FAC_UC)
-        ws_floats = kp * nb * h + nU * nb * kp + kp * p * L + kp * p + kp * h
+        ws_floats = kp * nb * h + nU * nb * kp + kp * p * L + kp * p + kp * h + nU * kp * p * L
         ws = torch.empty(ws_floats, device=Xwin.device, dtype=torch.float32)
         dims = factor_dims(K, p, L, h, Bmax=nb)
         xw = Xwin[b0:b0 + nb].contiguous()
