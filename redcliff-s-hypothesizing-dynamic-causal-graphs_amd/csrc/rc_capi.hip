@@ -94,7 +94,7 @@ size_t redcliff_fac_param_count(const RedcliffDims* d) { return d ? (size_t)rc_f
 int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out) {
   if (check_dims(d) != 0) return REDCLIFF_EINVAL;
   const WsOff o = rc_ws_off(*d);
-  const int64_t v[] = {o.T, o.R, o.f1, o.w, o.a, o.y, o.G, o.G0, o.w1, o.gq, o.dwp, o.dAadj, o.dWi, o.dS, o.dgb, o.S, o.dZ,
+  const int64_t v[] = {o.T, o.R, o.f1, o.w, o.a, o.y, o.G, o.G0, o.w1, o.gq, o.ebp, o.ecnt, o.gfc1, o.dwp, o.dAadj, o.dWi, o.dS, o.dgb, o.S, o.dZ,
                        o.amat, o.lossp, o.xsim, o.gfc, o.total};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_out && i < nv; ++i) out[i] = v[i];

@@ -5,6 +5,7 @@
 #include "redcliff_hip.h"
 
 #define RC_BLOCK 256
+#define RC_TRACE_FLOATS 4096  // trace builds: u64 phase-timing slots at the end of the workspace
 #define RC_LDS_LIMIT_FLOATS 16384  // 64 KiB of dynamic LDS per workgroup
 
 // Offsets (in floats) inside one replica's packed embedder parameters.
@@ -27,6 +28,9 @@ struct WsOff {
   int64_t G0;     // [K][p][p]         lag-free group norms of W0
   int64_t w1;     // [K][p][h]         pre-update snapshot of the factor output weights
   int64_t gq;     // [nU][K][p][p*L]   squared layer-0 group norms, partial over hidden chunks
+  int64_t ebp;    // [p*nch][nbw][pst] embedder-backward partials per (node, chunk, window block)
+  int64_t ecnt;   // [p*nch]           arrival counters of those blocks (u32, self-resetting)
+  int64_t gfc1;   // [M1][p*H]         fc1 weight gradient (combined by the node blocks)
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
   int64_t dWi;    // [p][n][F][H]      graph-conv weight gradient partials (per node)
@@ -78,6 +82,23 @@ __host__ __device__ inline int rc_nchunk(const RedcliffDims& d) { return (d.H + 
 #define FAC_UC 16
 __host__ __device__ inline int rc_nuchunk(const RedcliffDims& d) { return (d.h + FAC_UC - 1) / FAC_UC; }
 
+// Embedder backward node blocks: BC windows each (16, fewer if the LDS tiles do not fit).
+__host__ __device__ inline int rc_emb_node_floats(const RedcliffDims& d, int BC) {
+  const int nF = d.n * d.F;
+  return 4 * BC * d.K + d.K * d.M1 + d.M1 * EMB_HC + nF * (EMB_HC + 1) + d.n * d.p + 8 + 4 * d.F + RC_BLOCK +
+         BC * (2 * d.M1 + 2 * EMB_HC + 2 * nF + d.p * d.F);
+}
+__host__ __device__ inline int rc_emb_bc(const RedcliffDims& d) {
+  int BC = 16;
+  while (BC > 1 && rc_emb_node_floats(d, BC) > RC_LDS_LIMIT_FLOATS) BC >>= 1;
+  return BC;
+}
+__host__ __device__ inline int rc_emb_nbw(const RedcliffDims& d) { return (d.Bmax + rc_emb_bc(d) - 1) / rc_emb_bc(d); }
+// floats per partial record: fc1 chunk | W_i chunk | dS rows i >= 1 | dgamma | dbeta | fc2W fc2b fc1b (group 0)
+__host__ __device__ inline int rc_emb_pstride(const RedcliffDims& d) {
+  return d.M1 * EMB_HC + d.n * d.F * EMB_HC + (d.n - 1) * d.p + 2 * d.F + d.K * d.M1 + d.K + d.M1;
+}
+
 inline int64_t rc_align64(int64_t x) { return (x + 63) & ~(int64_t)63; }
 
 inline WsOff rc_ws_off(const RedcliffDims& d) {
@@ -94,6 +115,9 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.G0 = x; x = rc_align64(x + K * p * p);
   o.w1 = x; x = rc_align64(x + K * p * d.h);
   o.gq = x; x = rc_align64(x + (int64_t)rc_nuchunk(d) * K * p * p * d.L);
+  o.ebp = x; x = rc_align64(x + (int64_t)p * rc_nchunk(d) * rc_emb_nbw(d) * rc_emb_pstride(d));
+  o.ecnt = x; x = rc_align64(x + p * rc_nchunk(d));
+  o.gfc1 = x; x = rc_align64(x + (int64_t)d.M1 * p * d.H);
   o.dwp = x; x = rc_align64(x + p * B * K);
   o.dAadj = x; x = rc_align64(x + K * p * p);
   o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);
@@ -105,6 +129,9 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.lossp = x; x = rc_align64(x + p + K * p + 8);
   o.xsim = x; x = rc_align64(x + B * p);
   o.gfc = x; x = rc_align64(x + K * d.M1 + K + d.M1);
+#ifdef RC_TRACE
+  x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
+#endif
   o.total = x;
   return o;
 }
@@ -145,11 +172,95 @@ struct StepCtx {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Phase timing (trace builds, -DRC_TRACE): thread 0 of a workgroup stores wall_clock64()
+// (100 MHz) into u64 slot `slot` of the trace area at the end of the replica's workspace.
+#ifdef RC_TRACE
+#define RC_MARK(wsbase, total, slot)                                                              \
+  do {                                                                                            \
+    if (threadIdx.x == 0)                                                                         \
+      reinterpret_cast<unsigned long long*>((wsbase) + (total) - RC_TRACE_FLOATS)[slot] = wall_clock64(); \
+  } while (0)
+#else
+#define RC_MARK(wsbase, total, slot) \
+  do {                               \
+  } while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------------
 // device helpers
 __device__ inline float rc_wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// Division by a block-uniform runtime divisor without the ~40-instruction integer divide:
+// q = (n * ceil(2^40 / d)) >> 40, exact for 0 <= n < 2^24 (error term n / 2^40 < 1 / d).
+struct RcDiv {
+  unsigned long long m;
+  int d;
+  __device__ inline explicit RcDiv(int dd) : m(dd > 1 ? ((1ull << 40) + (unsigned long long)dd - 1) / (unsigned)dd : 0ull), d(dd) {}
+  __device__ inline int div(int n) const {
+    return d == 1 ? n : (int)(((unsigned long long)(unsigned)n * m) >> 40);
+  }
+  __device__ inline int mod(int n) const { return n - div(n) * d; }
+};
+
+// Global -> LDS staging with U independent loads in flight per thread: the loads of U
+// elements are issued before any of them is consumed, so a staging loop costs ~N/(U*256)
+// memory latencies instead of N/256.  ld(e) returns element e, st(e, v) consumes it.
+template <int U, class Ld, class St>
+__device__ inline void rc_stage(int N, Ld ld, St st) {
+  for (int base = threadIdx.x; base < N; base += U * RC_BLOCK) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * RC_BLOCK;
+      v[u] = e < N ? ld(e) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = base + u * RC_BLOCK;
+      if (e < N) st(e, v[u]);
+    }
+  }
+}
+
+// Several staging segments with all their loads in flight together: round r issues the
+// loads of elements [r*U*256, (r+1)*U*256) of EVERY segment, then stores them.  A segment
+// is rc_seg<U>(N, ld, st); U is its loads per thread per round.
+template <int U, class Ld, class St>
+struct RcSeg {
+  int N;
+  Ld ld;
+  St st;
+  float v[U];
+  __device__ inline bool active(int r) const { return r * U * RC_BLOCK < N; }
+  __device__ inline void load(int r) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = r * U * RC_BLOCK + u * RC_BLOCK + (int)threadIdx.x;
+      v[u] = e < N ? ld(e) : 0.f;
+    }
+  }
+  __device__ inline void store(int r) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = r * U * RC_BLOCK + u * RC_BLOCK + (int)threadIdx.x;
+      if (e < N) st(e, v[u]);
+    }
+  }
+};
+template <int U, class Ld, class St>
+__device__ inline RcSeg<U, Ld, St> rc_seg(int N, Ld ld, St st) {
+  return RcSeg<U, Ld, St>{N, ld, st, {}};
+}
+template <class... S>
+__device__ inline void rc_stage_all(S&&... s) {
+  for (int r = 0; (s.active(r) || ...); ++r) {
+    (s.load(r), ...);
+    (s.store(r), ...);
+  }
 }
 
 // Block-wide sum; every thread gets the result.  `red` must hold >= RC_BLOCK/64 floats.

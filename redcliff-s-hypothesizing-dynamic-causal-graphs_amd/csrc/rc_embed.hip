@@ -53,6 +53,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_l
   if (nb <= 0) return;
   const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
   const int pF = p * F, pH = p * H, nFH = n * F * H;
+  const RcDiv dF(F), dp(p), dpF(pF), dnpF(n * pF), dpH(pH), dH(H);
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -69,6 +70,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_l
   float* beta = alpha + F;
 
   bn_affine(c, r, E, alpha, beta, nullptr, nullptr);
+  if (blockIdx.x == 0) {  // arrival counters of the embedder backward (they also self-reset)
+    unsigned* cnt = reinterpret_cast<unsigned*>(ws + c.wo.ecnt);
+    for (int e = tid; e < p * rc_nchunk(d); e += RC_BLOCK) cnt[e] = 0u;
+  }
   const float* S = ws + c.wo.S;
   for (int e = tid; e < n * p * p; e += RC_BLOCK) Sl[e] = S[e];
   const float* gw = E + c.eo.gcW;
@@ -78,14 +83,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_l
   __syncthreads();
   // window rows are contiguous in the channel index: read (s, f, ch), store x_bn[s][ch][f]
   for (int e = tid; e < nb * pF; e += RC_BLOCK) {
-    const int s = e / pF, rem = e - s * pF, f = rem / p, ch = rem - f * p;
+    const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), ch = rem - f * p;
     const float x = X[(c.row0 + b0 + s) * d.T * p + (int64_t)(c.Lmax - F + f) * p + ch];
     xs[s * pF + ch * F + f] = x * alpha[f] + beta[f];
   }
   __syncthreads();
   // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x))
   for (int e = tid; e < nb * n * pF; e += RC_BLOCK) {
-    const int s = e / (n * pF), rem = e - s * n * pF, i = rem / pF, q = rem - i * pF, ch = q / F, f = q - ch * F;
+    const int s = dnpF.div(e), rem = e - s * n * pF, i = dpF.div(rem), q = rem - i * pF, ch = dF.div(q), f = q - ch * F;
     float v;
     if (i == 0) {
       v = xs[s * pF + q];
@@ -101,7 +106,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_l
   __syncthreads();
   // Z = sum_i T_i W_i ; R = relu(Z)
   for (int e = tid; e < nb * pH; e += RC_BLOCK) {
-    const int s = e / pH, rem = e - s * pH, ch = rem / H, hh = rem - ch * H;
+    const int s = dpH.div(e), rem = e - s * pH, ch = dH.div(rem), hh = rem - ch * H;
     float acc = 0.f;
     for (int i = 0; i < n; ++i) {
       const float* trow = Tl + (s * n + i) * pF + ch * F;
@@ -158,109 +163,49 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_l
   }
 }
 
-// dL/d(raw embedder output) for every window of the batch, into LDS dr[B][K].
-// Sums the factor-side gradient (per-channel partials from the factor kernel) with the
-// supervised-score MSE and factor-weight L1 terms, through the optional sigmoid.
-__device__ void build_draw(const StepCtx& c, int r, float* dr) {
+// dL/d(raw embedder output) of one window / factor: the factor-side gradient gw (sum of
+// the per-channel partials written by the factor kernel) plus the supervised-score MSE and
+// factor-weight L1 terms, through the optional sigmoid (compute_loss, :633-666).
+__device__ inline float draw_value(const StepCtx& c, int r, int k, float raw, float gw, float y) {
   const RedcliffDims& d = c.d;
-  const int K = d.K, B = c.B, nsup = d.nsup;
-  const float* ws = c.ws + r * c.wss;
+  const int K = d.K, nsup = d.nsup;
   const RedcliffReplicaHyper& hy = c.hyp[r];
-  const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const int ncol = nsup > 0 ? nsup : K;  // columns of factor_scores[0] (state_label_preds)
-  for (int e = threadIdx.x; e < B * K; e += blockDim.x) {
-    const int b = e / K, k = e - b * K;
-    const float raw = ws[c.wo.w + (int64_t)b * K + k];
-    const float weff = sig ? rc_sigmoid(ecc * raw) : raw;
-    float gw = 0.f;
-    if (fac_grad)
-      for (int j = 0; j < d.p; ++j) gw += ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k];
-    float graw = sig ? gw * ecc * weff * (1.f - weff) : gw;
-    if (k < ncol) {
-      // score used by the factor MSE and the L1: class logits when supervised, else w
-      const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
-      float gsl = 0.f;
-      if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) {
-        const float y = c.lab[r * c.labr + (c.row0 + b) * K + k];
-        gsl += hy.c_factor * (2.f / (float)(B * nsup)) * (sl - y);
-      }
-      if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
-      if (nsup > 0)
-        graw += sig ? gsl * sl * (1.f - sl) : gsl;
-      else
-        graw += sig ? gsl * ecc * weff * (1.f - weff) : gsl;
-    }
-    dr[e] = graw;
+  const float weff = sig ? rc_sigmoid(ecc * raw) : raw;
+  float graw = sig ? gw * ecc * weff * (1.f - weff) : gw;
+  if (k < ncol) {
+    // score used by the factor MSE and the L1: class logits when supervised, else w
+    const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
+    float gsl = 0.f;
+    if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) gsl += hy.c_factor * (2.f / (float)(c.B * nsup)) * (sl - y);
+    if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
+    if (nsup > 0)
+      graw += sig ? gsl * sl * (1.f - sl) : gsl;
+    else
+      graw += sig ? gsl * ecc * weff * (1.f - weff) : gsl;
   }
+  return graw;
 }
 
 // ------------------------------------------------------------------------------------------
-// K3 head: fc2 / fc1-bias gradients, loss values, confusion matrix.  (blockIdx.x == p)
+// K3 head workgroup (launched only for loss values / the confusion matrix): the
+// coefficient-normalised loss terms of validate_training and the factor-score confusion.
 __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
   const RedcliffDims& d = c.d;
-  const int K = d.K, M1 = d.M1, B = c.B, p = d.p, nsup = d.nsup;
+  const int K = d.K, B = c.B, p = d.p, nsup = d.nsup;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const int tid = threadIdx.x;
-  float* dr = sm;
-  float* red = dr + ((d.Bmax * K + 1) & ~1);  // even offset: doubles follow
-  if (c.flags & RC_STEP_A) {
-    // dfc2W[k][m] = sum_b dr[b][k] relu(f1[b][m]); dfc2b[k] = sum_b dr[b][k];
-    // dfc1b[m] = sum_b [f1[b][m] > 0] sum_k dr[b][k] fc2W[k][m]      (f1 staged BCH rows at a time)
-    build_draw(c, r, dr);
-    float* fc2s = red + 64;                  // [K][M1]
-    float* f1c = fc2s + K * M1;              // [BCH][M1]
-    const int BCH = 64;
-    for (int e = tid; e < K * M1; e += RC_BLOCK) fc2s[e] = E[c.eo.fc2W + e];
-    const float* f1 = ws + c.wo.f1;
-    float* gfc = ws + c.wo.gfc;
-    const int nout = K * M1 + K + M1;
-    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // nout <= 16*64 + 16 + 64 < 5*256
-    for (int bc = 0; bc < B; bc += BCH) {
-      const int nbc = min(BCH, B - bc);
-      __syncthreads();
-      for (int e = tid; e < nbc * M1; e += RC_BLOCK) f1c[e] = f1[(int64_t)bc * M1 + e];
-      __syncthreads();
-#pragma unroll
-      for (int kk = 0; kk < 5; ++kk) {
-        const int e = tid + kk * RC_BLOCK;
-        if (e >= nout) continue;
-        float g = acc[kk];
-        if (e < K * M1) {
-          const int k = e / M1, m = e - k * M1;
-          for (int s = 0; s < nbc; ++s) g += dr[(bc + s) * K + k] * fmaxf(f1c[s * M1 + m], 0.f);
-        } else if (e < K * M1 + K) {
-          const int k = e - K * M1;
-          for (int s = 0; s < nbc; ++s) g += dr[(bc + s) * K + k];
-        } else {
-          const int m = e - K * M1 - K;
-          for (int s = 0; s < nbc; ++s) {
-            if (f1c[s * M1 + m] > 0.f) {
-              float t = 0.f;
-              for (int k = 0; k < K; ++k) t += dr[(bc + s) * K + k] * fc2s[k * M1 + m];
-              g += t;
-            }
-          }
-        }
-        acc[kk] = g;
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const int e = tid + kk * RC_BLOCK;
-      if (e < nout) gfc[e] = acc[kk];
-    }
-  }
-  if (!(c.flags & (RC_VALUES | RC_CONFUSION))) return;
-  __syncthreads();
+  float* red = sm;                                        // [8]
+  double* dred = reinterpret_cast<double*>(sm + 8);       // [8]
+  int* hist = reinterpret_cast<int*>(sm + 32);            // [nsup][nsup]
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const float* wraw = ws + c.wo.w;
   const int ncol = nsup > 0 ? nsup : K;
-  double* dred = reinterpret_cast<double*>(red + 8);
   if (c.flags & RC_VALUES) {
     // supervised MSE and factor-weight L1 (values)
     double fsum = 0.0, l1 = 0.0;
@@ -328,10 +273,12 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
       acc[ACC_BATCHES] += 1.0;
     }
   }
-  if ((c.flags & RC_CONFUSION) && nsup > 0 && tid == 0) {
-    // np.argmax (first maximum) of state_label_preds[0] and of the labels (:801-803)
-    int* conf = c.conf + (int64_t)r * nsup * nsup;
-    for (int b = 0; b < B; ++b) {
+  if ((c.flags & RC_CONFUSION) && nsup > 0) {
+    // np.argmax (first maximum) of state_label_preds[0] and of the labels (:801-803);
+    // integer counts, so the LDS atomics are order-independent
+    for (int e = tid; e < nsup * nsup; e += RC_BLOCK) hist[e] = 0;
+    __syncthreads();
+    for (int b = tid; b < B; b += RC_BLOCK) {
       int pred = 0, lab = 0;
       float best = 0.f, bestl = 0.f;
       for (int k = 0; k < nsup; ++k) {
@@ -341,178 +288,271 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
         if (k == 0 || sl > best) { best = sl; pred = k; }
         if (k == 0 || y > bestl) { bestl = y; lab = k; }
       }
-      conf[lab * nsup + pred] += 1;
+      atomicAdd(&hist[lab * nsup + pred], 1);
     }
+    __syncthreads();
+    int* conf = c.conf + (int64_t)r * nsup * nsup;
+    for (int e = tid; e < nsup * nsup; e += RC_BLOCK) conf[e] += hist[e];
   }
 }
 
-// K3 node/column-chunk workgroup (node c, hidden columns [h0, h0+HC)): fc1 columns of the
-// chunk (gradient + Adam), graph-conv output gradient dZ, partials of dW_i (over c),
-// dS_i[c][:] and the BatchNorm affine gradients (over c and chunk).  Everything the
-// chunk touches is staged in LDS, BC windows at a time.
-__device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, float* sm) {
+// K3 node workgroup (node c, hidden columns [h0, h0+HC), windows [wb*BC, wb*BC+nbc)):
+// dL/dw_raw of its windows, dL/dfc1 of the chunk's columns, graph-conv output gradient dZ,
+// and partial sums over its windows of dfc1W, dW_i, dS_i[c][:], the BatchNorm affine
+// gradients and (node 0, chunk 0) the fc2 / fc1-bias gradients.  The partials of the nbw
+// window blocks of one (node, chunk) are combined in fixed order by the block that arrives
+// last (agent-scope release / ticket / acquire, cdna_hip_programming.md §6 Guideline 16).
+// All inputs of a block are staged into LDS by one multi-segment pass (one memory latency
+// for everything instead of one per array).
+__device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, float* sm) {
   const RedcliffDims& d = c.d;
   const int K = d.K, M1 = d.M1, B = c.B, p = d.p, H = d.H, F = d.F, n = d.n;
-  const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC;
+  const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC, HP = EMB_HC + 1;
   const int h0 = ch * HC, hc = min(HC, H - h0);
   const int nch = rc_nchunk(d);
+  const int nbw = (B + BC - 1) / BC, nbw_max = rc_emb_nbw(d);
+  const int bw0 = wb * BC, nbc = min(BC, B - bw0);
+  const int grp = node * nch + ch;
+  const bool head_grads = (grp == 0);  // fc2 / fc1-bias partials ride on group 0
   float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
   const int tid = threadIdx.x;
 
-  float* dr = sm;                        // [Bmax][K]
-  float* fc2s = dr + d.Bmax * K;         // [K][M1]
+  float* dr = sm;                        // [BC][K]
+  float* wrl = dr + BC * K;              // [BC][K]   raw embedder output
+  float* labl = wrl + BC * K;            // [BC][K]   labels
+  float* dwl = labl + BC * K;            // [BC][K]   factor-side dL/dw (sum over channels)
+  float* fc2s = dwl + BC * K;            // [K][M1]
   float* FW = fc2s + K * M1;             // [M1][HC]  fc1 columns of the chunk
-  float* WiC = FW + M1 * HC;             // [n][F][HC]
-  float* Srow = WiC + nF * HC;           // [n][p]    row `node` of each support
-  float* rs = Srow + n * p;              // [n]       row sums
-  float* alpha = rs + 4;                 // [F]
+  float* WiC = FW + M1 * HC;             // [n][F][HC+1]
+  float* Srow = WiC + nF * HP;           // [n][p]    row `node` of each support
+  float* rs = Srow + n * p;              // [4]       row sums
+  int* tk = reinterpret_cast<int*>(rs + 4);  // [4]   arrival ticket broadcast
+  float* alpha = rs + 8;                 // [F]
   float* beta = alpha + F;               // [F]
   float* mean = beta + F;                // [F]
   float* inv = mean + F;                 // [F]
   float* red = inv + F;                  // [RC_BLOCK]
-  float* df1c = red + RC_BLOCK;          // [BC][M1]
+  float* f1r = red + RC_BLOCK;           // [BC][M1]  fc1 pre-activations
+  float* df1c = f1r + BC * M1;           // [BC][M1]
   float* Rc = df1c + BC * M1;            // [BC][HC]
   float* dZc = Rc + BC * HC;             // [BC][HC]
   float* Tc = dZc + BC * HC;             // [BC][n][F]   T_i row `node`
   float* dTc = Tc + BC * nF;             // [BC][n][F]
   float* xc = dTc + BC * nF;             // [BC][p][F]   raw window
 
-  build_draw(c, r, dr);
+  const RcDiv dF(F), dp(p), dpF(pF), dnF(nF), dK(K), dM1(M1);
+  const bool trace = (blockIdx.x == 0 && r == 0);
+#define NMARK(i) if (trace) RC_MARK(ws, c.wo.total, 256 + (i))
+  NMARK(0);
+  if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 600 + 2 * blockIdx.x);
   bn_affine(c, r, E, alpha, beta, mean, inv);
-  for (int e = tid; e < K * M1; e += RC_BLOCK) fc2s[e] = E[c.eo.fc2W + e];
-  for (int e = tid; e < M1 * HC; e += RC_BLOCK) {
-    const int m = e / HC, hh = e - m * HC;
-    FW[e] = hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;
-  }
-  for (int e = tid; e < nF * HC; e += RC_BLOCK) {
-    const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
-    WiC[e] = hh < hc ? E[c.eo.gcW + ((int64_t)i * F + f) * H + h0 + hh] : 0.f;
-  }
+  // ---- one staging pass over 11 segments, all loads of a round in flight together
+  const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
+  const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
+  const float* f1 = ws + c.wo.f1;
+  const float* Rg = ws + c.wo.R;
+  const float* Tg = ws + c.wo.T;
   const float* S = ws + c.wo.S;
-  for (int e = tid; e < n * p; e += RC_BLOCK) {
-    const int i = e / p, cc = e - i * p;
-    Srow[e] = S[((int64_t)i * p + node) * p + cc];
-  }
+  const float* wraw = ws + c.wo.w;
+  const float* dwp = ws + c.wo.dwp;
+  rc_stage_all(
+      rc_seg<1>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
+      rc_seg<4>(M1 * HC, [&](int e) {
+        const int m = e / HC, hh = e - m * HC;
+        return hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;
+      }, [&](int e, float v) { FW[e] = v; }),
+      rc_seg<4>(nF * HC, [&](int e) {
+        const int eh = e >> 4, i = dF.div(eh), f = eh - i * F, hh = e & 15;  // HC == 16
+        return hh < hc ? E[c.eo.gcW + ((int64_t)i * F + f) * H + h0 + hh] : 0.f;
+      }, [&](int e, float v) { WiC[(e / HC) * HP + e % HC] = v; }),
+      rc_seg<1>(n * p, [&](int e) {
+        const int i = dp.div(e), cc = e - i * p;
+        return S[((int64_t)i * p + node) * p + cc];
+      }, [&](int e, float v) { Srow[e] = v; }),
+      rc_seg<1>(nbc * HC, [&](int e) {
+        const int s = e / HC, hh = e - s * HC;
+        return hh < hc ? Rg[(int64_t)(bw0 + s) * pH + node * H + h0 + hh] : 0.f;
+      }, [&](int e, float v) { Rc[e] = v; }),
+      rc_seg<4>(nbc * nF, [&](int e) {
+        const int s = dnF.div(e), rem = e - s * nF, i = dF.div(rem), f = rem - i * F;
+        return Tg[(int64_t)(bw0 + s) * n * pF + i * pF + node * F + f];
+      }, [&](int e, float v) { Tc[e] = v; }),
+      rc_seg<16>(nbc * pF, [&](int e) {
+        const int s = dpF.div(e), rem = e - s * pF;  // rem = f * p + cc (contiguous in the window row)
+        return X[(c.row0 + bw0 + s) * d.T * p + (int64_t)(c.Lmax - F) * p + rem];
+      }, [&](int e, float v) {
+        const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), cc = rem - f * p;
+        xc[s * pF + cc * F + f] = v;
+      }),
+      rc_seg<4>(nbc * M1, [&](int e) { return f1[(int64_t)bw0 * M1 + e]; }, [&](int e, float v) { f1r[e] = v; }),
+      rc_seg<1>(nbc * K, [&](int e) { return wraw[(int64_t)bw0 * K + e]; }, [&](int e, float v) { wrl[e] = v; }),
+      rc_seg<1>(nbc * K, [&](int e) { return lab_on ? c.lab[r * c.labr + (c.row0 + bw0) * K + e] : 0.f; },
+                [&](int e, float v) { labl[e] = v; }),
+      rc_seg<1>(nbc * K, [&](int e) {
+        const int s = dK.div(e), k = e - s * K;
+        float g = 0.f;
+        if (fac_grad) {
+#pragma unroll 4
+          for (int j = 0; j < p; ++j) g += dwp[((int64_t)j * d.Bmax + bw0 + s) * K + k];
+        }
+        return g;
+      }, [&](int e, float v) { dwl[e] = v; }));
   __syncthreads();
   if (tid < n) {
     float t = 0.f;
     for (int cc = 0; cc < p; ++cc) t += Srow[tid * p + cc];
     rs[tid] = t;
   }
-  // accumulators: dfc1W chunk (M1*HC <= 1024 -> 4 / thread), dW_i chunk (n*F*HC <= 4096 -> 16 / thread)
+  for (int e = tid; e < nbc * K; e += RC_BLOCK) dr[e] = draw_value(c, r, dK.mod(e), wrl[e], dwl[e], labl[e]);
+  __syncthreads();
+  // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
+  for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
+    const int s = dM1.div(e), m = e - s * M1;
+    float g = 0.f;
+    if (f1r[e] > 0.f)
+      for (int k = 0; k < K; ++k) g += dr[s * K + k] * fc2s[k * M1 + m];
+    df1c[e] = g;
+  }
+  __syncthreads();
+  NMARK(1);
+  // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
+  for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
+    const int s = e / HC, hh = e - s * HC;
+    const float* dfr = df1c + s * M1;
+    float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
+    int m = 0;
+    for (; m + 3 < M1; m += 4) {
+      g0 += dfr[m] * FW[m * HC + hh];
+      g1 += dfr[m + 1] * FW[(m + 1) * HC + hh];
+      g2 += dfr[m + 2] * FW[(m + 2) * HC + hh];
+      g3 += dfr[m + 3] * FW[(m + 3) * HC + hh];
+    }
+    for (; m < M1; ++m) g0 += dfr[m] * FW[m * HC + hh];
+    const float g = (g0 + g1) + (g2 + g3);
+    dZc[e] = Rc[e] > 0.f ? g : 0.f;
+  }
+  // dfc1W chunk partial: afc[m][hh] = sum_s df1[s][m] R[s][hh]   (M1*HC <= 1024 -> 4 / thread)
   float afc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < nbc; ++s) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (e < M1 * HC) afc[k] += df1c[s * M1 + e / HC] * Rc[s * HC + e % HC];
+    }
+  }
+  // group 0: dfc2W[k][m] = sum_s dr[s][k] relu(f1[s][m]); dfc2b[k] = sum_s dr[s][k]; dfc1b[m] = sum_s df1[s][m]
+  const int nout = K * M1 + K + M1;  // <= 16*64 + 16 + 64 < 5*256
+  float agf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  if (head_grads) {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (e >= nout) continue;
+      float g = 0.f;
+      if (e < K * M1) {
+        const int k = dM1.div(e), m = e - k * M1;
+        for (int s = 0; s < nbc; ++s) g += dr[s * K + k] * fmaxf(f1r[s * M1 + m], 0.f);
+      } else if (e < K * M1 + K) {
+        const int k = e - K * M1;
+        for (int s = 0; s < nbc; ++s) g += dr[s * K + k];
+      } else {
+        const int m = e - K * M1 - K;
+        for (int s = 0; s < nbc; ++s) g += df1c[s * M1 + m];
+      }
+      agf[kk] = g;
+    }
+  }
+  __syncthreads();
+  NMARK(2);
+  // dW_i chunk partial: awi[i][f][hh] = sum_s T_i[s][f] dZ[s][hh]   (n*F*HC <= 4096 -> 16 / thread)
   float awi[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) awi[k] = 0.f;
-  // dS_i[node][c'] (i >= 1) and BN partials, reduced at the end through LDS
+  const int nwi = (nF * HC + RC_BLOCK - 1) / RC_BLOCK;
+  for (int s = 0; s < nbc; ++s) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (k < nwi && e < nF * HC) awi[k] += Tc[s * nF + e / HC] * dZc[s * HC + e % HC];
+    }
+  }
+  // dT_i[s][f] = sum_hh dZ[s][hh] W_i[f][hh]
+  for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
+    const int s = dnF.div(e), rem = e - s * nF;
+    const float* wr = WiC + rem * HP;
+    const float* dz = dZc + s * HC;
+    float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < HC; hh += 2) {
+      t0 += dz[hh] * wr[hh];
+      t1 += dz[hh + 1] * wr[hh + 1];
+    }
+    dTc[e] = t0 + t1;
+  }
+  __syncthreads();
+  NMARK(3);
+  // dS_i[node][c'] (i >= 1) and BatchNorm affine partials, windows split over thread slices
   const int nS = (n - 1) * p;
   const int nslS = nS > 0 ? RC_BLOCK / nS : 0, oS = nS > 0 ? tid % nS : 0, slS = nS > 0 ? tid / nS : 1;
   const int nslF = RC_BLOCK / F, oF = tid % F, slF = tid / F;
   float aS = 0.f, aG = 0.f, aB = 0.f;
-  const float* f1 = ws + c.wo.f1;
-  const float* Rg = ws + c.wo.R;
-  const float* Tg = ws + c.wo.T;
-  for (int bc = 0; bc < B; bc += BC) {
-    const int nbc = min(BC, B - bc);
-    for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
-      const int s = e / M1, m = e - s * M1, b = bc + s;
-      float g = 0.f;
-      if (f1[(int64_t)b * M1 + m] > 0.f)
-        for (int k = 0; k < K; ++k) g += dr[b * K + k] * fc2s[k * M1 + m];
-      df1c[e] = g;
+  if (slS < nslS) {
+    const int i = 1 + oS / p, cp = oS - (i - 1) * p;
+    for (int s = slS; s < nbc; s += nslS) {
+      const float* dt = dTc + s * nF + i * F;
+      const float* xr = xc + s * pF + cp * F;
+      for (int f = 0; f < F; ++f) aS += dt[f] * (xr[f] * alpha[f] + beta[f]);
     }
-    for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
-      const int s = e / HC, hh = e - s * HC;
-      Rc[e] = hh < hc ? Rg[(int64_t)(bc + s) * pH + node * H + h0 + hh] : 0.f;
-    }
-    for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
-      const int s = e / nF, rem = e - s * nF, i = rem / F, f = rem - i * F;
-      Tc[e] = Tg[(int64_t)(bc + s) * n * pF + i * pF + node * F + f];
-    }
-    for (int e = tid; e < nbc * pF; e += RC_BLOCK) {
-      const int s = e / pF, rem = e - s * pF, f = rem / p, cc = rem - f * p;
-      xc[s * pF + cc * F + f] = X[(c.row0 + bc + s) * d.T * p + (int64_t)(c.Lmax - F + f) * p + cc];
-    }
-    __syncthreads();
-    for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
-      const int s = e / HC, hh = e - s * HC;
-      float g = 0.f;
-      for (int m = 0; m < M1; ++m) g += df1c[s * M1 + m] * FW[m * HC + hh];
-      dZc[e] = Rc[e] > 0.f ? g : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = tid + k * RC_BLOCK;
-      if (e < M1 * HC) {
-        const int m = e / HC, hh = e - m * HC;
-        float a = afc[k];
-        for (int s = 0; s < nbc; ++s) a += df1c[s * M1 + m] * Rc[s * HC + hh];
-        afc[k] = a;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tid + k * RC_BLOCK;
-      if (e < nF * HC) {
-        const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
-        float a = awi[k];
-        for (int s = 0; s < nbc; ++s) a += Tc[s * nF + i * F + f] * dZc[s * HC + hh];
-        awi[k] = a;
-      }
-    }
-    for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
-      const int s = e / nF, rem = e - s * nF;
-      const float* wr = WiC + rem * HC;
-      const float* dz = dZc + s * HC;
-      float t = 0.f;
-      for (int hh = 0; hh < HC; ++hh) t += dz[hh] * wr[hh];
-      dTc[e] = t;
-    }
-    __syncthreads();
-    // dS_i[node][c'] (i >= 1): output oS, windows split over nslS thread slices
-    if (slS < nslS) {
-      const int i = 1 + oS / p, cp = oS - (i - 1) * p;
-      float t = 0.f;
-      for (int s = slS; s < nbc; s += nslS) {
-        const float* dt = dTc + s * nF + i * F;
-        const float* xr = xc + s * pF + cp * F;
-        for (int f = 0; f < F; ++f) t += dt[f] * (xr[f] * alpha[f] + beta[f]);
-      }
-      aS += t;
-    }
-    // BatchNorm affine gradients of feature oF, windows split over nslF thread slices
-    if (slF < nslF) {
-      const int f = oF;
-      const float mu = mean[f], iv = inv[f];
-      for (int s = slF; s < nbc; s += nslF) {
-        const float* xs_ = xc + s * pF + f;
-        for (int i = 0; i < n; ++i) {
-          float u;
-          if (i == 0) {
-            u = (xs_[node * F] - mu) * iv;
-          } else {
-            u = 0.f;
-            for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xs_[cc * F] - mu) * iv);
-          }
-          const float dt = dTc[s * nF + i * F + f];
-          aG += dt * u;
-          aB += dt * rs[i];
-        }
-      }
-    }
-    __syncthreads();
   }
-  // reduce the thread slices in fixed order
-  const int64_t part = (int64_t)node * nch + ch;
+  if (slF < nslF) {
+    const int f = oF;
+    const float mu = mean[f], iv = inv[f];
+    for (int s = slF; s < nbc; s += nslF) {
+      const float* xs_ = xc + s * pF + f;
+      for (int i = 0; i < n; ++i) {
+        float u;
+        if (i == 0) {
+          u = (xs_[node * F] - mu) * iv;
+        } else {
+          u = 0.f;
+          for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xs_[cc * F] - mu) * iv);
+        }
+        const float dt = dTc[s * nF + i * F + f];
+        aG += dt * u;
+        aB += dt * rs[i];
+      }
+    }
+  }
+  // ---- publish this block's partials:
+  //      [grp][wb][ afc M1*HC | awi nF*HC | dS nS | dgamma F | dbeta F | (group 0) dfc2W dfc2b dfc1b ]
+  const int pst = rc_emb_pstride(d);
+  const int ofs_w = M1 * HC, ofs_s = ofs_w + nF * HC, ofs_g = ofs_s + nS, ofs_h = ofs_g + 2 * F;
+  float* part = ws + c.wo.ebp + ((int64_t)grp * nbw_max + wb) * pst;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = tid + k * RC_BLOCK;
+    if (e < M1 * HC) part[e] = afc[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = tid + k * RC_BLOCK;
+    if (k < nwi && e < nF * HC) part[ofs_w + e] = awi[k];
+  }
+  if (head_grads) {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int e = tid + kk * RC_BLOCK;
+      if (e < nout) part[ofs_h + e] = agf[kk];
+    }
+  }
   red[tid] = (slS < nslS) ? aS : 0.f;
   __syncthreads();
   if (tid < nS) {
     float t = 0.f;
     for (int q = 0; q < nslS; ++q) t += red[q * nS + tid];
-    ws[c.wo.dS + part * n * p + p + tid] = t;  // layout [part][n][p], rows i >= 1
+    part[ofs_s + tid] = t;
   }
   __syncthreads();
   red[tid] = (slF < nslF) ? aG : 0.f;
@@ -520,7 +560,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, 
   if (tid < F) {
     float t = 0.f;
     for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
-    ws[c.wo.dgb + (part * 2 + 0) * F + tid] = t;
+    part[ofs_g + tid] = t;
   }
   __syncthreads();
   red[tid] = (slF < nslF) ? aB : 0.f;
@@ -528,48 +568,80 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int BC, 
   if (tid < F) {
     float t = 0.f;
     for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
-    ws[c.wo.dgb + (part * 2 + 1) * F + tid] = t;
+    part[ofs_g + F + tid] = t;
   }
-  // fc1 columns of this chunk: Adam (no other workgroup reads them in this kernel)
-  if (c.flags & RC_STEP_A) {
-    const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
-    float* P = E + c.eo.fc1W;
-    float* Mm = c.embM + r * c.es + c.eo.fc1W;
-    float* V = c.embV + r * c.es + c.eo.fc1W;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = tid + k * RC_BLOCK;
-      if (e < M1 * HC) {
-        const int m = e / HC, hh = e - m * HC;
-        if (hh < hc) {
-          const int64_t idx = (int64_t)m * pH + node * H + h0 + hh;
-          float pp = P[idx], mm = Mm[idx], vv = V[idx];
-          rc_adam(pp, mm, vv, afc[k], as);
-          P[idx] = pp; Mm[idx] = mm; V[idx] = vv;
-        }
-      }
-    }
+  NMARK(4);
+  // release (every wave drains its stores, one lane publishes at agent scope), then the ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws + c.wo.ecnt);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tk[0] = (int)__hip_atomic_fetch_add(&cnt[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  __syncthreads();
+  NMARK(7);
+  if (tk[0] != nbw - 1) {
+    if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 601 + 2 * blockIdx.x);
+    return;
+  }
+  // ---- last arriver: acquire, then combine the nbw partials in window-block order
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&cnt[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  NMARK(5);
+  const float* base = ws + c.wo.ebp + (int64_t)grp * nbw_max * pst;
   float* dWi = ws + c.wo.dWi + (int64_t)node * n * F * H;
+  float* gfc1 = ws + c.wo.gfc1;
+  const int64_t pout = (int64_t)node * nch + ch;
+  rc_stage<4>(head_grads ? pst : ofs_h, [&](int e) {
+    float t = 0.f;
+    for (int w0 = 0; w0 < nbw; w0 += 8) {
+      float v[8];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * RC_BLOCK;
-    if (e < nF * HC) {
-      const int i = e / (F * HC), rem = e - i * F * HC, f = rem / HC, hh = rem - f * HC;
-      if (hh < hc) dWi[((int64_t)i * F + f) * H + h0 + hh] = awi[k];
+      for (int q = 0; q < 8; ++q) v[q] = (w0 + q < nbw) ? base[(int64_t)(w0 + q) * pst + e] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (w0 + q < nbw) t += v[q];
     }
-  }
+    return t;
+  }, [&](int e, float t) {
+    if (e < ofs_w) {
+      const int m = e / HC, hh = e - m * HC;  // dfc1W columns of the chunk (Adam in k_emb_final)
+      if (hh < hc) gfc1[(int64_t)m * pH + node * H + h0 + hh] = t;
+    } else if (e < ofs_s) {
+      const int q = e - ofs_w, qh = q >> 4, i = dF.div(qh), f = qh - i * F, hh = q & 15;  // HC == 16
+      if (hh < hc) dWi[((int64_t)i * F + f) * H + h0 + hh] = t;
+    } else if (e < ofs_g) {
+      ws[c.wo.dS + pout * n * p + p + (e - ofs_s)] = t;  // layout [part][n][p], rows i >= 1
+    } else if (e < ofs_h) {
+      ws[c.wo.dgb + pout * 2 * F + (e - ofs_g)] = t;     // [part][2][F]: dgamma, dbeta
+    } else {
+      ws[c.wo.gfc + (e - ofs_h)] = t;                    // dfc2W | dfc2b | dfc1b
+    }
+  });
+  NMARK(6);
+  if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 601 + 2 * blockIdx.x);
+#undef NMARK
 }
 
-// grid (p * nchunk + 1, R): workgroups [0, p*nchunk) are node/column chunks, the last one is the head.
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int head_only, int BC) {
+// grid (p * nchunk * nbw [+ 1], R): workgroups [0, p*nchunk*nbw) are (node, column chunk,
+// window block) blocks; the optional last one is the head (loss values / confusion).
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int BC) {
   extern __shared__ float sm[];
   const int r = blockIdx.y;
   const int nch = rc_nchunk(c.d);
-  if (head_only || (int)blockIdx.x == c.d.p * nch)
+  const int nbw = (c.B + BC - 1) / BC;
+  if ((int)blockIdx.x == nnode) {
     emb_bwd_head(c, r, sm);
-  else
-    emb_bwd_node(c, r, blockIdx.x / nch, blockIdx.x % nch, BC, sm);
+  } else {
+    const int grp = blockIdx.x / nbw, wb = blockIdx.x - grp * nbw;
+    emb_bwd_node(c, r, grp / nch, grp % nch, wb, BC, sm);
+  }
 }
 
 // Supports of normalize_A(A) into S[n][p][p] (S_0 = I, S_1 = L, S_i = S_{i-1} L).
@@ -623,8 +695,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   float* ws = c.ws + r * c.wss;
   const bool stepA = c.flags & RC_STEP_A;
   const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
-  const int nFH = n * F * H, nfc = K * M1 + K + M1;
-  const int total = nFH + nfc + 2 * F;
+  const int nFH = n * F * H, nfc = K * M1 + K + M1, nf1 = M1 * p * H;
+  const int total = nFH + nfc + 2 * F + nf1;
   if ((int)blockIdx.x < nw) {
     if (!stepA) return;
     const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
@@ -632,6 +704,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     float g = 0.f;
     int64_t idx;
     if (e < nFH) {
+#pragma unroll 8
       for (int cc = 0; cc < p; ++cc) g += ws[c.wo.dWi + (int64_t)cc * nFH + e];
       idx = c.eo.gcW + e;
     } else if (e < nFH + nfc) {
@@ -640,12 +713,17 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       if (q < K * M1) idx = c.eo.fc2W + q;
       else if (q < K * M1 + K) idx = c.eo.fc2b + (q - K * M1);
       else idx = c.eo.fc1b + (q - K * M1 - K);
-    } else {
+    } else if (e < nFH + nfc + 2 * F) {
       const int q = e - nFH - nfc;
       const int which = q / F, f = q - which * F;  // 0: gamma, 1: beta
       const int nparts = p * rc_nchunk(d);
+#pragma unroll 8
       for (int pt = 0; pt < nparts; ++pt) g += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
       idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
+    } else {
+      const int q = e - nFH - nfc - 2 * F;  // fc1 weight (gradient combined by the node blocks)
+      g = ws[c.wo.gfc1 + q];
+      idx = c.eo.fc1W + q;
     }
     float pp = E[idx], mm = Mm[idx], vv = V[idx];
     rc_adam(pp, mm, vv, g, as);
@@ -793,7 +871,7 @@ int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
     const int x = v ? atoi(v) : 0;
     return (x >= 1 && x <= 4) ? x : 0;
   }();
-  int SB = sb_env ? sb_env : 2, w_lds = 1;
+  int SB = sb_env ? sb_env : 1, w_lds = 1;
   while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) --SB;
   if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) w_lds = 0;
   if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
@@ -803,21 +881,9 @@ int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
   return rc_check(hipGetLastError(), "k_emb_fwd");
 }
 
-static size_t emb_bwd_node_floats(const RedcliffDims& d, int BC) {
-  const size_t nF = (size_t)d.n * d.F;
-  return (size_t)d.Bmax * d.K + (size_t)d.K * d.M1 + (size_t)d.M1 * EMB_HC + nF * EMB_HC + (size_t)d.n * d.p + 4 +
-         4 * d.F + RC_BLOCK + (size_t)BC * (d.M1 + 2 * EMB_HC + 2 * nF + (size_t)d.p * d.F);
-}
-
-static int emb_bwd_bc(const RedcliffDims& d) {
-  int BC = 32;
-  while (BC > 1 && emb_bwd_node_floats(d, BC) > RC_LDS_LIMIT_FLOATS) BC >>= 1;
-  return BC;
-}
-
 size_t rc_emb_bwd_lds(const RedcliffDims& d) {
-  const size_t head = (size_t)d.Bmax * d.K + 2 + 64 + (size_t)d.K * d.M1 + 64 * (size_t)d.M1;
-  const size_t node = emb_bwd_node_floats(d, emb_bwd_bc(d));
+  const size_t head = 32 + (size_t)d.nsup * d.nsup;
+  const size_t node = rc_emb_node_floats(d, rc_emb_bc(d));
   return (head > node ? head : node) * sizeof(float);
 }
 
@@ -825,17 +891,17 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   const RedcliffDims& d = c.d;
   const size_t lds = rc_emb_bwd_lds(d);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  const int BC = emb_bwd_bc(d);
-  if (node_wgs)
-    hipLaunchKernelGGL(k_emb_bwd, dim3(d.p * rc_nchunk(d) + 1, d.R), dim3(RC_BLOCK), lds, s, c, 0, BC);
-  else
-    hipLaunchKernelGGL(k_emb_bwd, dim3(1, d.R), dim3(RC_BLOCK), lds, s, c, 1, BC);
+  const int BC = rc_emb_bc(d);
+  const int nnode = node_wgs ? d.p * rc_nchunk(d) * ((c.B + BC - 1) / BC) : 0;
+  const int head = (c.flags & (RC_VALUES | RC_CONFUSION)) ? 1 : 0;
+  if (nnode + head == 0) return 0;
+  hipLaunchKernelGGL(k_emb_bwd, dim3(nnode + head, d.R), dim3(RC_BLOCK), lds, s, c, nnode, BC);
   return rc_check(hipGetLastError(), "k_emb_bwd");
 }
 
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
-  const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F;
+  const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
   const int nw = (total + RC_BLOCK - 1) / RC_BLOCK;
   hipLaunchKernelGGL(k_emb_final, dim3(nw + 1, d.R), dim3(RC_BLOCK), 0, s, c, nw);
   return rc_check(hipGetLastError(), "k_emb_final");

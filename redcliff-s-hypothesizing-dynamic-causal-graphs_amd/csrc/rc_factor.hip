@@ -22,9 +22,9 @@ namespace {
 #define FB_BT 32    // batch rows per backward tile
 #define FB_QT 64    // dW0 columns per backward tile
 
-__device__ inline float xwin(const StepCtx& c, const float* X, int b, int q) {
+__device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
   const int L = c.d.L;
-  const int t = q % L, ch = q / L;
+  const int ch = dL.div(q), t = q - ch * L;
   return X[((c.row0 + b) * c.d.T + (c.Lmax - L + t)) * c.d.p + ch];
 }
 
@@ -50,6 +50,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd(StepCtx c) {
   const float* X = c.X + r * c.xr;
   const int tid = threadIdx.x, tb = tid >> 4, tu = tid & 15;
   const int u = u0 + tu;
+  const RcDiv dL(d.L);
 
   __shared__ float Xs[FK_BT * (FK_QT + 1)];
   __shared__ float Ws[FAC_UC * (FK_QT + 1)];
@@ -59,16 +60,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd(StepCtx c) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
     for (int q0 = 0; q0 < Q; q0 += FK_QT) {
-      for (int e = tid; e < FK_BT * FK_QT; e += RC_BLOCK) {
+      rc_stage<8>(FK_BT * FK_QT, [&](int e) {
         const int bb = e / FK_QT, qq = e - bb * FK_QT;
         const int b = bc + bb, q = q0 + qq;
-        Xs[bb * (FK_QT + 1) + qq] = (b < c.B && q < Q) ? xwin(c, X, b, q) : 0.f;
-      }
-      for (int e = tid; e < FAC_UC * FK_QT; e += RC_BLOCK) {
+        return (b < c.B && q < Q) ? xwin(c, dL, X, b, q) : 0.f;
+      }, [&](int e, float v) { Xs[(e / FK_QT) * (FK_QT + 1) + e % FK_QT] = v; });
+      rc_stage<2>(FAC_UC * FK_QT, [&](int e) {
         const int uu = e / FK_QT, qq = e - uu * FK_QT;
         const int q = q0 + qq;
-        Ws[uu * (FK_QT + 1) + qq] = (u0 + uu < h && q < Q) ? W0[(int64_t)(u0 + uu) * Q + q] : 0.f;
-      }
+        return (u0 + uu < h && q < Q) ? W0[(int64_t)(u0 + uu) * Q + q] : 0.f;
+      }, [&](int e, float v) { Ws[(e / FK_QT) * (FK_QT + 1) + e % FK_QT] = v; });
       __syncthreads();
       if (bc == 0 && tid < FK_QT && q0 + tid < Q) {
         // squared group norms of the chunk's 16 units (GC, models/cmlp.py:162-166), pre-update
@@ -132,6 +133,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const int tid = threadIdx.x;
   const int B = c.B;
+  const RcDiv dL(d.L), dK(K);
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const bool fgrad = (c.flags & RC_STEP_B) || (c.flags & RC_STEP_A);
@@ -147,23 +149,39 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   float* lwt = Acol + p;       // [L]
   float* red = lwt + L;        // [16]
   float* dAp = red + 16;       // [p*Ls]
-  float* tiles = dAp + p * c.Ls;
+  float* ybuf = dAp + p * c.Ls;  // [Bmax][K]
+  float* tiles = ybuf + d.Bmax * d.K;
 
   // ---- part 1: mixture x_sim = sum_k w_k y_k, forecast residual, dL/dy and dL/dw (forecast)
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)B) : 0.f;
+  // ybuf[b][k'] = sum over hidden chunks of the per-factor predictions (fixed order)
+  rc_stage<2>(B * K, [&](int e) {
+    const int b = dK.div(e), kk = e - b * K;
+    const float* yp = ws + c.wo.y + ((int64_t)b * K + kk) * p + j;
+    const int64_t qs = (int64_t)d.Bmax * K * p;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = q < nU ? yp[q * qs] : 0.f;
+    float yv = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nU) yv += v[q];
+    return yv;
+  }, [&](int e, float v) { ybuf[e] = v; });
+  __syncthreads();
   float fsum = 0.f;
   for (int b = tid; b < B; b += RC_BLOCK) {
     const float* wr = ws + c.wo.w + (int64_t)b * K;
-    float xs = 0.f, yk = 0.f;
+    const float xt = (c.flags & (RC_LOSS_FORECAST | RC_VALUES)) ? X[((c.row0 + b) * d.T + c.Lmax) * p + j] : 0.f;
+    float xs = 0.f;
     for (int kk = 0; kk < K; ++kk) {
-      float yv = 0.f;
-      for (int q = 0; q < nU; ++q) yv += ws[c.wo.y + (((int64_t)q * d.Bmax + b) * K + kk) * p + j];
+      const float yv = ybuf[b * K + kk];
       const float we = sig ? rc_sigmoid(ecc * wr[kk]) : wr[kk];
       xs = (kk == 0) ? we * yv : xs + we * yv;
-      if (kk == k) yk = yv;
     }
+    const float yk = ybuf[b * K + k];
     // the target X[:, Lmax] exists only when a loss is requested (forward() passes X[:, :Lmax])
-    const float res = (c.flags & (RC_LOSS_FORECAST | RC_VALUES)) ? xs - X[((c.row0 + b) * d.T + c.Lmax) * p + j] : 0.f;
+    const float res = (c.flags & (RC_LOSS_FORECAST | RC_VALUES)) ? xs - xt : 0.f;
     const float wb = sig ? rc_sigmoid(ecc * wr[k]) : wr[k];
     const float g = gscale * res;
     wk[b] = wb;
@@ -307,21 +325,19 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   for (int bb0 = 0; bb0 < B; bb0 += FB_BT) {
     __syncthreads();
-    for (int e = tid; e < FB_BT * FAC_UC; e += RC_BLOCK) {
+    rc_stage<2>(FB_BT * FAC_UC, [&](int e) {
       const int bb = e / FAC_UC, uu = e - bb * FAC_UC;
       const int b = bb0 + bb, u = u0 + uu;
-      float dz = 0.f;
-      if (b < B && u < h) {
-        const float av = aw[(int64_t)b * h + u];
-        dz = av > 0.f ? dyl[b] * w1s[uu] : 0.f;
-      }
-      dZs[bb * (FAC_UC + 1) + uu] = dz;
-    }
-    for (int e = tid; e < FB_BT * FB_QT; e += RC_BLOCK) {
+      return (b < B && u < h) ? aw[(int64_t)b * h + u] : 0.f;
+    }, [&](int e, float av) {
+      const int bb = e / FAC_UC, uu = e - bb * FAC_UC;
+      dZs[bb * (FAC_UC + 1) + uu] = av > 0.f ? dyl[bb0 + bb] * w1s[uu] : 0.f;
+    });
+    rc_stage<8>(FB_BT * FB_QT, [&](int e) {
       const int bb = e / FB_QT, qq = e - bb * FB_QT;
       const int b = bb0 + bb, q = q0 + qq;
-      Xs[bb * (FB_QT + 1) + qq] = (b < B && q < Q) ? xwin(c, X, b, q) : 0.f;
-    }
+      return (b < B && q < Q) ? xwin(c, dL, X, b, q) : 0.f;
+    }, [&](int e, float v) { Xs[(e / FB_QT) * (FB_QT + 1) + e % FB_QT] = v; });
     __syncthreads();
 #pragma unroll 8
     for (int bb = 0; bb < FB_BT; ++bb) {
@@ -351,7 +367,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
 
 int fac_bwd_lds_floats(const RedcliffDims& d, int Ls) {
   const int Q = d.p * d.L;
-  return 2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + 512 + FB_BT * (FAC_UC + 1) + FB_BT * (FB_QT + 1) + FAC_UC;
+  return 2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + d.Bmax * d.K + 512 + FB_BT * (FAC_UC + 1) + FB_BT * (FB_QT + 1) + FAC_UC;
 }
 
 }  // namespace

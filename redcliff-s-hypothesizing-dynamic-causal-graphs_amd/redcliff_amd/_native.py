@@ -24,7 +24,7 @@ CONFUSION = 1 << 8
 STORE_OUTPUTS = 1 << 9
 REFRESH_SUPPORTS = 1 << 10
 
-WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "dwp", "dAadj", "dWi", "dS", "dgb", "S", "dZ", "amat",
+WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt", "gfc1", "dwp", "dAadj", "dWi", "dS", "dgb", "S", "dZ", "amat",
               "lossp", "xsim", "gfc", "total")
 
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
