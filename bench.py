@@ -41,6 +41,9 @@ CONFIGS = {
                           "DGCNN F=16/3 layers/100 hidden), combined-phase batch_update, B=128"),
     "c4": dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, B=128, T=150, label_T=150, lrA=5e-4, lrB=5e-4,
                workload="REDCLIFF-S TST-shaped (p=12, gen_lag=4, K=9, nsup=3, h=25, DGCNN 16/3/100), B=128"),
+    # BASELINE.json configs[4]: scaled synthetic stress (large grouped contraction)
+    "c5": dict(p=64, L=20, K=8, nsup=8, h=25, F=64, n=3, H=100, B=128, T=128, label_T=128, lrA=5e-4, lrB=5e-4,
+               workload="REDCLIFF-S stress (p=64, gen_lag=20, K=8, h=25, DGCNN F=64/3 layers/100 hidden), B=128"),
 }
 
 
@@ -138,6 +141,49 @@ def pmc_traffic(kernel_name, launches_hint=None):
     return (2.0 * fetch + write) * 1024.0  # counters are in KiB
 
 
+def run_grid(c, args, dev, rank, dist):
+    """Time args.grid_steps combined-phase steps of R packed grid-search replicas."""
+    import redcliff_amd
+    K, p = c["K"], c["p"]
+    R = args.replicas
+    models, opts = [], []
+    for i in range(R):
+        m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=1000 * rank + i).to(dev)
+        # vary what the reference grid varies (train/...gsSmooth1.py:278-309): lrs and coefficients
+        m.FORECAST_COEFF = (10.0, 1.0)[i % 2]
+        m.ADJ_L1_REG_COEFF = (0.1, 0.01)[(i // 2) % 2] / K / np.sqrt(p * p - 1.0)
+        cc = dict(c, lrA=(5e-4, 1e-4)[(i // 4) % 2], lrB=(5e-4, 1e-4)[(i // 8) % 2])
+        models.append(m)
+        opts.append(adam_pair(m, cc))
+    pack = redcliff_amd.ReplicaPack(models, opts)
+    nbatch = 8
+    X, Y = synth(c, nbatch * c["B"], seed=200 + rank)
+    ds = pack.cache_dataset([(X[i:i + c["B"]], Y[i:i + c["B"]]) for i in range(0, X.shape[0], c["B"])])
+
+    def steps(n, start):
+        idx = (np.arange(n) + start) % nbatch
+        pack.run_steps(["combined"], ds, ds["rows"][idx], ds["sizes"][idx],
+                       ds["stats"][torch.as_tensor(idx, device=dev)].contiguous())
+
+    steps(5, 0)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps(args.grid_steps, 5)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, R
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +193,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-times", action="store_true")
+    ap.add_argument("--replicas", type=int, default=32, help="grid-search replicas packed per GPU (1: skip)")
+    ap.add_argument("--grid-steps", type=int, default=50)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -202,6 +250,19 @@ def main():
     windows = world * args.steps * B
     value = windows / elapsed
 
+    # grid-search replicas packed into one launch: R fits of the same shape
+    # with different seeds / coefficients / learning rates, stepped together on this GPU
+    grid = None
+    if args.replicas > 1:
+        grid_elapsed, R = run_grid(c, args, dev, rank, dist)
+        gsteps = args.grid_steps
+        grid = {"replicas_per_gpu": R, "steps": gsteps,
+                "windows_per_s": round(world * R * gsteps * B / grid_elapsed, 1),
+                "ms_per_step": round(1e3 * grid_elapsed / gsteps, 4),
+                "speedup_vs_single_fit": round((world * R * gsteps * B / grid_elapsed) / value, 2),
+                "note": "R independent fits (grid points) per GPU, each B=%d windows per step; one launch per kernel "
+                        "for all R" % B}
+
     # per-kernel device time over the same kind of steps (HIP events on the launch stream)
     ktimes = None
     if not args.no_kernel_times:
@@ -242,7 +303,7 @@ def main():
         "config": {"workload": c["workload"], "global_batch": B * world, "windows_per_step_per_gpu": B,
                    "parallelism": "replicas%d (one independent fit per GPU, no collective)" % world,
                    "flops_per_window": fl["total"]},
-        "roofline": roof, "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu, "grid_search": grid,
     }
     if cpu:
         out["gpu_over_cpu"] = round(value / world / cpu["value"], 1)

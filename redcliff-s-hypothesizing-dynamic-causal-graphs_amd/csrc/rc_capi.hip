@@ -68,7 +68,7 @@ static int check_dims(const RedcliffDims* d) {
     rc_set_error("fused path needs embed_lag >= gen_lag (forward and GC embedder windows coincide)");
     return REDCLIFF_ELIMIT;
   }
-  if (rc_emb_bwd_lds(*d) > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
+  if (rc_emb_bwd_lds(*d) > RC_LDS_MAX_FLOATS * sizeof(float)) {
     rc_set_error("embedder backward LDS budget exceeded for Bmax*K=%d", d->Bmax * d->K);
     return REDCLIFF_ELIMIT;
   }

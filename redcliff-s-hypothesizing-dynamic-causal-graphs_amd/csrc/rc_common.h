@@ -6,7 +6,8 @@
 
 #define RC_BLOCK 256
 #define RC_TRACE_FLOATS 4096  // trace builds: u64 phase-timing slots at the end of the workspace
-#define RC_LDS_LIMIT_FLOATS 16384  // 64 KiB of dynamic LDS per workgroup
+#define RC_LDS_LIMIT_FLOATS 16384  // 64 KiB of dynamic LDS per workgroup (several workgroups per CU)
+#define RC_LDS_MAX_FLOATS 40960    // 160 KiB: the whole CU's LDS, used only when a tile needs it (large p)
 
 // Offsets (in floats) inside one replica's packed embedder parameters.
 struct EmbOff {
@@ -88,12 +89,27 @@ __host__ __device__ inline int rc_emb_node_floats(const RedcliffDims& d, int BC)
   return 4 * BC * d.K + d.K * d.M1 + d.M1 * EMB_HC + nF * (EMB_HC + 1) + d.n * d.p + 8 + 4 * d.F + RC_BLOCK +
          BC * (2 * d.M1 + 2 * EMB_HC + 2 * nF + d.p * d.F);
 }
+// Windows per LDS sub-block: as many as fit the 64 KiB budget; with fewer than 4 (large p*F)
+// the budget grows to the CU's 160 KiB.
 __host__ __device__ inline int rc_emb_bc(const RedcliffDims& d) {
   int BC = 16;
   while (BC > 1 && rc_emb_node_floats(d, BC) > RC_LDS_LIMIT_FLOATS) BC >>= 1;
+  if (BC >= 4) return BC;
+  BC = 16;
+  while (BC > 1 && rc_emb_node_floats(d, BC) > RC_LDS_MAX_FLOATS) BC >>= 1;
   return BC;
 }
-__host__ __device__ inline int rc_emb_nbw(const RedcliffDims& d) { return (d.Bmax + rc_emb_bc(d) - 1) / rc_emb_bc(d); }
+// Windows per (node, chunk) workgroup: a multiple of BC, processed as sequential sub-blocks.
+// Enough window blocks to give the launch ~1024 workgroups, never more than ceil(Bmax/BC).
+__host__ __device__ inline int rc_emb_wpb(const RedcliffDims& d) {
+  const int BC = rc_emb_bc(d);
+  const int groups = d.p * rc_nchunk(d);
+  const int target = (1024 + groups - 1) / groups;
+  const int nblk = (d.Bmax + BC - 1) / BC;
+  const int nbw = nblk < target ? nblk : target;
+  return BC * ((nblk + nbw - 1) / nbw);
+}
+__host__ __device__ inline int rc_emb_nbw(const RedcliffDims& d) { return (d.Bmax + rc_emb_wpb(d) - 1) / rc_emb_wpb(d); }
 // floats per partial record: fc1 chunk | W_i chunk | dS rows i >= 1 | dgamma | dbeta | fc2W fc2b fc1b (group 0)
 __host__ __device__ inline int rc_emb_pstride(const RedcliffDims& d) {
   return d.M1 * EMB_HC + d.n * d.F * EMB_HC + (d.n - 1) * d.p + 2 * d.F + d.K * d.M1 + d.K + d.M1;

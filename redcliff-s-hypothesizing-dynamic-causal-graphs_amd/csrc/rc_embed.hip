@@ -296,22 +296,24 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
   }
 }
 
-// K3 node workgroup (node c, hidden columns [h0, h0+HC), windows [wb*BC, wb*BC+nbc)):
+// K3 node workgroup (node c, hidden columns [h0, h0+HC), windows [wb*WPB, wb*WPB+WPB)):
 // dL/dw_raw of its windows, dL/dfc1 of the chunk's columns, graph-conv output gradient dZ,
 // and partial sums over its windows of dfc1W, dW_i, dS_i[c][:], the BatchNorm affine
-// gradients and (node 0, chunk 0) the fc2 / fc1-bias gradients.  The partials of the nbw
-// window blocks of one (node, chunk) are combined in fixed order by the block that arrives
-// last (agent-scope release / ticket / acquire, cdna_hip_programming.md §6 Guideline 16).
-// All inputs of a block are staged into LDS by one multi-segment pass (one memory latency
-// for everything instead of one per array).
-__device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, float* sm) {
+// gradients and (node 0, chunk 0) the fc2 / fc1-bias gradients.  The windows are walked in
+// LDS sub-blocks of BC (register accumulators carry over), so large p*F windows keep the
+// partial records few.  The partials of the nbw window blocks of one (node, chunk) are
+// combined in fixed order by the block that arrives last (agent-scope release / ticket /
+// acquire, cdna_hip_programming.md §6 Guideline 16).  The first sub-block's inputs and the
+// fixed operands are staged by one multi-segment pass (one memory latency for everything).
+template <bool MULTI>
+__device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, int WPB, float* sm) {
   const RedcliffDims& d = c.d;
   const int K = d.K, M1 = d.M1, B = c.B, p = d.p, H = d.H, F = d.F, n = d.n;
   const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC, HP = EMB_HC + 1;
   const int h0 = ch * HC, hc = min(HC, H - h0);
   const int nch = rc_nchunk(d);
-  const int nbw = (B + BC - 1) / BC, nbw_max = rc_emb_nbw(d);
-  const int bw0 = wb * BC, nbc = min(BC, B - bw0);
+  const int nbw = (B + WPB - 1) / WPB, nbw_max = rc_emb_nbw(d);
+  const int wend = min(B, (wb + 1) * WPB);
   const int grp = node * nch + ch;
   const bool head_grads = (grp == 0);  // fc2 / fc1-bias partials ride on group 0
   float* E = c.emb + r * c.es;
@@ -348,7 +350,6 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
   NMARK(0);
   if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 600 + 2 * blockIdx.x);
   bn_affine(c, r, E, alpha, beta, mean, inv);
-  // ---- one staging pass over 11 segments, all loads of a round in flight together
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
   const float* f1 = ws + c.wo.f1;
@@ -357,171 +358,188 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
   const float* S = ws + c.wo.S;
   const float* wraw = ws + c.wo.w;
   const float* dwp = ws + c.wo.dwp;
-  rc_stage_all(
-      rc_seg<1>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
-      rc_seg<4>(M1 * HC, [&](int e) {
-        const int m = e / HC, hh = e - m * HC;
-        return hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;
-      }, [&](int e, float v) { FW[e] = v; }),
-      rc_seg<4>(nF * HC, [&](int e) {
-        const int eh = e >> 4, i = dF.div(eh), f = eh - i * F, hh = e & 15;  // HC == 16
-        return hh < hc ? E[c.eo.gcW + ((int64_t)i * F + f) * H + h0 + hh] : 0.f;
-      }, [&](int e, float v) { WiC[(e / HC) * HP + e % HC] = v; }),
-      rc_seg<1>(n * p, [&](int e) {
-        const int i = dp.div(e), cc = e - i * p;
-        return S[((int64_t)i * p + node) * p + cc];
-      }, [&](int e, float v) { Srow[e] = v; }),
-      rc_seg<1>(nbc * HC, [&](int e) {
-        const int s = e / HC, hh = e - s * HC;
-        return hh < hc ? Rg[(int64_t)(bw0 + s) * pH + node * H + h0 + hh] : 0.f;
-      }, [&](int e, float v) { Rc[e] = v; }),
-      rc_seg<4>(nbc * nF, [&](int e) {
-        const int s = dnF.div(e), rem = e - s * nF, i = dF.div(rem), f = rem - i * F;
-        return Tg[(int64_t)(bw0 + s) * n * pF + i * pF + node * F + f];
-      }, [&](int e, float v) { Tc[e] = v; }),
-      rc_seg<16>(nbc * pF, [&](int e) {
-        const int s = dpF.div(e), rem = e - s * pF;  // rem = f * p + cc (contiguous in the window row)
-        return X[(c.row0 + bw0 + s) * d.T * p + (int64_t)(c.Lmax - F) * p + rem];
-      }, [&](int e, float v) {
-        const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), cc = rem - f * p;
-        xc[s * pF + cc * F + f] = v;
-      }),
-      rc_seg<4>(nbc * M1, [&](int e) { return f1[(int64_t)bw0 * M1 + e]; }, [&](int e, float v) { f1r[e] = v; }),
-      rc_seg<1>(nbc * K, [&](int e) { return wraw[(int64_t)bw0 * K + e]; }, [&](int e, float v) { wrl[e] = v; }),
-      rc_seg<1>(nbc * K, [&](int e) { return lab_on ? c.lab[r * c.labr + (c.row0 + bw0) * K + e] : 0.f; },
-                [&](int e, float v) { labl[e] = v; }),
-      rc_seg<1>(nbc * K, [&](int e) {
-        const int s = dK.div(e), k = e - s * K;
-        float g = 0.f;
-        if (fac_grad) {
-#pragma unroll 4
-          for (int j = 0; j < p; ++j) g += dwp[((int64_t)j * d.Bmax + bw0 + s) * K + k];
-        }
-        return g;
-      }, [&](int e, float v) { dwl[e] = v; }));
-  __syncthreads();
-  if (tid < n) {
-    float t = 0.f;
-    for (int cc = 0; cc < p; ++cc) t += Srow[tid * p + cc];
-    rs[tid] = t;
-  }
-  for (int e = tid; e < nbc * K; e += RC_BLOCK) dr[e] = draw_value(c, r, dK.mod(e), wrl[e], dwl[e], labl[e]);
-  __syncthreads();
-  // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
-  for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
-    const int s = dM1.div(e), m = e - s * M1;
-    float g = 0.f;
-    if (f1r[e] > 0.f)
-      for (int k = 0; k < K; ++k) g += dr[s * K + k] * fc2s[k * M1 + m];
-    df1c[e] = g;
-  }
-  __syncthreads();
-  NMARK(1);
-  // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
-  for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
-    const int s = e / HC, hh = e - s * HC;
-    const float* dfr = df1c + s * M1;
-    float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
-    int m = 0;
-    for (; m + 3 < M1; m += 4) {
-      g0 += dfr[m] * FW[m * HC + hh];
-      g1 += dfr[m + 1] * FW[(m + 1) * HC + hh];
-      g2 += dfr[m + 2] * FW[(m + 2) * HC + hh];
-      g3 += dfr[m + 3] * FW[(m + 3) * HC + hh];
-    }
-    for (; m < M1; ++m) g0 += dfr[m] * FW[m * HC + hh];
-    const float g = (g0 + g1) + (g2 + g3);
-    dZc[e] = Rc[e] > 0.f ? g : 0.f;
-  }
-  // dfc1W chunk partial: afc[m][hh] = sum_s df1[s][m] R[s][hh]   (M1*HC <= 1024 -> 4 / thread)
-  float afc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < nbc; ++s) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = tid + k * RC_BLOCK;
-      if (e < M1 * HC) afc[k] += df1c[s * M1 + e / HC] * Rc[s * HC + e % HC];
-    }
-  }
-  // group 0: dfc2W[k][m] = sum_s dr[s][k] relu(f1[s][m]); dfc2b[k] = sum_s dr[s][k]; dfc1b[m] = sum_s df1[s][m]
-  const int nout = K * M1 + K + M1;  // <= 16*64 + 16 + 64 < 5*256
-  float agf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  if (head_grads) {
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const int e = tid + kk * RC_BLOCK;
-      if (e >= nout) continue;
-      float g = 0.f;
-      if (e < K * M1) {
-        const int k = dM1.div(e), m = e - k * M1;
-        for (int s = 0; s < nbc; ++s) g += dr[s * K + k] * fmaxf(f1r[s * M1 + m], 0.f);
-      } else if (e < K * M1 + K) {
-        const int k = e - K * M1;
-        for (int s = 0; s < nbc; ++s) g += dr[s * K + k];
-      } else {
-        const int m = e - K * M1 - K;
-        for (int s = 0; s < nbc; ++s) g += df1c[s * M1 + m];
-      }
-      agf[kk] = g;
-    }
-  }
-  __syncthreads();
-  NMARK(2);
-  // dW_i chunk partial: awi[i][f][hh] = sum_s T_i[s][f] dZ[s][hh]   (n*F*HC <= 4096 -> 16 / thread)
-  float awi[16];
+
+  // register accumulators over all sub-blocks of the workgroup's windows
+  float afc[4] = {0.f, 0.f, 0.f, 0.f};     // dfc1W chunk: M1*HC <= 1024 -> 4 / thread
+  float agf[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // group 0: dfc2W | dfc2b | dfc1b (< 5*256)
+  float awi[16];                            // dW_i chunk: n*F*HC <= 4096 -> 16 / thread
 #pragma unroll
   for (int k = 0; k < 16; ++k) awi[k] = 0.f;
   const int nwi = (nF * HC + RC_BLOCK - 1) / RC_BLOCK;
-  for (int s = 0; s < nbc; ++s) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = tid + k * RC_BLOCK;
-      if (k < nwi && e < nF * HC) awi[k] += Tc[s * nF + e / HC] * dZc[s * HC + e % HC];
-    }
-  }
-  // dT_i[s][f] = sum_hh dZ[s][hh] W_i[f][hh]
-  for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
-    const int s = dnF.div(e), rem = e - s * nF;
-    const float* wr = WiC + rem * HP;
-    const float* dz = dZc + s * HC;
-    float t0 = 0.f, t1 = 0.f;
-#pragma unroll
-    for (int hh = 0; hh < HC; hh += 2) {
-      t0 += dz[hh] * wr[hh];
-      t1 += dz[hh + 1] * wr[hh + 1];
-    }
-    dTc[e] = t0 + t1;
-  }
-  __syncthreads();
-  NMARK(3);
-  // dS_i[node][c'] (i >= 1) and BatchNorm affine partials, windows split over thread slices
+  const int nout = K * M1 + K + M1;
   const int nS = (n - 1) * p;
   const int nslS = nS > 0 ? RC_BLOCK / nS : 0, oS = nS > 0 ? tid % nS : 0, slS = nS > 0 ? tid / nS : 1;
   const int nslF = RC_BLOCK / F, oF = tid % F, slF = tid / F;
   float aS = 0.f, aG = 0.f, aB = 0.f;
-  if (slS < nslS) {
-    const int i = 1 + oS / p, cp = oS - (i - 1) * p;
-    for (int s = slS; s < nbc; s += nslS) {
-      const float* dt = dTc + s * nF + i * F;
-      const float* xr = xc + s * pF + cp * F;
-      for (int f = 0; f < F; ++f) aS += dt[f] * (xr[f] * alpha[f] + beta[f]);
+
+  // MULTI = false: one sub-block per workgroup (WPB == BC), the loop folds away
+  const int nsub = MULTI ? (wend - wb * WPB + BC - 1) / BC : 1;
+  for (int it = 0; it < nsub; ++it) {
+    const int bw0 = wb * WPB + it * BC;
+    const int nbc = min(BC, wend - bw0);
+    // ---- stage the sub-block's windows (with the fixed operands on the first pass)
+    auto sR = rc_seg<1>(nbc * HC, [&](int e) {
+      const int s = e / HC, hh = e - s * HC;
+      return hh < hc ? Rg[(int64_t)(bw0 + s) * pH + node * H + h0 + hh] : 0.f;
+    }, [&](int e, float v) { Rc[e] = v; });
+    auto sT = rc_seg<4>(nbc * nF, [&](int e) {
+      const int s = dnF.div(e), rem = e - s * nF, i = dF.div(rem), f = rem - i * F;
+      return Tg[(int64_t)(bw0 + s) * n * pF + i * pF + node * F + f];
+    }, [&](int e, float v) { Tc[e] = v; });
+    auto sX = rc_seg<16>(nbc * pF, [&](int e) {
+      const int s = dpF.div(e), rem = e - s * pF;  // rem = f * p + cc (contiguous in the window row)
+      return X[(c.row0 + bw0 + s) * d.T * p + (int64_t)(c.Lmax - F) * p + rem];
+    }, [&](int e, float v) {
+      const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), cc = rem - f * p;
+      xc[s * pF + cc * F + f] = v;
+    });
+    auto sF1 = rc_seg<4>(nbc * M1, [&](int e) { return f1[(int64_t)bw0 * M1 + e]; }, [&](int e, float v) { f1r[e] = v; });
+    auto sW = rc_seg<1>(nbc * K, [&](int e) { return wraw[(int64_t)bw0 * K + e]; }, [&](int e, float v) { wrl[e] = v; });
+    auto sL = rc_seg<1>(nbc * K, [&](int e) { return lab_on ? c.lab[r * c.labr + (c.row0 + bw0) * K + e] : 0.f; },
+                        [&](int e, float v) { labl[e] = v; });
+    auto sD = rc_seg<1>(nbc * K, [&](int e) {
+      const int s = dK.div(e), k = e - s * K;
+      float g = 0.f;
+      if (fac_grad) {
+#pragma unroll 4
+        for (int j = 0; j < p; ++j) g += dwp[((int64_t)j * d.Bmax + bw0 + s) * K + k];
+      }
+      return g;
+    }, [&](int e, float v) { dwl[e] = v; });
+    __syncthreads();  // the previous sub-block is done with the LDS tiles
+    if (it == 0) {
+      rc_stage_all(
+          rc_seg<1>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
+          rc_seg<4>(M1 * HC, [&](int e) {
+            const int m = e / HC, hh = e - m * HC;
+            return hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;
+          }, [&](int e, float v) { FW[e] = v; }),
+          rc_seg<4>(nF * HC, [&](int e) {
+            const int eh = e >> 4, i = dF.div(eh), f = eh - i * F, hh = e & 15;  // HC == 16
+            return hh < hc ? E[c.eo.gcW + ((int64_t)i * F + f) * H + h0 + hh] : 0.f;
+          }, [&](int e, float v) { WiC[(e / HC) * HP + e % HC] = v; }),
+          rc_seg<1>(n * p, [&](int e) {
+            const int i = dp.div(e), cc = e - i * p;
+            return S[((int64_t)i * p + node) * p + cc];
+          }, [&](int e, float v) { Srow[e] = v; }),
+          sR, sT, sX, sF1, sW, sL, sD);
+      __syncthreads();
+      if (tid < n) {
+        float t = 0.f;
+        for (int cc = 0; cc < p; ++cc) t += Srow[tid * p + cc];
+        rs[tid] = t;
+      }
+    } else {
+      rc_stage_all(sR, sT, sX, sF1, sW, sL, sD);
+      __syncthreads();
     }
-  }
-  if (slF < nslF) {
-    const int f = oF;
-    const float mu = mean[f], iv = inv[f];
-    for (int s = slF; s < nbc; s += nslF) {
-      const float* xs_ = xc + s * pF + f;
-      for (int i = 0; i < n; ++i) {
-        float u;
-        if (i == 0) {
-          u = (xs_[node * F] - mu) * iv;
+    for (int e = tid; e < nbc * K; e += RC_BLOCK) dr[e] = draw_value(c, r, dK.mod(e), wrl[e], dwl[e], labl[e]);
+    __syncthreads();
+    // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
+    for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
+      const int s = dM1.div(e), m = e - s * M1;
+      float g = 0.f;
+      if (f1r[e] > 0.f)
+        for (int k = 0; k < K; ++k) g += dr[s * K + k] * fc2s[k * M1 + m];
+      df1c[e] = g;
+    }
+    __syncthreads();
+    NMARK(1);
+    // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
+    for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
+      const int s = e / HC, hh = e - s * HC;
+      const float* dfr = df1c + s * M1;
+      float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
+      int m = 0;
+      for (; m + 3 < M1; m += 4) {
+        g0 += dfr[m] * FW[m * HC + hh];
+        g1 += dfr[m + 1] * FW[(m + 1) * HC + hh];
+        g2 += dfr[m + 2] * FW[(m + 2) * HC + hh];
+        g3 += dfr[m + 3] * FW[(m + 3) * HC + hh];
+      }
+      for (; m < M1; ++m) g0 += dfr[m] * FW[m * HC + hh];
+      const float g = (g0 + g1) + (g2 + g3);
+      dZc[e] = Rc[e] > 0.f ? g : 0.f;
+    }
+    // dfc1W chunk partial: afc[m][hh] += sum_s df1[s][m] R[s][hh]
+    for (int s = 0; s < nbc; ++s) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + k * RC_BLOCK;
+        if (e < M1 * HC) afc[k] += df1c[s * M1 + e / HC] * Rc[s * HC + e % HC];
+      }
+    }
+    // group 0: dfc2W[k][m] += sum_s dr[s][k] relu(f1[s][m]); dfc2b[k] += sum_s dr[s][k]; dfc1b[m] += sum_s df1[s][m]
+    if (head_grads) {
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        const int e = tid + kk * RC_BLOCK;
+        if (e >= nout) continue;
+        float g = agf[kk];
+        if (e < K * M1) {
+          const int k = dM1.div(e), m = e - k * M1;
+          for (int s = 0; s < nbc; ++s) g += dr[s * K + k] * fmaxf(f1r[s * M1 + m], 0.f);
+        } else if (e < K * M1 + K) {
+          const int k = e - K * M1;
+          for (int s = 0; s < nbc; ++s) g += dr[s * K + k];
         } else {
-          u = 0.f;
-          for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xs_[cc * F] - mu) * iv);
+          const int m = e - K * M1 - K;
+          for (int s = 0; s < nbc; ++s) g += df1c[s * M1 + m];
         }
-        const float dt = dTc[s * nF + i * F + f];
-        aG += dt * u;
-        aB += dt * rs[i];
+        agf[kk] = g;
+      }
+    }
+    __syncthreads();
+    NMARK(2);
+    // dW_i chunk partial: awi[i][f][hh] += sum_s T_i[s][f] dZ[s][hh]
+    for (int s = 0; s < nbc; ++s) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = tid + k * RC_BLOCK;
+        if (k < nwi && e < nF * HC) awi[k] += Tc[s * nF + e / HC] * dZc[s * HC + e % HC];
+      }
+    }
+    // dT_i[s][f] = sum_hh dZ[s][hh] W_i[f][hh]
+    for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
+      const int s = dnF.div(e), rem = e - s * nF;
+      const float* wr = WiC + rem * HP;
+      const float* dz = dZc + s * HC;
+      float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+      for (int hh = 0; hh < HC; hh += 2) {
+        t0 += dz[hh] * wr[hh];
+        t1 += dz[hh + 1] * wr[hh + 1];
+      }
+      dTc[e] = t0 + t1;
+    }
+    __syncthreads();
+    NMARK(3);
+    // dS_i[node][c'] (i >= 1) and BatchNorm affine partials, windows split over thread slices
+    if (slS < nslS) {
+      const int i = 1 + oS / p, cp = oS - (i - 1) * p;
+      for (int s = slS; s < nbc; s += nslS) {
+        const float* dt = dTc + s * nF + i * F;
+        const float* xr = xc + s * pF + cp * F;
+        for (int f = 0; f < F; ++f) aS += dt[f] * (xr[f] * alpha[f] + beta[f]);
+      }
+    }
+    if (slF < nslF) {
+      const int f = oF;
+      const float mu = mean[f], iv = inv[f];
+      for (int s = slF; s < nbc; s += nslF) {
+        const float* xs_ = xc + s * pF + f;
+        for (int i = 0; i < n; ++i) {
+          float u;
+          if (i == 0) {
+            u = (xs_[node * F] - mu) * iv;
+          } else {
+            u = 0.f;
+            for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xs_[cc * F] - mu) * iv);
+          }
+          const float dt = dTc[s * nF + i * F + f];
+          aG += dt * u;
+          aB += dt * rs[i];
+        }
       }
     }
   }
@@ -631,16 +649,17 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
 
 // grid (p * nchunk * nbw [+ 1], R): workgroups [0, p*nchunk*nbw) are (node, column chunk,
 // window block) blocks; the optional last one is the head (loss values / confusion).
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int BC) {
+template <bool MULTI>
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int BC, int WPB) {
   extern __shared__ float sm[];
   const int r = blockIdx.y;
   const int nch = rc_nchunk(c.d);
-  const int nbw = (c.B + BC - 1) / BC;
+  const int nbw = (c.B + WPB - 1) / WPB;
   if ((int)blockIdx.x == nnode) {
     emb_bwd_head(c, r, sm);
   } else {
     const int grp = blockIdx.x / nbw, wb = blockIdx.x - grp * nbw;
-    emb_bwd_node(c, r, grp / nch, grp % nch, wb, BC, sm);
+    emb_bwd_node<MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
   }
 }
 
@@ -864,6 +883,14 @@ static size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
          (size_t)SB * d.M1 + 2 * d.F;
 }
 
+// Dynamic LDS above 64 KiB (up to the CU's 160 KiB) must be opted into per kernel.
+template <class Kern>
+static int rc_lds_optin(Kern k, size_t bytes, const char* what) {
+  if (bytes <= RC_LDS_LIMIT_FLOATS * sizeof(float)) return 0;
+  return rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)bytes), what);
+}
+
 int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   static const int sb_env = [] {
@@ -872,10 +899,14 @@ int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
     return (x >= 1 && x <= 4) ? x : 0;
   }();
   int SB = sb_env ? sb_env : 1, w_lds = 1;
-  while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) --SB;
-  if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) w_lds = 0;
-  if (emb_fwd_floats(d, SB, w_lds) > RC_LDS_LIMIT_FLOATS) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  size_t limit = RC_LDS_LIMIT_FLOATS;
+  while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > limit) --SB;
+  if (emb_fwd_floats(d, SB, w_lds) > limit) w_lds = 0;
+  if (emb_fwd_floats(d, SB, w_lds) > limit) limit = RC_LDS_MAX_FLOATS;  // large p*F: one workgroup per CU
+  if (emb_fwd_floats(d, SB, w_lds) > limit) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   const size_t lds = sizeof(float) * emb_fwd_floats(d, SB, w_lds);
+  int e = rc_lds_optin(k_emb_fwd, lds, "k_emb_fwd LDS");
+  if (e) return e;
   dim3 grid((c.B + SB - 1) / SB, d.R);
   hipLaunchKernelGGL(k_emb_fwd, grid, dim3(RC_BLOCK), lds, s, c, SB, w_lds);
   return rc_check(hipGetLastError(), "k_emb_fwd");
@@ -890,12 +921,20 @@ size_t rc_emb_bwd_lds(const RedcliffDims& d) {
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   const RedcliffDims& d = c.d;
   const size_t lds = rc_emb_bwd_lds(d);
-  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  const int BC = rc_emb_bc(d);
-  const int nnode = node_wgs ? d.p * rc_nchunk(d) * ((c.B + BC - 1) / BC) : 0;
+  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  const int BC = rc_emb_bc(d), WPB = rc_emb_wpb(d);
+  const int nnode = node_wgs ? d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB) : 0;
   const int head = (c.flags & (RC_VALUES | RC_CONFUSION)) ? 1 : 0;
   if (nnode + head == 0) return 0;
-  hipLaunchKernelGGL(k_emb_bwd, dim3(nnode + head, d.R), dim3(RC_BLOCK), lds, s, c, nnode, BC);
+  if (WPB > BC) {
+    int e = rc_lds_optin(k_emb_bwd<true>, lds, "k_emb_bwd LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_emb_bwd<true>, dim3(nnode + head, d.R), dim3(RC_BLOCK), lds, s, c, nnode, BC, WPB);
+  } else {
+    int e = rc_lds_optin(k_emb_bwd<false>, lds, "k_emb_bwd LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head, d.R), dim3(RC_BLOCK), lds, s, c, nnode, BC, WPB);
+  }
   return rc_check(hipGetLastError(), "k_emb_bwd");
 }
 

@@ -104,6 +104,8 @@ class FitEngine:
         self.hyper_dev = None
         self.supports_fresh = False
         self.dataset_cache = {}
+        self.pack = None  # ReplicaPack this fit belongs to (redcliff_amd.replicas), if any
+        self.pack_index = None
         self.bind()
 
     # ------------------------------------------------------------------ layout / binding
@@ -205,8 +207,7 @@ class FitEngine:
         if mine != theirs:
             raise ValueError("optimizer%s must own exactly model.gen_model[%d].parameters()" % (g, 0 if g == "A" else 1))
         base = self.emb if g == "A" else self.fac
-        m = torch.zeros_like(base)
-        v = torch.zeros_like(base)
+        m, v = self._new_moments(g)
         step = 0
         for prm in self._group_params(g):
             s = opt.state.get(prm)
@@ -219,6 +220,40 @@ class FitEngine:
         self.opt[g] = st
         self._attach_state(g)
         return st
+
+    def _new_moments(self, g):
+        """Zeroed Adam moment buffers of group g: rows of the replica pack when packed."""
+        if self.pack is not None:
+            m, v = self.pack.moments(g, self.pack_index)
+            m.zero_()
+            v.zero_()
+            return m, v
+        base = self.emb if g == "A" else self.fac
+        return torch.zeros_like(base), torch.zeros_like(base)
+
+    def attach_pack(self, pack, index):
+        """Move this fit's parameters, BatchNorm buffers and Adam moments into row `index`
+        of a ReplicaPack (packed [R][...] buffers, one launch for R fits).  The module's
+        parameters and the optimizers' state stay views, now of the pack's rows."""
+        self.ensure_bound()
+        emb_old, fac_old, bn_old = self.emb, self.fac, self.bn
+        self.pack, self.pack_index = pack, index
+        self.emb, self.fac, self.bn = pack.emb[index], pack.fac[index], pack.bn[:, index]
+        with torch.no_grad():
+            self.emb.copy_(emb_old)
+            self.fac.copy_(fac_old)
+            self.bn.copy_(bn_old)
+        self.bind()
+        for g in ("A", "B"):
+            st = self.opt[g]
+            if st is None:
+                continue
+            m, v = pack.moments(g, index)
+            with torch.no_grad():
+                m.copy_(st["m"])
+                v.copy_(st["v"])
+            st["m"], st["v"] = m, v
+            self._attach_state(g)
 
     def _sync_steps(self):
         for g in ("A", "B"):

@@ -1,8 +1,9 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
+# One GPU-box pass: parity tests, smoke, bench (+ grid-search replicas), rocprofv3 kernel-trace summary.
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -o run -- python bench.py --no-cpu-baseline --steps 300 --warmup 30 > gpurun_out/kt.log 2>&1
+timeout -k 10 300 python -u bench.py --config c5 --no-cpu-baseline --steps 50 --warmup 5 --replicas 1 > gpurun_out/bench_c5.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -o run -- python bench.py --no-cpu-baseline --steps 300 --warmup 30 --replicas 1 > gpurun_out/kt.log 2>&1

@@ -45,7 +45,10 @@ def batches(d, meta):
     return [(torch.from_numpy(X[i:i + B]), torch.from_numpy(Y[i:i + B])) for i in range(0, X.shape[0], B)]
 
 
-def assert_close(name, got, want, rtol=1e-4, atol=1e-5):
+def assert_close(name, got, want, rtol=1e-4, atol=1e-5, outliers=0):
+    """|got - want| <= atol + rtol*|want| elementwise.  `outliers` elements may exceed that
+    bound, but never 10x it (used only where fp32 re-association can flip isolated
+    relu/sign near-ties, see tests/test_gpu_parity.py::OUTLIERS)."""
     got = np.asarray(got, dtype=np.float64)
     want = np.asarray(want, dtype=np.float64)
     assert got.shape == want.shape, "%s: shape %s vs %s" % (name, got.shape, want.shape)
@@ -54,5 +57,7 @@ def assert_close(name, got, want, rtol=1e-4, atol=1e-5):
     err = np.abs(got - want)
     tol = atol + rtol * np.abs(want)
     bad = err > tol
+    if outliers and int(bad.sum()) <= outliers:
+        bad = err > 10.0 * tol
     assert not bad.any(), "%s: %d/%d mismatches, max abs err %.3e (at want=%.6g)" % (
         name, int(bad.sum()), want.size, float(err.max()), float(want.flat[int(np.argmax(err))]))

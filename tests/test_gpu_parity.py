@@ -34,7 +34,7 @@ def make_opts(m, lrA, lrB):
     return oA, oB
 
 
-def compare_state(tag, model, want, rtol=RTOL, atol=ATOL):
+def compare_state(tag, model, want, rtol=RTOL, atol=ATOL, outliers=0):
     got = dict((k, v.detach().cpu().numpy()) for k, v in model.state_dict().items() if not k.startswith("gen_model."))
     assert set(got) == set(want)
     for k in want:
@@ -42,7 +42,7 @@ def compare_state(tag, model, want, rtol=RTOL, atol=ATOL):
             assert int(got[k]) == int(want[k]), tag + k
             continue
         scale = max(1.0, float(np.abs(want[k]).max()))
-        assert_close("%s/%s" % (tag, k), got[k], want[k], rtol, atol * scale)
+        assert_close("%s/%s" % (tag, k), got[k], want[k], rtol, atol * scale, outliers)
 
 
 def test_native_library_is_the_compute_path():
@@ -150,6 +150,8 @@ CONFIGS = {
     # C4 TST-shaped: p=12, L=4, K=9 (3 supervised), h=25, F=16, 3 layers, 100 hidden, T=150
     "C4": dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, B=128, T=150, label_T=150),
 }
+# C5 stress: p=64, L=20, K=8, h=25, F=64, 3 layers, 100 hidden (B=32 keeps the oracle to seconds)
+C5 = dict(p=64, L=20, K=8, nsup=8, h=25, F=64, n=3, H=100, B=32, T=128, label_T=128)
 
 
 def oracle_and_hip(cfg, seed=0):
@@ -217,6 +219,56 @@ def test_published_configs_three_phases_vs_oracle(cname):
     b = np.stack([np.stack([g.cpu().numpy() for g in row]) for row in gm])
     assert_close("GC", b, a, 1e-4, 1e-5)
     np.testing.assert_array_equal(b > 0, a > 0)
+
+
+def test_stress_config_vs_oracle():
+    """C5 (BASELINE configs[4]): p=64, L=20, K=8 -- one step of each phase vs the oracle.
+
+    At this size the layer-0 contraction is p*L = 1280 long and a step evaluates B*K*p*h =
+    0.4M relu gates and B*K*p*p*L = 21M adjacency-L1 signs.  Any other fp32 summation order
+    (the oracle's MKL conv vs the kernels') flips the odd near-tie gate; a flipped gate changes
+    the gradient of a whole hidden unit's layer-0 row, and Adam's eps-normalised update turns
+    that into a weight change of up to ~lr.  The check is therefore: every tensor within the
+    usual tolerance except at most 5% of its elements, and those within 3*lr per Adam step;
+    the validation losses within 1e-3 relative; GC tensors within 5e-3 relative (a flipped
+    unit moves a group norm by ~0.2%) and the thresholded GC graphs identical."""
+    cfg = C5
+    o, m = oracle_and_hip(cfg)
+    X, Y = synth(cfg, cfg["B"], seed=5)
+    from oracle.redcliff_oracle import make_optimizers
+    lr = 5e-4
+    oA, oB = make_optimizers(o, lr, 1e-4, 1e-4, lr, 1e-4, 1e-4)
+    hA, hB = make_optimizers(m, lr, 1e-4, 1e-4, lr, 1e-4, 1e-4)
+    for epoch in (0, 1, 2):
+        o.batch_update(epoch, 0, X, Y, oA, oB, 1)
+        m.batch_update(epoch, 0, X, Y, hA, hB, 1)
+    want = dict((k, v.detach().numpy()) for k, v in o.state_dict().items() if not k.startswith("gen_model."))
+    got = dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items() if not k.startswith("gen_model."))
+    for k in want:
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(want[k]), k
+            continue
+        g, w = got[k].astype(np.float64), want[k].astype(np.float64)
+        err = np.abs(g - w)
+        bad = err > 5e-6 * max(1.0, np.abs(w).max()) + 2e-4 * np.abs(w)
+        assert bad.mean() <= 0.05, "%s: %d/%d elements off" % (k, int(bad.sum()), w.size)
+        assert err.max() <= 3 * lr * 2, "%s: max err %.3e beyond what a flipped gate can explain" % (k, err.max())
+    Xv, Yv = synth(cfg, 40, seed=9)
+    ov = o.validate([(Xv, Yv)])
+    hv = m.validate_training([(Xv, Yv)], 1, cfg["p"], *[[] for _ in range(5)])
+    for i, k in enumerate(["forecast", "factor", "cos", "fw_l1", "smooth", "adj"]):
+        assert_close("val/" + k, hv[i], ov[k], 1e-3, 1e-6)
+    o.eval()
+    m.eval()
+    Lm = max(cfg["L"], cfg["F"])
+    with torch.no_grad():
+        go = o.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm], threshold=False, ignore_lag=True)
+        gm = m.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm].cuda(), threshold=False, ignore_lag=True)
+    a = np.stack([np.stack([g.numpy() for g in row]) for row in go])
+    b = np.stack([np.stack([g.cpu().numpy() for g in row]) for row in gm])
+    assert_close("GC", b, a, 5e-3, 1e-5)
+    clear = np.abs(a) > 1e-5  # thresholded graph (GC > 0) identical wherever the sign is not a tie
+    np.testing.assert_array_equal((b > 0)[clear], (a > 0)[clear])
 
 
 def test_fit_trace_matches_reference():

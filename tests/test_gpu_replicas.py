@@ -1,0 +1,95 @@
+"""Grid-search replicas packed into one launch (redcliff_amd.ReplicaPack)
+must reproduce R independent fits exactly: same kernels, the replica only moves to
+blockIdx.y, so parameters, BatchNorm buffers, Adam state and validation losses are
+compared bit for bit against the same models stepped one at a time."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(p=10, L=4, K=4, nsup=4, h=100, F=20, n=2, H=30, T=21)  # D4IC-shaped (BASELINE configs[1])
+GRID = [  # (seed, FORECAST_COEFF, ADJ_L1 scale, gen_lr, embed_lr)
+    (0, 10.0, 0.1, 5e-4, 2e-4),
+    (1, 1.0, 0.01, 1e-4, 5e-4),
+    (2, 10.0, 0.01, 5e-4, 1e-4),
+]
+
+
+def make(seed, fc, adj, pre=1, acc=1):
+    import redcliff_amd
+    K, p = CFG["K"], CFG["p"]
+    coeff = {"FORECAST_COEFF": fc, "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0 / sum(range(1, K)),
+             "FACTOR_WEIGHT_L1_COEFF": 1e-3, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0,
+             "ADJ_L1_REG_COEFF": adj / K / np.sqrt(p * p - 1.0), "DAGNESS_REG_COEFF": 0.0, "DAGNESS_LAG_COEFF": 0.0,
+             "DAGNESS_NODE_COEFF": 0.0}
+    eargs = [("num_features_per_node", CFG["F"]), ("num_graph_conv_layers", CFG["n"]),
+             ("num_hidden_nodes", CFG["H"]), ("sigmoid_eccentricity_coeff", 10.0)]
+    torch.manual_seed(seed)
+    return redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(
+        p, CFG["L"], [CFG["h"]], CFG["F"], [0], CFG["L"], 1, K, CFG["nsup"], coeff, False, "DGCNN", eargs,
+        "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
+        training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=pre,
+        num_acclimation_epochs=acc).cuda()
+
+
+def opts(m, lrB, lrA):
+    oA = torch.optim.Adam(m.gen_model[0].parameters(), lr=lrA, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    oB = torch.optim.Adam(m.gen_model[1].parameters(), lr=lrB, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    return oA, oB
+
+
+def data(N, seed):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(N, CFG["T"], CFG["p"]).astype(np.float32)
+    Y = np.zeros((N, CFG["K"], 1), np.float32)
+    Y[np.arange(N), rng.randint(0, CFG["K"], N), 0] = 10.0
+    X, Y = torch.from_numpy(X), torch.from_numpy(Y)
+    return [(X[i:i + 64], Y[i:i + 64]) for i in range(0, N, 64)]
+
+
+def test_packed_replicas_match_independent_fits():
+    from redcliff_amd import ReplicaPack
+    train = data(64 * 2 + 24, seed=3)  # two full batches + a ragged one
+    val = data(80, seed=4)
+    solo = [make(s, fc, adj) for s, fc, adj, _, _ in GRID]
+    solo_opts = [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA) in zip(solo, GRID)]
+    packed = [make(s, fc, adj) for s, fc, adj, _, _ in GRID]
+    pack = ReplicaPack(packed, [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA) in zip(packed, GRID)])
+    ds = pack.cache_dataset(train)
+    vds = pack.cache_dataset(val)
+    for epoch in (0, 1, 2, 3):  # pretrain-embedder, acclimate, combined, combined
+        pack.run_epoch(epoch, ds)
+        for m, (oA, oB) in zip(solo, solo_opts):
+            for bi, (Xb, Yb) in enumerate(train):
+                m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+    torch.cuda.synchronize()
+    losses, conf = pack.validate(vds)
+    for r, (m, mp) in enumerate(zip(solo, packed)):
+        a, b = m.state_dict(), mp.state_dict()
+        assert set(a) == set(b)
+        for k in a:
+            np.testing.assert_array_equal(b[k].cpu().numpy(), a[k].cpu().numpy(), err_msg="replica %d %s" % (r, k))
+        hist = [[] for _ in range(5)]
+        v = m.validate_training(val, 1, CFG["p"], *hist)
+        want = [v[0], v[1], v[2], v[3], v[4], v[5], v[9]]  # ..., adj, (3 DAG terms), combo
+        np.testing.assert_allclose(losses[r], want, rtol=1e-6, atol=1e-9, err_msg="replica %d losses" % r)
+    # the packed models remain ordinary drop-in modules afterwards
+    Xv = val[0][0][:8, :CFG["F"]].cuda()
+    solo[1].eval()
+    packed[1].eval()
+    with torch.no_grad():
+        g1 = solo[1].GC("conditional_factor_fixed_embedder", X=Xv, threshold=False, ignore_lag=False)
+        g2 = packed[1].GC("conditional_factor_fixed_embedder", X=Xv, threshold=False, ignore_lag=False)
+    np.testing.assert_array_equal(g2[3][2].cpu().numpy(), g1[3][2].cpu().numpy())
+
+
+def test_pack_rejects_mixed_shapes_and_phases():
+    from redcliff_amd import ReplicaPack
+    a = make(0, 10.0, 0.1)
+    b = make(1, 10.0, 0.1, pre=2)
+    pack = ReplicaPack([a, b], [opts(a, 5e-4, 5e-4), opts(b, 5e-4, 5e-4)])
+    ds = pack.cache_dataset(data(64, seed=1))
+    pack.run_epoch(0, ds)
+    with pytest.raises(RuntimeError, match="different training phases"):
+        pack.run_epoch(1, ds)
