@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 1
+#define REDCLIFF_ABI_VERSION 2
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -49,6 +49,9 @@ extern "C" {
 #define RC_CONFUSION     (1 << 8)  /* accumulate the factor-score confusion matrix (:786-803)    */
 #define RC_STORE_OUTPUTS (1 << 9)  /* run the factor forward even without a loss (model.forward)  */
 #define RC_REFRESH_SUPPORTS (1 << 10) /* recompute the DGCNN Chebyshev supports before the step  */
+#define RC_GRAD_ONLY     (1 << 11) /* data-parallel shard: write the gradients of the RC_STEP_*
+                                      groups to grad_emb / grad_fac instead of applying Adam
+                                      (redcliff_adam_apply runs after the all-reduce)            */
 
 /* Shapes shared by every call. */
 typedef struct RedcliffDims {
@@ -112,6 +115,14 @@ typedef struct RedcliffStepArgs {
   void* ws; size_t ws_bytes;                       /* workspace                        */
   double* acc;        /* [R][8] validation accumulators (may be NULL without RC_VALUES) */
   int32_t* confusion; /* [R][nsup][nsup] (may be NULL without RC_CONFUSION)              */
+  /* data-parallel shards: this call processes B of the B_global windows of
+   * the global batch.  Batch-mean terms (forecast MSE :629, factor MSE :638-661) and the
+   * BatchNorm running-variance correction use B_global; batch sums (fw-L1, adj-L1) do not
+   * scale, so the shard gradients of all ranks sum to the full-batch gradient.  bn_stats
+   * must be the statistics of the GLOBAL batch.  B_global == 0 means B_global = B.       */
+  int32_t B_global;
+  int32_t pad_;
+  float* grad_emb; float* grad_fac;  /* RC_GRAD_ONLY outputs, same layout/stride as emb / fac */
 } RedcliffStepArgs;
 
 int redcliff_abi_version(void);
@@ -167,6 +178,14 @@ int redcliff_gc_norms(const RedcliffDims* d, const float* fac, int64_t fac_strid
 /* In-place proximal step on layer-0 weights, penalty 0=GL 1=GSGL 2=H (models/cmlp.py:117-144). */
 int redcliff_prox(const RedcliffDims* d, float* fac, int64_t fac_stride, float lam, float lr, int32_t penalty,
                   void* stream);
+
+/* Adam (torch.optim.Adam, coupled L2, general_utils/model_utils.py:747-762) of one
+ * parameter group from a gradient buffer: group 0 = embedder (hyper[r].A), 1 = factors
+ * (hyper[r].B); n floats per replica at `stride`; t = 1-based step number.  The
+ * data-parallel step is  train_step(RC_GRAD_ONLY) -> all-reduce(grad) -> adam_apply. */
+int redcliff_adam_apply(const RedcliffDims* d, float* params, float* exp_avg, float* exp_avg_sq, const float* grad,
+                        int64_t n, int64_t stride, const RedcliffReplicaHyper* hyper, int32_t group, int32_t t,
+                        void* stream);
 
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()

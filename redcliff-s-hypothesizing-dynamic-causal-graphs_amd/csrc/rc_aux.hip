@@ -59,7 +59,40 @@ __global__ __launch_bounds__(RC_BLOCK) void k_prox(RedcliffDims d, float* fac, i
   }
 }
 
+// Adam from a gradient buffer (data-parallel step, after the all-reduce).  grid (ceil(n/1024), R),
+// 4 elements per thread, float4 loads when the rows are 16-byte aligned.
+__global__ __launch_bounds__(RC_BLOCK) void k_adam_apply(float* P, float* M, float* V, const float* G, int64_t n,
+                                                         int64_t stride, const RedcliffReplicaHyper* hyp, int group,
+                                                         int t) {
+  const int r = blockIdx.y;
+  const RcAdamScalars s = rc_adam_scalars(group == 0 ? hyp[r].A : hyp[r].B, t);
+  const int64_t off = (int64_t)r * stride;
+  const int64_t i0 = ((int64_t)blockIdx.x * RC_BLOCK + threadIdx.x) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = i0 + k;
+    if (i >= n) break;
+    float pp = P[off + i], mm = M[off + i], vv = V[off + i];
+    rc_adam(pp, mm, vv, G[off + i], s);
+    P[off + i] = pp; M[off + i] = mm; V[off + i] = vv;
+  }
+}
+
 }  // namespace
+
+extern "C" int redcliff_adam_apply(const RedcliffDims* d, float* params, float* exp_avg, float* exp_avg_sq,
+                                   const float* grad, int64_t n, int64_t stride, const RedcliffReplicaHyper* hyper,
+                                   int32_t group, int32_t t, void* stream) {
+  if (!d || !params || !exp_avg || !exp_avg_sq || !grad || !hyper || n < 0 || t < 1 || (group != 0 && group != 1)) {
+    rc_set_error("adam_apply: bad arguments");
+    return REDCLIFF_EINVAL;
+  }
+  if (n == 0) return 0;
+  const int64_t nb = (n + 4 * RC_BLOCK - 1) / (4 * RC_BLOCK);
+  hipLaunchKernelGGL(k_adam_apply, dim3((unsigned)nb, d->R), dim3(RC_BLOCK), 0, (hipStream_t)stream, params, exp_avg,
+                     exp_avg_sq, grad, n, stride, hyper, group, t);
+  return rc_check(hipGetLastError(), "k_adam_apply");
+}
 
 extern "C" int redcliff_gc_norms(const RedcliffDims* d, const float* fac, int64_t fac_stride, float* G, float* G0,
                                  void* stream) {

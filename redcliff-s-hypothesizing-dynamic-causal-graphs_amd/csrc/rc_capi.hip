@@ -141,13 +141,25 @@ static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
   }
   if ((a->flags & RC_VALUES) && !a->acc) { rc_set_error("RC_VALUES needs acc"); return REDCLIFF_EINVAL; }
   if ((a->flags & RC_CONFUSION) && d.nsup > 0 && !a->confusion) { rc_set_error("RC_CONFUSION needs confusion"); return REDCLIFF_EINVAL; }
-  if ((a->flags & (RC_STEP_A | RC_STEP_B)) && (!a->emb_m || !a->emb_v || !a->fac_m || !a->fac_v)) {
+  const bool grad_only = a->flags & RC_GRAD_ONLY;
+  if ((a->flags & (RC_STEP_A | RC_STEP_B)) && !grad_only && (!a->emb_m || !a->emb_v || !a->fac_m || !a->fac_v)) {
     rc_set_error("optimizer state missing");
+    return REDCLIFF_EINVAL;
+  }
+  if (grad_only && (((a->flags & RC_STEP_A) && !a->grad_emb) || ((a->flags & RC_STEP_B) && !a->grad_fac))) {
+    rc_set_error("RC_GRAD_ONLY needs grad_emb / grad_fac for the stepped groups");
+    return REDCLIFF_EINVAL;
+  }
+  if (a->B_global != 0 && a->B_global < a->B) {
+    rc_set_error("B_global=%d smaller than the shard B=%d", a->B_global, a->B);
     return REDCLIFF_EINVAL;
   }
   memset(&c, 0, sizeof(c));
   c.d = d;
   c.B = a->B;
+  c.Bg = a->B_global ? a->B_global : a->B;
+  c.gE = a->grad_emb;
+  c.gF = a->grad_fac;
   c.Lmax = rc_lmax(d);
   c.Ls = rc_ls(d);
   c.flags = a->flags;

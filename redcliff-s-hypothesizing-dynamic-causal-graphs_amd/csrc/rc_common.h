@@ -171,6 +171,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
 struct StepCtx {
   RedcliffDims d;
   int B, Lmax, Ls, flags, nbn;
+  int Bg;      // windows of the global batch (data-parallel normalisation; == B on one device)
   int tA, tB;  // Adam step numbers (1-based)
   const float* X; int64_t xr; int64_t row0;
   const float* lab; int64_t labr;
@@ -182,6 +183,7 @@ struct StepCtx {
   float* ws; int64_t wss;
   double* acc;
   int* conf;
+  float *gE, *gF;  // RC_GRAD_ONLY gradient outputs (emb / fac layouts)
   EmbOff eo;
   FacOff fo;
   WsOff wo;
@@ -336,6 +338,19 @@ __device__ inline void rc_adam(float& p, float& m, float& v, float g, const RcAd
   v = v * s.b2 + (s.omb2 * g) * g;
   const float denom = sqrtf(v) / s.bc2s + s.eps;
   p = p + s.neg_step * (m / denom);
+}
+
+// Apply Adam to element idx of a group, or (data-parallel shard, RC_GRAD_ONLY) store its
+// gradient for the all-reduce; weight decay is added by Adam, once, after the reduction.
+__device__ inline void rc_update(const StepCtx& c, float* P, float* M, float* V, float* G, int64_t idx, float g,
+                                 const RcAdamScalars& s) {
+  if (c.flags & RC_GRAD_ONLY) {
+    G[idx] = g;
+    return;
+  }
+  float pp = P[idx], mm = M[idx], vv = V[idx];
+  rc_adam(pp, mm, vv, g, s);
+  P[idx] = pp; M[idx] = mm; V[idx] = vv;
 }
 
 // Shared host-side helpers (defined in rc_capi.hip).

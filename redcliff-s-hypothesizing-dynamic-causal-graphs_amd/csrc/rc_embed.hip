@@ -179,7 +179,7 @@ __device__ inline float draw_value(const StepCtx& c, int r, int k, float raw, fl
     // score used by the factor MSE and the L1: class logits when supervised, else w
     const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
     float gsl = 0.f;
-    if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) gsl += hy.c_factor * (2.f / (float)(c.B * nsup)) * (sl - y);
+    if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) gsl += hy.c_factor * (2.f / (float)(c.Bg * nsup)) * (sl - y);
     if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
     if (nsup > 0)
       graw += sig ? gsl * sl * (1.f - sl) : gsl;
@@ -253,11 +253,11 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
     if (tid == 0) {
       const float* lp = ws + c.wo.lossp;
       double fore = 0.0;
-      for (int j = 0; j < p; ++j) fore += (double)lp[j] / (double)B;
+      for (int j = 0; j < p; ++j) fore += (double)lp[j] / (double)c.Bg;
       fore *= hy.c_forecast;
       double adj = 0.0;
       for (int e = 0; e < K * p; ++e) adj += lp[p + e];
-      const double factor = nsup > 0 ? hy.c_factor * fsum / (double)(B * nsup) : 0.0;
+      const double factor = nsup > 0 ? hy.c_factor * fsum / (double)(c.Bg * nsup) : 0.0;
       const double fwl1 = hy.c_fwl1 * (l1 - 1.0);
       const double cosv = hy.c_cos * cs;
       const double smooth = 0.0;  // num_sims == 1
@@ -744,9 +744,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       g = ws[c.wo.gfc1 + q];
       idx = c.eo.fc1W + q;
     }
-    float pp = E[idx], mm = Mm[idx], vv = V[idx];
-    rc_adam(pp, mm, vv, g, as);
-    E[idx] = pp; Mm[idx] = mm; V[idx] = vv;
+    rc_update(c, E, Mm, V, c.gE + r * c.es, idx, g, as);
     return;
   }
   // ---- adjacency workgroup
@@ -817,18 +815,18 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       float g = (A[e] > 0.f) ? (dL[e] * dinv[i] * dinv[j] + dd[i]) : 0.f;
       if (c.flags & RC_LOSS_ADJ)
         for (int k = 0; k < K; ++k) g += ws[c.wo.dAadj + (int64_t)k * pp2 + e];
-      float pv = A[e], mv = Mm[c.eo.A + e], vv = V[c.eo.A + e];
-      rc_adam(pv, mv, vv, g, as);
-      A[e] = pv; Mm[c.eo.A + e] = mv; V[c.eo.A + e] = vv;
+      rc_update(c, E, Mm, V, c.gE + r * c.es, c.eo.A + e, g, as);
     }
     __syncthreads();
-    dev_supports(A, ws + c.wo.S, dinv, p, n);
+    // supports for the next step (after a gradient-only shard step A changes later, in
+    // redcliff_adam_apply, and the host refreshes them)
+    if (!(c.flags & RC_GRAD_ONLY)) dev_supports(A, ws + c.wo.S, dinv, p, n);
   }
   // BatchNorm running statistics (torch: double math, momentum*stat + (1-momentum)*running)
   if (c.nbn > 0 && tid < F) {
     const double* st = c.bns + r * c.bnsr;
     const double mom = c.hyp[r].bn_momentum;
-    const double N = (double)c.B * p;
+    const double N = (double)c.Bg * p;  // unbiased correction over the global batch
     const double mean = st[tid], var_u = st[F + tid] * N / (N - 1.0);
     float rm = c.rm[r * F + tid], rv = c.rv[r * F + tid];
     for (int t = 0; t < c.nbn; ++t) {

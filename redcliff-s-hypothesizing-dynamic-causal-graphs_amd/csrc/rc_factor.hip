@@ -127,6 +127,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   float* P = c.fac + r * c.fs;
   float* PM = c.facM + r * c.fs;
   float* PV = c.facV + r * c.fs;
+  float* GF = c.gF + r * c.fs;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   float* tiles = ybuf + d.Bmax * d.K;
 
   // ---- part 1: mixture x_sim = sum_k w_k y_k, forecast residual, dL/dy and dL/dw (forecast)
-  const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)B) : 0.f;
+  const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
   // ybuf[b][k'] = sum over hidden chunks of the per-factor predictions (fixed order)
   rc_stage<2>(B * K, [&](int e) {
     const int b = dK.div(e), kk = e - b * K;
@@ -303,13 +304,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
       }
       const int64_t ib = c.fo.b0 + (int64_t)kj * h + u0 + tid;
       const int64_t iw = c.fo.W1 + (int64_t)kj * h + u0 + tid;
-      rc_adam(P[ib], PM[ib], PV[ib], g0, as);
-      rc_adam(P[iw], PM[iw], PV[iw], g1, as);
+      rc_update(c, P, PM, PV, GF, ib, g0, as);
+      rc_update(c, P, PM, PV, GF, iw, g1, as);
     }
-    if (uc == 0 && tid == 0) {
-      const int64_t i1 = c.fo.b1 + kj;
-      rc_adam(P[i1], PM[i1], PV[i1], db1, as);
-    }
+    if (uc == 0 && tid == 0) rc_update(c, P, PM, PV, GF, c.fo.b1 + kj, db1, as);
     __syncthreads();
   }
 
@@ -317,6 +315,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
   float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
   float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
+  float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
   float* dZs = tiles + 512;                  // [FB_BT][FAC_UC+1]
   float* Xs = dZs + FB_BT * (FAC_UC + 1);    // [FB_BT][FB_QT+1]
   float* w1s = Xs + FB_BT * (FB_QT + 1);     // [FAC_UC]
@@ -354,12 +353,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
         const int q = q0 + tq + 16 * jj;
         if (q >= Q) continue;
         const int64_t idx = (int64_t)u * Q + q;
-        float pw = W0[idx];
         float g = acc[jj];
-        if (adj_grad && Gs[q] > 0.f) g += dGs[q] * (pw / Gs[q]);
-        float mm = M0[idx], vv = V0[idx];
-        rc_adam(pw, mm, vv, g, as);
-        W0[idx] = pw; M0[idx] = mm; V0[idx] = vv;
+        if (adj_grad && Gs[q] > 0.f) g += dGs[q] * (W0[idx] / Gs[q]);
+        rc_update(c, W0, M0, V0, G0w, idx, g, as);
       }
     }
   }
@@ -406,6 +402,7 @@ extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const f
   c.d.Bmax = B;
   c.d.T = d->L;
   c.B = B;
+  c.Bg = B;
   c.Lmax = d->L;
   c.Ls = d->L;
   c.X = Xwin;

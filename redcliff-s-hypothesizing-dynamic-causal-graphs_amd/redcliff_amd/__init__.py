@@ -9,6 +9,8 @@ from .redcliff_factor_score_embedders import (DGCNN_Embedder, MLPClassifierForMu
 from .redcliff_s_cmlp import REDCLIFF_S_CMLP
 from .redcliff_s_cmlp_withStateSmoothing import REDCLIFF_S_CMLP_withStateSmoothing
 from .replicas import ReplicaPack
+from .data_parallel import DataParallelFit
 
 __all__ = ["MLP", "cMLP", "DGCNN", "DGCNN_Model", "DGCNN_Embedder", "cEmbedder", "MLPClassifierForSingleObjective",
-           "MLPClassifierForMultipleObjectives", "REDCLIFF_S_CMLP", "REDCLIFF_S_CMLP_withStateSmoothing", "ReplicaPack"]
+           "MLPClassifierForMultipleObjectives", "REDCLIFF_S_CMLP", "REDCLIFF_S_CMLP_withStateSmoothing", "ReplicaPack",
+           "DataParallelFit"]

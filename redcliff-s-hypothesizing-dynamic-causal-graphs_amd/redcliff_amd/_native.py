@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
@@ -23,6 +23,7 @@ VALUES = 1 << 7
 CONFUSION = 1 << 8
 STORE_OUTPUTS = 1 << 9
 REFRESH_SUPPORTS = 1 << 10
+GRAD_ONLY = 1 << 11
 
 WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt", "gfc1", "dwp", "dAadj", "dWi", "dS", "dgb", "S", "dZ", "amat",
               "lossp", "xsim", "gfc", "total")
@@ -30,7 +31,7 @@ WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
-            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times")
+            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final")
 
 
@@ -65,7 +66,8 @@ class StepArgs(ctypes.Structure):
                 ("bn_rm", _vp), ("bn_rv", _vp),
                 ("hyper", _vp),
                 ("ws", _vp), ("ws_bytes", ctypes.c_size_t),
-                ("acc", _vp), ("confusion", _vp)]
+                ("acc", _vp), ("confusion", _vp),
+                ("B_global", ctypes.c_int32), ("pad_", ctypes.c_int32), ("grad_emb", _vp), ("grad_fac", _vp)]
 
 
 def adam_hyper(lr, betas, eps, weight_decay):
@@ -105,6 +107,8 @@ def lib():
     L.redcliff_prox.argtypes = [ctypes.POINTER(Dims), _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_int32, _vp]
     L.redcliff_kernel_timing.argtypes = [ctypes.c_int32]
     L.redcliff_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64), ctypes.c_int32]
+    L.redcliff_adam_apply.argtypes = [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _i64, _i64, _vp, ctypes.c_int32,
+                                      ctypes.c_int32, _vp]
     for name in EXPORTED[2:]:
         if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count"):
             getattr(L, name).restype = ctypes.c_int

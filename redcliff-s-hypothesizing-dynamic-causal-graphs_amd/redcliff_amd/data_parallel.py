@@ -1,0 +1,126 @@
+"""Data-parallel REDCLIFF-S fitting for large recordings (BASELINE configs[3]).
+
+The reference fits one model per process (no torch.distributed anywhere).  For the LFP
+recordings (TST, many windows per subject) one fit is spread over the GPUs of a node:
+
+  * every rank holds the whole (device-resident) training set and the same model
+    (parameters broadcast from rank 0 at construction);
+  * each global batch of B windows is split into world_size contiguous shards; rank g runs
+    the fused step on its shard in gradient-only mode (RC_GRAD_ONLY) with B_global = B, so
+    batch-mean terms (forecast MSE :629, factor MSE :638-661) are scaled by 1/B and batch
+    sums (fw-L1 :666, adj-L1 :696-715) are not: the shard gradients sum to the full-batch
+    gradient.  The cos-sim penalty carries no gradient (metrics.py:380);
+  * BatchNorm uses the statistics of the GLOBAL batch (precomputed from the data, which
+    every rank has), so no SyncBN collective is needed and the running statistics advance
+    identically on every rank;
+  * one all-reduce (sum) of one flat fp32 gradient buffer per update (embedder + factor
+    groups, 0.4-0.9 MB at the published configs) over RCCL / xGMI, then the replicated Adam
+    update (redcliff_adam_apply) -- every rank ends every step with identical parameters.
+
+Works with any torch.distributed backend whose all_reduce takes device tensors ("nccl" =
+RCCL on ROCm for the real thing; "gloo" for tests on one GPU).
+"""
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native as nat
+from .engine import _stream, flags_for, phase_of_epoch
+from .kernels import ptr
+
+
+def shard_of(B, world, rank):
+    """Contiguous shard (offset, size) of rank `rank` in a batch of B windows: sizes differ by
+    at most one, the first B % world ranks take the extra window."""
+    base, extra = divmod(int(B), int(world))
+    size = base + (1 if rank < extra else 0)
+    off = rank * base + min(rank, extra)
+    return off, size
+
+
+class DataParallelFit:
+    """One REDCLIFF-S fit sharded over the ranks of `group` (default: the world)."""
+
+    def __init__(self, model, optimizerA, optimizerB, group=None):
+        if not dist.is_initialized():
+            raise RuntimeError("DataParallelFit needs torch.distributed.init_process_group first")
+        self.model = model
+        self.oA, self.oB = optimizerA, optimizerB
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.eng = eng = model.engine()
+        eng.ensure_bound()
+        eng.bind_optimizer("A", optimizerA)
+        eng.bind_optimizer("B", optimizerB)
+        # identical starting point on every rank (rank 0's parameters and BN buffers)
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        for t in (eng.emb, eng.fac, eng.bn):
+            dist.broadcast(t, src, group=group)
+        eng.invalidate()
+        self.PA, self.PB = eng.emb.numel(), eng.fac.numel()
+        self.grad = torch.zeros(self.PA + self.PB, device=eng.device, dtype=torch.float32)
+        self.gE, self.gF = self.grad[:self.PA], self.grad[self.PA:]
+        self.comm_bytes = 0
+
+    def cache_dataset(self, loader):
+        return self.eng.cache_dataset(loader)
+
+    def _step(self, kind, ds, bi):
+        eng = self.eng
+        flags, nbn = flags_for(kind, eng.nsup)
+        stepA, stepB = bool(flags & nat.STEP_A), bool(flags & nat.STEP_B)
+        B = int(ds["sizes"][bi])
+        off, Bl = shard_of(B, self.world, self.rank)
+        if Bl < 1:
+            raise ValueError("batch %d has %d windows for %d ranks: every rank needs at least one window"
+                             % (bi, B, self.world))
+        d = eng.workspace(ds["Bmax"], ds["T"])
+        stats = ds["stats"][bi:bi + 1] if flags & nat.BN_TRAIN else None
+        a = eng._args(d, flags | nat.GRAD_ONLY, nbn, ds["X"], ds["lab"], stats)
+        a.row0 = int(ds["rows"][bi]) + off
+        a.B = Bl
+        a.B_global = B
+        a.grad_emb, a.grad_fac = ptr(self.gE), ptr(self.gF)
+        nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "data-parallel shard step")
+        # one collective per update: the stepped groups' gradients, summed over ranks
+        buf = self.grad if (stepA and stepB) else (self.gE if stepA else self.gF)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
+        self.comm_bytes += buf.numel() * 4
+        hyp = eng._hyper()
+        d1 = eng.dims(ds["Bmax"], ds["T"])
+        for g, on, P, buf_g, n in (("A", stepA, eng.emb, self.gE, self.PA), ("B", stepB, eng.fac, self.gF, self.PB)):
+            if not on:
+                continue
+            st = eng.opt[g]
+            nat.check(nat.lib().redcliff_adam_apply(ctypes.byref(d1), ptr(P), ptr(st["m"]), ptr(st["v"]), ptr(buf_g),
+                                                    n, n, ptr(hyp), 0 if g == "A" else 1, st["t"] + 1, _stream()),
+                      "adam_apply")
+        eng._after(flags, nbn, 1)
+        eng.supports_fresh = False  # A moved after the step's own support refresh
+
+    def run_epoch(self, epoch, ds):
+        """The batch_update phase of `epoch` (...withStateSmoothing.py:741-759) over every global
+        batch of `ds`, sharded over the ranks."""
+        kinds = phase_of_epoch(self.model, epoch)
+        self.eng.conf.zero_()
+        for bi in range(int(ds["len"])):
+            for kind in kinds:
+                self._step(kind, ds, bi)
+        self.model._set_module_modes(kinds[-1] if kinds else None)
+
+    def train_confusion(self):
+        """Factor-score confusion matrix of the last epoch summed over ranks (:786-803)."""
+        c = self.eng.conf.clone()
+        dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
+        n = max(self.eng.nsup, 1)
+        return c.cpu().numpy().reshape(n, n)
+
+
+def global_batches(n_windows, B):
+    """(rows, sizes) of consecutive global batches, as the reference DataLoader yields them."""
+    rows = np.arange(0, n_windows, B, dtype=np.int64)
+    sizes = np.minimum(B, n_windows - rows).astype(np.int32)
+    return rows, sizes

@@ -1,0 +1,116 @@
+"""Data-parallel fit (redcliff_amd.DataParallelFit, SURVEY.md 8(e) / BASELINE configs[3]) on the
+GPU: two ranks (gloo, both on cuda:0 -- the box has one GPU; the product uses RCCL) each
+run the fused step on their shard in gradient-only mode, all-reduce the flat gradient and
+apply the replicated Adam.  Both ranks must end bit-identical, and equal the single-device
+full-batch fused fit within fp32 re-association of the gradient sum."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "redcliff-s-hypothesizing-dynamic-causal-graphs_amd")
+# TST-shaped (configs[3]) with smaller batches: p=12, L=4, K=9 (3 supervised), h=25, DGCNN 16/3/100
+CFG = dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, T=40, B=48, N=48 * 2 + 20)
+EPOCHS = (0, 1, 2, 3)  # pretrain-embedder, acclimate, combined, combined
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _model():
+    import redcliff_amd
+    c = CFG
+    K, p = c["K"], c["p"]
+    coeff = {"FORECAST_COEFF": 10.0, "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0 / sum(range(1, K)),
+             "FACTOR_WEIGHT_L1_COEFF": 1e-3, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0,
+             "ADJ_L1_REG_COEFF": 0.1 / K / np.sqrt(p * p - 1.0), "DAGNESS_REG_COEFF": 0.0, "DAGNESS_LAG_COEFF": 0.0,
+             "DAGNESS_NODE_COEFF": 0.0}
+    eargs = [("num_features_per_node", c["F"]), ("num_graph_conv_layers", c["n"]), ("num_hidden_nodes", c["H"]),
+             ("sigmoid_eccentricity_coeff", 10.0)]
+    torch.manual_seed(0)
+    m = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(
+        p, c["L"], [c["h"]], c["F"], [0], c["L"], 1, K, c["nsup"], coeff, False, "DGCNN", eargs,
+        "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
+        training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=1,
+        num_acclimation_epochs=1).cuda()
+    oA = torch.optim.Adam(m.gen_model[0].parameters(), lr=5e-4, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    oB = torch.optim.Adam(m.gen_model[1].parameters(), lr=5e-4, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    return m, oA, oB
+
+
+def _loader():
+    c = CFG
+    rng = np.random.RandomState(7)
+    X = rng.randn(c["N"], c["T"], c["p"]).astype(np.float32)
+    for t in range(2, c["T"]):
+        X[:, t] += 0.4 * X[:, t - 1] - 0.2 * X[:, t - 2]
+    Y = np.zeros((c["N"], c["K"], c["T"]), np.float32)
+    Y[np.arange(c["N"]), rng.randint(0, c["K"], c["N"]), :] = 1.0
+    X, Y = torch.from_numpy(X), torch.from_numpy(Y)
+    return [(X[i:i + c["B"]], Y[i:i + c["B"]]) for i in range(0, c["N"], c["B"])]
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from redcliff_amd import DataParallelFit
+    m, oA, oB = _model()
+    dp = DataParallelFit(m, oA, oB)
+    ds = dp.cache_dataset(_loader())
+    for epoch in EPOCHS:
+        dp.run_epoch(epoch, ds)
+    conf = dp.train_confusion()
+    torch.cuda.synchronize()
+    sd = dict((k, v.detach().cpu()) for k, v in m.state_dict().items())
+    torch.save({"state": sd, "conf": torch.from_numpy(conf)}, os.path.join(outdir, "rank%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_data_parallel_matches_full_batch(tmp_path):
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn",
+                       join=True)
+    r0 = torch.load(str(tmp_path / "rank0.pt"), weights_only=True)
+    r1 = torch.load(str(tmp_path / "rank1.pt"), weights_only=True)
+    for k in r0["state"]:
+        np.testing.assert_array_equal(r0["state"][k].numpy(), r1["state"][k].numpy(), err_msg="ranks differ: " + k)
+    # single-device, full-batch fused fit of the same model on the same batches
+    m, oA, oB = _model()
+    loader = _loader()
+    eng = m.engine()
+    ds = eng.cache_dataset(loader)
+    for epoch in EPOCHS:
+        eng.conf.zero_()
+        for bi, (Xb, Yb) in enumerate(loader):
+            m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+    conf = eng.conf.cpu().numpy().reshape(CFG["nsup"], CFG["nsup"])  # last epoch's counts
+    del ds
+    want = m.state_dict()
+    for k, v in want.items():
+        got = r0["state"][k].numpy().astype(np.float64)
+        w = v.detach().cpu().numpy().astype(np.float64)
+        if k.endswith("num_batches_tracked"):
+            assert int(got) == int(w), k
+            continue
+        tol = 5e-6 * max(1.0, np.abs(w).max()) + 2e-4 * np.abs(w)
+        bad = np.abs(got - w) > tol
+        assert not bad.any(), "%s: %d/%d off, max err %.3e" % (k, int(bad.sum()), w.size, np.abs(got - w).max())
+    np.testing.assert_array_equal(r0["conf"].numpy(), conf)
