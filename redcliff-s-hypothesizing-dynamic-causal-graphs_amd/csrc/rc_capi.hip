@@ -95,7 +95,7 @@ int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out
   if (check_dims(d) != 0) return REDCLIFF_EINVAL;
   const WsOff o = rc_ws_off(*d);
   const int64_t v[] = {o.T, o.R, o.f1, o.w, o.a, o.y, o.G, o.G0, o.w1, o.gq, o.ebp, o.ecnt, o.gfc1, o.dwp, o.dAadj, o.dWi, o.dS, o.dgb, o.S, o.dZ,
-                       o.amat, o.lossp, o.xsim, o.gfc, o.total};
+                       o.amat, o.lossp, o.xsim, o.gfc, o.xw, o.dyl, o.dgs, o.total};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_out && i < nv; ++i) out[i] = v[i];
   return nv;
@@ -197,8 +197,13 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   }
   if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd(c, s); }))) return e;
   if (fac) {
-    if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd(c, s); }))) return e;
-    if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
+    if (rc_fac_use_mfma(c.d)) {  // large p*L: grouped GEMMs on the matrix cores
+      if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd_mfma(c, s); }))) return e;
+      if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd_mfma(c, s); }))) return e;
+    } else {
+      if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd(c, s); }))) return e;
+      if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
+    }
   }
   if (emb_grad) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;

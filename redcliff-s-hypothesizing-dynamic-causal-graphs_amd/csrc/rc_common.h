@@ -43,6 +43,9 @@ struct WsOff {
   int64_t lossp;  // [p + K*p + 8]     per-batch loss partials
   int64_t xsim;   // [Bmax][p]         mixed forecast
   int64_t gfc;    // [K*M1 + K + M1]   fc2W / fc2b / fc1b gradients (applied in the final kernel)
+  int64_t xw;     // [Bmax][Qp]        factor input windows, q = c*L + t (MFMA path; Qp = Q rounded to 32)
+  int64_t dyl;    // [K*p][Bmax]       dL/d(prediction of network kj) per window (MFMA path)
+  int64_t dgs;    // [K*p][p*L]        adjacency-L1 gradient wrt the lagged group norms (MFMA path)
   int64_t total;
 };
 
@@ -116,6 +119,8 @@ __host__ __device__ inline int rc_emb_pstride(const RedcliffDims& d) {
 }
 
 inline int64_t rc_align64(int64_t x) { return (x + 63) & ~(int64_t)63; }
+// layer-0 contraction length p*L rounded up to the MFMA staging chunk
+__host__ __device__ inline int rc_qpad(const RedcliffDims& d) { return (d.p * d.L + 31) & ~31; }
 
 inline WsOff rc_ws_off(const RedcliffDims& d) {
   WsOff o;
@@ -145,6 +150,9 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.lossp = x; x = rc_align64(x + p + K * p + 8);
   o.xsim = x; x = rc_align64(x + B * p);
   o.gfc = x; x = rc_align64(x + K * d.M1 + K + d.M1);
+  o.xw = x; x = rc_align64(x + B * rc_qpad(d));
+  o.dyl = x; x = rc_align64(x + K * p * B);
+  o.dgs = x; x = rc_align64(x + K * p * p * d.L);
 #ifdef RC_TRACE
   x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
 #endif
@@ -361,6 +369,11 @@ int rc_check(hipError_t e, const char* what);
 int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s);
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s);
 int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
+// MFMA path of the factor networks (large p*L): window transpose, GEMM forward, per-network
+// mixing / penalties / small-parameter updates, GEMM dW0 + Adam.
+bool rc_fac_use_mfma(const RedcliffDims& d);
+int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s);
+int rc_launch_fac_bwd_mfma(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,

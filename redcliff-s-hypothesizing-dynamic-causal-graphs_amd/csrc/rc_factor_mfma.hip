@@ -1,0 +1,489 @@
+// rc_factor_mfma.hip -- the K x p factor networks as grouped GEMMs on the gfx950 matrix
+// cores, for layer-0 contractions long enough to pay off (the stress config p=64, L=20:
+// p*L = 1280, K*p*h = 12,800 hidden units; BASELINE configs[4]).
+//
+// Reference: models/cmlp.py:12-35 (MLP: Conv1d(p, h, L) -> ReLU -> Conv1d(h, 1, 1)),
+// models/cmlp.py:147-167 (group norms), ...withStateSmoothing.py:326-385 (x_sim mixing),
+// :629 (forecast MSE), :696-715 (lag-weighted adjacency L1 of w_bk G_k + A^T).
+//
+// With num_sims == 1 the factor forward is one GEMM  Z[b][(kj,u)] = sum_q Xw[b][q] W0[kj][u][q]
+// (B x p*L x K*p*h) and the layer-0 weight gradient another, dW0[kj][u][q] = sum_b dZ[b][(kj,u)]
+// Xw[b][q].  Both run on v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate: every product rounded
+// once, exactly an fmaf chain -- cdna_hip_programming.md §3): one 32-column block = one network
+// (hidden units padded to 32), so the bias / ReLU / output-layer epilogue and the Adam update
+// stay per network.  The small per-network work between the GEMMs (mixing, residual, penalty
+// gradients, output-layer updates) runs once per network in k_fac_mix instead of once per tile.
+//
+// Kernel chain: k_xwin (windows -> Xw[b][q], q = c*L + t) -> k_fac_fwd_mfma -> k_fac_mix ->
+// k_fac_bwd_mfma (dW0 GEMM + adjacency-L1 term + Adam epilogue).
+#include <cstdlib>
+#include <cstring>
+
+#include "rc_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define MF_BT 64   // windows per forward tile (2 row blocks of 32)
+#define MF_QC 32   // contraction chunk per staging step (16 MFMA k-steps)
+#define MB_QT 128  // dW0 columns per backward tile
+#define MB_BC 32   // windows per backward staging step
+
+__device__ inline float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Row index of accumulator register `reg` of lane `lane` in a 32x32 MFMA tile (columns = lane & 31).
+__device__ inline int mf_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+// ------------------------------------------------------------------------------------------
+// Window transpose: Xw[b][c*L + t] = X[row0 + b][Lmax - L + t][c], zero-padded to Qp columns.
+// grid (B, R); reads one contiguous L*p window, writes one Xw row.
+__global__ __launch_bounds__(RC_BLOCK) void k_xwin(StepCtx c) {
+  const int r = blockIdx.y, b = blockIdx.x;
+  const RedcliffDims& d = c.d;
+  const int L = d.L, p = d.p, Q = p * L, Qp = rc_qpad(d);
+  const float* src = c.X + r * c.xr + ((c.row0 + b) * d.T + (c.Lmax - L)) * p;
+  float* dst = c.ws + r * c.wss + c.wo.xw + (int64_t)b * Qp;
+  const RcDiv dp(p);
+  for (int e = threadIdx.x; e < Qp; e += RC_BLOCK) {
+    if (e < Q) {
+      const int t = dp.div(e), ch = e - t * p;
+      dst[ch * L + t] = src[e];
+    } else {
+      dst[e] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Forward GEMM.  grid (ceil(K*p/2), ceil(B/64), R); 4 waves: wave w owns rows 32*(w&1) of the
+// 64-row tile and network kj0 + (w>>1), one 32x32 accumulator.  The next chunk's operands are
+// loaded into registers while the current chunk's 16 MFMA k-steps run from LDS.
+// Epilogue: a = relu(z + b0) -> ws.a (backward), y = sum_u W1[u] a[u] + b1 -> ws.y chunk 0,
+// squared group norms gq[kj][q] = sum_u W0[u][q]^2 (first row block), W1 snapshot.
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.z;
+  const int kj0 = blockIdx.x * 2, b0 = blockIdx.y * MF_BT;
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p;
+  const float* P = c.fac + r * c.fs;
+  float* ws = c.ws + r * c.wss;
+  const float* Xw = ws + c.wo.xw;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nb = min(MF_BT, c.B - b0);
+
+  __shared__ float Xs[MF_BT][MF_QC + 1];
+  __shared__ float Ws[64][MF_QC + 1];  // [net*32 + u][q]
+
+  // staging maps: X 64x32 = 512 float4 (2 per thread); W 64x32 = 2048 floats (8 per thread)
+  float4 xr[2];
+  float wr[8];
+  auto load = [&](int q0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * RC_BLOCK, row = e >> 3, c4 = (e & 7) * 4;
+      xr[i] = row < nb ? ld4(Xw + (int64_t)(b0 + row) * Qp + q0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + i * RC_BLOCK, uu = e >> 5, qq = e & 31;
+      const int kj = kj0 + (uu >> 5), u = uu & 31, q = q0 + qq;
+      wr[i] = (kj < KP && u < h && q < Q) ? P[c.fo.W0 + ((int64_t)kj * h + u) * Q + q] : 0.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + i * RC_BLOCK, row = e >> 3, c4 = (e & 7) * 4;
+      Xs[row][c4] = xr[i].x;
+      Xs[row][c4 + 1] = xr[i].y;
+      Xs[row][c4 + 2] = xr[i].z;
+      Xs[row][c4 + 3] = xr[i].w;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + i * RC_BLOCK;
+      Ws[e >> 5][e & 31] = wr[i];
+    }
+  };
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const int arow = 32 * (wv & 1) + (lane & 31), bcol = 32 * (wv >> 1) + (lane & 31), kh = lane >> 5;
+  load(0);
+  for (int q0 = 0; q0 < Qp; q0 += MF_QC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (q0 + MF_QC < Qp) load(q0 + MF_QC);
+    if (blockIdx.y == 0 && tid < 64) {  // GC group norms of this chunk (pre-update weights)
+      const int kj = kj0 + (tid >> 5), q = q0 + (tid & 31);
+      if (kj < KP && q < Q) {
+        float sq = 0.f;
+        for (int u = 0; u < 32; ++u) {
+          const float w = Ws[(tid >> 5) * 32 + u][tid & 31];
+          sq += w * w;
+        }
+        ws[c.wo.gq + (int64_t)kj * Q + q] = sq;
+      }
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < MF_QC; k0 += 2) {
+      const float a = Xs[arow][k0 + kh];
+      const float bv = Ws[bcol][k0 + kh];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+    }
+  }
+  // ---- epilogue
+  const int kj = kj0 + (wv >> 1), u = lane & 31;
+  if (kj >= KP) return;
+  const int k = kj / p, j = kj - k * p;
+  const bool uv = u < h;
+  const float bu = uv ? P[c.fo.b0 + (int64_t)kj * h + u] : 0.f;
+  const float w1 = uv ? P[c.fo.W1 + (int64_t)kj * h + u] : 0.f;
+  const float b1 = P[c.fo.b1 + kj];
+  if (blockIdx.y == 0 && (wv & 1) == 0 && lane < 32 && uv) ws[c.wo.w1 + (int64_t)kj * h + u] = w1;
+  const int nU = rc_nuchunk(d);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int b = b0 + 32 * (wv & 1) + mf_row(reg, lane);
+    const float a = uv ? fmaxf(acc[reg] + bu, 0.f) : 0.f;
+    if (uv && b < c.B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+    float ys = w1 * a;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);  // within the 32-lane half
+    if ((lane & 31) < nU && b < c.B)  // chunk 0 holds the sum, the other hidden-chunk slots 0
+      ws[c.wo.y + (((int64_t)(lane & 31) * d.Bmax + b) * K + k) * p + j] = (lane & 31) == 0 ? ys + b1 : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-network work between the GEMMs.  grid (K*p, R), one workgroup per network kj:
+//   x_sim = sum_k w_k y_k, forecast residual, dL/dy (-> ws.dyl), dL/dw (forecast + adjacency
+//   terms, -> ws.dwp), group norms G / G0, adjacency-L1 value and its gradients wrt the
+//   lagged group norms (-> ws.dgs, used by the dW0 epilogue) and A (-> ws.dAadj), and the
+//   output-layer / hidden-bias gradients + Adam (b0, W1, b1).
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, kj = blockIdx.x;
+  const int p = d.p, h = d.h, K = d.K, L = d.L, Q = p * L, B = c.B;
+  const int k = kj / p, j = kj - k * p;
+  float* P = c.fac + r * c.fs;
+  float* PM = c.facM + r * c.fs;
+  float* PV = c.facV + r * c.fs;
+  float* GF = c.gF + r * c.fs;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const int tid = threadIdx.x;
+  const bool sig = d.use_sigmoid;
+  const float ecc = d.sigmoid_ecc;
+  const bool fgrad = (c.flags & RC_STEP_B) || (c.flags & RC_STEP_A);
+  const bool adj_grad = fgrad && (c.flags & RC_LOSS_ADJ);
+  const bool values = c.flags & RC_VALUES;
+  const int Ls = c.Ls;
+
+  extern __shared__ float sm[];
+  float* dyl = sm;             // [Bmax]
+  float* wk = dyl + d.Bmax;    // [Bmax]  w_bk (post-sigmoid)
+  float* Gs = wk + d.Bmax;     // [Q]
+  float* sqs = Gs + Q;         // [Q]
+  float* Acol = sqs + Q;       // [p]
+  float* lwt = Acol + p;       // [L]
+  float* red = lwt + L;        // [16]
+  float* dAp = red + 16;       // [p*Ls]
+  float* ybuf = dAp + p * Ls;  // [Bmax][K]
+  float* rA = ybuf + d.Bmax * K;  // [256]
+  float* rB = rA + RC_BLOCK;      // [256]
+
+  // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
+  const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
+  for (int e = tid; e < B * K; e += RC_BLOCK) {
+    const int b = e / K, kk = e - b * K;
+    ybuf[e] = ws[c.wo.y + ((int64_t)b * K + kk) * p + j];
+  }
+  __syncthreads();
+  float fsum = 0.f;
+  for (int b = tid; b < B; b += RC_BLOCK) {
+    const float* wr = ws + c.wo.w + (int64_t)b * K;
+    const bool tgt = c.flags & (RC_LOSS_FORECAST | RC_VALUES);
+    const float xt = tgt ? X[((c.row0 + b) * d.T + c.Lmax) * p + j] : 0.f;
+    float xs = 0.f;
+    for (int kk = 0; kk < K; ++kk) {
+      const float we = sig ? rc_sigmoid(ecc * wr[kk]) : wr[kk];
+      xs = (kk == 0) ? we * ybuf[b * K + kk] : xs + we * ybuf[b * K + kk];
+    }
+    const float res = tgt ? xs - xt : 0.f;
+    const float wb = sig ? rc_sigmoid(ecc * wr[k]) : wr[k];
+    const float g = gscale * res;
+    wk[b] = wb;
+    dyl[b] = g * wb;
+    ws[c.wo.dyl + (int64_t)kj * d.Bmax + b] = g * wb;
+    if (fgrad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = g * ybuf[b * K + k];
+    if (k == 0) {
+      fsum += res * res;
+      ws[c.wo.xsim + (int64_t)b * p + j] = xs;
+    }
+  }
+  if (values && k == 0) {
+    const float t = rc_block_sum(fsum, red);
+    if (tid == 0) ws[c.wo.lossp + j] = t;
+  }
+  // ---- group norms G[kj][c][t], G0[kj][c] (cmlp.py:147-167) from the forward's squared norms
+  for (int e = tid; e < Q; e += RC_BLOCK) {
+    const float sq = ws[c.wo.gq + (int64_t)kj * Q + e];
+    sqs[e] = sq;
+    Gs[e] = sqrtf(sq);
+    ws[c.wo.G + (int64_t)kj * Q + e] = Gs[e];
+  }
+  __syncthreads();
+  for (int cc = tid; cc < p; cc += RC_BLOCK) {
+    float sq = 0.f;
+    for (int t = 0; t < L; ++t) sq += sqs[cc * L + t];
+    ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
+  }
+  // ---- adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j]
+  const bool adj_on = adj_grad || values;
+  if (adj_on) {
+    for (int cc = tid; cc < p; cc += RC_BLOCK) Acol[cc] = E[c.eo.A + cc * p + j];
+    for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
+    __syncthreads();
+    float vsum = 0.f;
+    for (int b = tid; b < B; b += RC_BLOCK) {
+      const float wb = wk[b];
+      float t = 0.f, v = 0.f;
+      for (int cc = 0; cc < p; ++cc)
+        for (int i = 0; i < Ls; ++i) {
+          const float g = Gs[cc * L + (L - Ls + i)];
+          const float val = wb * g + Acol[cc];
+          t += lwt[i] * rc_sign(val) * g;
+          v += lwt[i] * fabsf(val);
+        }
+      if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] += hy.c_adj * t;
+      vsum += v;
+    }
+    if (values) {
+      const float t = rc_block_sum(vsum, red);
+      if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * t;
+    }
+  }
+  if (c.flags & RC_STEP_B) {  // dL/dG for the dW0 epilogue (zero outside the lag slice)
+    for (int q = tid; q < Q; q += RC_BLOCK) {
+      const int cc = q / L, t = q - cc * L, i = t - (L - Ls);
+      float v = 0.f;
+      if (adj_grad && i >= 0) {
+        const float g = Gs[q];
+        float sw = 0.f;
+        for (int b = 0; b < B; ++b) sw += rc_sign(wk[b] * g + Acol[cc]) * wk[b];
+        v = hy.c_adj * lwt[i] * sw;
+      }
+      ws[c.wo.dgs + (int64_t)kj * Q + q] = v;
+    }
+  }
+  if (adj_grad && (c.flags & RC_STEP_A)) {
+    for (int e = tid; e < p * Ls; e += RC_BLOCK) {
+      const int cc = e / Ls, i = e - cc * Ls;
+      const float g = Gs[cc * L + (L - Ls + i)];
+      float s1 = 0.f;
+      for (int b = 0; b < B; ++b) s1 += rc_sign(wk[b] * g + Acol[cc]);
+      dAp[e] = hy.c_adj * lwt[i] * s1;
+    }
+    __syncthreads();
+    for (int cc = tid; cc < p; cc += RC_BLOCK) {
+      float s = 0.f;
+      for (int i = 0; i < Ls; ++i) s += dAp[cc * Ls + i];
+      ws[c.wo.dAadj + ((int64_t)k * p + cc) * p + j] = s;  // d/dA[c][j]
+    }
+  }
+  if (!(c.flags & RC_STEP_B)) return;
+  __syncthreads();
+  // ---- output layer / hidden bias gradients + Adam: 32 units x 8 batch slices per pass
+  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
+  const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
+  const float* W1 = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by the forward
+  float db1 = 0.f;
+  for (int b = tid; b < B; b += RC_BLOCK) db1 += dyl[b];
+  db1 = rc_block_sum(db1, red);
+  for (int u0 = 0; u0 < h; u0 += 32) {
+    const int uu = tid & 31, part = tid >> 5, u = u0 + uu;
+    float dW1u = 0.f, db0u = 0.f;
+    if (u < h) {
+      const float w1 = W1[u];
+      for (int b = part; b < B; b += 8) {
+        const float av = aw[(int64_t)b * h + u];
+        dW1u += dyl[b] * av;
+        db0u += av > 0.f ? dyl[b] * w1 : 0.f;
+      }
+    }
+    __syncthreads();
+    rA[tid] = dW1u;
+    rB[tid] = db0u;
+    __syncthreads();
+    if (tid < 32 && u0 + tid < h) {
+      float g1 = 0.f, g0 = 0.f;
+      for (int s = 0; s < 8; ++s) {
+        g1 += rA[s * 32 + tid];
+        g0 += rB[s * 32 + tid];
+      }
+      rc_update(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + u0 + tid, g0, as);
+      rc_update(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + u0 + tid, g1, as);
+    }
+  }
+  if (tid == 0) rc_update(c, P, PM, PV, GF, c.fo.b1 + kj, db1, as);
+}
+
+// ------------------------------------------------------------------------------------------
+// dW0 GEMM + adjacency-L1 term + Adam.  grid (ceil(K*p/2), ceil(Q/128), R); wave w owns
+// network kj0 + (w&1) and dW0 columns [q0 + 64*(w>>1), +64) as two 32x32 accumulators
+// (rows = hidden units).  The batch is the contraction: chunks of 32 windows, dZ built on
+// the fly from the forward's activations, dL/dy and the W1 snapshot.
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.z;
+  const int kj0 = blockIdx.x * 2, q0 = blockIdx.y * MB_QT;
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p, B = c.B;
+  float* P = c.fac + r * c.fs;
+  float* PM = c.facM + r * c.fs;
+  float* PV = c.facV + r * c.fs;
+  float* GF = c.gF + r * c.fs;
+  const float* ws = c.ws + r * c.wss;
+  const float* Xw = ws + c.wo.xw;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+
+  __shared__ float Zs[2][MB_BC][33];      // dZ[net][b][u]
+  __shared__ float Xs[MB_BC][MB_QT + 4];  // Xw[b][q0 + .]
+  __shared__ float w1s[64];
+
+  if (tid < 64) {
+    const int kj = kj0 + (tid >> 5), u = tid & 31;
+    w1s[tid] = (kj < KP && u < h) ? ws[c.wo.w1 + (int64_t)kj * h + u] : 0.f;
+  }
+  // staging maps: dZ 2x32x32 = 2048 (8 per thread: net, b, u); X 32x128 = 1024 float4 (4 per thread)
+  float zr[8];
+  float4 xr[4];
+  auto load = [&](int bb0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31, u = e & 31;
+      const int kj = kj0 + net, b = bb0 + bb;
+      float v = 0.f;
+      if (kj < KP && u < h && b < B) {
+        const float av = ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u];
+        v = av > 0.f ? ws[c.wo.dyl + (int64_t)kj * d.Bmax + b] : 0.f;
+      }
+      zr[i] = v;  // times w1[u] at store time
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * RC_BLOCK, bb = e >> 5, c4 = (e & 31) * 4;
+      const int b = bb0 + bb, q = q0 + c4;
+      xr[i] = (b < B && q < Qp) ? ld4(Xw + (int64_t)b * Qp + q) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31, u = e & 31;
+      Zs[net][bb][u] = zr[i] * w1s[net * 32 + u];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * RC_BLOCK, bb = e >> 5, c4 = (e & 31) * 4;
+      Xs[bb][c4] = xr[i].x;
+      Xs[bb][c4 + 1] = xr[i].y;
+      Xs[bb][c4 + 2] = xr[i].z;
+      Xs[bb][c4 + 3] = xr[i].w;
+    }
+  };
+
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
+  const int net = wv & 1, qh = 64 * (wv >> 1), kh = lane >> 5, l31 = lane & 31;
+  load(0);
+  for (int bb0 = 0; bb0 < B; bb0 += MB_BC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (bb0 + MB_BC < B) load(bb0 + MB_BC);
+#pragma unroll
+    for (int k0 = 0; k0 < MB_BC; k0 += 2) {
+      const float a = Zs[net][k0 + kh][l31];  // A[i = u][k = b]
+      const float x0 = Xs[k0 + kh][qh + l31];  // B[k = b][j = q]
+      const float x1 = Xs[k0 + kh][qh + 32 + l31];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, x0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, x1, acc1, 0, 0, 0);
+    }
+  }
+  // ---- epilogue: + adjacency term through the group norms, then Adam (or store the gradient)
+  const int kj = kj0 + net;
+  if (kj >= KP) return;
+  const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
+  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
+  float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
+  float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
+  float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
+  float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int q = q0 + qh + 32 * half + l31;
+    if (q >= Q) continue;
+    float dg = 0.f, gn = 0.f;
+    if (adj_grad) {
+      dg = ws[c.wo.dgs + (int64_t)kj * Q + q];
+      gn = ws[c.wo.G + (int64_t)kj * Q + q];
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int u = mf_row(reg, lane);
+      if (u >= h) continue;
+      const int64_t idx = (int64_t)u * Q + q;
+      float g = half == 0 ? acc0[reg] : acc1[reg];
+      if (adj_grad && gn > 0.f) g += dg * (W0[idx] / gn);
+      rc_update(c, W0, M0, V0, G0w, idx, g, as);
+    }
+  }
+}
+
+size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
+  const int Q = d.p * d.L;
+  return sizeof(float) * (size_t)(2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + d.Bmax * d.K + 2 * RC_BLOCK);
+}
+
+}  // namespace
+
+// Path choice: the matrix-core path needs one 32-column block per network (h <= 32) and pays
+// off once the contraction is long; REDCLIFF_FAC_PATH=mfma|vector overrides (tests, tuning).
+bool rc_fac_use_mfma(const RedcliffDims& d) {
+  const char* v = getenv("REDCLIFF_FAC_PATH");  // read per call: tests switch paths in-process
+  const int env = !v ? 0 : (!strcmp(v, "mfma") ? 1 : (!strcmp(v, "vector") ? 2 : 0));
+  if (d.h > 32) return false;
+  if (env == 1) return true;
+  if (env == 2) return false;
+  return d.p * d.L >= 256;
+}
+
+int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int KP = d.K * d.p;
+  hipLaunchKernelGGL(k_xwin, dim3(c.B, d.R), dim3(RC_BLOCK), 0, s, c);
+  int e = rc_check(hipGetLastError(), "k_xwin");
+  if (e) return e;
+  hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((KP + 1) / 2, (c.B + MF_BT - 1) / MF_BT, d.R), dim3(RC_BLOCK), 0, s, c);
+  return rc_check(hipGetLastError(), "k_fac_fwd_mfma");
+}
+
+int rc_launch_fac_bwd_mfma(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int KP = d.K * d.p, Q = d.p * d.L;
+  const size_t lds = fac_mix_lds(d, c.Ls);
+  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor mixing: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  hipLaunchKernelGGL(k_fac_mix, dim3(KP, d.R), dim3(RC_BLOCK), lds, s, c);
+  int e = rc_check(hipGetLastError(), "k_fac_mix");
+  if (e || !(c.flags & RC_STEP_B)) return e;
+  hipLaunchKernelGGL(k_fac_bwd_mfma, dim3((KP + 1) / 2, (Q + MB_QT - 1) / MB_QT, d.R), dim3(RC_BLOCK), 0, s, c);
+  return rc_check(hipGetLastError(), "k_fac_bwd_mfma");
+}

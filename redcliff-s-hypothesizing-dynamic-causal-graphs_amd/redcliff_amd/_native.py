@@ -26,7 +26,7 @@ REFRESH_SUPPORTS = 1 << 10
 GRAD_ONLY = 1 << 11
 
 WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt", "gfc1", "dwp", "dAadj", "dWi", "dS", "dgb", "S", "dZ", "amat",
-              "lossp", "xsim", "gfc", "total")
+              "lossp", "xsim", "gfc", "xw", "dyl", "dgs", "total")
 
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",

@@ -186,8 +186,12 @@ def synth(cfg, N, seed):
     return torch.from_numpy(X), torch.from_numpy(Y)
 
 
-@pytest.mark.parametrize("cname", list(CONFIGS))
-def test_published_configs_three_phases_vs_oracle(cname):
+@pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1K4", "mfma"), ("C4", "mfma")])
+def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
+    """path "mfma" forces the matrix-core factor kernels (rc_factor_mfma.hip, normally chosen
+    for p*L >= 256) onto the published shapes."""
+    if path != "auto":
+        monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     cfg = CONFIGS[cname]
     o, m = oracle_and_hip(cfg)
     X, Y = synth(cfg, 2 * cfg["B"] + 40, seed=5)
