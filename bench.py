@@ -281,12 +281,17 @@ def main():
     fl = flops_per_window(c)
     roof = None
     if ktimes:
+        # timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch);
+        # on the matrix-core path "fac_fwd" = k_xwin + k_fac_fwd_mfma, "fac_bwd" = k_fac_mix + k_fac_bwd_mfma
+        mfma = ktimes.get("fac_fwd", (0, 0))[1] > 0
+        if not mfma:
+            fl["emb_fwd"] += fl["fac_fwd"]
         dom = max((k for k in ktimes if k != "supports"), key=lambda k: ktimes[k][0])
         avg_ms = ktimes[dom][0]
         flops = fl.get(dom, 0) * B
         achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-        kname = {"emb_fwd": "k_emb_fwd", "fac_fwd": "k_fac_fwd", "fac_bwd": "k_fac_bwd", "emb_bwd": "k_emb_bwd",
-                 "emb_final": "k_emb_final"}[dom]
+        kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_mfma", "fac_bwd": "k_fac_bwd_mfma" if mfma else "k_fac_bwd",
+                 "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final"}[dom]
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
                 "traffic": pmc_traffic(kname), "avg_launch_us": round(avg_ms * 1e3, 2),

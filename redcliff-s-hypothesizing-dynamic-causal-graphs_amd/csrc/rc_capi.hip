@@ -195,15 +195,14 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if ((e = timed(KT_SUPPORTS, s, [&] { return rc_launch_supports(c.d, c.emb, c.es, c.ws, c.wss, c.eo, c.wo, s); })))
       return e;
   }
-  if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd(c, s); }))) return e;
-  if (fac) {
-    if (rc_fac_use_mfma(c.d)) {  // large p*L: grouped GEMMs on the matrix cores
-      if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd_mfma(c, s); }))) return e;
-      if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd_mfma(c, s); }))) return e;
-    } else {
-      if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd(c, s); }))) return e;
-      if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
-    }
+  const bool mfma = fac && rc_fac_use_mfma(c.d);
+  // forward: embedder + vector-path factor networks share one launch ("fwd" timing slot)
+  if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_forward(c, s, true, fac && !mfma); }))) return e;
+  if (mfma) {  // large p*L: grouped GEMMs on the matrix cores
+    if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd_mfma(c, s); }))) return e;
+    if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd_mfma(c, s); }))) return e;
+  } else if (fac) {
+    if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
   }
   if (emb_grad) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;

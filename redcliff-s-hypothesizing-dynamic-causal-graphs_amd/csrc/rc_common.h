@@ -5,7 +5,7 @@
 #include "redcliff_hip.h"
 
 #define RC_BLOCK 256
-#define RC_TRACE_FLOATS 4096  // trace builds: u64 phase-timing slots at the end of the workspace
+#define RC_TRACE_FLOATS 32768  // trace builds: u64 timing slots at the end of the workspace (8 kernels x 2048)
 #define RC_LDS_LIMIT_FLOATS 16384  // 64 KiB of dynamic LDS per workgroup (several workgroups per CU)
 #define RC_LDS_MAX_FLOATS 40960    // 160 KiB: the whole CU's LDS, used only when a tile needs it (large p)
 
@@ -198,17 +198,34 @@ struct StepCtx {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Phase timing (trace builds, -DRC_TRACE): thread 0 of a workgroup stores wall_clock64()
-// (100 MHz) into u64 slot `slot` of the trace area at the end of the replica's workspace.
+// Workgroup timing (trace builds, -DRC_TRACE): thread 0 of workgroup x < 1024 of replica 0
+// stores wall_clock64() (100 MHz) at its start / end into u64 slot kid*2048 + 2x (+1) of the
+// trace area at the end of the workspace (scripts/phase_trace.py reads them back).
+#define RC_KID_EMB_FWD 0
+#define RC_KID_FAC_FWD 1
+#define RC_KID_FAC_BWD 2
+#define RC_KID_EMB_BWD 3
+#define RC_KID_EMB_FINAL 4
+#define RC_KID_FAC_MIX 5
 #ifdef RC_TRACE
-#define RC_MARK(wsbase, total, slot)                                                              \
+#define RC_WG_MARK(wsbase, total, kid, end)                                                        \
   do {                                                                                            \
-    if (threadIdx.x == 0)                                                                         \
-      reinterpret_cast<unsigned long long*>((wsbase) + (total) - RC_TRACE_FLOATS)[slot] = wall_clock64(); \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < 1024)               \
+      reinterpret_cast<unsigned long long*>((wsbase) + (total) - RC_TRACE_FLOATS)[(kid) * 2048 + 2 * blockIdx.x + (end)] = \
+          wall_clock64();                                                                         \
+  } while (0)
+// phase mark i of workgroup `bx` == 0 of replica 0 (slot 6*2048 + i)
+#define RC_PHASE(wsbase, total, bx, i)                                                            \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && (bx) == 0 && blockIdx.y == 0 && blockIdx.z == 0)                       \
+      reinterpret_cast<unsigned long long*>((wsbase) + (total) - RC_TRACE_FLOATS)[6 * 2048 + (i)] = wall_clock64(); \
   } while (0)
 #else
-#define RC_MARK(wsbase, total, slot) \
-  do {                               \
+#define RC_WG_MARK(wsbase, total, kid, end) \
+  do {                                      \
+  } while (0)
+#define RC_PHASE(wsbase, total, bx, i) \
+  do {                                 \
   } while (0)
 #endif
 
@@ -366,7 +383,8 @@ void rc_set_error(const char* fmt, ...);
 int rc_check(hipError_t e, const char* what);
 
 // Launchers implemented in the kernel translation units.
-int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s);
+// embedder forward and / or vector-path factor forward in one launch (rc_forward.hip)
+int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac);
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s);
 int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
 // MFMA path of the factor networks (large p*L): window transpose, GEMM forward, per-network

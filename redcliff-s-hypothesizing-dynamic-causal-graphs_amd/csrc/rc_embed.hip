@@ -42,127 +42,6 @@ __device__ void bn_affine(const StepCtx& c, int r, const float* E, float* alpha,
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// K1: embedder forward.  grid (ceil(B/SB), R); one workgroup handles SB windows with the
-// supports S_i and (when they fit) the graph-conv weights W_i staged in LDS.
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_fwd(StepCtx c, int SB, int w_lds) {
-  const RedcliffDims& d = c.d;
-  const int r = blockIdx.y;
-  const int b0 = blockIdx.x * SB;
-  const int nb = min(SB, c.B - b0);
-  if (nb <= 0) return;
-  const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
-  const int pF = p * F, pH = p * H, nFH = n * F * H;
-  const RcDiv dF(F), dp(p), dpF(pF), dnpF(n * pF), dpH(pH), dH(H);
-  const float* E = c.emb + r * c.es;
-  float* ws = c.ws + r * c.wss;
-  const float* X = c.X + r * c.xr;
-  const int tid = threadIdx.x;
-
-  extern __shared__ float sm[];
-  float* xs = sm;                      // [SB][p][F]   x_bn
-  float* Sl = xs + SB * pF;            // [n][p][p]
-  float* Wl = Sl + n * p * p;          // [n][F][H]    (w_lds)
-  float* Tl = Wl + (w_lds ? nFH : 0);  // [SB][n][p][F]
-  float* Rl = Tl + SB * n * pF;        // [SB][p*H]
-  float* f1l = Rl + SB * pH;           // [SB][M1]
-  float* alpha = f1l + SB * M1;
-  float* beta = alpha + F;
-
-  bn_affine(c, r, E, alpha, beta, nullptr, nullptr);
-  if (blockIdx.x == 0) {  // arrival counters of the embedder backward (they also self-reset)
-    unsigned* cnt = reinterpret_cast<unsigned*>(ws + c.wo.ecnt);
-    for (int e = tid; e < p * rc_nchunk(d); e += RC_BLOCK) cnt[e] = 0u;
-  }
-  const float* S = ws + c.wo.S;
-  for (int e = tid; e < n * p * p; e += RC_BLOCK) Sl[e] = S[e];
-  const float* gw = E + c.eo.gcW;
-  if (w_lds)
-    for (int e = tid; e < nFH; e += RC_BLOCK) Wl[e] = gw[e];
-  const float* Wsrc = w_lds ? Wl : gw;
-  __syncthreads();
-  // window rows are contiguous in the channel index: read (s, f, ch), store x_bn[s][ch][f]
-  for (int e = tid; e < nb * pF; e += RC_BLOCK) {
-    const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), ch = rem - f * p;
-    const float x = X[(c.row0 + b0 + s) * d.T * p + (int64_t)(c.Lmax - F + f) * p + ch];
-    xs[s * pF + ch * F + f] = x * alpha[f] + beta[f];
-  }
-  __syncthreads();
-  // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x))
-  for (int e = tid; e < nb * n * pF; e += RC_BLOCK) {
-    const int s = dnpF.div(e), rem = e - s * n * pF, i = dpF.div(rem), q = rem - i * pF, ch = dF.div(q), f = q - ch * F;
-    float v;
-    if (i == 0) {
-      v = xs[s * pF + q];
-    } else {
-      v = 0.f;
-      const float* Srow = Sl + (i * p + ch) * p;
-      const float* xc = xs + s * pF + f;
-      for (int cc = 0; cc < p; ++cc) v += Srow[cc] * xc[cc * F];
-    }
-    Tl[e] = v;
-    ws[c.wo.T + (int64_t)(b0 + s) * n * pF + rem] = v;
-  }
-  __syncthreads();
-  // Z = sum_i T_i W_i ; R = relu(Z)
-  for (int e = tid; e < nb * pH; e += RC_BLOCK) {
-    const int s = dpH.div(e), rem = e - s * pH, ch = dH.div(rem), hh = rem - ch * H;
-    float acc = 0.f;
-    for (int i = 0; i < n; ++i) {
-      const float* trow = Tl + (s * n + i) * pF + ch * F;
-      const float* wc = Wsrc + i * F * H + hh;
-      for (int f = 0; f < F; ++f) acc += trow[f] * wc[f * H];
-    }
-    const float v = fmaxf(acc, 0.f);
-    Rl[e] = v;
-    ws[c.wo.R + (int64_t)(b0 + s) * pH + rem] = v;
-  }
-  __syncthreads();
-  // fc1: wave wv owns rows [wv*RW, wv*RW+RW) (RW <= 16); lanes split the p*H contraction.
-  // All RW weight loads of a column step are issued together (one HBM/L2 latency per step).
-  const float* W1 = E + c.eo.fc1W;
-  const int lane = tid & 63, wv = tid >> 6;
-  const int RW = (M1 + 3) / 4, m0 = wv * RW;
-  float acc[16][4];
-#pragma unroll
-  for (int j = 0; j < 16; ++j)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc[j][s] = 0.f;
-  for (int q = lane; q < pH; q += 64) {
-    float w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = (j < RW && m0 + j < M1) ? W1[(int64_t)(m0 + j) * pH + q] : 0.f;
-    float rv[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[j][s] += w[j] * rv[s];
-  }
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int m = m0 + j;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float t = rc_wave_sum(acc[j][s]);
-      if (j < RW && m < M1 && s < nb && lane == 0) {
-        const float v = t + E[c.eo.fc1b + m];
-        f1l[s * M1 + m] = v;
-        ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = v;
-      }
-    }
-  }
-  __syncthreads();
-  for (int e = tid; e < nb * K; e += RC_BLOCK) {
-    const int s = e / K, k = e - s * K;
-    const float* w2 = E + c.eo.fc2W + (int64_t)k * M1;
-    float acc = 0.f;
-    for (int m = 0; m < M1; ++m) acc += w2[m] * fmaxf(f1l[s * M1 + m], 0.f);
-    ws[c.wo.w + (int64_t)(b0 + s) * K + k] = acc + E[c.eo.fc2b + k];
-  }
-}
-
 // dL/d(raw embedder output) of one window / factor: the factor-side gradient gw (sum of
 // the per-channel partials written by the factor kernel) plus the supervised-score MSE and
 // factor-weight L1 terms, through the optional sigmoid (compute_loss, :633-666).
@@ -345,10 +224,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
   float* xc = dTc + BC * nF;             // [BC][p][F]   raw window
 
   const RcDiv dF(F), dp(p), dpF(pF), dnF(nF), dK(K), dM1(M1);
-  const bool trace = (blockIdx.x == 0 && r == 0);
-#define NMARK(i) if (trace) RC_MARK(ws, c.wo.total, 256 + (i))
-  NMARK(0);
-  if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 600 + 2 * blockIdx.x);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 33);
   bn_affine(c, r, E, alpha, beta, mean, inv);
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
@@ -433,6 +309,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       rc_stage_all(sR, sT, sX, sF1, sW, sL, sD);
       __syncthreads();
     }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 34);
     for (int e = tid; e < nbc * K; e += RC_BLOCK) dr[e] = draw_value(c, r, dK.mod(e), wrl[e], dwl[e], labl[e]);
     __syncthreads();
     // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
@@ -444,7 +321,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       df1c[e] = g;
     }
     __syncthreads();
-    NMARK(1);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 35);
     // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
     for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
       const int s = e / HC, hh = e - s * HC;
@@ -490,7 +367,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       }
     }
     __syncthreads();
-    NMARK(2);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 36);
     // dW_i chunk partial: awi[i][f][hh] += sum_s T_i[s][f] dZ[s][hh]
     for (int s = 0; s < nbc; ++s) {
 #pragma unroll
@@ -513,7 +390,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       dTc[e] = t0 + t1;
     }
     __syncthreads();
-    NMARK(3);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 37);
     // dS_i[node][c'] (i >= 1) and BatchNorm affine partials, windows split over thread slices
     if (slS < nslS) {
       const int i = 1 + oS / p, cp = oS - (i - 1) * p;
@@ -543,6 +420,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       }
     }
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 38);
   // ---- publish this block's partials:
   //      [grp][wb][ afc M1*HC | awi nF*HC | dS nS | dgamma F | dbeta F | (group 0) dfc2W dfc2b dfc1b ]
   const int pst = rc_emb_pstride(d);
@@ -588,7 +466,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
     for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
     part[ofs_g + F + tid] = t;
   }
-  NMARK(4);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 39);
   // release (every wave drains its stores, one lane publishes at agent scope), then the ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -599,11 +477,11 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
     tk[0] = (int)__hip_atomic_fetch_add(&cnt[grp], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  NMARK(7);
   if (tk[0] != nbw - 1) {
-    if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 601 + 2 * blockIdx.x);
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
     return;
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 40);
   // ---- last arriver: acquire, then combine the nbw partials in window-block order
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -611,7 +489,6 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
     __hip_atomic_store(&cnt[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  NMARK(5);
   const float* base = ws + c.wo.ebp + (int64_t)grp * nbw_max * pst;
   float* dWi = ws + c.wo.dWi + (int64_t)node * n * F * H;
   float* gfc1 = ws + c.wo.gfc1;
@@ -642,9 +519,8 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       ws[c.wo.gfc + (e - ofs_h)] = t;                    // dfc2W | dfc2b | dfc1b
     }
   });
-  NMARK(6);
-  if (r == 0 && blockIdx.x < 700) RC_MARK(ws, c.wo.total, 601 + 2 * blockIdx.x);
-#undef NMARK
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 41);
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
 }
 
 // grid (p * nchunk * nbw [+ 1], R): workgroups [0, p*nchunk*nbw) are (node, column chunk,
@@ -655,8 +531,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int 
   const int r = blockIdx.y;
   const int nch = rc_nchunk(c.d);
   const int nbw = (c.B + WPB - 1) / WPB;
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 32);
   if ((int)blockIdx.x == nnode) {
     emb_bwd_head(c, r, sm);
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
   } else {
     const int grp = blockIdx.x / nbw, wb = blockIdx.x - grp * nbw;
     emb_bwd_node<MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
@@ -716,6 +595,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
   const int nFH = n * F * H, nfc = K * M1 + K + M1, nf1 = M1 * p * H;
   const int total = nFH + nfc + 2 * F + nf1;
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 0);
   if ((int)blockIdx.x < nw) {
     if (!stepA) return;
     const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
@@ -745,6 +625,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       idx = c.eo.fc1W + q;
     }
     rc_update(c, E, Mm, V, c.gE + r * c.es, idx, g, as);
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
     return;
   }
   // ---- adjacency workgroup
@@ -836,6 +717,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     c.rm[r * F + tid] = rm;
     c.rv[r * F + tid] = rv;
   }
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
 }
 
 // BatchNorm batch statistics for consecutive batches.  grid (nbatch, R).
@@ -875,39 +757,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bn_stats(RedcliffDims d, const flo
 
 // ------------------------------------------------------------------------------------------
 // host launchers
-static size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
-  const size_t pF = (size_t)d.p * d.F, pH = (size_t)d.p * d.H;
-  return SB * pF + (size_t)d.n * d.p * d.p + (w_lds ? (size_t)d.n * d.F * d.H : 0) + SB * d.n * pF + SB * pH +
-         (size_t)SB * d.M1 + 2 * d.F;
-}
-
 // Dynamic LDS above 64 KiB (up to the CU's 160 KiB) must be opted into per kernel.
 template <class Kern>
 static int rc_lds_optin(Kern k, size_t bytes, const char* what) {
   if (bytes <= RC_LDS_LIMIT_FLOATS * sizeof(float)) return 0;
   return rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)bytes), what);
-}
-
-int rc_launch_emb_fwd(const StepCtx& c, hipStream_t s) {
-  const RedcliffDims& d = c.d;
-  static const int sb_env = [] {
-    const char* v = getenv("REDCLIFF_EMB_SB");  // tuning knob: windows per forward workgroup
-    const int x = v ? atoi(v) : 0;
-    return (x >= 1 && x <= 4) ? x : 0;
-  }();
-  int SB = sb_env ? sb_env : 1, w_lds = 1;
-  size_t limit = RC_LDS_LIMIT_FLOATS;
-  while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > limit) --SB;
-  if (emb_fwd_floats(d, SB, w_lds) > limit) w_lds = 0;
-  if (emb_fwd_floats(d, SB, w_lds) > limit) limit = RC_LDS_MAX_FLOATS;  // large p*F: one workgroup per CU
-  if (emb_fwd_floats(d, SB, w_lds) > limit) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  const size_t lds = sizeof(float) * emb_fwd_floats(d, SB, w_lds);
-  int e = rc_lds_optin(k_emb_fwd, lds, "k_emb_fwd LDS");
-  if (e) return e;
-  dim3 grid((c.B + SB - 1) / SB, d.R);
-  hipLaunchKernelGGL(k_emb_fwd, grid, dim3(RC_BLOCK), lds, s, c, SB, w_lds);
-  return rc_check(hipGetLastError(), "k_emb_fwd");
 }
 
 size_t rc_emb_bwd_lds(const RedcliffDims& d) {

@@ -1,0 +1,373 @@
+// rc_forward.hip -- forward half of the fused REDCLIFF-S step on gfx950: the DGCNN embedder
+// and (vector path) the K x p factor networks, as ONE launch.
+//
+// The two forwards depend only on the window X and the parameters, so their workgroups share
+// a grid: blocks [0, nemb) run the embedder on SB windows each, blocks [nemb, nemb + nfac) run
+// one (factor, channel network, 16-unit hidden chunk) each.  One launch instead of two removes
+// a kernel boundary and overlaps the two latency chains (at D4IC both are single waves of
+// workgroups whose time is their own dependent global round trips).  Every workgroup issues
+// all of its global loads in one multi-segment staging pass before computing.
+//
+// Reference: models/redcliff_factor_score_embedders.py:335-392 + models/dgcnn.py:15-64 +
+// torcheeg 1.1.3 DGCNN (restated in oracle/torcheeg_dgcnn.py):
+//   x_bn = BN1(x); L = D^-1/2 relu(A) D^-1/2; Z = sum_i (S_i x_bn) W_i; w = fc2(relu(fc1(vec(relu(Z)))))
+// and models/cmlp.py:12-35 / :90-101 (MLP: Conv1d(p, h, L) -> ReLU -> Conv1d(h, 1, 1)),
+// models/cmlp.py:147-167 (group norms of layer-0 weights, pre-update).
+#include <cstdlib>
+
+#include "rc_common.h"
+
+namespace {
+
+#define FK_BT 128  // windows per factor-forward tile (16 row groups x 8)
+#define FQ_MAX 96  // layer-0 contraction staged in one pass up to this length
+
+__device__ inline int fq_tile(const RedcliffDims& d) { return d.p * d.L <= FQ_MAX ? d.p * d.L : 32; }
+
+// ------------------------------------------------------------------------------------------
+// Embedder forward of windows [bx*SB, bx*SB + SB).
+__device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float* sm) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y;
+  const int b0 = bx * SB;
+  const int nb = min(SB, c.B - b0);
+  if (nb <= 0) return;
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 0);
+  RC_PHASE(c.ws, c.wo.total, bx, 0);
+  const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
+  const int pF = p * F, pH = p * H, nFH = n * F * H;
+  const RcDiv dF(F), dp(p), dpF(pF), dnpF(n * pF), dpH(pH), dH(H);
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr;
+  const int tid = threadIdx.x;
+
+  float* xs = sm;                      // [SB][p][F]   raw window, then x_bn
+  float* Sl = xs + SB * pF;            // [n][p][p]
+  float* Wl = Sl + n * p * p;          // [n][F][H]    (w_lds)
+  float* Tl = Wl + (w_lds ? nFH : 0);  // [SB][n][p][F]
+  float* Rl = Tl + SB * n * pF;        // [SB][p*H]
+  float* f1l = Rl + SB * pH;           // [SB][M1]
+  float* fc2s = f1l + SB * M1;         // [K][M1]
+  float* fb1 = fc2s + K * M1;          // [M1]
+  float* fb2 = fb1 + M1;               // [K]
+  float* alpha = fb2 + K;              // [F]
+  float* beta = alpha + F;             // [F]
+
+  if (blockIdx.x == 0) {  // arrival counters of the embedder backward (they also self-reset)
+    unsigned* cnt = reinterpret_cast<unsigned*>(ws + c.wo.ecnt);
+    for (int e = tid; e < p * rc_nchunk(d); e += RC_BLOCK) cnt[e] = 0u;
+  }
+  // BatchNorm statistics (torch forms the scale in double in train mode), issued first
+  RC_PHASE(c.ws, c.wo.total, bx, 1);
+  const bool train = c.flags & RC_BN_TRAIN;
+  double st_mean = 0.0, st_var = 0.0;
+  float bw = 0.f, bb = 0.f;
+  if (tid < F) {
+    if (train) {
+      st_mean = c.bns[r * c.bnsr + tid];
+      st_var = c.bns[r * c.bnsr + F + tid];
+    } else {
+      st_mean = c.rm[r * F + tid];
+      st_var = c.rv[r * F + tid];
+    }
+    bw = E[c.eo.bnw + tid];
+    bb = E[c.eo.bnb + tid];
+  }
+  const float* S = ws + c.wo.S;
+  const float* gw = E + c.eo.gcW;
+  rc_stage_all(
+      rc_seg<1>(n * p * p, [&](int e) { return S[e]; }, [&](int e, float v) { Sl[e] = v; }),
+      rc_seg<8>(w_lds ? nFH : 0, [&](int e) { return gw[e]; }, [&](int e, float v) { Wl[e] = v; }),
+      // window rows are contiguous in the channel index: read (s, f, ch), store [s][ch][f]
+      rc_seg<4>(nb * pF, [&](int e) {
+        const int s = dpF.div(e), rem = e - s * pF;
+        return X[(c.row0 + b0 + s) * d.T * p + (int64_t)(c.Lmax - F) * p + rem];
+      }, [&](int e, float v) {
+        const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), ch = rem - f * p;
+        xs[s * pF + ch * F + f] = v;
+      }),
+      rc_seg<2>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
+      rc_seg<1>(M1 + K, [&](int e) { return e < M1 ? E[c.eo.fc1b + e] : E[c.eo.fc2b + e - M1]; },
+                [&](int e, float v) { fb1[e] = v; }));  // fb2 follows fb1
+  RC_PHASE(c.ws, c.wo.total, bx, 2);
+  if (tid < F) {
+    // torch CPU batch_norm: y = x * alpha + beta, alpha = invstd * gamma, beta = bias - mean * alpha
+    const float mean = (float)st_mean;
+    const float inv = train ? (float)(1.0 / sqrt(st_var + c.hyp[r].bn_eps))
+                            : 1.0f / sqrtf((float)st_var + (float)c.hyp[r].bn_eps);
+    const float a = inv * bw;
+    alpha[tid] = a;
+    beta[tid] = bb - mean * a;
+  }
+  __syncthreads();
+  for (int e = tid; e < nb * pF; e += RC_BLOCK) {
+    const int f = dF.mod(e);
+    xs[e] = xs[e] * alpha[f] + beta[f];
+  }
+  __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, bx, 3);
+  // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x))
+  for (int e = tid; e < nb * n * pF; e += RC_BLOCK) {
+    const int s = dnpF.div(e), rem = e - s * n * pF, i = dpF.div(rem), q = rem - i * pF, ch = dF.div(q), f = q - ch * F;
+    float v;
+    if (i == 0) {
+      v = xs[s * pF + q];
+    } else {
+      v = 0.f;
+      const float* Srow = Sl + (i * p + ch) * p;
+      const float* xc = xs + s * pF + f;
+      for (int cc = 0; cc < p; ++cc) v += Srow[cc] * xc[cc * F];
+    }
+    Tl[e] = v;
+    ws[c.wo.T + (int64_t)(b0 + s) * n * pF + rem] = v;
+  }
+  __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, bx, 4);
+  // fc1 weights of the first column step are issued before the graph convolution runs
+  const float* W1 = E + c.eo.fc1W;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int RW = (M1 + 3) / 4, m0 = wv * RW;
+  float wcur[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) wcur[j] = (j < RW && m0 + j < M1 && lane < pH) ? W1[(int64_t)(m0 + j) * pH + lane] : 0.f;
+  RC_PHASE(c.ws, c.wo.total, bx, 5);
+  // Z = sum_i T_i W_i ; R = relu(Z)
+  const float* Wsrc = w_lds ? Wl : gw;
+  for (int e = tid; e < nb * pH; e += RC_BLOCK) {
+    const int s = dpH.div(e), rem = e - s * pH, ch = dH.div(rem), hh = rem - ch * H;
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains hide the LDS latency
+    for (int i = 0; i < n; ++i) {
+      const float* trow = Tl + (s * n + i) * pF + ch * F;
+      const float* wc = Wsrc + i * F * H + hh;
+      int f = 0;
+      for (; f + 3 < F; f += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a4[u] += trow[f + u] * wc[(f + u) * H];
+      }
+      for (; f < F; ++f) a4[0] += trow[f] * wc[f * H];
+    }
+    const float v = fmaxf((a4[0] + a4[1]) + (a4[2] + a4[3]), 0.f);
+    Rl[e] = v;
+    ws[c.wo.R + (int64_t)(b0 + s) * pH + rem] = v;
+  }
+  __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, bx, 6);
+  // fc1: wave wv owns rows [wv*RW, wv*RW+RW) (RW <= 16); lanes split the p*H contraction.
+  // The next column step's weights are loaded while the current one is multiplied.
+  float acc[16][4];
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[j][s] = 0.f;
+  for (int q = lane; q < pH; q += 64) {
+    float wnext[16];
+    const int qn = q + 64;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) wnext[j] = (j < RW && m0 + j < M1 && qn < pH) ? W1[(int64_t)(m0 + j) * pH + qn] : 0.f;
+    float rv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[j][s] += wcur[j] * rv[s];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) wcur[j] = wnext[j];
+  }
+  // reduce-scatter of the 16 row partials over the 64 lanes: 17 shuffles per window instead of
+  // 16 full reductions (96); afterwards lane l holds row (l >> 2) & 15 in every lane of its quad
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s >= nb) break;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = acc[j][s];
+#pragma unroll
+    for (int half = 8; half >= 1; half >>= 1) {
+      const int off = half * 4;  // lane bit that selects the kept half: 32, 16, 8, 4
+      const bool hi = lane & off;
+#pragma unroll
+      for (int i = 0; i < half; ++i) {
+        const float send = hi ? v[i] : v[i + half];
+        const float keep = hi ? v[i + half] : v[i];
+        v[i] = keep + __shfl_xor(send, off, 64);
+      }
+    }
+    float t = v[0];
+    t += __shfl_xor(t, 2, 64);
+    t += __shfl_xor(t, 1, 64);
+    const int j = (lane >> 2) & 15, m = m0 + j;
+    if ((lane & 3) == 0 && j < RW && m < M1) {
+      const float val = t + fb1[m];
+      f1l[s * M1 + m] = val;
+      ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = val;
+    }
+  }
+  __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, bx, 7);
+  for (int e = tid; e < nb * K; e += RC_BLOCK) {
+    const int s = e / K, k = e - s * K;
+    const float* w2 = fc2s + k * M1;
+    float a = 0.f;
+    for (int m = 0; m < M1; ++m) a += w2[m] * fmaxf(f1l[s * M1 + m], 0.f);
+    ws[c.wo.w + (int64_t)(b0 + s) * K + k] = a + fb2[k];
+  }
+  RC_PHASE(c.ws, c.wo.total, bx, 8);
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 1);
+}
+
+size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
+  const size_t pF = (size_t)d.p * d.F, pH = (size_t)d.p * d.H;
+  return SB * pF + (size_t)d.n * d.p * d.p + (w_lds ? (size_t)d.n * d.F * d.H : 0) + SB * d.n * pF + SB * pH +
+         (size_t)SB * d.M1 + (size_t)d.K * d.M1 + d.M1 + d.K + 2 * d.F;
+}
+
+// ------------------------------------------------------------------------------------------
+// Factor forward of one (factor, channel network, FAC_UC-unit hidden chunk): relu activations
+// a[kj][b][u], partial outputs y[uc][b][k][j] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk
+// 0), the chunk's squared layer-0 group norms gq[uc][kj][q] and a snapshot of W1.
+// The whole window block and weight chunk are staged in one pass when p*L <= FQ_MAX.
+__device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
+  const int L = c.d.L;
+  const int ch = dL.div(q), t = q - ch * L;
+  return X[((c.row0 + b) * c.d.T + (c.Lmax - L + t)) * c.d.p + ch];
+}
+
+__device__ void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
+  const RedcliffDims& d = c.d;
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 0);
+  const int nU = rc_nuchunk(d);
+  const int r = blockIdx.y, kj = bx / nU, uc = bx - kj * nU;
+  const int p = d.p, h = d.h, K = d.K;
+  const int k = kj / p, j = kj - k * p;
+  const int Q = p * d.L, QT = fq_tile(d), QP = QT + 1;
+  const int u0 = uc * FAC_UC;
+  const float* P = c.fac + r * c.fs;
+  const float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
+  const float* b0 = P + c.fo.b0 + (int64_t)kj * h;
+  const float* W1 = P + c.fo.W1 + (int64_t)kj * h;
+  const float b1 = uc == 0 ? P[c.fo.b1 + kj] : 0.f;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr;
+  const int tid = threadIdx.x, tb = tid >> 4, tu = tid & 15;
+  const int u = u0 + tu;
+  const RcDiv dL(d.L), dQT(QT);
+  float* Xs = sm;                // [FK_BT][QT+1]
+  float* Ws = Xs + FK_BT * QP;   // [FAC_UC][QT+1]
+  const float bu = u < h ? b0[u] : 0.f, w1 = u < h ? W1[u] : 0.f;
+
+  for (int bc = 0; bc < c.B; bc += FK_BT) {
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int q0 = 0; q0 < Q; q0 += QT) {
+      if (q0 > 0 || bc > 0) __syncthreads();
+      rc_stage_all(
+          rc_seg<24>(FK_BT * QT, [&](int e) {
+            const int bb = dQT.div(e), qq = e - bb * QT;
+            const int b = bc + bb, q = q0 + qq;
+            return (b < c.B && q < Q) ? xwin(c, dL, X, b, q) : 0.f;
+          }, [&](int e, float v) { Xs[dQT.div(e) * QP + dQT.mod(e)] = v; }),
+          rc_seg<4>(FAC_UC * QT, [&](int e) {
+            const int uu = dQT.div(e), qq = e - uu * QT;
+            const int q = q0 + qq;
+            return (u0 + uu < h && q < Q) ? W0[(int64_t)(u0 + uu) * Q + q] : 0.f;
+          }, [&](int e, float v) { Ws[dQT.div(e) * QP + dQT.mod(e)] = v; }));
+      __syncthreads();
+      if (bc == 0)
+        for (int qq = tid; qq < QT && q0 + qq < Q; qq += RC_BLOCK) {
+          // squared group norms of the chunk's 16 units (GC, models/cmlp.py:162-166), pre-update
+          float sq = 0.f;
+          for (int uu = 0; uu < FAC_UC; ++uu) {
+            const float w = Ws[uu * QP + qq];
+            sq += w * w;
+          }
+          ws[c.wo.gq + ((int64_t)uc * K * p + kj) * Q + q0 + qq] = sq;
+        }
+      const int qn = min(QT, Q - q0);
+#pragma unroll 8
+      for (int qq = 0; qq < qn; ++qq) {
+        const float wv = Ws[tu * QP + qq];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += Xs[(tb + 16 * i) * QP + qq] * wv;
+      }
+    }
+    if (bc == 0 && tb == 0 && u < h) ws[c.wo.w1 + (int64_t)kj * h + u] = w1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int b = bc + tb + 16 * i;
+      float ys = 0.f;
+      if (u < h) {
+        const float a = fmaxf(acc[i] + bu, 0.f);
+        if (b < c.B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+        ys = w1 * a;
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);
+      if (tu == 0 && b < c.B) ws[c.wo.y + (((int64_t)uc * d.Bmax + b) * K + k) * p + j] = ys + b1;
+    }
+  }
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 1);
+}
+
+size_t fac_fwd_floats(const RedcliffDims& d) {
+  const int QT = d.p * d.L <= FQ_MAX ? d.p * d.L : 32;
+  return (size_t)(FK_BT + FAC_UC) * (QT + 1);
+}
+
+// grid (nemb + nfac, R): embedder blocks first, then factor blocks.
+__global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_lds, int nemb) {
+  extern __shared__ float sm[];
+  if ((int)blockIdx.x < nemb)
+    emb_fwd_body(c, blockIdx.x, SB, w_lds, sm);
+  else
+    fac_fwd_body(c, blockIdx.x - nemb, sm);
+}
+
+}  // namespace
+
+// Dynamic LDS above 64 KiB (up to the CU's 160 KiB) must be opted into per kernel.
+template <class Kern>
+static int lds_optin(Kern k, size_t bytes, const char* what) {
+  if (bytes <= RC_LDS_LIMIT_FLOATS * sizeof(float)) return 0;
+  return rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)bytes), what);
+}
+
+// One launch of the embedder forward (with_emb) and / or the vector-path factor forward (with_fac).
+int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac) {
+  const RedcliffDims& d = c.d;
+  int SB = 1, w_lds = 1, nemb = 0;
+  size_t lds = 0;
+  if (with_emb) {
+    static const int sb_env = [] {
+      const char* v = getenv("REDCLIFF_EMB_SB");  // tuning knob: windows per forward workgroup
+      const int x = v ? atoi(v) : 0;
+      return (x >= 1 && x <= 4) ? x : 0;
+    }();
+    SB = sb_env ? sb_env : 1;
+    size_t limit = RC_LDS_LIMIT_FLOATS;
+    while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > limit) --SB;
+    if (emb_fwd_floats(d, SB, w_lds) > limit) w_lds = 0;
+    if (emb_fwd_floats(d, SB, w_lds) > limit) limit = RC_LDS_MAX_FLOATS;  // large p*F: one workgroup per CU
+    if (emb_fwd_floats(d, SB, w_lds) > limit) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+    lds = emb_fwd_floats(d, SB, w_lds);
+    nemb = (c.B + SB - 1) / SB;
+  }
+  int nfac = 0;
+  if (with_fac) {
+    if (d.h > 128 || d.p * d.L > 4096) { rc_set_error("factor forward: h <= 128 and p*L <= 4096 required"); return REDCLIFF_ELIMIT; }
+    nfac = d.K * d.p * rc_nuchunk(d);
+    const size_t f = fac_fwd_floats(d);
+    lds = f > lds ? f : lds;
+  }
+  if (nemb + nfac == 0) return 0;
+  lds *= sizeof(float);
+  int e = lds_optin(k_forward, lds, "k_forward LDS");
+  if (e) return e;
+  hipLaunchKernelGGL(k_forward, dim3(nemb + nfac, d.R), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb);
+  return rc_check(hipGetLastError(), "k_forward");
+}
+
+int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s) { return rc_launch_forward(c, s, false, true); }

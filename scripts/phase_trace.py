@@ -1,10 +1,10 @@
-"""Per-phase wall-clock breakdown of the fused step (trace build, -DRC_TRACE).
+"""Per-kernel workgroup timing of the fused step (trace build, -DRC_TRACE).
 
     python scripts/phase_trace.py [--config d4ic]
 
 Loads libredcliff_hip_trace.so, runs a few combined-phase steps of bench.py's workload and
-prints the deltas between the RC_MARK slots (100 MHz wall clock) of the last step.
-Slot map: 256+i = embedder-backward node workgroup 0 (i = 0..7); 600+2b / 601+2b = start / end of node block b.
+prints, for the last step, each kernel's start (relative to the first), span, start spread
+of its workgroups and their duration distribution (RC_WG_MARK slots, 100 MHz wall clock).
 """
 import argparse
 import os
@@ -43,23 +43,25 @@ def main():
     eng.run_steps(["combined"], ds["X"], ds["lab"], stats, d, ds["rows"][idx], ds["sizes"][idx], oA, oB)
     torch.cuda.synchronize()
     tot = eng.ws_off["total"]
-    tr = eng.ws[tot - 4096:tot].cpu().numpy().view(np.uint64).astype(np.int64)
-    def span(lo, hi, label):
-        t = tr[lo:hi]
-        print("%s:" % label)
-        for i in range(1, len(t)):
-            if t[i] and t[i - 1]:
-                print("  mark %d -> %d : %8.2f us" % (lo + i - 1, lo + i, (t[i] - t[i - 1]) / 100.0))
-    span(256, 264, "emb_bwd node WG 0 (marks 5/6 only if it arrived last; 7 = ticket)")
-    se = tr[600:2000].reshape(-1, 2)
-    se = se[(se[:, 0] > 0) & (se[:, 1] > 0)]
-    if len(se):
-        t0 = se[:, 0].min()
-        dur = (se[:, 1] - se[:, 0]) / 100.0
-        print("emb_bwd node blocks: %d traced; start spread %.2f us; end max %.2f us after first start" % (
-            len(se), (se[:, 0].max() - se[:, 0].min()) / 100.0, (se[:, 1].max() - t0) / 100.0))
-        print("  duration min/median/max %.2f / %.2f / %.2f us" % (dur.min(), np.median(dur), dur.max()))
-
+    tr = eng.ws[tot - 32768:tot].cpu().numpy().view(np.uint64).astype(np.int64).reshape(8, 2048)
+    names = ["emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix"]
+    t_first = min(int(tr[k][0::2][tr[k][0::2] > 0].min()) for k in range(len(names)) if (tr[k][0::2] > 0).any())
+    ph = tr[6]
+    for lo, hi, label in ((0, 16, "emb_fwd WG0 phases"), (16, 32, "fac_bwd WG0 phases"), (32, 48, "emb_bwd WG0 phases")):
+        t = ph[lo:hi]
+        idx = [i for i in range(hi - lo) if t[i] > 0]
+        if len(idx) > 1:
+            print(label + ": " + "  ".join("%d->%d %.2f" % (lo + a, lo + b, (t[b] - t[a]) / 100.0) for a, b in zip(idx, idx[1:])))
+    for k, name in enumerate(names):
+        st, en = tr[k][0::2], tr[k][1::2]
+        ok = (st > 0) & (en > 0)
+        if not ok.any():
+            continue
+        st, en = st[ok], en[ok]
+        dur = (en - st) / 100.0
+        print("%-9s WGs %4d  start %7.2f us  span %7.2f us  start spread %6.2f  WG dur min/med/max %6.2f %6.2f %6.2f"
+              % (name, ok.sum(), (st.min() - t_first) / 100.0, (en.max() - st.min()) / 100.0,
+                 (st.max() - st.min()) / 100.0, dur.min(), np.median(dur), dur.max()))
 
 
 if __name__ == "__main__":
