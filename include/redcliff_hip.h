@@ -187,6 +187,15 @@ int redcliff_adam_apply(const RedcliffDims* d, float* params, float* exp_avg, fl
                         int64_t n, int64_t stride, const RedcliffReplicaHyper* hyper, int32_t group, int32_t t,
                         void* stream);
 
+/* Batched fp32 GEMM, row-major: C[b] = alpha * op(A[b]) op(B[b]) + beta * C[b], op = X or X^T
+ * (trans flag), A/B/C of batch b at X + b * stride_x.  The contraction of the generic
+ * (non-fused) path: cEmbedder / Vanilla embedders (models/redcliff_factor_score_embedders.py:
+ * 51-331), num_sims > 1 roll-outs and the per-step weighting forward mode
+ * (models/redcliff_s_cmlp_withStateSmoothing.py:253-323), composed on the host with autograd. */
+int redcliff_gemm(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_t K, float alpha, const float* A,
+                  int64_t lda, int64_t stride_a, const float* B, int64_t ldb, int64_t stride_b, float beta, float* C,
+                  int64_t ldc, int64_t stride_c, int32_t batch, void* stream);
+
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()
  * synchronises them and returns per-kernel totals (ids 0..5: supports, emb_fwd, fac_fwd,

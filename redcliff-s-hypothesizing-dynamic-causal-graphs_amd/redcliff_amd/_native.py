@@ -31,7 +31,7 @@ WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
-            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply")
+            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final")
 
 
@@ -109,6 +109,9 @@ def lib():
     L.redcliff_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64), ctypes.c_int32]
     L.redcliff_adam_apply.argtypes = [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _i64, _i64, _vp, ctypes.c_int32,
                                       ctypes.c_int32, _vp]
+    L.redcliff_gemm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.c_float, _vp, _i64, _i64, _vp, _i64, _i64, ctypes.c_float, _vp, _i64, _i64,
+                                ctypes.c_int32, _vp]
     for name in EXPORTED[2:]:
         if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count"):
             getattr(L, name).restype = ctypes.c_int

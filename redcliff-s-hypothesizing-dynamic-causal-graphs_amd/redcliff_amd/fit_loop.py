@@ -47,7 +47,8 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
         raise NotImplementedError("prior-initialised factors (prior_factors_path) are not on the fused path")
     if output_length != 1:
         raise NotImplementedError("output_length must be 1")
-    eng = model.engine()
+    fused = model.fused_supported()
+    eng = model.engine() if fused else None
     nsup, K, p = model.num_supervised_factors, model.num_factors_nK, model.num_chans
     thresholds = [0.0]
     h = dict((k, []) for k in HIST_KEYS)
@@ -73,18 +74,27 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
             h[k] = list(getattr(model, "chkpt_" + k))[:iter_start]
         best_loss, best_it = model.chkpt_best_loss, model.chkpt_best_it
 
-    train = eng.cache_dataset(X_train)
-    val = eng.cache_dataset(X_val)
-    d_train = eng.workspace(max(train["Bmax"], val["Bmax"]), train["T"])
+    if fused:
+        train = eng.cache_dataset(X_train)
+        val = eng.cache_dataset(X_val)
+        d_train = eng.workspace(max(train["Bmax"], val["Bmax"]), train["T"])
     Lm = model.Lmax
 
     for it in range(iter_start, max_iter):
         if verbose:
             print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
         kinds = phase_of_epoch(model, it)
-        eng.conf.zero_()
-        d_train = eng.workspace(train["Bmax"], train["T"])
-        if len(kinds) == 1:
+        if not fused:  # generic path: the reference's batch loop (...withStateSmoothing.py:1331-1364)
+            cm = np.zeros((max(nsup, 1), max(nsup, 1)))
+            for bi, (Xb, Yb) in enumerate(X_train):
+                model.batch_update(it, bi, Xb, Yb, oA, oB, output_length,
+                                   running_factor_score_confusion_matrix=cm if nsup > 0 else None)
+        else:
+            eng.conf.zero_()
+            d_train = eng.workspace(train["Bmax"], train["T"])
+        if not fused:
+            pass
+        elif len(kinds) == 1:
             eng.run_steps(kinds, train["X"], train["lab"], train["stats"], d_train, train["rows"], train["sizes"], oA, oB)
         else:  # several updates per batch: batch-major order as in batch_update
             F2 = train["stats"].shape[1] * train["stats"].shape[2]
@@ -95,7 +105,8 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
             del F2
         model._set_module_modes(kinds[-1] if kinds else None)
         if nsup > 0:
-            cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
+            if fused:
+                cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
             TPR, TNR, FPR, FNR, ACC = _confusion(cm)
             for key, v in zip(("acc", "tpr", "tnr", "fpr", "fnr"), (ACC, TPR, TNR, FPR, FNR)):
                 cm_train[key].append(v)
@@ -104,8 +115,11 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
         model.factor_score_embedder.eval()
         for f in model.factors:
             f.eval()
-        nfirst = int(val["sizes"][0])
-        Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
+        if fused:
+            nfirst = int(val["sizes"][0])
+            Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
+        else:
+            Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(), torch.float32)
         with torch.no_grad():
             est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
             est_np = [[g.detach().cpu().numpy() for g in row] for row in est]

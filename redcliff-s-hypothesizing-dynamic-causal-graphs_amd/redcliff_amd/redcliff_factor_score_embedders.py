@@ -75,6 +75,11 @@ class cEmbedder(nn.Module):
         self.sigmoid = nn.Sigmoid() if use_sigmoid_restriction else None
         self.networks = nn.ModuleList([MLP(self.num_series, lag, hidden) for _ in range(num_factor_preds)])
 
+    def forward(self, X, use_final_activation=True):
+        """(B, lag, p) windows -> (w (B, K), class logits (B, nsup) | None) on the HIP GEMM."""
+        from .generic import cembedder_forward
+        return cembedder_forward(self, X, use_final_activation)
+
     def GC(self, threshold=True, ignore_lag=True, combine_wavelet_representations=False, rank_wavelets=False):
         from . import kernels
         W = torch.stack([net.layers[0].weight for net in self.networks])
@@ -94,7 +99,7 @@ class _Wrap:
 
 
 class MLPClassifierForSingleObjective(nn.Module):
-    """models/redcliff_factor_score_embedders.py:51-100 (parameter tree and init only)."""
+    """models/redcliff_factor_score_embedders.py:51-100 (forward on the HIP GEMM: redcliff_amd.generic)."""
 
     def __init__(self, num_series, num_in_timesteps, num_factor_scores, hidden_sizes, use_sigmoid_restriction,
                  sigmoid_eccentricity_coeff=10.):
@@ -114,10 +119,15 @@ class MLPClassifierForSingleObjective(nn.Module):
                       bias=False),
             nn.ReLU())
         self.unsup_factor_weighting_layer = nn.Linear(hidden_sizes[0], num_factor_scores, bias=False)
+        self.num_out_classes = 0
+
+    def forward(self, X, use_final_activation=True):
+        from .generic import vanilla_forward
+        return vanilla_forward(self, X, use_final_activation)
 
 
 class MLPClassifierForMultipleObjectives(nn.Module):
-    """models/redcliff_factor_score_embedders.py:104-179 (parameter tree and init only)."""
+    """models/redcliff_factor_score_embedders.py:104-179 (forward on the HIP GEMM: redcliff_amd.generic)."""
 
     def __init__(self, num_series, num_in_timesteps, num_factor_scores, num_out_classes, hidden_sizes,
                  use_sigmoid_restriction, sigmoid_eccentricity_coeff=10.):
@@ -142,3 +152,7 @@ class MLPClassifierForMultipleObjectives(nn.Module):
                                                           num_factor_scores - num_out_classes, bias=False)
         else:
             self.unsup_factor_weighting_layer = None
+
+    def forward(self, X, use_final_activation=True):
+        from .generic import vanilla_forward
+        return vanilla_forward(self, X, use_final_activation)

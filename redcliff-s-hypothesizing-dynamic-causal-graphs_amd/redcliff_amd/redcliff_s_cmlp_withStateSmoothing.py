@@ -131,6 +131,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
     def __getstate__(self):
         st = self.__dict__.copy()
         st["_engine"] = None
+        st.pop("_generic_path", None)
         return st
 
     @property
@@ -160,6 +161,23 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         self.factor_score_embedder.owner = weakref.ref(self)
         return self._engine
 
+    def _generic(self):
+        """The generic GPU path (redcliff_amd.generic) for configurations outside the fused chain."""
+        W = self.factors[0].networks[0].layers[0].weight
+        if not W.is_cuda:
+            raise RuntimeError("REDCLIFF-S on MI355X: move the model to the GPU first (model.cuda()); "
+                               "there is no CPU path")
+        nat.lib()
+        g = self.__dict__.get("_generic_path")
+        if g is None:
+            from .generic import GenericPath
+            g = GenericPath(self)
+            self.__dict__["_generic_path"] = g
+        return g
+
+    def _device(self):
+        return self.factors[0].networks[0].layers[0].weight.device
+
     # ------------------------------------------------------------------ forward
     def _labels_from_w(self, w_raw):
         emb = self.factor_score_embedder
@@ -175,6 +193,18 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
 
     def _embed_windows(self, Xw, use_final_activation=True):
         """DGCNN_Embedder.forward on time-major windows Xw (B, F, p)."""
+        if not self.fused_supported():
+            from .generic import dgcnn_forward
+            emb = self.factor_score_embedder
+            w = dgcnn_forward(emb.dgcnn.dgcnn, Xw.to(self._device(), torch.float32).transpose(1, 2))
+            logits = None
+            if self.num_supervised_factors > 0:
+                logits = w[:, :self.num_supervised_factors]
+                if use_final_activation and emb.use_sigmoid_restriction:
+                    logits = torch.sigmoid(logits)
+            if emb.use_sigmoid_restriction:
+                w = torch.sigmoid(emb.sigmoid_eccentricity_coeff * w)
+            return w, logits
         eng = self.engine()
         B, F, p = Xw.shape
         pad = self.Lmax - F
@@ -190,6 +220,8 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
     def forward(self, X, factor_weightings=None):
         """X (B, T, p) -> (x_sim (B, S, p), [per-factor predictions], [w], [state labels] * S)
         (...withStateSmoothing.py:326-412).  Uses the last embed_lag / gen_lag steps of X."""
+        if not self.fused_supported():
+            return self._generic().forward(X.to(self._device(), torch.float32), factor_weightings)
         if factor_weightings is not None:
             raise NotImplementedError("externally supplied factor_weightings are not supported on the fused path")
         eng = self.engine()
@@ -221,6 +253,9 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         """The nine GC estimate modes of ...withStateSmoothing.py:415-620 (DGCNN embedder)."""
         if rank_wavelets:
             raise NotImplementedError("rank_wavelets needs wavelet_level != None")
+        if not self.fused_supported():
+            Xd = None if X is None else X.to(self._device(), torch.float32)
+            return self._generic().GC(gc_est_mode, Xd, threshold, ignore_lag, combine_wavelet_representations)
         if self.factor_score_embedder_type != "DGCNN":
             raise NotImplementedError("GC on the fused path is implemented for the DGCNN embedder")
         ls = min(self.gen_lag, self.embed_lag)
@@ -253,11 +288,22 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         raise ValueError("GC EST MODE == " + str(gc_est_mode) + " IS NOT SUPPORTED")
 
     # ------------------------------------------------------------------ loss (values)
-    @torch.no_grad()
     def compute_loss(self, conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
                      node_dag_scale=0.1, embedder_pretrain_loss=False, factor_pretrain_loss=False):
-        """Loss terms of ...withStateSmoothing.py:624-731 as values.  Gradients of the
-        training objective are produced by the fused step (batch_update), not by autograd."""
+        """Loss terms of ...withStateSmoothing.py:624-731.  On the fused configuration they are
+        values (the fused step produces the gradients); on the generic path they carry autograd."""
+        if not self.fused_supported():
+            dev = self._device()
+            return self._generic().compute_loss(conditioning_X.to(dev, torch.float32), preds, targets.to(dev),
+                                                factor_scores, factor_labels, gc_est_mode,
+                                                embedder_pretrain_loss=embedder_pretrain_loss,
+                                                factor_pretrain_loss=factor_pretrain_loss)
+        with torch.no_grad():
+            return self._fused_loss_values(conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
+                                           embedder_pretrain_loss, factor_pretrain_loss)
+
+    def _fused_loss_values(self, conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
+                           embedder_pretrain_loss, factor_pretrain_loss):
         gc = self.GC(gc_est_mode, X=conditioning_X, threshold=False, ignore_lag=True)
         gc_lagged = self.GC(gc_est_mode, X=conditioning_X, threshold=False, ignore_lag=False)
         dev = preds.device
@@ -317,8 +363,18 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             raise NotImplementedError("FreezeByBatch training modes are not on the fused path")
         if output_length != 1:
             raise NotImplementedError("output_length must be 1 (num_sims * output_length target steps)")
-        eng = self.engine()
         kinds = phase_of_epoch(self, epoch_num)
+        if not self.fused_supported():
+            dev = self._device()
+            n = self.num_supervised_factors
+            conf = np.zeros((n, n)) if (running_factor_score_confusion_matrix is not None and n > 0) else None
+            self._generic().batch_update(kinds, X.to(dev, torch.float32), Y.to(dev, torch.float32), optimizerA,
+                                         optimizerB, output_length, conf)
+            self._set_module_modes(kinds[-1] if kinds else None)
+            if conf is not None:
+                running_factor_score_confusion_matrix += conf
+            return best_model, running_factor_score_confusion_matrix
+        eng = self.engine()
         Xd, lab, st, d = eng.stage(X, Y)
         if running_factor_score_confusion_matrix is not None:
             eng.conf.zero_()
@@ -342,6 +398,14 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                           factor_score_val_tpr_history=None, factor_score_val_tnr_history=None,
                           factor_score_val_fpr_history=None, factor_score_val_fnr_history=None):
         """...withStateSmoothing.py:1650-1790: coefficient-normalised loss terms averaged over batches."""
+        if not self.fused_supported():
+            for f in self.factors:
+                f.eval()
+            avg, conf = self._generic().validate(X_val, output_length)
+            acc = [avg[k] for k in ("forecast", "factor", "cos", "fw_l1", "smooth", "adj", "combo")] + [1.0]
+            return self._validation_tuple(acc, 1.0, conf, factor_score_val_acc_history,
+                                          factor_score_val_tpr_history, factor_score_val_tnr_history,
+                                          factor_score_val_fpr_history, factor_score_val_fnr_history)
         eng = self.engine()
         self.factor_score_embedder.eval()
         for f in self.factors:
@@ -349,7 +413,11 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         ds = eng.cache_dataset(X_val)
         d = eng.workspace(ds["Bmax"], ds["T"])
         acc, conf = eng.run_values(ds["X"], ds["lab"], d, ds["rows"], ds["sizes"])
-        nb = float(ds["len"])
+        return self._validation_tuple(acc, float(ds["len"]), conf, factor_score_val_acc_history,
+                                      factor_score_val_tpr_history, factor_score_val_tnr_history,
+                                      factor_score_val_fpr_history, factor_score_val_fnr_history)
+
+    def _validation_tuple(self, acc, nb, conf, acc_h, tpr_h, tnr_h, fpr_h, fnr_h):
         vals = [acc[nat_i] / nb for nat_i in range(7)]
         forecast, factor, cos, fwl1, smooth, adj, combo = vals
         out = [forecast, factor, cos, fwl1]
@@ -358,13 +426,12 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         out += [adj, 0.0, 0.0, 0.0, combo]
         if self.num_supervised_factors > 0:
             TPR, TNR, FPR, FNR, ACC = _confusion_rates(conf)
-            factor_score_val_acc_history.append(ACC)
-            factor_score_val_tpr_history.append(TPR)
-            factor_score_val_tnr_history.append(TNR)
-            factor_score_val_fpr_history.append(FPR)
-            factor_score_val_fnr_history.append(FNR)
-            out += [factor_score_val_acc_history, factor_score_val_tpr_history, factor_score_val_tnr_history,
-                    factor_score_val_fpr_history, factor_score_val_fnr_history]
+            acc_h.append(ACC)
+            tpr_h.append(TPR)
+            tnr_h.append(TNR)
+            fpr_h.append(FPR)
+            fnr_h.append(FNR)
+            out += [acc_h, tpr_h, tnr_h, fpr_h, fnr_h]
         return tuple(out)
 
     # ------------------------------------------------------------------ fit

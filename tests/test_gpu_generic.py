@@ -1,0 +1,135 @@
+"""The generic GPU path (redcliff_amd.generic: HIP GEMM contractions, autograd) against the
+reference's golden vectors, for every configuration outside the fused chain:
+cEmbedder, the Vanilla embedders, num_sims = 2 roll-outs with the smoothing penalty, and the
+per-step factor weighting forward mode (models/redcliff_s_cmlp_withStateSmoothing.py:253-412,
+models/redcliff_factor_score_embedders.py:51-331).
+
+Tolerance as the fused-path tests: rtol 1e-4 (north star), atol 1e-5 on near-zero entries."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_close, batches, ctor_args, load, state
+
+pytestmark = pytest.mark.gpu
+
+GENERIC_SCENARIOS = ["cemb", "vanilla", "dgcnn_sims2", "dgcnn_eachstep"]
+RTOL, ATOL = 1e-4, 1e-5
+
+
+def build(meta):
+    import redcliff_amd
+    args, kw = ctor_args(meta)
+    torch.manual_seed(meta["seed"])
+    cls = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing if meta["smoothing_class"] else redcliff_amd.REDCLIFF_S_CMLP
+    m = cls(*args, **kw).float().cuda()
+    assert not m.fused_supported(), "scenario is expected to run on the generic path"
+    return m
+
+
+def compare_state(tag, model, want, rtol=RTOL, atol=ATOL):
+    got = dict((k, v.detach().cpu().numpy()) for k, v in model.state_dict().items() if not k.startswith("gen_model."))
+    assert set(got) == set(want)
+    for k in want:
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(want[k]), tag + k
+            continue
+        scale = max(1.0, float(np.abs(want[k]).max()))
+        assert_close("%s/%s" % (tag, k), got[k], want[k], rtol, atol * scale)
+
+
+@pytest.mark.parametrize("name", GENERIC_SCENARIOS)
+def test_init_is_the_reference_init(name):
+    d, meta = load(name)
+    compare_state("init", build(meta), state(d, "init"), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("name", GENERIC_SCENARIOS)
+def test_eval_forward_gc_loss(name):
+    d, meta = load(name)
+    m = build(meta)
+    m.eval()
+    Xb, Yb = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    X = Xb[:, :Lm, :].cuda()
+    with torch.no_grad():
+        x_sim, fpreds, fws, labels = m(X)
+        assert_close("x_sim", x_sim.cpu().numpy(), d["eval/x_sim"], RTOL, ATOL)
+        assert_close("w", fws[0].cpu().numpy(), d["eval/w"], RTOL, ATOL)
+        assert_close("labels0", labels[0].cpu().numpy(), d["eval/labels0"], RTOL, ATOL)
+        for key in [k for k in d.files if k.startswith("eval/gc/")]:
+            _, _, mode, ign, comb = key.split("/")
+            gcs = m.GC(mode, X=X, threshold=False, ignore_lag=ign == "ign1",
+                       combine_wavelet_representations=comb == "comb1")
+            arr = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in gcs])
+            assert_close(key, arr, d[key], RTOL, ATOL)
+        tgt = Xb[:, Lm:Lm + meta["S"], :].cuda()
+        for flag in ("combined", "emb", "fac"):
+            combo, terms = m.compute_loss(X[:, :meta["F"], :], x_sim, tgt, labels, Yb.cuda(), meta["gc_mode"],
+                                          embedder_pretrain_loss=flag == "emb", factor_pretrain_loss=flag == "fac")
+            assert_close("combo/" + flag, float(combo), d["eval/loss/%s/combo" % flag], RTOL, ATOL)
+            for i, t in enumerate(terms):
+                want = d["eval/loss/%s/t%d" % (flag, i)]
+                if np.isnan(want):
+                    assert t is None
+                else:
+                    assert_close("term%d/%s" % (i, flag), float(t), want, RTOL, ATOL)
+
+
+@pytest.mark.parametrize("name", GENERIC_SCENARIOS)
+def test_train_mode_forward(name):
+    d, meta = load(name)
+    m = build(meta)
+    m.train()
+    Xb, _ = batches(d, meta)[0]
+    with torch.no_grad():
+        x_sim, _, fws, _ = m(Xb[:, :max(meta["L"], meta["F"]), :].cuda())
+    assert_close("train x_sim", x_sim.cpu().numpy(), d["train_fwd/x_sim"], RTOL, ATOL)
+    assert_close("train w", fws[0].cpu().numpy(), d["train_fwd/w"], RTOL, ATOL)
+
+
+@pytest.mark.parametrize("name", GENERIC_SCENARIOS)
+def test_batch_update_schedule_and_validation(name):
+    d, meta = load(name)
+    m = build(meta)
+    oA = torch.optim.Adam(m.gen_model[0].parameters(), lr=meta["lrA"], betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    oB = torch.optim.Adam(m.gen_model[1].parameters(), lr=meta["lrB"], betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+    bs = batches(d, meta)
+    step = 0
+    for epoch in meta["epochs"]:
+        for bi, (Xb, Yb) in enumerate(bs):
+            m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+            step += 1
+            compare_state("step%d" % step, m, state(d, "step%d" % step))
+    assert step == int(d["nsteps"])
+    hist = [[] for _ in range(5)] if meta["nsup"] > 0 else []
+    vals = m.validate_training(bs, 1, meta["p"], *hist)
+    names = ["forecast", "factor", "cos", "fw_l1", "smooth", "adj", "dag_reg", "dag_lag", "dag_node", "combo"]
+    if not meta["smoothing_class"]:
+        names = ["forecast", "factor", "cos", "fw_l1", "adj", "dag_reg", "dag_lag", "dag_node", "combo"]
+    for n_, v in zip(names, vals):
+        if ("val/" + n_) in d.files:
+            assert_close("val/" + n_, v, d["val/" + n_], 1e-4, 1e-6)
+
+
+def test_hip_gemm_against_fp64():
+    """redcliff_gemm in all four transpose combinations, batched and broadcast."""
+    from redcliff_amd.generic import _raw_bmm, bmm
+    g = torch.Generator().manual_seed(0)
+    for (M, N, K) in ((1, 1, 1), (7, 65, 33), (64, 64, 16), (130, 3, 257)):
+        for ta in (0, 1):
+            for tb in (0, 1):
+                a = torch.randn((3,) + ((K, M) if ta else (M, K)), generator=g)
+                b = torch.randn((1,) + ((N, K) if tb else (K, N)), generator=g)
+                got = _raw_bmm(a.cuda(), b.cuda(), ta, tb).cpu().double()
+                A = a.double().transpose(1, 2) if ta else a.double()
+                Bm = b.double().transpose(1, 2) if tb else b.double()
+                # fp32 fmaf chain over K terms vs fp64: |err| <~ K * 2^-24 * sum|a b|
+                np.testing.assert_allclose(got.numpy(), torch.matmul(A, Bm).numpy(), rtol=1e-4, atol=1e-4)
+    a = torch.randn(1, 9, 5, generator=g).cuda().requires_grad_()
+    b = torch.randn(4, 5, 6, generator=g).cuda().requires_grad_()
+    (bmm(a, b) ** 2).sum().backward()
+    a2, b2 = a.detach().cpu().double().requires_grad_(), b.detach().cpu().double().requires_grad_()
+    (torch.matmul(a2, b2) ** 2).sum().backward()
+    np.testing.assert_allclose(a.grad.cpu().numpy(), a2.grad.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(b.grad.cpu().numpy(), b2.grad.numpy(), rtol=1e-5, atol=1e-5)
