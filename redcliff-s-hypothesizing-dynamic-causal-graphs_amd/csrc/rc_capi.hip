@@ -179,6 +179,7 @@ static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
   c.eo = rc_emb_off(d);
   c.fo = rc_fac_off(d);
   c.wo = wo;
+  rc_emb_partial_layout(c, rc_emb_use_gemm(d));
   return 0;
 }
 
@@ -196,15 +197,25 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
       return e;
   }
   const bool mfma = fac && rc_fac_use_mfma(c.d);
-  // forward: embedder + vector-path factor networks share one launch ("fwd" timing slot)
-  if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_forward(c, s, true, fac && !mfma); }))) return e;
+  const bool egemm = rc_emb_use_gemm(c.d);
+  // forward: embedder + vector-path factor networks share one launch ("fwd" timing slot); the
+  // GEMM-shaped embedder (large p*F) is its own chain, the factor forward then follows it
+  if (egemm) {
+    if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd_gemm(c, s); }))) return e;
+    if (fac && !mfma && (e = timed(KT_FAC_FWD, s, [&] { return rc_launch_forward(c, s, false, true); }))) return e;
+  } else if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_forward(c, s, true, fac && !mfma); }))) {
+    return e;
+  }
   if (mfma) {  // large p*L: grouped GEMMs on the matrix cores
     if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd_mfma(c, s); }))) return e;
     if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd_mfma(c, s); }))) return e;
   } else if (fac) {
     if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
   }
-  if (emb_grad) {
+  if (emb_grad && egemm) {
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd_gemm(c, s); }))) return e;
+    if ((fl & (RC_VALUES | RC_CONFUSION)) && (e = rc_launch_emb_bwd(c, s, false))) return e;  // head only
+  } else if (emb_grad) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;

@@ -46,6 +46,11 @@ struct WsOff {
   int64_t xw;     // [Bmax][Qp]        factor input windows, q = c*L + t (MFMA path; Qp = Q rounded to 32)
   int64_t dyl;    // [K*p][Bmax]       dL/d(prediction of network kj) per window (MFMA path)
   int64_t dgs;    // [K*p][p*L]        adjacency-L1 gradient wrt the lagged group norms (MFMA path)
+  int64_t f1p;    // [64][Bmax][M1]    fc1 split-K partials (GEMM embedder)
+  int64_t edf1;   // [Bmax][M1]        dL/d fc1 pre-activation (GEMM embedder)
+  int64_t edT;    // [Bmax][p][n][F]   dL/dT_i (GEMM embedder; T itself is [Bmax][p][n][F] there)
+  int64_t edX;    // [Bmax][p][F]      dL/d x_bn (GEMM embedder)
+  int64_t eAf;    // [p][p*n]          [S_0^T | ... | S_{n-1}^T] interleaved (GEMM embedder)
   int64_t total;
 };
 
@@ -142,7 +147,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.dwp = x; x = rc_align64(x + p * B * K);
   o.dAadj = x; x = rc_align64(x + K * p * p);
   o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);
-  o.dS = x; x = rc_align64(x + p * rc_nchunk(d) * d.n * p);
+  o.dS = x; x = rc_align64(x + (rc_nchunk(d) > 16 ? rc_nchunk(d) : 16) * d.n * p * p);
   o.dgb = x; x = rc_align64(x + p * rc_nchunk(d) * 2 * d.F);
   o.S = x; x = rc_align64(x + d.n * p * p);
   o.dZ = x; x = rc_align64(x + p * B * d.H);
@@ -153,6 +158,11 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.xw = x; x = rc_align64(x + B * rc_qpad(d));
   o.dyl = x; x = rc_align64(x + K * p * B);
   o.dgs = x; x = rc_align64(x + K * p * p * d.L);
+  o.f1p = x; x = rc_align64(x + 64 * B * d.M1);
+  o.edf1 = x; x = rc_align64(x + B * d.M1);
+  o.edT = x; x = rc_align64(x + B * p * d.n * d.F);
+  o.edX = x; x = rc_align64(x + B * p * d.F);
+  o.eAf = x; x = rc_align64(x + p * p * d.n);
 #ifdef RC_TRACE
   x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
 #endif
@@ -192,6 +202,10 @@ struct StepCtx {
   double* acc;
   int* conf;
   float *gE, *gF;  // RC_GRAD_ONLY gradient outputs (emb / fac layouts)
+  // layout of the embedder-backward partials the final kernel reduces (node-chunk kernel vs GEMM path):
+  // dS_i[cc][c'] = sum_s ws.dS[cc*dsCC + s*dsS + i*dsI + c'], s < dsN;  BN affine: ws.dgb[s][2][F], s < dgN
+  int dsN, dgN;
+  int64_t dsCC, dsS, dsI;
   EmbOff eo;
   FacOff fo;
   WsOff wo;
@@ -392,6 +406,11 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
 bool rc_fac_use_mfma(const RedcliffDims& d);
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s);
 int rc_launch_fac_bwd_mfma(const StepCtx& c, hipStream_t s);
+// GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
+bool rc_emb_use_gemm(const RedcliffDims& d);
+void rc_emb_partial_layout(StepCtx& c, bool gemm);
+int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
+int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,

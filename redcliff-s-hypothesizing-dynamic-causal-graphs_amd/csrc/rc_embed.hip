@@ -615,9 +615,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     } else if (e < nFH + nfc + 2 * F) {
       const int q = e - nFH - nfc;
       const int which = q / F, f = q - which * F;  // 0: gamma, 1: beta
-      const int nparts = p * rc_nchunk(d);
-#pragma unroll 8
-      for (int pt = 0; pt < nparts; ++pt) g += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
+      // fixed-order sum of the c.dgN partial records (4 independent chains)
+      float g4[4] = {0.f, 0.f, 0.f, 0.f};
+      int pt = 0;
+      for (; pt + 3 < c.dgN; pt += 4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g4[u] += ws[c.wo.dgb + ((int64_t)(pt + u) * 2 + which) * F + f];
+      for (; pt < c.dgN; ++pt) g4[0] += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
+      g = (g4[0] + g4[1]) + (g4[2] + g4[3]);
       idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
     } else {
       const int q = e - nFH - nfc - 2 * F;  // fc1 weight (gradient combined by the node blocks)
@@ -628,29 +633,32 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
     return;
   }
-  // ---- adjacency workgroup
+  // ---- adjacency workgroup: every p x p operand lives in LDS (dynamic, (n + 5) p^2 floats)
   const int tid = threadIdx.x;
-  __shared__ float dinv[64], dsum[64], dd[64];
+  extern __shared__ float sm[];
   const int pp2 = p * p;
-  float* Ar = ws + c.wo.amat;           // relu(A)
-  float* dL = Ar + pp2;
-  float* dSw = dL + pp2;                // working copies of dS_1..dS_{n-1}
-  const float* S = ws + c.wo.S;         // pre-update supports (S_1 = L)
+  float* Al = sm;                       // A (pre-update)
+  float* Ar = Al + pp2;                 // relu(A)
+  float* dL = Ar + pp2;                 // dL/dL (the normalised Laplacian)
+  float* dSw = dL + pp2;                // dS_1 .. dS_{n-1}
+  float* Sl = dSw + (n - 1) * pp2;      // supports S_0 .. S_{n-1} (pre-update; S_1 = L)
+  float* dinv = Sl + n * pp2;           // [64]
+  float* dsum = dinv + 64;              // [64]
+  float* dd = dsum + 64;                // [64]
   if (stepA) {
     float* A = E + c.eo.A;
-    for (int e = tid; e < pp2; e += RC_BLOCK) {
-      Ar[e] = fmaxf(A[e], 0.f);
-      dL[e] = 0.f;
-    }
-    {  // dS_i[c][c'] = sum over column chunks of node c's partials (layout [c][chunk][n][p])
-      const int nch = rc_nchunk(d);
-      for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) {
-        const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
-        float t = 0.f;
-        for (int chk = 0; chk < nch; ++chk) t += ws[c.wo.dS + (((int64_t)cc * nch + chk) * n + i) * p + cp];
-        dSw[e] = t;
-      }
-    }
+    const float* S = ws + c.wo.S;
+    rc_stage_all(
+        rc_seg<4>(pp2, [&](int e) { return A[e]; }, [&](int e, float v) { Al[e] = v; Ar[e] = fmaxf(v, 0.f); }),
+        rc_seg<8>(n * pp2, [&](int e) { return S[e]; }, [&](int e, float v) { Sl[e] = v; }),
+        // dS_i[c][c'] = fixed-order sum of the backward kernel's partial records
+        rc_seg<8>((n - 1) * pp2, [&](int e) {
+          const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
+          float t = 0.f;
+          for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
+          return t;
+        }, [&](int e, float v) { dSw[e] = v; }));
+    for (int e = tid; e < pp2; e += RC_BLOCK) dL[e] = 0.f;
     __syncthreads();
     for (int i = tid; i < p; i += RC_BLOCK) {
       float s = 0.f;
@@ -663,8 +671,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     for (int l = n - 1; l >= 2; --l) {
       const float* dSl = dSw + (int64_t)(l - 1) * pp2;
       float* dSprev = dSw + (int64_t)(l - 2) * pp2;
-      const float* Sprev = S + (int64_t)(l - 1) * pp2;
-      const float* Lm = S + pp2;
+      const float* Sprev = Sl + (int64_t)(l - 1) * pp2;
+      const float* Lm = Sl + pp2;
       for (int e = tid; e < pp2; e += RC_BLOCK) {
         const int a = e / p, b = e - a * p;
         float t1 = 0.f, t2 = 0.f;
@@ -689,19 +697,55 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       dd[i] = g * (-0.5f) * dinv[i] * dinv[i] * dinv[i];
     }
     __syncthreads();
-    const RedcliffReplicaHyper& hy = c.hyp[r];
-    (void)hy;
     for (int e = tid; e < pp2; e += RC_BLOCK) {
       const int i = e / p, j = e - i * p;
-      float g = (A[e] > 0.f) ? (dL[e] * dinv[i] * dinv[j] + dd[i]) : 0.f;
+      float g = (Al[e] > 0.f) ? (dL[e] * dinv[i] * dinv[j] + dd[i]) : 0.f;
       if (c.flags & RC_LOSS_ADJ)
         for (int k = 0; k < K; ++k) g += ws[c.wo.dAadj + (int64_t)k * pp2 + e];
-      rc_update(c, E, Mm, V, c.gE + r * c.es, c.eo.A + e, g, as);
+      if (c.flags & RC_GRAD_ONLY) {
+        c.gE[r * c.es + c.eo.A + e] = g;
+      } else {
+        float pv = Al[e], mv = Mm[c.eo.A + e], vv = V[c.eo.A + e];
+        rc_adam(pv, mv, vv, g, as);
+        A[e] = pv; Mm[c.eo.A + e] = mv; V[c.eo.A + e] = vv;
+        Al[e] = pv;  // the new A for the supports below
+      }
     }
     __syncthreads();
-    // supports for the next step (after a gradient-only shard step A changes later, in
-    // redcliff_adam_apply, and the host refreshes them)
-    if (!(c.flags & RC_GRAD_ONLY)) dev_supports(A, ws + c.wo.S, dinv, p, n);
+    // supports of the updated A for the next step, computed in LDS (after a gradient-only shard
+    // step A changes later, in redcliff_adam_apply, and the host refreshes them)
+    if (!(c.flags & RC_GRAD_ONLY)) {
+      for (int i = tid; i < p; i += RC_BLOCK) {
+        float s = 0.f;
+        for (int j = 0; j < p; ++j) s += fmaxf(Al[i * p + j], 0.f);
+        dinv[i] = 1.f / sqrtf(s + 1e-10f);
+      }
+      __syncthreads();
+      float* Sg = ws + c.wo.S;
+      for (int e = tid; e < pp2; e += RC_BLOCK) {
+        const int i = e / p, j = e - i * p;
+        const float s0 = (i == j) ? 1.f : 0.f;
+        Sg[e] = s0;
+        if (n > 1) {
+          const float lv = (dinv[i] * fmaxf(Al[e], 0.f)) * dinv[j];
+          Sl[pp2 + e] = lv;
+          Sg[pp2 + e] = lv;
+        }
+      }
+      __syncthreads();
+      for (int l = 2; l < n; ++l) {
+        const float* prev = Sl + (int64_t)(l - 1) * pp2;
+        const float* Lm = Sl + pp2;
+        for (int e = tid; e < pp2; e += RC_BLOCK) {
+          const int i = e / p, j = e - i * p;
+          float t = 0.f;
+          for (int k = 0; k < p; ++k) t += prev[i * p + k] * Lm[k * p + j];
+          Sl[(int64_t)l * pp2 + e] = t;
+          Sg[(int64_t)l * pp2 + e] = t;
+        }
+        __syncthreads();
+      }
+    }
   }
   // BatchNorm running statistics (torch: double math, momentum*stat + (1-momentum)*running)
   if (c.nbn > 0 && tid < F) {
@@ -795,7 +839,11 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
   const int nw = (total + RC_BLOCK - 1) / RC_BLOCK;
-  hipLaunchKernelGGL(k_emb_final, dim3(nw + 1, d.R), dim3(RC_BLOCK), 0, s, c, nw);
+  const size_t lds = sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * d.p + 3 * 64);
+  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  int e = rc_lds_optin(k_emb_final, lds, "k_emb_final LDS");
+  if (e) return e;
+  hipLaunchKernelGGL(k_emb_final, dim3(nw + 1, d.R), dim3(RC_BLOCK), lds, s, c, nw);
   return rc_check(hipGetLastError(), "k_emb_final");
 }
 

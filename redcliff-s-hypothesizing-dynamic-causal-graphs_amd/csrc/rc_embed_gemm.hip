@@ -1,0 +1,369 @@
+// rc_embed_gemm.hip -- the DGCNN factor-score embedder as a chain of GEMMs, for large node
+// counts / feature windows (the stress config p=64, F=64: p*F = 4096 per window), where the
+// per-window workgroups of rc_forward.hip / rc_embed.hip would re-read every window once per
+// (node, column chunk) block and run out of LDS.
+//
+// Reference: models/redcliff_factor_score_embedders.py:335-392, models/dgcnn.py:15-64 and the
+// torcheeg 1.1.3 DGCNN (restated in oracle/torcheeg_dgcnn.py).  Layout: T[b][c][i][f]
+// (T_0 = x_bn), so the graph convolution over all windows and nodes is ONE product
+//   Z[(b,c)][h] = sum_{(i,f)} T[(b,c)][(i,f)] gcW[(i,f)][h]      (B*p x n*F x H)
+// because the packed graph-conv weights gcW[n][F][H] are exactly that (n*F) x H matrix.
+//
+// forward:  prep (x_bn)  ->  T_i = S_i x_bn (per window, i >= 1)  ->  R = relu(T gcW)
+//           ->  fc1 split-K partials  ->  head (f1, relu, fc2 -> w)
+// backward: dhead (dL/dw_raw, dL/df1, fc2 / fc1-bias gradients)  ->  dfc1W = df1^T R
+//           ->  dZ = [R > 0] df1 fc1W  ->  dW = T^T dZ (p split-K slices, summed by the final
+//           kernel)  ->  dT = dZ gcW^T  ->  dx_bn = sum_i S_i^T dT_i  ->  dS_i = sum_b dT_i x_bn^T
+//           (window-group slices)  ->  BatchNorm affine partials.  The final kernel (rc_embed.hip,
+//           k_emb_final) applies Adam, the Chebyshev / normalize_A backward and the BN running stats.
+// Every contraction is the shared GEMM core (rc_gemm.h); the replica axis is a host loop.
+#include <cstdlib>
+#include <cstring>
+
+#include "rc_gemm.h"
+
+namespace {
+
+// x_bn[b][c][0][f] = X[row0 + b][Lmax - F + f][c] * alpha_f + beta_f    grid (B, R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, b = blockIdx.x;
+  const int p = d.p, F = d.F, n = d.n;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr + ((c.row0 + b) * d.T + (c.Lmax - F)) * p;
+  __shared__ float alpha[64], beta[64];
+  const int tid = threadIdx.x;
+  if (tid < F) {
+    const bool train = c.flags & RC_BN_TRAIN;
+    float mean, inv;
+    if (train) {
+      mean = (float)c.bns[r * c.bnsr + tid];
+      inv = (float)(1.0 / sqrt(c.bns[r * c.bnsr + F + tid] + c.hyp[r].bn_eps));
+    } else {
+      mean = c.rm[r * F + tid];
+      inv = 1.0f / sqrtf(c.rv[r * F + tid] + (float)c.hyp[r].bn_eps);
+    }
+    const float a = inv * E[c.eo.bnw + tid];
+    alpha[tid] = a;
+    beta[tid] = E[c.eo.bnb + tid] - mean * a;
+  }
+  __syncthreads();
+  float* T = ws + c.wo.T + (int64_t)b * p * n * F;
+  const RcDiv dp(p);
+  for (int e = tid; e < p * F; e += RC_BLOCK) {  // read (f, c) contiguous, write [c][0][f]
+    const int f = dp.div(e), ch = e - f * p;
+    T[(int64_t)ch * n * F + f] = X[e] * alpha[f] + beta[f];
+  }
+}
+
+// [S_0^T | S_1^T | ...] interleaved for dx_bn = sum_i S_i^T dT_i:  Af[c][c'*n + i] = S_i[c'][c]
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_afull(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.x, p = d.p, n = d.n;
+  float* ws = c.ws + r * c.wss;
+  const float* S = ws + c.wo.S;
+  for (int e = threadIdx.x; e < p * p * n; e += RC_BLOCK) {
+    const int cc = e / (p * n), rem = e - cc * p * n, cp = rem / n, i = rem - cp * n;
+    ws[c.wo.eAf + e] = S[((int64_t)i * p + cp) * p + cc];
+  }
+}
+
+// f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (ceil(B/16), R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, b0 = blockIdx.x * 16;
+  const int M1 = d.M1, K = d.K;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  __shared__ float f1s[16][64];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 16 * M1; e += RC_BLOCK) {
+    const int s = e / M1, m = e - s * M1, b = b0 + s;
+    if (b >= c.B) continue;
+    float v = 0.f;
+    for (int q = 0; q < nsplit; ++q) v += ws[c.wo.f1p + ((int64_t)q * d.Bmax + b) * M1 + m];
+    v += E[c.eo.fc1b + m];
+    f1s[s][m] = v;
+    ws[c.wo.f1 + (int64_t)b * M1 + m] = v;
+  }
+  __syncthreads();
+  for (int e = tid; e < 16 * K; e += RC_BLOCK) {
+    const int s = e / K, k = e - s * K, b = b0 + s;
+    if (b >= c.B) continue;
+    float a = 0.f;
+    for (int m = 0; m < M1; ++m) a += E[c.eo.fc2W + k * M1 + m] * fmaxf(f1s[s][m], 0.f);
+    ws[c.wo.w + (int64_t)b * K + k] = a + E[c.eo.fc2b + k];
+  }
+}
+
+// dL/d(raw embedder output) (the same rule as the node-chunk kernel, rc_embed.hip), dL/df1,
+// and the fc2 weight / fc2 bias / fc1 bias gradients.  grid (1, R): one workgroup per replica.
+__device__ inline float lemb_draw(const StepCtx& c, int r, int k, float raw, float gw, float y) {
+  const RedcliffDims& d = c.d;
+  const int K = d.K, nsup = d.nsup;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const bool sig = d.use_sigmoid;
+  const float ecc = d.sigmoid_ecc;
+  const int ncol = nsup > 0 ? nsup : K;
+  const float weff = sig ? rc_sigmoid(ecc * raw) : raw;
+  float graw = sig ? gw * ecc * weff * (1.f - weff) : gw;
+  if (k < ncol) {
+    const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
+    float gsl = 0.f;
+    if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) gsl += hy.c_factor * (2.f / (float)(c.Bg * nsup)) * (sl - y);
+    if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
+    if (nsup > 0)
+      graw += sig ? gsl * sl * (1.f - sl) : gsl;
+    else
+      graw += sig ? gsl * ecc * weff * (1.f - weff) : gsl;
+  }
+  return graw;
+}
+
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y;
+  const int K = d.K, M1 = d.M1, p = d.p, B = c.B;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  extern __shared__ float sm[];
+  float* dr = sm;               // [B][K]
+  float* fc2s = dr + B * K;     // [K][M1]
+  const int tid = threadIdx.x;
+  const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
+  const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
+  for (int e = tid; e < K * M1; e += RC_BLOCK) fc2s[e] = E[c.eo.fc2W + e];
+  for (int e = tid; e < B * K; e += RC_BLOCK) {
+    const int b = e / K, k = e - b * K;
+    float g = 0.f;
+    if (fac_grad)
+      for (int j = 0; j < p; ++j) g += ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k];
+    const float y = lab_on ? c.lab[r * c.labr + (c.row0 + b) * K + k] : 0.f;
+    dr[e] = lemb_draw(c, r, k, ws[c.wo.w + e], g, y);
+  }
+  __syncthreads();
+  const float* f1 = ws + c.wo.f1;
+  float* df1 = ws + c.wo.edf1;
+  for (int e = tid; e < B * M1; e += RC_BLOCK) {
+    const int b = e / M1, m = e - b * M1;
+    float g = 0.f;
+    if (f1[e] > 0.f)
+      for (int k = 0; k < K; ++k) g += dr[b * K + k] * fc2s[k * M1 + m];
+    df1[e] = g;
+  }
+  __syncthreads();
+  // dfc2W[k][m] = sum_b dr[b][k] relu(f1[b][m]); dfc2b[k] = sum_b dr[b][k]; dfc1b[m] = sum_b df1[b][m]
+  const int nout = K * M1 + K + M1;
+  for (int e = tid; e < nout; e += RC_BLOCK) {
+    float g = 0.f;
+    if (e < K * M1) {
+      const int k = e / M1, m = e - k * M1;
+      for (int b = 0; b < B; ++b) g += dr[b * K + k] * fmaxf(f1[(int64_t)b * M1 + m], 0.f);
+    } else if (e < K * M1 + K) {
+      const int k = e - K * M1;
+      for (int b = 0; b < B; ++b) g += dr[b * K + k];
+    } else {
+      const int m = e - K * M1 - K;
+      for (int b = 0; b < B; ++b) g += df1[(int64_t)b * M1 + m];
+    }
+    ws[c.wo.gfc + e] = g;
+  }
+}
+
+// BatchNorm affine partials: slot s of c.dgN sums rows (b, c) [s*rows, (s+1)*rows) of
+//   dgamma[f] = sum dx_bn[b][c][f] * xhat[b][c][f],  dbeta[f] = sum dx_bn[b][c][f].  grid (dgN, R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, s = blockIdx.x;
+  const int p = d.p, F = d.F;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr;
+  const int nrows = c.B * p, per = (nrows + c.dgN - 1) / c.dgN;
+  const int r0 = s * per, r1 = min(nrows, r0 + per);
+  const int tid = threadIdx.x, f = tid % F, sl = tid / F, nsl = RC_BLOCK / F;
+  __shared__ float red[2][RC_BLOCK];
+  const bool train = c.flags & RC_BN_TRAIN;
+  float mean = 0.f, inv = 0.f;
+  if (sl < nsl) {
+    if (train) {
+      mean = (float)c.bns[r * c.bnsr + f];
+      inv = (float)(1.0 / sqrt(c.bns[r * c.bnsr + F + f] + c.hyp[r].bn_eps));
+    } else {
+      mean = c.rm[r * F + f];
+      inv = 1.0f / sqrtf(c.rv[r * F + f] + (float)c.hyp[r].bn_eps);
+    }
+  }
+  float ag = 0.f, ab = 0.f;
+  if (sl < nsl)
+    for (int row = r0 + sl; row < r1; row += nsl) {
+      const int b = row / p, cc = row - b * p;
+      const float dx = ws[c.wo.edX + (int64_t)row * F + f];
+      const float x = X[((c.row0 + b) * d.T + (c.Lmax - F + f)) * p + cc];
+      ag += dx * ((x - mean) * inv);
+      ab += dx;
+    }
+  red[0][tid] = ag;
+  red[1][tid] = ab;
+  __syncthreads();
+  if (tid < F) {
+    float g = 0.f, bb = 0.f;
+    for (int q = 0; q < nsl; ++q) {
+      g += red[0][q * F + tid];
+      bb += red[1][q * F + tid];
+    }
+    ws[c.wo.dgb + ((int64_t)s * 2) * F + tid] = g;
+    ws[c.wo.dgb + ((int64_t)s * 2 + 1) * F + tid] = bb;
+  }
+}
+
+// dS_i slices -> slot 0 (fixed order), so the final kernel's adjacency workgroup reads one record.
+// grid (ceil((n-1) p^2 / 256), R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_dsred(StepCtx c, int nds) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, p = d.p, n = d.n;
+  const int64_t pp2 = (int64_t)p * p;
+  const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
+  if (e >= (n - 1) * pp2) return;
+  float* dS = c.ws + r * c.wss + c.wo.dS + pp2 + e;  // rows i >= 1 of slot 0
+  const int64_t ss = (int64_t)n * pp2;
+  float t4[4] = {0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 3 < nds; s += 4)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t4[u] += dS[(s + u) * ss];
+  for (; s < nds; ++s) t4[0] += dS[s * ss];
+  dS[0] = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+}
+
+// splits of the fc1 contraction (p*H): largest divisor of p*H that is <= 64 with >= 64 terms each
+int fc1_splits(const RedcliffDims& d) {
+  const int pH = d.p * d.H;
+  for (int s = 64; s > 1; --s)
+    if (pH % s == 0 && pH / s >= 64) return s;
+  return 1;
+}
+
+// window groups of the dS product: a power-of-two divisor of B, at most 16
+int ds_splits(int B) {
+  int s = 16;
+  while (s > 1 && B % s) s >>= 1;
+  return s;
+}
+
+}  // namespace
+
+bool rc_emb_use_gemm(const RedcliffDims& d) {
+  const char* v = getenv("REDCLIFF_EMB_PATH");  // read per call: tests switch paths in-process
+  if (v && !strcmp(v, "gemm")) return d.F <= 64;
+  if (v && !strcmp(v, "fused")) return false;
+  return d.p >= 32 && d.F <= 64;
+}
+
+void rc_emb_partial_layout(StepCtx& c, bool gemm) {
+  const RedcliffDims& d = c.d;
+  const int nch = rc_nchunk(d), n = d.n, p = d.p;
+  if (gemm) {  // dS partials [s][i][cc][c'] over window groups, reduced into slot 0; BN partials over row slices
+    c.dsN = 1;
+    c.dsCC = p;
+    c.dsS = (int64_t)n * p * p;
+    c.dsI = (int64_t)p * p;
+    c.dgN = p * nch < 64 ? p * nch : 64;
+  } else {  // node-chunk kernel: [node][chunk][i][c'] and one BN record per (node, chunk)
+    c.dsN = nch;
+    c.dsCC = (int64_t)nch * n * p;
+    c.dsS = (int64_t)n * p;
+    c.dsI = p;
+    c.dgN = p * nch;
+  }
+}
+
+int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
+  const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F;
+  if (F > 64 || M1 > 64) { rc_set_error("GEMM embedder: F <= 64 and M1 <= 64 required"); return REDCLIFF_ELIMIT; }
+  hipLaunchKernelGGL(k_lemb_prep, dim3(B, d.R), dim3(RC_BLOCK), 0, s, c);
+  int e = rc_check(hipGetLastError(), "k_lemb_prep");
+  const int nsp = fc1_splits(d), Ks = p * H / nsp;
+  for (int r = 0; r < d.R && !e; ++r) {
+    float* ws = c.ws + r * c.wss;
+    const float* E = c.emb + r * c.es;
+    float* T = ws + c.wo.T;
+    // T_i[b] = S_i x_bn[b]  (p x p x F per window)
+    for (int i = 1; i < n && !e; ++i)
+      e = rc_gemm_launch(rc_gemm_args(0, 0, p, F, p, ws + c.wo.S + (int64_t)i * p * p, p, 0, T, nF, pnF, T + i * F, nF,
+                                      pnF), B, s, "emb T_i");
+    if (e) break;
+    // R = relu(T gcW): (B*p) x (n*F) x H
+    RcGemm g = rc_gemm_args(0, 0, B * p, H, (int)nF, T, nF, 0, E + c.eo.gcW, H, 0, ws + c.wo.R, H, 0);
+    g.epi = RC_EPI_RELU;
+    if ((e = rc_gemm_launch(g, 1, s, "emb graph conv"))) break;
+    // fc1 partials over nsp slices of the p*H contraction
+    e = rc_gemm_launch(rc_gemm_args(0, 1, B, M1, Ks, ws + c.wo.R, (int64_t)p * H, Ks, E + c.eo.fc1W, (int64_t)p * H, Ks,
+                                    ws + c.wo.f1p, M1, (int64_t)d.Bmax * M1), nsp, s, "emb fc1");
+  }
+  if (e) return e;
+  hipLaunchKernelGGL(k_lemb_head, dim3((B + 15) / 16, d.R), dim3(RC_BLOCK), 0, s, c, nsp);
+  return rc_check(hipGetLastError(), "k_lemb_head");
+}
+
+int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
+  const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F, pH = (int64_t)p * H;
+  const size_t lds = sizeof(float) * ((size_t)B * d.K + (size_t)d.K * M1);
+  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("GEMM embedder head: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  hipLaunchKernelGGL(k_lemb_dhead, dim3(1, d.R), dim3(RC_BLOCK), lds, s, c);
+  int e = rc_check(hipGetLastError(), "k_lemb_dhead");
+  if (!e) {
+    hipLaunchKernelGGL(k_lemb_afull, dim3(d.R), dim3(RC_BLOCK), 0, s, c);
+    e = rc_check(hipGetLastError(), "k_lemb_afull");
+  }
+  const int nds = ds_splits(B), wps = B / nds;
+  for (int r = 0; r < d.R && !e; ++r) {
+    float* ws = c.ws + r * c.wss;
+    const float* E = c.emb + r * c.es;
+    const float* T = ws + c.wo.T;
+    const float* df1 = ws + c.wo.edf1;
+    // dfc1W = df1^T R   (M1 x B x p*H), applied by the final kernel's Adam
+    if ((e = rc_gemm_launch(rc_gemm_args(1, 0, M1, (int)pH, B, df1, M1, 0, ws + c.wo.R, pH, 0, ws + c.wo.gfc1, pH, 0),
+                            1, s, "emb dfc1W")))
+      break;
+    // dZ = [R > 0] (df1 fc1W)   (B x M1 x p*H)
+    RcGemm g = rc_gemm_args(0, 0, B, (int)pH, M1, df1, M1, 0, E + c.eo.fc1W, pH, 0, ws + c.wo.dZ, pH, 0);
+    g.epi = RC_EPI_MASK;
+    g.aux = ws + c.wo.R;
+    g.ldaux = pH;
+    if ((e = rc_gemm_launch(g, 1, s, "emb dZ"))) break;
+    // dW slices: dWi[s] = T[rows s]^T dZ[rows s], p slices of B rows of the (b, c) axis
+    if ((e = rc_gemm_launch(rc_gemm_args(1, 0, (int)nF, H, B, T, nF, (int64_t)B * nF, ws + c.wo.dZ, H, (int64_t)B * H,
+                                         ws + c.wo.dWi, H, nF * H), p, s, "emb dW")))
+      break;
+    // dT = dZ gcW^T   ((B*p) x H x n*F)
+    if ((e = rc_gemm_launch(rc_gemm_args(0, 1, B * p, (int)nF, H, ws + c.wo.dZ, H, 0, E + c.eo.gcW, H, 0, ws + c.wo.edT,
+                                         nF, 0), 1, s, "emb dT")))
+      break;
+    // dx_bn[b] = Af dT[b]   (p x p*n x F per window)
+    if ((e = rc_gemm_launch(rc_gemm_args(0, 0, p, F, p * n, ws + c.wo.eAf, (int64_t)p * n, 0, ws + c.wo.edT, F, pnF,
+                                         ws + c.wo.edX, F, (int64_t)p * F), B, s, "emb dx_bn")))
+      break;
+    // dS_i slices: sum over the windows of group z of dT_i[b] x_bn[b]^T   (p x wps*F x p)
+    for (int i = 1; i < n && !e; ++i) {
+      RcGemm q = rc_gemm_args(0, 1, p, p, wps * F, ws + c.wo.edT + i * F, nF, (int64_t)wps * pnF, T, nF, (int64_t)wps * pnF,
+                              ws + c.wo.dS + (int64_t)i * p * p, p, c.dsS);
+      q.Kblk = F;
+      q.rA = pnF;
+      q.rB = pnF;
+      e = rc_gemm_launch(q, nds, s, "emb dS");
+    }
+  }
+  if (e) return e;
+  const int ndr = (int)(((int64_t)(n - 1) * p * p + RC_BLOCK - 1) / RC_BLOCK);
+  if (n > 1) {
+    hipLaunchKernelGGL(k_lemb_dsred, dim3(ndr, d.R), dim3(RC_BLOCK), 0, s, c, nds);
+    if ((e = rc_check(hipGetLastError(), "k_lemb_dsred"))) return e;
+  }
+  hipLaunchKernelGGL(k_lemb_bn, dim3(c.dgN, d.R), dim3(RC_BLOCK), 0, s, c);
+  return rc_check(hipGetLastError(), "k_lemb_bn");
+}

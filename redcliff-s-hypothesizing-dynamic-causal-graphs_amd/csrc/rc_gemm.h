@@ -1,0 +1,128 @@
+// rc_gemm.h -- fp32 GEMM core shared by the generic path (rc_generic.hip) and the GEMM-shaped
+// embedder for large p*F (rc_embed_gemm.hip).
+//
+//   C[z] = alpha * sum_{kb} op(A[z] + kb*rA) op(B[z] + kb*rB) + beta * C[z]   (then an epilogue)
+//
+// row-major, op(X) = X or X^T; z = blockIdx.z (batch / split-K slice); the contraction index
+// k in [0, K) is split as k = kb * Kblk + kr, which lets one launch sum products over many
+// small matrices (e.g. over the windows of a batch) without materialising per-window partials.
+// 64x64 output tile per 256-thread workgroup, 4x4 outputs per thread, K staged through LDS in
+// steps of 16; each output is an in-order fmaf chain over k (deterministic).
+#pragma once
+#include "rc_common.h"
+
+#define RC_GEMM_T 64
+#define RC_GEMM_K 16
+
+enum { RC_EPI_NONE = 0, RC_EPI_RELU = 1, RC_EPI_MASK = 2 };  // MASK: times (aux > 0)
+
+struct RcGemm {
+  int ta, tb, M, N, K;
+  const float* A; int64_t lda, sA;
+  const float* B; int64_t ldb, sB;
+  float* C; int64_t ldc, sC;
+  float alpha, beta;
+  int Kblk; int64_t rA, rB;
+  int epi;
+  const float* aux; int64_t ldaux, sAux;
+};
+
+inline RcGemm rc_gemm_args(int ta, int tb, int M, int N, int K, const float* A, int64_t lda, int64_t sA,
+                           const float* B, int64_t ldb, int64_t sB, float* C, int64_t ldc, int64_t sC) {
+  RcGemm g;
+  g.ta = ta; g.tb = tb; g.M = M; g.N = N; g.K = K;
+  g.A = A; g.lda = lda; g.sA = sA;
+  g.B = B; g.ldb = ldb; g.sB = sB;
+  g.C = C; g.ldc = ldc; g.sC = sC;
+  g.alpha = 1.f; g.beta = 0.f;
+  g.Kblk = K > 0 ? K : 1; g.rA = 0; g.rB = 0;
+  g.epi = RC_EPI_NONE; g.aux = nullptr; g.ldaux = 0; g.sAux = 0;
+  return g;
+}
+
+__global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
+  const int bz = blockIdx.z;
+  const float* A = g.A + bz * g.sA;
+  const float* B = g.B + bz * g.sB;
+  float* C = g.C + bz * g.sC;
+  const int n0 = blockIdx.x * RC_GEMM_T, m0 = blockIdx.y * RC_GEMM_T;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const RcDiv dkb(g.Kblk);
+  __shared__ float As[RC_GEMM_K][RC_GEMM_T + 4];  // As[k][m]
+  __shared__ float Bs[RC_GEMM_K][RC_GEMM_T + 4];  // Bs[k][n]
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int k0 = 0; k0 < g.K; k0 += RC_GEMM_K) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // issue all loads of the step before storing any
+      const int e = tid + r * RC_BLOCK;  // 1024 elements of each 16x64 tile
+      int kk, mm;
+      if (g.ta) { kk = e >> 6; mm = e & 63; } else { mm = e >> 4; kk = e & 15; }
+      const int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < g.M && gk < g.K) {
+        const int kb = dkb.div(gk), kr = gk - kb * g.Kblk;
+        const float* Ab = A + kb * g.rA;
+        v = g.ta ? Ab[(int64_t)kr * g.lda + gm] : Ab[(int64_t)gm * g.lda + kr];
+      }
+      av[r] = v;
+      int kb2, nb;
+      if (g.tb) { nb = e >> 4; kb2 = e & 15; } else { kb2 = e >> 6; nb = e & 63; }
+      const int gn = n0 + nb, gk2 = k0 + kb2;
+      float w = 0.f;
+      if (gn < g.N && gk2 < g.K) {
+        const int kb = dkb.div(gk2), kr = gk2 - kb * g.Kblk;
+        const float* Bb = B + kb * g.rB;
+        w = g.tb ? Bb[(int64_t)gn * g.ldb + kr] : Bb[(int64_t)kr * g.ldb + gn];
+      }
+      bv[r] = w;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = tid + r * RC_BLOCK;
+      if (g.ta) As[e >> 6][e & 63] = av[r]; else As[e & 15][e >> 4] = av[r];
+      if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e >> 6][e & 63] = bv[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < RC_GEMM_K; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gm = m0 + ty * 4 + i;
+    if (gm >= g.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gn = n0 + tx * 4 + j;
+      if (gn >= g.N) continue;
+      float* cp = C + (int64_t)gm * g.ldc + gn;
+      float v = g.beta == 0.f ? g.alpha * acc[i][j] : g.alpha * acc[i][j] + g.beta * *cp;
+      if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
+      else if (g.epi == RC_EPI_MASK) v = g.aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
+      *cp = v;
+    }
+  }
+}
+
+inline int rc_gemm_launch(const RcGemm& g, int batch, hipStream_t s, const char* what) {
+  if (g.M <= 0 || g.N <= 0 || batch <= 0) return 0;
+  if (batch > 65535) { rc_set_error("%s: batch %d > 65535", what, batch); return REDCLIFF_ELIMIT; }
+  dim3 grid((g.N + RC_GEMM_T - 1) / RC_GEMM_T, (g.M + RC_GEMM_T - 1) / RC_GEMM_T, batch);
+  hipLaunchKernelGGL(k_rc_gemm, grid, dim3(RC_BLOCK), 0, s, g);
+  return rc_check(hipGetLastError(), what);
+}

@@ -186,12 +186,16 @@ def synth(cfg, N, seed):
     return torch.from_numpy(X), torch.from_numpy(Y)
 
 
-@pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1K4", "mfma"), ("C4", "mfma")])
+@pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1K4", "mfma"), ("C4", "mfma"),
+                                                                        ("C1K4", "embgemm"), ("C2", "embgemm")])
 def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
     """path "mfma" forces the matrix-core factor kernels (rc_factor_mfma.hip, normally chosen
-    for p*L >= 256) onto the published shapes."""
-    if path != "auto":
+    for p*L >= 256), "embgemm" the GEMM-shaped embedder (rc_embed_gemm.hip, normally chosen for
+    p >= 32) onto the published shapes."""
+    if path == "mfma":
         monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    elif path == "embgemm":
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
     cfg = CONFIGS[cname]
     o, m = oracle_and_hip(cfg)
     X, Y = synth(cfg, 2 * cfg["B"] + 40, seed=5)
