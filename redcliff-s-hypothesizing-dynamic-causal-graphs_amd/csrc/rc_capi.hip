@@ -213,8 +213,12 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
   }
   if (emb_grad && egemm) {
-    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd_gemm(c, s); }))) return e;
-    if ((fl & (RC_VALUES | RC_CONFUSION)) && (e = rc_launch_emb_bwd(c, s, false))) return e;  // head only
+    // GEMM chain, then the fused kernel without node workgroups (head / adjacency-L1 reduce)
+    if ((e = timed(KT_EMB_BWD, s, [&] {
+           const int e2 = rc_launch_emb_bwd_gemm(c, s);
+           return e2 ? e2 : rc_launch_emb_bwd(c, s, false);
+         })))
+      return e;
   } else if (emb_grad) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {

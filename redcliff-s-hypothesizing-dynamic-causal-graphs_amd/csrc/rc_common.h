@@ -147,7 +147,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.dwp = x; x = rc_align64(x + p * B * K);
   o.dAadj = x; x = rc_align64(x + K * p * p);
   o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);
-  o.dS = x; x = rc_align64(x + (rc_nchunk(d) > 16 ? rc_nchunk(d) : 16) * d.n * p * p);
+  o.dS = x; x = rc_align64(x + (rc_nchunk(d) > 64 ? rc_nchunk(d) : 64) * d.n * p * p);
   o.dgb = x; x = rc_align64(x + p * rc_nchunk(d) * 2 * d.F);
   o.S = x; x = rc_align64(x + d.n * p * p);
   o.dZ = x; x = rc_align64(x + p * B * d.H);
@@ -319,6 +319,11 @@ __device__ inline void rc_stage_all(S&&... s) {
     (s.store(r), ...);
   }
 }
+
+// fp32 matrix cores: v_mfma_f32_32x32x2f32 accumulator, and the row of accumulator register
+// `reg` of lane `lane` in its 32x32 tile (columns = lane & 31).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ inline int mf_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
 // Block-wide sum; every thread gets the result.  `red` must hold >= RC_BLOCK/64 floats.
 __device__ inline float rc_block_sum(float v, float* red) {

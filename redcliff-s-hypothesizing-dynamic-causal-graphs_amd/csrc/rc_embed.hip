@@ -523,17 +523,33 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
 }
 
-// grid (p * nchunk * nbw [+ 1], R): workgroups [0, p*nchunk*nbw) are (node, column chunk,
-// window block) blocks; the optional last one is the head (loss values / confusion).
+// Adjacency-L1 gradient of A summed over the K factors' records, in place into record 0
+// (fixed order, every load in flight at once: K <= 16).
+__device__ void emb_bwd_dadj(const StepCtx& c, int r, int blk) {
+  const int pp2 = c.d.p * c.d.p, e = blk * RC_BLOCK + threadIdx.x;
+  if (e >= pp2) return;
+  float* dA = c.ws + r * c.wss + c.wo.dAadj;
+  float t = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (k < c.d.K) t += dA[(int64_t)k * pp2 + e];
+  dA[e] = t;
+}
+
+// grid (p * nchunk * nbw [+ 1] [+ nred], R): workgroups [0, p*nchunk*nbw) are (node, column
+// chunk, window block) blocks; then the optional head (loss values / confusion), then the
+// adjacency-L1 reduce workgroups.
 template <bool MULTI>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int BC, int WPB) {
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   extern __shared__ float sm[];
   const int r = blockIdx.y;
   const int nch = rc_nchunk(c.d);
   const int nbw = (c.B + WPB - 1) / WPB;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 32);
-  if ((int)blockIdx.x == nnode) {
+  if ((int)blockIdx.x >= nnode + head) {
+    emb_bwd_dadj(c, r, (int)blockIdx.x - nnode - head);
+  } else if ((int)blockIdx.x == nnode) {
     emb_bwd_head(c, r, sm);
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
   } else {
@@ -542,47 +558,99 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int 
   }
 }
 
-// Supports of normalize_A(A) into S[n][p][p] (S_0 = I, S_1 = L, S_i = S_{i-1} L).
-__device__ void dev_supports(const float* A, float* S, float* dinv, int p, int n) {
-  const int tid = threadIdx.x;
-  for (int i = tid; i < p; i += blockDim.x) {
-    float s = 0.f;
-    for (int j = 0; j < p; ++j) s += fmaxf(A[i * p + j], 0.f);
-    dinv[i] = 1.f / sqrtf(s + 1e-10f);
+// ---- adjacency algebra for p <= 64 in one workgroup, operands in LDS with row stride P = p + 1
+
+// Row sums over j < p of f(i, j), i < p: four lanes per row, each summing a strided quarter,
+// combined in fixed order; out(i, s) runs on the row's first lane.
+template <class Fn, class Out>
+__device__ inline void lds_rowsum(int p, Fn f, Out out) {
+  const int i = threadIdx.x >> 2, sub = threadIdx.x & 3;
+  float s = 0.f;
+  if (i < p)
+    for (int j = sub; j < p; j += 4) s += f(i, j);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  if (i < p && sub == 0) out(i, s);
+}
+
+// p x p product op(X) op(Y) on the matrix cores: wave w owns the 32x32 output tile
+// (w >> 1, w & 1); entries at or beyond p are zero padding.  out(a, b, v) receives each
+// in-range result (one writer per entry).
+template <bool TX, bool TY, class Out>
+__device__ inline void lds_mm(const float* X, const float* Y, int p, int P, Out out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int a0 = 32 * (wv >> 1), b0 = 32 * (wv & 1);
+  if (a0 >= p || b0 >= p) return;
+  const int l31 = lane & 31, kh = lane >> 5, ai = a0 + l31, bj = b0 + l31;
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int k0 = 0; k0 < p; k0 += 2) {
+    const int k = k0 + kh;
+    const float x = (k < p && ai < p) ? (TX ? X[k * P + ai] : X[ai * P + k]) : 0.f;
+    const float y = (k < p && bj < p) ? (TY ? Y[bj * P + k] : Y[k * P + bj]) : 0.f;
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
   }
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int a = a0 + mf_row(reg, lane);
+    if (a < p && bj < p) out(a, bj, acc[reg]);
+  }
+}
+
+// Supports of normalize_A(A) (S_0 = I, S_1 = L, S_l = S_{l-1} L): A padded in LDS, L and its
+// powers built in LDS slots 1..n-1 of Sl and written densely to S[n][p][p].  Used by the
+// optimizer's adjacency workgroup and by k_supports, so both produce the same bits.
+__device__ void supports_lds(const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
+  const int P = p + 1, PP = p * P, pp2 = p * p;
+  const RcDiv dpv(p);
+  lds_rowsum(p, [&](int i, int j) { return fmaxf(Al[i * P + j], 0.f); },
+             [&](int i, float s) { dinv[i] = 1.f / sqrtf(s + 1e-10f); });
   __syncthreads();
-  for (int e = tid; e < p * p; e += blockDim.x) {
-    const int i = e / p, j = e - i * p;
+  for (int e = threadIdx.x; e < pp2; e += RC_BLOCK) {
+    const int i = dpv.div(e), j = e - i * p;
     S[e] = (i == j) ? 1.f : 0.f;
-    if (n > 1) S[p * p + e] = (dinv[i] * fmaxf(A[e], 0.f)) * dinv[j];
+    if (n > 1) {
+      const float lv = (dinv[i] * fmaxf(Al[i * P + j], 0.f)) * dinv[j];
+      Sl[PP + i * P + j] = lv;
+      S[pp2 + e] = lv;
+    }
   }
   __syncthreads();
   for (int l = 2; l < n; ++l) {
-    const float* prev = S + (int64_t)(l - 1) * p * p;
-    const float* Lm = S + (int64_t)p * p;
-    float* out = S + (int64_t)l * p * p;
-    for (int e = tid; e < p * p; e += blockDim.x) {
-      const int i = e / p, j = e - i * p;
-      float t = 0.f;
-      for (int k = 0; k < p; ++k) t += prev[i * p + k] * Lm[k * p + j];
-      out[e] = t;
-    }
+    float* out = Sl + l * PP;
+    float* og = S + (int64_t)l * pp2;
+    lds_mm<false, false>(Sl + (l - 1) * PP, Sl + PP, p, P, [&](int a, int b, float v) {
+      out[a * P + b] = v;
+      og[a * p + b] = v;
+    });
     __syncthreads();
   }
 }
 
+// Supports for every replica from its current A (initialisation and host refreshes).
+// grid (R), dynamic LDS (n + 1) p (p + 1) + 64 floats.
 __global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const float* emb, int64_t es, float* ws,
                                                        int64_t wss, EmbOff eo, WsOff wo) {
-  const int r = blockIdx.x;
-  __shared__ float dinv[64];
-  dev_supports(emb + r * es + eo.A, ws + r * wss + wo.S, dinv, d.p, d.n);
+  const int r = blockIdx.x, p = d.p, P = p + 1;
+  extern __shared__ float sm[];
+  const float* A = emb + r * es + eo.A;
+  for (int e = threadIdx.x; e < p * p; e += RC_BLOCK) {
+    const int i = e / p;
+    sm[i * P + (e - i * p)] = A[e];
+  }
+  __syncthreads();
+  supports_lds(sm, sm + p * P, ws + r * wss + wo.S, sm + (d.n + 1) * p * P, p, d.n);
 }
 
 // ------------------------------------------------------------------------------------------
-// K4: embedder optimizer finalisation.  Workgroups [0, nw) apply Adam to W_i, fc2, fc1 bias,
-// BN affine (reducing per-node partials in fixed order); workgroup nw handles the
+// K4: embedder optimizer finalisation.  Workgroups [1, nw] apply Adam to W_i, fc2, fc1 bias,
+// BN affine (reducing per-node partials in fixed order); workgroup 0 handles the
 // adjacency A (Chebyshev + normalize_A backward, adjacency-L1 gradient), the BN running
 // statistics and recomputes the supports for the next step.
+// NR = elements of a p x p matrix per thread (p * p <= NR * RC_BLOCK): staging width and the
+// register prefetch; small adjacencies get the short code (one-shot code is fetched cold).
+template <int NR>
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y;
@@ -596,9 +664,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   const int nFH = n * F * H, nfc = K * M1 + K + M1, nf1 = M1 * p * H;
   const int total = nFH + nfc + 2 * F + nf1;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 0);
-  if ((int)blockIdx.x < nw) {
+  // workgroup 0 is the adjacency workgroup (the longest; dispatched first), 1..nw the parameters
+  if (blockIdx.x > 0) {
     if (!stepA) return;
-    const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
+    const int e = (blockIdx.x - 1) * RC_BLOCK + threadIdx.x;
     if (e >= total) return;
     float g = 0.f;
     int64_t idx;
@@ -633,120 +702,107 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
     return;
   }
-  // ---- adjacency workgroup: every p x p operand lives in LDS (dynamic, (n + 5) p^2 floats)
+  // ---- adjacency workgroup: every p x p operand lives in LDS (dynamic, (2n + 2) p (p+1)
+  // floats, rows padded to P = p + 1); the p x p products run on the matrix cores
   const int tid = threadIdx.x;
   extern __shared__ float sm[];
-  const int pp2 = p * p;
-  float* Al = sm;                       // A (pre-update)
-  float* Ar = Al + pp2;                 // relu(A)
-  float* dL = Ar + pp2;                 // dL/dL (the normalised Laplacian)
-  float* dSw = dL + pp2;                // dS_1 .. dS_{n-1}
-  float* Sl = dSw + (n - 1) * pp2;      // supports S_0 .. S_{n-1} (pre-update; S_1 = L)
-  float* dinv = Sl + n * pp2;           // [64]
-  float* dsum = dinv + 64;              // [64]
-  float* dd = dsum + 64;                // [64]
+  const int pp2 = p * p, P = p + 1, PP = p * P;
+  const RcDiv dpv(p);
+  float* Al = sm;                  // A (pre-update, then the updated A)
+  float* Ar = Al + PP;             // relu(A)
+  float* dL = Ar + PP;             // dL/dL (the normalised Laplacian)
+  float* dSw = dL + PP;            // dS_1 .. dS_{n-1}
+  float* Sl = dSw + (n - 1) * PP;  // slot 0: adjacency-L1 gradient of A; slots 1..n-1: S_1 .. S_{n-1}
+  float* dinv = Sl + n * PP;       // [64]
+  float* dd = dinv + 64;           // [64]
+  // dense index e of a stack of p x p matrices -> padded LDS index
+  auto at = [&](int e) { const int i = dpv.div(e); return i * P + (e - i * p); };
+  RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 48);
   if (stepA) {
     float* A = E + c.eo.A;
     const float* S = ws + c.wo.S;
+    const bool adjL1 = c.flags & RC_LOSS_ADJ;
+    const bool adam = !(c.flags & RC_GRAD_ONLY);
+    // A's Adam moments, prefetched into registers
+    float mreg[NR], vreg[NR];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int e = tid + u * RC_BLOCK;
+      const bool in = adam && e < pp2;
+      mreg[u] = in ? Mm[c.eo.A + e] : 0.f;
+      vreg[u] = in ? V[c.eo.A + e] : 0.f;
+    }
+    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 49);
     rc_stage_all(
-        rc_seg<4>(pp2, [&](int e) { return A[e]; }, [&](int e, float v) { Al[e] = v; Ar[e] = fmaxf(v, 0.f); }),
-        rc_seg<8>(n * pp2, [&](int e) { return S[e]; }, [&](int e, float v) { Sl[e] = v; }),
+        rc_seg<NR>(pp2, [&](int e) { return A[e]; }, [&](int e, float v) {
+          const int q = at(e);
+          Al[q] = v;
+          Ar[q] = fmaxf(v, 0.f);
+        }),
+        rc_seg<NR>((n - 1) * pp2, [&](int e) { return S[pp2 + e]; }, [&](int e, float v) { Sl[PP + at(e)] = v; }),
         // dS_i[c][c'] = fixed-order sum of the backward kernel's partial records
-        rc_seg<8>((n - 1) * pp2, [&](int e) {
+        rc_seg<NR>((n - 1) * pp2, [&](int e) {
           const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
           float t = 0.f;
           for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
           return t;
-        }, [&](int e, float v) { dSw[e] = v; }));
-    for (int e = tid; e < pp2; e += RC_BLOCK) dL[e] = 0.f;
+        }, [&](int e, float v) { dSw[at(e)] = v; }),
+        // adjacency-L1 gradient (summed over the factors by k_emb_bwd's reduce workgroups)
+        rc_seg<NR>(adjL1 ? pp2 : 0, [&](int e) { return ws[c.wo.dAadj + e]; }, [&](int e, float v) { Sl[at(e)] = v; }));
+    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 50);
+    for (int e = tid; e < pp2; e += RC_BLOCK) dL[at(e)] = 0.f;
+    lds_rowsum(p, [&](int i, int j) { return Ar[i * P + j]; },
+               [&](int i, float s) { dinv[i] = 1.f / sqrtf(s + 1e-10f); });
     __syncthreads();
-    for (int i = tid; i < p; i += RC_BLOCK) {
-      float s = 0.f;
-      for (int j = 0; j < p; ++j) s += Ar[i * p + j];
-      dsum[i] = s;
-      dinv[i] = 1.f / sqrtf(s + 1e-10f);
-    }
-    __syncthreads();
+    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 51);
     // back through S_l = S_{l-1} L, l = n-1 .. 2
     for (int l = n - 1; l >= 2; --l) {
-      const float* dSl = dSw + (int64_t)(l - 1) * pp2;
-      float* dSprev = dSw + (int64_t)(l - 2) * pp2;
-      const float* Sprev = Sl + (int64_t)(l - 1) * pp2;
-      const float* Lm = Sl + pp2;
-      for (int e = tid; e < pp2; e += RC_BLOCK) {
-        const int a = e / p, b = e - a * p;
-        float t1 = 0.f, t2 = 0.f;
-        for (int k = 0; k < p; ++k) {
-          t1 += dSl[a * p + k] * Lm[b * p + k];     // (dS_l L^T)[a][b]
-          t2 += Sprev[k * p + a] * dSl[k * p + b];  // (S_{l-1}^T dS_l)[a][b]
-        }
-        dSprev[e] += t1;
-        dL[e] += t2;
-      }
+      const float* dSl = dSw + (l - 1) * PP;
+      float* dSprev = dSw + (l - 2) * PP;
+      const float* Sprev = Sl + (l - 1) * PP;
+      const float* Lm = Sl + PP;
+      lds_mm<false, true>(dSl, Lm, p, P, [&](int a, int b, float v) { dSprev[a * P + b] += v; });  // dS_l L^T
+      lds_mm<true, false>(Sprev, dSl, p, P, [&](int a, int b, float v) { dL[a * P + b] += v; });   // S_{l-1}^T dS_l
       __syncthreads();
     }
     if (n >= 2) {
-      for (int e = tid; e < pp2; e += RC_BLOCK) dL[e] += dSw[e];
-      __syncthreads();
-    }
-    // normalize_A backward: L[i][j] = dinv_i relu(A)[i][j] dinv_j, dinv_i = (sum_j relu(A)[i][j] + 1e-10)^-1/2
-    for (int i = tid; i < p; i += RC_BLOCK) {
-      float g = 0.f;
-      for (int j = 0; j < p; ++j) g += dL[i * p + j] * Ar[i * p + j] * dinv[j] + dL[j * p + i] * dinv[j] * Ar[j * p + i];
-      // d(dinv)/d(sum) = -1/2 (sum + 1e-10)^-3/2
-      dd[i] = g * (-0.5f) * dinv[i] * dinv[i] * dinv[i];
-    }
-    __syncthreads();
-    for (int e = tid; e < pp2; e += RC_BLOCK) {
-      const int i = e / p, j = e - i * p;
-      float g = (Al[e] > 0.f) ? (dL[e] * dinv[i] * dinv[j] + dd[i]) : 0.f;
-      if (c.flags & RC_LOSS_ADJ)
-        for (int k = 0; k < K; ++k) g += ws[c.wo.dAadj + (int64_t)k * pp2 + e];
-      if (c.flags & RC_GRAD_ONLY) {
-        c.gE[r * c.es + c.eo.A + e] = g;
-      } else {
-        float pv = Al[e], mv = Mm[c.eo.A + e], vv = V[c.eo.A + e];
-        rc_adam(pv, mv, vv, g, as);
-        A[e] = pv; Mm[c.eo.A + e] = mv; V[c.eo.A + e] = vv;
-        Al[e] = pv;  // the new A for the supports below
-      }
-    }
-    __syncthreads();
-    // supports of the updated A for the next step, computed in LDS (after a gradient-only shard
-    // step A changes later, in redcliff_adam_apply, and the host refreshes them)
-    if (!(c.flags & RC_GRAD_ONLY)) {
-      for (int i = tid; i < p; i += RC_BLOCK) {
-        float s = 0.f;
-        for (int j = 0; j < p; ++j) s += fmaxf(Al[i * p + j], 0.f);
-        dinv[i] = 1.f / sqrtf(s + 1e-10f);
-      }
-      __syncthreads();
-      float* Sg = ws + c.wo.S;
       for (int e = tid; e < pp2; e += RC_BLOCK) {
-        const int i = e / p, j = e - i * p;
-        const float s0 = (i == j) ? 1.f : 0.f;
-        Sg[e] = s0;
-        if (n > 1) {
-          const float lv = (dinv[i] * fmaxf(Al[e], 0.f)) * dinv[j];
-          Sl[pp2 + e] = lv;
-          Sg[pp2 + e] = lv;
-        }
+        const int q = at(e);
+        dL[q] += dSw[q];
       }
       __syncthreads();
-      for (int l = 2; l < n; ++l) {
-        const float* prev = Sl + (int64_t)(l - 1) * pp2;
-        const float* Lm = Sl + pp2;
-        for (int e = tid; e < pp2; e += RC_BLOCK) {
-          const int i = e / p, j = e - i * p;
-          float t = 0.f;
-          for (int k = 0; k < p; ++k) t += prev[i * p + k] * Lm[k * p + j];
-          Sl[(int64_t)l * pp2 + e] = t;
-          Sg[(int64_t)l * pp2 + e] = t;
+    }
+    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 52);
+    // normalize_A backward: L[i][j] = dinv_i relu(A)[i][j] dinv_j, dinv_i = (sum_j relu(A)[i][j] + 1e-10)^-1/2,
+    // d(dinv)/d(sum) = -1/2 (sum + 1e-10)^-3/2
+    lds_rowsum(p, [&](int i, int j) {
+      return dL[i * P + j] * Ar[i * P + j] * dinv[j] + dL[j * P + i] * dinv[j] * Ar[j * P + i];
+    }, [&](int i, float g) { dd[i] = g * (-0.5f) * dinv[i] * dinv[i] * dinv[i]; });
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int e = tid + u * RC_BLOCK;
+      if (e < pp2) {
+        const int i = dpv.div(e), j = e - i * p, q = i * P + j;
+        float g = (Al[q] > 0.f) ? (dL[q] * dinv[i] * dinv[j] + dd[i]) : 0.f;
+        if (adjL1) g += Sl[q];
+        if (!adam) {
+          c.gE[r * c.es + c.eo.A + e] = g;
+        } else {
+          float pv = Al[q], mv = mreg[u], vv = vreg[u];
+          rc_adam(pv, mv, vv, g, as);
+          A[e] = pv; Mm[c.eo.A + e] = mv; V[c.eo.A + e] = vv;
+          Al[q] = pv;  // the new A for the supports below
         }
-        __syncthreads();
       }
     }
+    __syncthreads();
+    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 53);
+    // supports of the updated A for the next step (after a gradient-only shard step A changes
+    // later, in redcliff_adam_apply, and the host refreshes them)
+    if (adam) supports_lds(Al, Sl, ws + c.wo.S, dinv, p, n);
   }
+  RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 54);
   // BatchNorm running statistics (torch: double math, momentum*stat + (1-momentum)*running)
   if (c.nbn > 0 && tid < F) {
     const double* st = c.bns + r * c.bnsr;
@@ -822,15 +878,17 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   const int BC = rc_emb_bc(d), WPB = rc_emb_wpb(d);
   const int nnode = node_wgs ? d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB) : 0;
   const int head = (c.flags & (RC_VALUES | RC_CONFUSION)) ? 1 : 0;
-  if (nnode + head == 0) return 0;
+  const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
+  const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
+  if (nnode + head + nred == 0) return 0;
   if (WPB > BC) {
     int e = rc_lds_optin(k_emb_bwd<true>, lds, "k_emb_bwd LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_bwd<true>, dim3(nnode + head, d.R), dim3(RC_BLOCK), lds, s, c, nnode, BC, WPB);
+    hipLaunchKernelGGL(k_emb_bwd<true>, dim3(nnode + head + nred, d.R), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
   } else {
     int e = rc_lds_optin(k_emb_bwd<false>, lds, "k_emb_bwd LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head, d.R), dim3(RC_BLOCK), lds, s, c, nnode, BC, WPB);
+    hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head + nred, d.R), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
   }
   return rc_check(hipGetLastError(), "k_emb_bwd");
 }
@@ -839,17 +897,26 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
   const int nw = (total + RC_BLOCK - 1) / RC_BLOCK;
-  const size_t lds = sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * d.p + 3 * 64);
+  const size_t lds = sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * (d.p + 1) + 3 * 64);
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  int e = rc_lds_optin(k_emb_final, lds, "k_emb_final LDS");
-  if (e) return e;
-  hipLaunchKernelGGL(k_emb_final, dim3(nw + 1, d.R), dim3(RC_BLOCK), lds, s, c, nw);
+  if (d.p * d.p <= 4 * RC_BLOCK) {
+    int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + 1, d.R), dim3(RC_BLOCK), lds, s, c, nw);
+  } else {
+    int e = rc_lds_optin(k_emb_final<16>, lds, "k_emb_final LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, d.R), dim3(RC_BLOCK), lds, s, c, nw);
+  }
   return rc_check(hipGetLastError(), "k_emb_final");
 }
 
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,
                        WsOff wo, hipStream_t s) {
-  hipLaunchKernelGGL(k_supports, dim3(d.R), dim3(RC_BLOCK), 0, s, d, emb, es, ws, wss, eo, wo);
+  const size_t lds = sizeof(float) * ((size_t)(d.n + 1) * d.p * (d.p + 1) + 64);
+  int e = rc_lds_optin(k_supports, lds, "k_supports LDS");
+  if (e) return e;
+  hipLaunchKernelGGL(k_supports, dim3(d.R), dim3(RC_BLOCK), lds, s, d, emb, es, ws, wss, eo, wo);
   return rc_check(hipGetLastError(), "k_supports");
 }
 

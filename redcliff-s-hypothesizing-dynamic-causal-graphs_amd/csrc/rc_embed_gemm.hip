@@ -244,9 +244,9 @@ int fc1_splits(const RedcliffDims& d) {
   return 1;
 }
 
-// window groups of the dS product: a power-of-two divisor of B, at most 16
+// window groups of the dS product: a power-of-two divisor of B, at most 64
 int ds_splits(int B) {
-  int s = 16;
+  int s = 64;
   while (s > 1 && B % s) s >>= 1;
   return s;
 }

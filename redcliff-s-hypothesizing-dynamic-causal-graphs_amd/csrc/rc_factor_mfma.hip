@@ -23,17 +23,12 @@
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
 #define MF_BT 64   // windows per forward tile (2 row blocks of 32)
 #define MF_QC 32   // contraction chunk per staging step (16 MFMA k-steps)
 #define MB_QT 128  // dW0 columns per backward tile
 #define MB_BC 32   // windows per backward staging step
 
 __device__ inline float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-
-// Row index of accumulator register `reg` of lane `lane` in a 32x32 MFMA tile (columns = lane & 31).
-__device__ inline int mf_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
 // ------------------------------------------------------------------------------------------
 // Window transpose: Xw[b][c*L + t] = X[row0 + b][Lmax - L + t][c], zero-padded to Qp columns.
@@ -197,6 +192,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   float* ybuf = dAp + p * Ls;  // [Bmax][K]
   float* rA = ybuf + d.Bmax * K;  // [256]
   float* rB = rA + RC_BLOCK;      // [256]
+  float* dwf = rB + RC_BLOCK;     // [Bmax]  forecast part of dL/dw_bk
 
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
@@ -221,7 +217,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     wk[b] = wb;
     dyl[b] = g * wb;
     ws[c.wo.dyl + (int64_t)kj * d.Bmax + b] = g * wb;
-    if (fgrad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = g * ybuf[b * K + k];
+    dwf[b] = g * ybuf[b * K + k];
+    if (fgrad && !adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = dwf[b];
     if (k == 0) {
       fsum += res * res;
       ws[c.wo.xsim + (int64_t)b * p + j] = xs;
@@ -244,52 +241,66 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     for (int t = 0; t < L; ++t) sq += sqs[cc * L + t];
     ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
   }
-  // ---- adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j]
+  // ---- adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j] over the
+  // lag slice: pass 1 (thread = window b, half of the (c, lag) entries) gives the value and
+  // dL/dw_bk; pass 2 (thread = (c, lag) entry, loop over windows) gives dL/dG (-> ws.dgs) and
+  // dL/dA[c][j] (-> ws.dAadj) from one sign evaluation
   const bool adj_on = adj_grad || values;
   if (adj_on) {
     for (int cc = tid; cc < p; cc += RC_BLOCK) Acol[cc] = E[c.eo.A + cc * p + j];
     for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
     __syncthreads();
+    const int nls = p * Ls, hl = (nls + 1) / 2, half = tid & 1;
     float vsum = 0.f;
-    for (int b = tid; b < B; b += RC_BLOCK) {
-      const float wb = wk[b];
+    for (int b0 = 0; b0 < B; b0 += RC_BLOCK / 2) {
+      const int b = b0 + (tid >> 1);
       float t = 0.f, v = 0.f;
-      for (int cc = 0; cc < p; ++cc)
-        for (int i = 0; i < Ls; ++i) {
+      if (b < B) {
+        const float wb = wk[b];
+        const int e1 = min(nls, (half + 1) * hl);
+        int e = half * hl, cc = e / Ls, i = e - cc * Ls;
+        for (; e < e1; ++e) {
           const float g = Gs[cc * L + (L - Ls + i)];
           const float val = wb * g + Acol[cc];
           t += lwt[i] * rc_sign(val) * g;
           v += lwt[i] * fabsf(val);
+          if (++i == Ls) { i = 0; ++cc; }
         }
-      if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] += hy.c_adj * t;
-      vsum += v;
+      }
+      // the two halves of window b are adjacent lanes: combined in fixed order (first + second)
+      const float t_hi = __shfl_xor(t, 1), v_hi = __shfl_xor(v, 1);
+      if (half == 0 && b < B) {
+        if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = dwf[b] + hy.c_adj * (t + t_hi);
+        vsum += v + v_hi;
+      }
     }
     if (values) {
-      const float t = rc_block_sum(vsum, red);
-      if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * t;
+      const float vs = rc_block_sum(vsum, red);
+      if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * vs;
     }
   }
-  if (c.flags & RC_STEP_B) {  // dL/dG for the dW0 epilogue (zero outside the lag slice)
-    for (int q = tid; q < Q; q += RC_BLOCK) {
-      const int cc = q / L, t = q - cc * L, i = t - (L - Ls);
-      float v = 0.f;
-      if (adj_grad && i >= 0) {
-        const float g = Gs[q];
-        float sw = 0.f;
-        for (int b = 0; b < B; ++b) sw += rc_sign(wk[b] * g + Acol[cc]) * wk[b];
-        v = hy.c_adj * lwt[i] * sw;
+  if (adj_grad) {
+    const bool wg = c.flags & RC_STEP_B, ag = c.flags & RC_STEP_A;
+    for (int e = tid; e < p * Ls; e += RC_BLOCK) {
+      const int cc = e / Ls, i = e - cc * Ls;
+      const float g = Gs[cc * L + (L - Ls + i)], ac = Acol[cc];
+      float sw = 0.f, s1 = 0.f;
+      for (int b = 0; b < B; ++b) {
+        const float sg = rc_sign(wk[b] * g + ac);
+        sw += sg * wk[b];
+        s1 += sg;
       }
-      ws[c.wo.dgs + (int64_t)kj * Q + q] = v;
+      if (wg) ws[c.wo.dgs + (int64_t)kj * Q + cc * L + (L - Ls + i)] = hy.c_adj * lwt[i] * sw;
+      if (ag) dAp[e] = hy.c_adj * lwt[i] * s1;
+    }
+  }
+  if (c.flags & RC_STEP_B) {  // dL/dG is zero outside the lag slice (and everywhere without the adj-L1 term)
+    for (int q = tid; q < Q; q += RC_BLOCK) {
+      const int cc = q / L, tt = q - cc * L;
+      if (!adj_grad || tt < L - Ls) ws[c.wo.dgs + (int64_t)kj * Q + q] = 0.f;
     }
   }
   if (adj_grad && (c.flags & RC_STEP_A)) {
-    for (int e = tid; e < p * Ls; e += RC_BLOCK) {
-      const int cc = e / Ls, i = e - cc * Ls;
-      const float g = Gs[cc * L + (L - Ls + i)];
-      float s1 = 0.f;
-      for (int b = 0; b < B; ++b) s1 += rc_sign(wk[b] * g + Acol[cc]);
-      dAp[e] = hy.c_adj * lwt[i] * s1;
-    }
     __syncthreads();
     for (int cc = tid; cc < p; cc += RC_BLOCK) {
       float s = 0.f;
@@ -372,7 +383,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
       float v = 0.f;
       if (kj < KP && u < h && b < B) {
         const float av = ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u];
-        v = av > 0.f ? ws[c.wo.dyl + (int64_t)kj * d.Bmax + b] : 0.f;
+        const float dy = ws[c.wo.dyl + (int64_t)kj * d.Bmax + b];
+        v = av > 0.f ? dy : 0.f;
       }
       zr[i] = v;  // times w1[u] at store time
     }
@@ -423,34 +435,56 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
   if (kj >= KP) return;
   const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
+  const bool adam = !(c.flags & RC_GRAD_ONLY);
   float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
   float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
   float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
   float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
+  // every operand of the 32 updates this lane owns is loaded before the first store (the
+  // stores could alias the loads as far as the compiler knows, which would serialise them)
+  float dg[2], gn[2], pw[2][16], pm[2][16], pv[2][16];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int q = q0 + qh + 32 * half + l31;
+    const bool qin = q < Q;
+    dg[half] = (adj_grad && qin) ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
+    gn[half] = (adj_grad && qin) ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int u = mf_row(reg, lane);
+      const bool in = qin && u < h;
+      const int64_t idx = (int64_t)u * Q + q;
+      pw[half][reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
+      pm[half][reg] = (in && adam) ? M0[idx] : 0.f;
+      pv[half][reg] = (in && adam) ? V0[idx] : 0.f;
+    }
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int q = q0 + qh + 32 * half + l31;
     if (q >= Q) continue;
-    float dg = 0.f, gn = 0.f;
-    if (adj_grad) {
-      dg = ws[c.wo.dgs + (int64_t)kj * Q + q];
-      gn = ws[c.wo.G + (int64_t)kj * Q + q];
-    }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int u = mf_row(reg, lane);
       if (u >= h) continue;
       const int64_t idx = (int64_t)u * Q + q;
       float g = half == 0 ? acc0[reg] : acc1[reg];
-      if (adj_grad && gn > 0.f) g += dg * (W0[idx] / gn);
-      rc_update(c, W0, M0, V0, G0w, idx, g, as);
+      if (adj_grad && gn[half] > 0.f) g += dg[half] * (pw[half][reg] / gn[half]);
+      if (!adam) {
+        G0w[idx] = g;
+      } else {
+        rc_adam(pw[half][reg], pm[half][reg], pv[half][reg], g, as);
+        W0[idx] = pw[half][reg];
+        M0[idx] = pm[half][reg];
+        V0[idx] = pv[half][reg];
+      }
     }
   }
 }
 
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
   const int Q = d.p * d.L;
-  return sizeof(float) * (size_t)(2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + d.Bmax * d.K + 2 * RC_BLOCK);
+  return sizeof(float) * (size_t)(2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + d.Bmax * d.K + 2 * RC_BLOCK + d.Bmax);
 }
 
 }  // namespace

@@ -55,10 +55,11 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  for (int k0 = 0; k0 < g.K; k0 += RC_GEMM_K) {
-    float av[4], bv[4];
+  // the next K step's operands are loaded into registers while the current step multiplies
+  float av[4], bv[4];
+  auto load = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {  // issue all loads of the step before storing any
+    for (int r = 0; r < 4; ++r) {
       const int e = tid + r * RC_BLOCK;  // 1024 elements of each 16x64 tile
       int kk, mm;
       if (g.ta) { kk = e >> 6; mm = e & 63; } else { mm = e >> 4; kk = e & 15; }
@@ -81,6 +82,9 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
       }
       bv[r] = w;
     }
+  };
+  if (g.K > 0) load(0);
+  for (int k0 = 0; k0 < g.K; k0 += RC_GEMM_K) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int e = tid + r * RC_BLOCK;
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
       if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e >> 6][e & 63] = bv[r];
     }
     __syncthreads();
+    if (k0 + RC_GEMM_K < g.K) load(k0 + RC_GEMM_K);
 #pragma unroll
     for (int kk = 0; kk < RC_GEMM_K; ++kk) {
       float a[4], b[4];

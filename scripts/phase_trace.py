@@ -47,7 +47,8 @@ def main():
     names = ["emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix"]
     t_first = min(int(tr[k][0::2][tr[k][0::2] > 0].min()) for k in range(len(names)) if (tr[k][0::2] > 0).any())
     ph = tr[6]
-    for lo, hi, label in ((0, 16, "emb_fwd WG0 phases"), (16, 32, "fac_bwd WG0 phases"), (32, 48, "emb_bwd WG0 phases")):
+    for lo, hi, label in ((0, 16, "emb_fwd WG0 phases"), (16, 32, "fac_bwd WG0 phases"), (32, 48, "emb_bwd WG0 phases"),
+                            (48, 64, "emb_final adjacency WG phases")):
         t = ph[lo:hi]
         idx = [i for i in range(hi - lo) if t[i] > 0]
         if len(idx) > 1:
