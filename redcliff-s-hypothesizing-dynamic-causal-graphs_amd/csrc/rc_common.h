@@ -51,6 +51,7 @@ struct WsOff {
   int64_t edT;    // [Bmax][p][n][F]   dL/dT_i (GEMM embedder; T itself is [Bmax][p][n][F] there)
   int64_t edX;    // [Bmax][p][F]      dL/d x_bn (GEMM embedder)
   int64_t eAf;    // [p][p*n]          [S_0^T | ... | S_{n-1}^T] interleaved (GEMM embedder)
+  int64_t edr;    // [Bmax][K]         dL/d(raw embedder output) (GEMM embedder)
   int64_t total;
 };
 
@@ -163,6 +164,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.edT = x; x = rc_align64(x + B * p * d.n * d.F);
   o.edX = x; x = rc_align64(x + B * p * d.F);
   o.eAf = x; x = rc_align64(x + p * p * d.n);
+  o.edr = x; x = rc_align64(x + B * K);
 #ifdef RC_TRACE
   x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
 #endif

@@ -24,6 +24,9 @@
 
 namespace {
 
+// windows per k_lemb_dhead workgroup: 64 (window, factor) items of 4 lanes each (K <= 16)
+__host__ __device__ inline int lemb_wpw(const RedcliffDims& d) { return 64 / d.K; }
+
 // x_bn[b][c][0][f] = X[row0 + b][Lmax - F + f][c] * alpha_f + beta_f    grid (B, R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
   const RedcliffDims& d = c.d;
@@ -51,50 +54,60 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
   __syncthreads();
   float* T = ws + c.wo.T + (int64_t)b * p * n * F;
   const RcDiv dp(p);
-  for (int e = tid; e < p * F; e += RC_BLOCK) {  // read (f, c) contiguous, write [c][0][f]
-    const int f = dp.div(e), ch = e - f * p;
-    T[(int64_t)ch * n * F + f] = X[e] * alpha[f] + beta[f];
+  // read (f, c) contiguous, write [c][0][f]; every load of a round issued before its stores
+  for (int e0 = 0; e0 < p * F; e0 += 16 * RC_BLOCK) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + u * RC_BLOCK + tid;
+      v[u] = e < p * F ? X[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int e = e0 + u * RC_BLOCK + tid;
+      if (e < p * F) {
+        const int f = dp.div(e), ch = e - f * p;
+        T[(int64_t)ch * n * F + f] = v[u] * alpha[f] + beta[f];
+      }
+    }
   }
 }
 
-// [S_0^T | S_1^T | ...] interleaved for dx_bn = sum_i S_i^T dT_i:  Af[c][c'*n + i] = S_i[c'][c]
-__global__ __launch_bounds__(RC_BLOCK) void k_lemb_afull(StepCtx c) {
-  const RedcliffDims& d = c.d;
-  const int r = blockIdx.x, p = d.p, n = d.n;
-  float* ws = c.ws + r * c.wss;
-  const float* S = ws + c.wo.S;
-  for (int e = threadIdx.x; e < p * p * n; e += RC_BLOCK) {
-    const int cc = e / (p * n), rem = e - cc * p * n, cp = rem / n, i = rem - cp * n;
-    ws[c.wo.eAf + e] = S[((int64_t)i * p + cp) * p + cc];
-  }
-}
-
-// f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (ceil(B/16), R)
+// f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (B, R): one window per
+// workgroup, lanes (m, g): g sums every 4th partial (all loads in flight), fixed-order combine.
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, b0 = blockIdx.x * 16;
+  const int r = blockIdx.y, b = blockIdx.x;
   const int M1 = d.M1, K = d.K;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
-  __shared__ float f1s[16][64];
-  const int tid = threadIdx.x;
-  for (int e = tid; e < 16 * M1; e += RC_BLOCK) {
-    const int s = e / M1, m = e - s * M1, b = b0 + s;
-    if (b >= c.B) continue;
-    float v = 0.f;
-    for (int q = 0; q < nsplit; ++q) v += ws[c.wo.f1p + ((int64_t)q * d.Bmax + b) * M1 + m];
+  __shared__ float f1s[64];
+  const int tid = threadIdx.x, m = tid >> 2, g = tid & 3;
+  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + m;
+  float v = 0.f;
+  if (m < M1) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {  // nsplit <= 64
+      const int q = g + 4 * u;
+      if (q < nsplit) v += part[(int64_t)q * d.Bmax * M1];
+    }
+  }
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  if (m < M1 && g == 0) {
     v += E[c.eo.fc1b + m];
-    f1s[s][m] = v;
+    f1s[m] = v;
     ws[c.wo.f1 + (int64_t)b * M1 + m] = v;
   }
   __syncthreads();
-  for (int e = tid; e < 16 * K; e += RC_BLOCK) {
-    const int s = e / K, k = e - s * K, b = b0 + s;
-    if (b >= c.B) continue;
-    float a = 0.f;
-    for (int m = 0; m < M1; ++m) a += E[c.eo.fc2W + k * M1 + m] * fmaxf(f1s[s][m], 0.f);
-    ws[c.wo.w + (int64_t)b * K + k] = a + E[c.eo.fc2b + k];
-  }
+  // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]): lanes (k, g) over every 4th m
+  const int k = tid >> 2;
+  float a = 0.f;
+  if (k < K)
+    for (int mm = g; mm < M1; mm += 4) a += E[c.eo.fc2W + k * M1 + mm] * fmaxf(f1s[mm], 0.f);
+  a += __shfl_xor(a, 1);
+  a += __shfl_xor(a, 2);
+  if (k < K && g == 0) ws[c.wo.w + (int64_t)b * K + k] = a + E[c.eo.fc2b + k];
 }
 
 // dL/d(raw embedder output) (the same rule as the node-chunk kernel, rc_embed.hip), dL/df1,
@@ -121,54 +134,91 @@ __device__ inline float lemb_draw(const StepCtx& c, int r, int k, float raw, flo
   return graw;
 }
 
+// grid (ceil(B / WPW), R), WPW = 64 / K windows per workgroup: lanes (item = (window, k), g),
+// g sums every 4th channel partial of the factor-side dL/dw (all loads in flight); then dL/df1
+// of the workgroup's windows.  dr -> ws.edr, df1 -> ws.edf1.
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y;
   const int K = d.K, M1 = d.M1, p = d.p, B = c.B;
+  const int WPW = lemb_wpw(d), b0 = blockIdx.x * WPW;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
-  extern __shared__ float sm[];
-  float* dr = sm;               // [B][K]
-  float* fc2s = dr + B * K;     // [K][M1]
-  const int tid = threadIdx.x;
+  __shared__ float drs[64];
+  const int tid = threadIdx.x, item = tid >> 2, g = tid & 3;
+  const int s = item / K, k = item - s * K, b = b0 + s;
+  const bool ok = item < WPW * K && b < B;
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
-  for (int e = tid; e < K * M1; e += RC_BLOCK) fc2s[e] = E[c.eo.fc2W + e];
-  for (int e = tid; e < B * K; e += RC_BLOCK) {
-    const int b = e / K, k = e - b * K;
-    float g = 0.f;
-    if (fac_grad)
-      for (int j = 0; j < p; ++j) g += ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k];
+  float t = 0.f;
+  if (ok && fac_grad) {
+    const float* dw = ws + c.wo.dwp + (int64_t)b * K + k;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {  // p <= 64
+      const int j = g + 4 * u;
+      if (j < p) t += dw[(int64_t)j * d.Bmax * K];
+    }
+  }
+  t += __shfl_xor(t, 1);
+  t += __shfl_xor(t, 2);
+  if (ok && g == 0) {
     const float y = lab_on ? c.lab[r * c.labr + (c.row0 + b) * K + k] : 0.f;
-    dr[e] = lemb_draw(c, r, k, ws[c.wo.w + e], g, y);
+    const float v = lemb_draw(c, r, k, ws[c.wo.w + (int64_t)b * K + k], t, y);
+    drs[item] = v;
+    ws[c.wo.edr + (int64_t)b * K + k] = v;
   }
   __syncthreads();
   const float* f1 = ws + c.wo.f1;
   float* df1 = ws + c.wo.edf1;
-  for (int e = tid; e < B * M1; e += RC_BLOCK) {
-    const int b = e / M1, m = e - b * M1;
-    float g = 0.f;
-    if (f1[e] > 0.f)
-      for (int k = 0; k < K; ++k) g += dr[b * K + k] * fc2s[k * M1 + m];
-    df1[e] = g;
+  for (int e = tid; e < WPW * M1; e += RC_BLOCK) {
+    const int sw = e / M1, m = e - sw * M1, bb = b0 + sw;
+    if (bb >= B) continue;
+    float gg = 0.f;
+    if (f1[(int64_t)bb * M1 + m] > 0.f)
+      for (int kk = 0; kk < K; ++kk) gg += drs[sw * K + kk] * E[c.eo.fc2W + kk * M1 + m];
+    df1[(int64_t)bb * M1 + m] = gg;
   }
-  __syncthreads();
-  // dfc2W[k][m] = sum_b dr[b][k] relu(f1[b][m]); dfc2b[k] = sum_b dr[b][k]; dfc1b[m] = sum_b df1[b][m]
+}
+
+// Workgroups [0, ngfc): fc2 weight / fc2 bias / fc1 bias gradients, 64 outputs per workgroup,
+// lanes (output, g) over every 4th window, fixed-order combine:
+//   dfc2W[k][m] = sum_b dr[b][k] relu(f1[b][m]); dfc2b[k] = sum_b dr[b][k]; dfc1b[m] = sum_b df1[b][m]
+// Workgroups [ngfc, ...): Af[c][c'*n + i] = S_i[c'][c] ([S_0^T | S_1^T | ...] interleaved, for
+// dx_bn = sum_i S_i^T dT_i).  grid (ngfc + ceil(p*p*n / 256), R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_gfc(StepCtx c, int ngfc) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, K = d.K, M1 = d.M1, B = c.B, p = d.p, n = d.n;
+  float* ws = c.ws + r * c.wss;
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x >= ngfc) {
+    const int e = ((int)blockIdx.x - ngfc) * RC_BLOCK + tid;
+    if (e >= p * p * n) return;
+    const int cc = e / (p * n), rem = e - cc * p * n, cp = rem / n, i = rem - cp * n;
+    ws[c.wo.eAf + e] = ws[c.wo.S + ((int64_t)i * p + cp) * p + cc];
+    return;
+  }
   const int nout = K * M1 + K + M1;
-  for (int e = tid; e < nout; e += RC_BLOCK) {
-    float g = 0.f;
-    if (e < K * M1) {
-      const int k = e / M1, m = e - k * M1;
-      for (int b = 0; b < B; ++b) g += dr[b * K + k] * fmaxf(f1[(int64_t)b * M1 + m], 0.f);
-    } else if (e < K * M1 + K) {
-      const int k = e - K * M1;
-      for (int b = 0; b < B; ++b) g += dr[b * K + k];
-    } else {
-      const int m = e - K * M1 - K;
-      for (int b = 0; b < B; ++b) g += df1[(int64_t)b * M1 + m];
-    }
-    ws[c.wo.gfc + e] = g;
+  const int e = blockIdx.x * 64 + (tid >> 2), g = tid & 3;
+  const float* dr = ws + c.wo.edr;
+  const float* f1 = ws + c.wo.f1;
+  const float* df1 = ws + c.wo.edf1;
+  float t = 0.f;
+  if (e < K * M1) {
+    const int k = e / M1, m = e - k * M1;
+#pragma unroll 8
+    for (int b = g; b < B; b += 4) t += dr[(int64_t)b * K + k] * fmaxf(f1[(int64_t)b * M1 + m], 0.f);
+  } else if (e < K * M1 + K) {
+    const int k = e - K * M1;
+#pragma unroll 8
+    for (int b = g; b < B; b += 4) t += dr[(int64_t)b * K + k];
+  } else if (e < nout) {
+    const int m = e - K * M1 - K;
+#pragma unroll 8
+    for (int b = g; b < B; b += 4) t += df1[(int64_t)b * M1 + m];
   }
+  t += __shfl_xor(t, 1);
+  t += __shfl_xor(t, 2);
+  if (e < nout && g == 0) ws[c.wo.gfc + e] = t;
 }
 
 // BatchNorm affine partials: slot s of c.dgN sums rows (b, c) [s*rows, (s+1)*rows) of
@@ -196,6 +246,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
   }
   float ag = 0.f, ab = 0.f;
   if (sl < nsl)
+#pragma unroll 8
     for (int row = r0 + sl; row < r1; row += nsl) {
       const int b = row / p, cc = row - b * p;
       const float dx = ws[c.wo.edX + (int64_t)row * F + f];
@@ -304,7 +355,7 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
                                     ws + c.wo.f1p, M1, (int64_t)d.Bmax * M1), nsp, s, "emb fc1");
   }
   if (e) return e;
-  hipLaunchKernelGGL(k_lemb_head, dim3((B + 15) / 16, d.R), dim3(RC_BLOCK), 0, s, c, nsp);
+  hipLaunchKernelGGL(k_lemb_head, dim3(B, d.R), dim3(RC_BLOCK), 0, s, c, nsp);
   return rc_check(hipGetLastError(), "k_lemb_head");
 }
 
@@ -312,13 +363,12 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F, pH = (int64_t)p * H;
-  const size_t lds = sizeof(float) * ((size_t)B * d.K + (size_t)d.K * M1);
-  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("GEMM embedder head: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  hipLaunchKernelGGL(k_lemb_dhead, dim3(1, d.R), dim3(RC_BLOCK), lds, s, c);
+  hipLaunchKernelGGL(k_lemb_dhead, dim3((B + lemb_wpw(d) - 1) / lemb_wpw(d), d.R), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_lemb_dhead");
   if (!e) {
-    hipLaunchKernelGGL(k_lemb_afull, dim3(d.R), dim3(RC_BLOCK), 0, s, c);
-    e = rc_check(hipGetLastError(), "k_lemb_afull");
+    const int ngfc = (d.K * M1 + d.K + M1 + 63) / 64, naf = (p * p * n + RC_BLOCK - 1) / RC_BLOCK;
+    hipLaunchKernelGGL(k_lemb_gfc, dim3(ngfc + naf, d.R), dim3(RC_BLOCK), 0, s, c, ngfc);
+    e = rc_check(hipGetLastError(), "k_lemb_gfc");
   }
   const int nds = ds_splits(B), wps = B / nds;
   for (int r = 0; r < d.R && !e; ++r) {

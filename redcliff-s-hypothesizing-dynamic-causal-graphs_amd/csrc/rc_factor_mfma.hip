@@ -194,6 +194,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   float* rB = rA + RC_BLOCK;      // [256]
   float* dwf = rB + RC_BLOCK;     // [Bmax]  forecast part of dL/dw_bk
 
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
   for (int e = tid; e < B * K; e += RC_BLOCK) {
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     const float t = rc_block_sum(fsum, red);
     if (tid == 0) ws[c.wo.lossp + j] = t;
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 17);
   // ---- group norms G[kj][c][t], G0[kj][c] (cmlp.py:147-167) from the forward's squared norms
   for (int e = tid; e < Q; e += RC_BLOCK) {
     const float sq = ws[c.wo.gq + (int64_t)kj * Q + e];
@@ -241,8 +243,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     for (int t = 0; t < L; ++t) sq += sqs[cc * L + t];
     ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 18);
   // ---- adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j] over the
-  // lag slice: pass 1 (thread = window b, half of the (c, lag) entries) gives the value and
+  // lag slice: pass 1 (thread = window b, half of the channels) gives the value and
   // dL/dw_bk; pass 2 (thread = (c, lag) entry, loop over windows) gives dL/dG (-> ws.dgs) and
   // dL/dA[c][j] (-> ws.dAadj) from one sign evaluation
   const bool adj_on = adj_grad || values;
@@ -250,21 +253,23 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     for (int cc = tid; cc < p; cc += RC_BLOCK) Acol[cc] = E[c.eo.A + cc * p + j];
     for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
     __syncthreads();
-    const int nls = p * Ls, hl = (nls + 1) / 2, half = tid & 1;
+    const int half = tid & 1, hp = (p + 1) / 2, c0 = half * hp, c1 = min(p, c0 + hp);
     float vsum = 0.f;
     for (int b0 = 0; b0 < B; b0 += RC_BLOCK / 2) {
       const int b = b0 + (tid >> 1);
       float t = 0.f, v = 0.f;
       if (b < B) {
         const float wb = wk[b];
-        const int e1 = min(nls, (half + 1) * hl);
-        int e = half * hl, cc = e / Ls, i = e - cc * Ls;
-        for (; e < e1; ++e) {
-          const float g = Gs[cc * L + (L - Ls + i)];
-          const float val = wb * g + Acol[cc];
-          t += lwt[i] * rc_sign(val) * g;
-          v += lwt[i] * fabsf(val);
-          if (++i == Ls) { i = 0; ++cc; }
+        for (int cc = c0; cc < c1; ++cc) {  // this lane's half of the channels
+          const float ac = Acol[cc];
+          const float* gr = Gs + cc * L + (L - Ls);
+#pragma unroll 4
+          for (int i = 0; i < Ls; ++i) {
+            const float g = gr[i];
+            const float val = wb * g + ac;
+            t += lwt[i] * rc_sign(val) * g;
+            v += lwt[i] * fabsf(val);
+          }
         }
       }
       // the two halves of window b are adjacent lanes: combined in fixed order (first + second)
@@ -279,12 +284,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
       if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * vs;
     }
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 19);
   if (adj_grad) {
     const bool wg = c.flags & RC_STEP_B, ag = c.flags & RC_STEP_A;
     for (int e = tid; e < p * Ls; e += RC_BLOCK) {
       const int cc = e / Ls, i = e - cc * Ls;
       const float g = Gs[cc * L + (L - Ls + i)], ac = Acol[cc];
       float sw = 0.f, s1 = 0.f;
+#pragma unroll 8
       for (int b = 0; b < B; ++b) {
         const float sg = rc_sign(wk[b] * g + ac);
         sw += sg * wk[b];
@@ -294,12 +301,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
       if (ag) dAp[e] = hy.c_adj * lwt[i] * s1;
     }
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 20);
   if (c.flags & RC_STEP_B) {  // dL/dG is zero outside the lag slice (and everywhere without the adj-L1 term)
     for (int q = tid; q < Q; q += RC_BLOCK) {
       const int cc = q / L, tt = q - cc * L;
       if (!adj_grad || tt < L - Ls) ws[c.wo.dgs + (int64_t)kj * Q + q] = 0.f;
     }
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 21);
   if (adj_grad && (c.flags & RC_STEP_A)) {
     __syncthreads();
     for (int cc = tid; cc < p; cc += RC_BLOCK) {
@@ -310,6 +319,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   }
   if (!(c.flags & RC_STEP_B)) return;
   __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 22);
   // ---- output layer / hidden bias gradients + Adam: 32 units x 8 batch slices per pass
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
   const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
@@ -343,6 +353,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     }
   }
   if (tid == 0) rc_update(c, P, PM, PV, GF, c.fo.b1 + kj, db1, as);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 23);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -411,10 +422,61 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
     }
   };
 
+  // The epilogue's operands (W0, Adam moments, adjacency-L1 terms) are loaded before the
+  // contraction, so their latency overlaps the matrix-core work.
+  const int net = wv & 1, qh = 64 * (wv >> 1), kh = lane >> 5, l31 = lane & 31;
+  const int kj = kj0 + net;
+  const bool kin = kj < KP;
+  const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
+  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
+  const bool adam = !(c.flags & RC_GRAD_ONLY);
+  float* W0 = P + c.fo.W0 + (int64_t)(kin ? kj : 0) * h * Q;
+  float* M0 = PM + c.fo.W0 + (int64_t)(kin ? kj : 0) * h * Q;
+  float* V0 = PV + c.fo.W0 + (int64_t)(kin ? kj : 0) * h * Q;
+  float* G0w = GF + c.fo.W0 + (int64_t)(kin ? kj : 0) * h * Q;
+  // one 32-column half of the lane's outputs at a time: half 0's operands are loaded before
+  // the contraction (their latency overlaps the matrix-core work), half 1's after it
+  float dg, gn, pw[16], pm[16], pv[16];
+  auto epi_load = [&](int half) {
+    const int q = q0 + qh + 32 * half + l31;
+    const bool qin = kin && q < Q;
+    dg = (adj_grad && qin) ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
+    gn = (adj_grad && qin) ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int u = mf_row(reg, lane);
+      const bool in = qin && u < h;
+      const int64_t idx = (int64_t)u * Q + q;
+      pw[reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
+      pm[reg] = (in && adam) ? M0[idx] : 0.f;
+      pv[reg] = (in && adam) ? V0[idx] : 0.f;
+    }
+  };
+  auto epi_store = [&](int half, const f32x16& acc) {
+    const int q = q0 + qh + 32 * half + l31;
+    if (!kin || q >= Q) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int u = mf_row(reg, lane);
+      if (u >= h) continue;
+      const int64_t idx = (int64_t)u * Q + q;
+      float g = acc[reg];
+      if (adj_grad && gn > 0.f) g += dg * (pw[reg] / gn);
+      if (!adam) {
+        G0w[idx] = g;
+      } else {
+        rc_adam(pw[reg], pm[reg], pv[reg], g, as);
+        W0[idx] = pw[reg];
+        M0[idx] = pm[reg];
+        V0[idx] = pv[reg];
+      }
+    }
+  };
+  epi_load(0);
+
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
-  const int net = wv & 1, qh = 64 * (wv >> 1), kh = lane >> 5, l31 = lane & 31;
   load(0);
   for (int bb0 = 0; bb0 < B; bb0 += MB_BC) {
     __syncthreads();
@@ -431,55 +493,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
     }
   }
   // ---- epilogue: + adjacency term through the group norms, then Adam (or store the gradient)
-  const int kj = kj0 + net;
-  if (kj >= KP) return;
-  const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
-  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
-  const bool adam = !(c.flags & RC_GRAD_ONLY);
-  float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
-  float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
-  float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
-  float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
-  // every operand of the 32 updates this lane owns is loaded before the first store (the
-  // stores could alias the loads as far as the compiler knows, which would serialise them)
-  float dg[2], gn[2], pw[2][16], pm[2][16], pv[2][16];
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int q = q0 + qh + 32 * half + l31;
-    const bool qin = q < Q;
-    dg[half] = (adj_grad && qin) ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
-    gn[half] = (adj_grad && qin) ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int u = mf_row(reg, lane);
-      const bool in = qin && u < h;
-      const int64_t idx = (int64_t)u * Q + q;
-      pw[half][reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
-      pm[half][reg] = (in && adam) ? M0[idx] : 0.f;
-      pv[half][reg] = (in && adam) ? V0[idx] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int q = q0 + qh + 32 * half + l31;
-    if (q >= Q) continue;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int u = mf_row(reg, lane);
-      if (u >= h) continue;
-      const int64_t idx = (int64_t)u * Q + q;
-      float g = half == 0 ? acc0[reg] : acc1[reg];
-      if (adj_grad && gn[half] > 0.f) g += dg[half] * (pw[half][reg] / gn[half]);
-      if (!adam) {
-        G0w[idx] = g;
-      } else {
-        rc_adam(pw[half][reg], pm[half][reg], pv[half][reg], g, as);
-        W0[idx] = pw[half][reg];
-        M0[idx] = pm[half][reg];
-        V0[idx] = pv[half][reg];
-      }
-    }
-  }
+  epi_store(0, acc0);
+  epi_load(1);
+  epi_store(1, acc1);
 }
 
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
