@@ -56,7 +56,7 @@ def flops_per_window(c):
     emb_fwd = 2 * ((n - 1) * p * p * F + n * p * F * H + 64 * p * H + 64 * K) + 4 * p * F
     emb_bwd = 2 * emb_fwd
     pen = 6 * K * p * p * min(L, F) + 6 * K * p * p + K * (K - 1) * p * p
-    return dict(fac_fwd=fac_fwd, fac_bwd=fac_bwd + pen, emb_fwd=emb_fwd, emb_bwd=emb_bwd, emb_final=0,
+    return dict(fac_fwd=fac_fwd, fac_bwd=fac_bwd + pen, emb_fwd=emb_fwd, emb_bwd=emb_bwd, emb_final=0, pen=pen,
                 total=fac_fwd + fac_bwd + emb_fwd + emb_bwd + pen)
 
 
@@ -281,17 +281,22 @@ def main():
     fl = flops_per_window(c)
     roof = None
     if ktimes:
-        # timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch);
-        # on the matrix-core path "fac_fwd" = k_xwin + k_fac_fwd_mfma, "fac_bwd" = k_fac_mix + k_fac_bwd_mfma
-        mfma = ktimes.get("fac_fwd", (0, 0))[1] > 0
-        if not mfma:
+        # timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch)
+        # or the GEMM embedder's forward chain; on the matrix-core path "fac_fwd" = k_xwin +
+        # k_fac_fwd_mfma, "fac_mix" = k_fac_mix, "fac_bwd" = k_fac_bwd_mfma.  With two kernel
+        # chains on two streams the slots overlap in time (the step is shorter than their sum).
+        mfma = ktimes.get("fac_mix", (0, 0))[1] > 0
+        if mfma:  # k_fac_mix carries the penalty terms, k_fac_bwd_mfma the dW0 contraction
+            fl["fac_mix"] = fl["pen"]
+            fl["fac_bwd"] -= fl["pen"]
+        elif ktimes.get("fac_fwd", (0, 0))[1] == 0:
             fl["emb_fwd"] += fl["fac_fwd"]
-        dom = max((k for k in ktimes if k != "supports"), key=lambda k: ktimes[k][0])
+        dom = max((k for k in ktimes if k in fl and k != "supports"), key=lambda k: ktimes[k][0])
         avg_ms = ktimes[dom][0]
         flops = fl.get(dom, 0) * B
         achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_mfma", "fac_bwd": "k_fac_bwd_mfma" if mfma else "k_fac_bwd",
-                 "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final"}[dom]
+                 "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final", "fac_mix": "k_fac_mix"}[dom]
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
                 "traffic": pmc_traffic(kname), "avg_launch_us": round(avg_ms * 1e3, 2),

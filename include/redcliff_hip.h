@@ -198,8 +198,12 @@ int redcliff_gemm(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_
 
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()
- * synchronises them and returns per-kernel totals (ids 0..5: supports, emb_fwd, fac_fwd,
- * fac_bwd, emb_bwd, emb_final).  Returns the number of kernel ids. */
+ * synchronises them and returns per-kernel totals (ids 0..6: supports, emb_fwd, fac_fwd,
+ * fac_bwd, emb_bwd, emb_final, fac_mix).  Returns the number of kernel ids.
+ * When the step splits into two kernel chains (GEMM-shaped embedder and / or matrix-core factor
+ * path), the factor chain runs on an internal second stream (one per host thread and device)
+ * forked from and joined back into `stream` with events, so stream ordering for the caller is
+ * unchanged. */
 int redcliff_kernel_timing(int32_t enable);
 int redcliff_kernel_times(double* total_ms, int64_t* counts, int32_t n);
 

@@ -8,7 +8,7 @@
 
 // ---- optional per-kernel HIP-event timing (bench / profiling only) -------------------------
 namespace {
-enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_N };
+enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_FAC_MIX, KT_N };
 struct TimedLaunch {
   int id;
   hipEvent_t a, b;
@@ -28,6 +28,42 @@ int timed(int id, hipStream_t s, F&& launch) {
   const int e2 = rc_check(hipEventRecord(t.b, s), "hipEventRecord");
   g_launches.push_back(t);
   return e ? e : e2;
+}
+}  // namespace
+
+// Second stream for the factor chain when the step splits into two independent kernel chains
+// (GEMM-shaped embedder and / or matrix-core factor path), joined back into the caller's
+// stream with events: per host thread and device, created on first use.
+namespace {
+struct AuxStream {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+thread_local AuxStream g_aux[16];
+
+int aux_stream(AuxStream** out) {
+  int dev = 0;
+  int e = rc_check(hipGetDevice(&dev), "hipGetDevice");
+  if (e) return e;
+  if (dev < 0 || dev >= 16) { rc_set_error("device %d outside the auxiliary-stream table", dev); return REDCLIFF_ELIMIT; }
+  AuxStream& a = g_aux[dev];
+  if (!a.s) {
+    // lowest priority: the embedder chain on the caller's stream is the critical path, the
+    // factor chain's long matrix-core launches fill the CUs it leaves idle
+    int least = 0, greatest = 0;
+    e = rc_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+    if (!e) e = rc_check(hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, least), "hipStreamCreateWithPriority");
+    for (int i = 0; i < 3 && !e; ++i) e = rc_check(hipEventCreateWithFlags(&a.ev[i], hipEventDisableTiming), "hipEventCreate");
+    if (e) return e;
+  }
+  *out = &a;
+  return 0;
+}
+
+// `to` waits for everything enqueued on `from` so far
+int stream_wait(hipStream_t to, hipStream_t from, hipEvent_t ev) {
+  int e = rc_check(hipEventRecord(ev, from), "hipEventRecord");
+  return e ? e : rc_check(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent");
 }
 }  // namespace
 
@@ -198,19 +234,38 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   }
   const bool mfma = fac && rc_fac_use_mfma(c.d);
   const bool egemm = rc_emb_use_gemm(c.d);
-  // forward: embedder + vector-path factor networks share one launch ("fwd" timing slot); the
-  // GEMM-shaped embedder (large p*F) is its own chain, the factor forward then follows it
+  // Two chains when either side is a multi-kernel chain -- stream s: embedder forward, mixing
+  // (needs w and the factor forward), embedder backward and optimizer; stream sf: factor
+  // forward, then (after the mixing) dW0 + Adam, which overlaps the embedder backward; joined
+  // at the end.  Otherwise everything runs on s.
+  const bool fork = fac && (egemm || mfma);
+  AuxStream* aux = nullptr;
+  hipStream_t sf = s;
+  if (fork) {
+    if ((e = aux_stream(&aux))) return e;
+    sf = aux->s;
+    if ((e = stream_wait(sf, s, aux->ev[0]))) return e;
+  }
+  // forward: the fused launch runs the embedder and (vector path, no fork) the factor networks
   if (egemm) {
     if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd_gemm(c, s); }))) return e;
-    if (fac && !mfma && (e = timed(KT_FAC_FWD, s, [&] { return rc_launch_forward(c, s, false, true); }))) return e;
-  } else if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_forward(c, s, true, fac && !mfma); }))) {
+  } else if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_forward(c, s, true, fac && !mfma && !fork); }))) {
     return e;
   }
-  if (mfma) {  // large p*L: grouped GEMMs on the matrix cores
-    if ((e = timed(KT_FAC_FWD, s, [&] { return rc_launch_fac_fwd_mfma(c, s); }))) return e;
-    if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd_mfma(c, s); }))) return e;
+  if (mfma) {
+    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_fac_fwd_mfma(c, sf); }))) return e;
+  } else if (fork) {
+    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_forward(c, sf, false, true); }))) return e;
+  }
+  if (mfma) {
+    if ((e = stream_wait(s, sf, aux->ev[1]))) return e;  // the mixing needs the factor forward
+    if ((e = timed(KT_FAC_MIX, s, [&] { return rc_launch_fac_mix(c, s); }))) return e;
+    if ((e = stream_wait(sf, s, aux->ev[0]))) return e;  // dW0 needs the mixing's dL/dy
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf); }))) return e;
   } else if (fac) {
-    if ((e = timed(KT_FAC_BWD, s, [&] { return rc_launch_fac_bwd(c, s); }))) return e;
+    if (fork && (e = stream_wait(sf, s, aux->ev[1]))) return e;  // the mixing needs the embedder output w
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf); }))) return e;
+    if (fork && (e = stream_wait(s, sf, aux->ev[0]))) return e;
   }
   if (emb_grad && egemm) {
     // GEMM chain, then the fused kernel without node workgroups (head / adjacency-L1 reduce)
@@ -227,6 +282,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   if (emb_grad || c.nbn > 0) {
     if ((e = timed(KT_EMB_FINAL, s, [&] { return rc_launch_emb_final(c, s); }))) return e;
   }
+  if (fork && (e = stream_wait(s, sf, aux->ev[2]))) return e;  // join: the caller's stream sees both chains
   return 0;
 }
 
@@ -250,7 +306,7 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
 // Per-kernel timing: while enabled every launch of redcliff_train_step is bracketed by
 // HIP events on its stream.  redcliff_kernel_times() waits for the recorded events,
 // adds the elapsed milliseconds per kernel (ids: supports, emb_fwd, fac_fwd, fac_bwd,
-// emb_bwd, emb_final) into total_ms[]/counts[] and clears the record.
+// emb_bwd, emb_final, fac_mix) into total_ms[]/counts[] and clears the record.
 int redcliff_kernel_timing(int32_t enable) {
   g_timing = enable != 0;
   return 0;

@@ -322,6 +322,10 @@ __device__ inline void rc_stage_all(S&&... s) {
   }
 }
 
+// Kernels of the embedder chain (the critical path when the factor chain runs concurrently on
+// a second stream) raise their waves' issue priority over the co-resident factor waves.
+__device__ inline void rc_critical_priority() { __builtin_amdgcn_s_setprio(2); }
+
 // fp32 matrix cores: v_mfma_f32_32x32x2f32 accumulator, and the row of accumulator register
 // `reg` of lane `lane` in its 32x32 tile (columns = lane & 31).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -412,7 +416,8 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
 // mixing / penalties / small-parameter updates, GEMM dW0 + Adam.
 bool rc_fac_use_mfma(const RedcliffDims& d);
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s);
-int rc_launch_fac_bwd_mfma(const StepCtx& c, hipStream_t s);
+int rc_launch_fac_mix(const StepCtx& c, hipStream_t s);   // mixing, loss terms, output layer (MFMA path)
+int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);
 void rc_emb_partial_layout(StepCtx& c, bool gemm);

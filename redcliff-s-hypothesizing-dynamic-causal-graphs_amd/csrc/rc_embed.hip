@@ -652,6 +652,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const flo
 // register prefetch; small adjacencies get the short code (one-shot code is fetched cold).
 template <int NR>
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y;
   const int p = d.p, n = d.n, F = d.F, H = d.H, K = d.K, M1 = d.M1;

@@ -29,6 +29,7 @@ __host__ __device__ inline int lemb_wpw(const RedcliffDims& d) { return 64 / d.K
 
 // x_bn[b][c][0][f] = X[row0 + b][Lmax - F + f][c] * alpha_f + beta_f    grid (B, R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y, b = blockIdx.x;
   const int p = d.p, F = d.F, n = d.n;
@@ -76,6 +77,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
 // f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (B, R): one window per
 // workgroup, lanes (m, g): g sums every 4th partial (all loads in flight), fixed-order combine.
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y, b = blockIdx.x;
   const int M1 = d.M1, K = d.K;
@@ -138,6 +140,7 @@ __device__ inline float lemb_draw(const StepCtx& c, int r, int k, float raw, flo
 // g sums every 4th channel partial of the factor-side dL/dw (all loads in flight); then dL/df1
 // of the workgroup's windows.  dr -> ws.edr, df1 -> ws.edf1.
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y;
   const int K = d.K, M1 = d.M1, p = d.p, B = c.B;
@@ -186,6 +189,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
 // Workgroups [ngfc, ...): Af[c][c'*n + i] = S_i[c'][c] ([S_0^T | S_1^T | ...] interleaved, for
 // dx_bn = sum_i S_i^T dT_i).  grid (ngfc + ceil(p*p*n / 256), R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_gfc(StepCtx c, int ngfc) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y, K = d.K, M1 = d.M1, B = c.B, p = d.p, n = d.n;
   float* ws = c.ws + r * c.wss;
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_gfc(StepCtx c, int ngfc) {
 // BatchNorm affine partials: slot s of c.dgN sums rows (b, c) [s*rows, (s+1)*rows) of
 //   dgamma[f] = sum dx_bn[b][c][f] * xhat[b][c][f],  dbeta[f] = sum dx_bn[b][c][f].  grid (dgN, R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y, s = blockIdx.x;
   const int p = d.p, F = d.F;
@@ -271,6 +276,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
 // dS_i slices -> slot 0 (fixed order), so the final kernel's adjacency workgroup reads one record.
 // grid (ceil((n-1) p^2 / 256), R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dsred(StepCtx c, int nds) {
+  rc_critical_priority();
   const RedcliffDims& d = c.d;
   const int r = blockIdx.y, p = d.p, n = d.n;
   const int64_t pp2 = (int64_t)p * p;

@@ -41,6 +41,7 @@ inline RcGemm rc_gemm_args(int ta, int tb, int M, int N, int K, const float* A, 
 }
 
 __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
+  rc_critical_priority();
   const int bz = blockIdx.z;
   const float* A = g.A + bz * g.sA;
   const float* B = g.B + bz * g.sB;
