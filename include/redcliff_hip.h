@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 2
+#define REDCLIFF_ABI_VERSION 3
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -195,6 +195,21 @@ int redcliff_adam_apply(const RedcliffDims* d, float* params, float* exp_avg, fl
 int redcliff_gemm(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_t K, float alpha, const float* A,
                   int64_t lda, int64_t stride_a, const float* B, int64_t ldb, int64_t stride_b, float beta, float* C,
                   int64_t ldc, int64_t stride_c, int32_t batch, void* stream);
+
+/* Per-epoch GC-progress metrics of fit() for S samples x G graphs (replaces the host loops of
+ * general_utils/model_utils.py:18-160 over general_utils/metrics.py:111-252, 396-430 and
+ * sklearn's roc_auc_score).  One workgroup per (sample, graph), 2 <= p <= 64, Lt <= 128:
+ *   est      float32 [S][nE][p][p][Lt]  GC estimates (the first G of each sample are scored)
+ *   truth    float64 [2][G][p][p]       true graphs summed over lags and max-normalised,
+ *                                       [0] as is, [1] with self-connections removed first
+ *   eps_pow  float64 [p]                eps_pow[k] = deltaConEps ** k (host pow)
+ *   out      float64 [S][G][6 + p]      f1, roc_auc, f1 (off-diagonal), roc_auc (off-diagonal),
+ *                                       deltacon0, deltacon0 with directed degrees, deltaffinity,
+ *                                       path-length MSE for k = 1 .. p-1
+ * roc_auc is NaN where sklearn would raise (truth without negatives, NaN scores). */
+int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt, const float* est,
+                         const double* truth, const double* eps_pow, double in_degree_coeff, double out_degree_coeff,
+                         double* out, void* stream);
 
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()

@@ -267,6 +267,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf); }))) return e;
     if (fork && (e = stream_wait(s, sf, aux->ev[0]))) return e;
   }
+  if ((fl & RC_VALUES) && (e = rc_launch_cos_values(c, s))) return e;  // before the head workgroup
   if (emb_grad && egemm) {
     // GEMM chain, then the fused kernel without node workgroups (head / adjacency-L1 reduce)
     if ((e = timed(KT_EMB_BWD, s, [&] {

@@ -52,6 +52,7 @@ struct WsOff {
   int64_t edX;    // [Bmax][p][F]      dL/d x_bn (GEMM embedder)
   int64_t eAf;    // [p][p*n]          [S_0^T | ... | S_{n-1}^T] interleaved (GEMM embedder)
   int64_t edr;    // [Bmax][K]         dL/d(raw embedder output) (GEMM embedder)
+  int64_t cosb;   // [Bmax] doubles    per-window cosine-similarity penalty values
   int64_t total;
 };
 
@@ -165,6 +166,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d) {
   o.edX = x; x = rc_align64(x + B * p * d.F);
   o.eAf = x; x = rc_align64(x + p * p * d.n);
   o.edr = x; x = rc_align64(x + B * K);
+  o.cosb = x; x = rc_align64(x + 2 * B);
 #ifdef RC_TRACE
   x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
 #endif
@@ -416,7 +418,8 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
 // mixing / penalties / small-parameter updates, GEMM dW0 + Adam.
 bool rc_fac_use_mfma(const RedcliffDims& d);
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s);
-int rc_launch_fac_mix(const StepCtx& c, hipStream_t s);   // mixing, loss terms, output layer (MFMA path)
+int rc_launch_fac_mix(const StepCtx& c, hipStream_t s);
+int rc_launch_cos_values(const StepCtx& c, hipStream_t s);  // per-window cos-sim penalty values (rc_embed.hip)   // mixing, loss terms, output layer (MFMA path)
 int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);

@@ -69,6 +69,75 @@ __device__ inline float draw_value(const StepCtx& c, int r, int k, float raw, fl
 }
 
 // ------------------------------------------------------------------------------------------
+// Cosine similarity of the lag-free conditional GC estimates (metrics.py:342-381), a value
+// only (the reference's torch.Tensor(list) drops its gradient):
+//   v_bk[r][c] = w_bk * G0[k][r][c] + A[c][r] - I[r][c],  cosb[b] = sum_{k1<k2} cos(v_bk1, v_bk2)
+// grid (B, R): one window per workgroup; per pair, lanes take strided elements, wave sums go to
+// LDS and one thread per pair combines the four waves in order.
+__global__ __launch_bounds__(RC_BLOCK) void k_cos_values(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = blockIdx.y, b = blockIdx.x, K = d.K, p = d.p, pp2 = p * p;
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const float* G0 = ws + c.wo.G0;
+  const float* A = E + c.eo.A;
+  const bool sig = d.use_sigmoid;
+  const float ecc = d.sigmoid_ecc;
+  const int npair = K * (K - 1) / 2;
+  __shared__ float part[120][4][3];  // K <= 16: at most 120 pairs
+  __shared__ float wk[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < K) {
+    const float raw = ws[c.wo.w + (int64_t)b * K + tid];
+    wk[tid] = sig ? rc_sigmoid(ecc * raw) : raw;
+  }
+  __syncthreads();
+  for (int q = 0; q < npair; ++q) {
+    int k1 = 0, rem = q;
+    while (rem >= K - 1 - k1) { rem -= K - 1 - k1; ++k1; }
+    const int k2 = k1 + 1 + rem;
+    const float w1 = wk[k1], w2 = wk[k2];
+    float dot = 0.f, n1 = 0.f, n2 = 0.f;
+    for (int e = tid; e < pp2; e += RC_BLOCK) {
+      const int rr = e / p, cc = e - rr * p;
+      const float at = A[cc * p + rr];
+      const float eye = (rr == cc ? 1.f : 0.f);
+      const float v1 = (w1 * G0[(int64_t)k1 * pp2 + e] + at) - eye;
+      const float v2 = (w2 * G0[(int64_t)k2 * pp2 + e] + at) - eye;
+      dot += v1 * v2;
+      n1 += v1 * v1;
+      n2 += v2 * v2;
+    }
+    dot = rc_wave_sum(dot);
+    n1 = rc_wave_sum(n1);
+    n2 = rc_wave_sum(n2);
+    if (lane == 0) {
+      part[q][wv][0] = dot;
+      part[q][wv][1] = n1;
+      part[q][wv][2] = n2;
+    }
+  }
+  __syncthreads();
+  __shared__ double cq[120];
+  if (tid < npair) {
+    float dot = 0.f, n1 = 0.f, n2 = 0.f;
+    for (int w = 0; w < RC_BLOCK / 64; ++w) {
+      dot += part[tid][w][0];
+      n1 += part[tid][w][1];
+      n2 += part[tid][w][2];
+    }
+    const float eps2 = 1e-16f;
+    cq[tid] = (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int q = 0; q < npair; ++q) t += cq[q];
+    reinterpret_cast<double*>(ws + c.wo.cosb)[b] = t;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // K3 head workgroup (launched only for loss values / the confusion matrix): the
 // coefficient-normalised loss terms of validate_training and the factor-score confusion.
 __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
@@ -101,32 +170,11 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
     }
     fsum = rc_block_sum_d(fsum, dred);
     l1 = rc_block_sum_d(l1, dred);
-    // cosine similarity of the lag-free conditional GC estimates (metrics.py:342-381):
-    // v_bk[r][c] = w_bk * G0[k][r][c] + A[c][r] - I[r][c]; value only (detached).
+    // cosine-similarity penalty: per-window sums from k_cos_values (ws.cosb), summed here
     double cs = 0.0;
-    const int npair = K * (K - 1) / 2;
-    const float* G0 = ws + c.wo.G0;
-    const float* A = E + c.eo.A;
-    for (int e = tid; e < B * npair; e += RC_BLOCK) {
-      const int b = e / npair;
-      int q = e - b * npair, k1 = 0;
-      while (q >= K - 1 - k1) { q -= K - 1 - k1; ++k1; }
-      const int k2 = k1 + 1 + q;
-      const float r1 = wraw[(int64_t)b * K + k1], r2 = wraw[(int64_t)b * K + k2];
-      const float w1 = sig ? rc_sigmoid(ecc * r1) : r1, w2 = sig ? rc_sigmoid(ecc * r2) : r2;
-      float dot = 0.f, n1 = 0.f, n2 = 0.f;
-      for (int rr = 0; rr < p; ++rr)
-        for (int cc = 0; cc < p; ++cc) {
-          const float at = A[cc * p + rr];
-          const float eye = (rr == cc ? 1.f : 0.f);
-          const float v1 = (w1 * G0[((int64_t)k1 * p + rr) * p + cc] + at) - eye;
-          const float v2 = (w2 * G0[((int64_t)k2 * p + rr) * p + cc] + at) - eye;
-          dot += v1 * v2;
-          n1 += v1 * v1;
-          n2 += v2 * v2;
-        }
-      const float eps2 = 1e-16f;
-      cs += (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
+    if (K > 1) {
+      const double* cb = reinterpret_cast<const double*>(ws + c.wo.cosb);
+      for (int b = tid; b < B; b += RC_BLOCK) cs += cb[b];
     }
     cs = (K > 1) ? rc_block_sum_d(cs, dred) : 0.0;
     if (tid == 0) {
@@ -892,6 +940,12 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
     hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head + nred, d.R), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
   }
   return rc_check(hipGetLastError(), "k_emb_bwd");
+}
+
+int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {
+  if (c.d.K < 2 || !(c.flags & RC_VALUES)) return 0;
+  hipLaunchKernelGGL(k_cos_values, dim3(c.B, c.d.R), dim3(RC_BLOCK), 0, s, c);
+  return rc_check(hipGetLastError(), "k_cos_values");
 }
 
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {

@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
@@ -31,7 +31,8 @@ WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
-            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm")
+            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm",
+            "redcliff_gc_progress")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix")
 
 
@@ -112,6 +113,8 @@ def lib():
     L.redcliff_gemm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                 ctypes.c_float, _vp, _i64, _i64, _vp, _i64, _i64, ctypes.c_float, _vp, _i64, _i64,
                                 ctypes.c_int32, _vp]
+    L.redcliff_gc_progress.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp]
     for name in EXPORTED[2:]:
         if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count"):
             getattr(L, name).restype = ctypes.c_int

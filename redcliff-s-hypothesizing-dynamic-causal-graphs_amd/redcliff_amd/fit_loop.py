@@ -27,8 +27,70 @@ HIST_KEYS = ["avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_pena
              "avg_dagness_node_loss", "avg_combo_loss"]
 
 
+class ParamSnapshot:
+    """``best_model`` of fit() on the fused path: the parameters (and BatchNorm buffers) at the
+    best epoch as copies of the engine's two packed parameter buffers, instead of the reference's
+    ``copy.deepcopy(self)`` every improving epoch (...withStateSmoothing.py:1553-1559), which
+    costs more than the epoch's training steps.  ``materialize()`` builds the module the reference
+    would hold (checkpoints); ``restore_into`` is restore_parameters (parameters only)."""
+
+    def __init__(self, model):
+        eng = model.engine()
+        eng.ensure_bound()
+        self.model = model
+        with torch.no_grad():
+            self.emb = eng.emb.clone()
+            self.fac = eng.fac.clone()
+            bn = eng.dgcnn.BN1
+            self.bn = (bn.running_mean.clone(), bn.running_var.clone(), bn.num_batches_tracked.clone())
+
+    def _slices(self, model):
+        """name -> (flat buffer, offset, numel) of every packed parameter of `model` (the fit's model)."""
+        eng = model.engine()
+        out = {}
+        for name, prm in model.named_parameters():
+            for base, flat in ((eng.emb, self.emb), (eng.fac, self.fac)):
+                off = (prm.data_ptr() - base.data_ptr()) // 4
+                if 0 <= off < base.numel() and prm.device == base.device:
+                    out[name] = (flat, off, prm.numel())
+                    break
+        return out
+
+    def restore_into(self, model):
+        eng = model.engine()
+        eng.ensure_bound()
+        with torch.no_grad():
+            eng.emb.copy_(self.emb)
+            eng.fac.copy_(self.fac)
+        eng.invalidate()  # A changed: the Chebyshev supports are recomputed before the next use
+
+    def materialize(self):
+        m = copy.deepcopy(self.model)
+        sl = self._slices(self.model)
+        with torch.no_grad():
+            for name, prm in m.named_parameters():
+                flat, off, n = sl[name]
+                prm.copy_(flat[off:off + n].view_as(prm))
+            bn = m.factor_score_embedder.dgcnn.dgcnn.BN1
+            bn.running_mean.copy_(self.bn[0])
+            bn.running_var.copy_(self.bn[1])
+            bn.num_batches_tracked.copy_(self.bn[2])
+        return m
+
+
+def _best_model(model, fused):
+    return ParamSnapshot(model) if fused else copy.deepcopy(model)
+
+
+def _as_module(best_model):
+    return best_model.materialize() if isinstance(best_model, ParamSnapshot) else best_model
+
+
 def restore_parameters(model, best_model):
     """general_utils/model_utils.py:309-313: parameters only, not buffers."""
+    if isinstance(best_model, ParamSnapshot):
+        best_model.restore_into(model)
+        return
     for params, best_params in zip(model.parameters(), best_model.parameters()):
         params.data = best_params
 
@@ -68,7 +130,7 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
     best_it, best_loss, best_model, iter_start = None, np.inf, None, 0
 
     if hasattr(model, "chkpt_best_it"):  # resume_training_from_checkpoint was called
-        best_model = copy.deepcopy(model)
+        best_model = _best_model(model, fused)
         iter_start = model.chkpt_best_it + 1
         for k in HIST_KEYS:
             h[k] = list(getattr(model, "chkpt_" + k))[:iter_start]
@@ -120,21 +182,40 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
             Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
         else:
             Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(), torch.float32)
+        # conditional GC modes on the fused path: estimates as stacked device tensors, metrics on
+        # the GPU (rc_metrics.hip); otherwise the host loops of the reference
+        dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
+            "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
         with torch.no_grad():
-            est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
-            est_np = [[g.detach().cpu().numpy() for g in row] for row in est]
-            nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
-                             combine_wavelet_representations=True)
-            nolag_np = [[g.detach().cpu().numpy() for g in row] for row in nolag]
+            if dev_metrics:
+                mode = model.primary_gc_est_mode
+                est_t = model._conditional_gc_stack(mode, Xv[:nsup], False, False, False)
+                nolag_np = model._conditional_gc_stack(mode, Xv, False, True, True).cpu().numpy()
+                est_host = est_t.cpu().numpy()
+                est_np = [[est_host[s, k] for k in range(est_host.shape[1])] for s in range(est_host.shape[0])]
+            else:
+                est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
+                est_np = [[g.detach().cpu().numpy() for g in row] for row in est]
+                nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
+                                 combine_wavelet_representations=True)
+                nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
         if GC is not None and nsup > 0:
-            f1_hist, roc_hist = M.track_roc_stats(GC, est_np, f1_hist, roc_hist, remove_self_connections=False)
-            f1_off, roc_off = M.track_roc_stats(GC, est_np, f1_off, roc_off, remove_self_connections=True)
-            dc_hist, dcdd_hist, daff_hist, plm_hist = M.track_deltacon_stats(
-                GC, est_np, p, dc_hist, dcdd_hist, daff_hist, plm_hist, deltaConEps, in_degree_coeff, out_degree_coeff)
+            if dev_metrics and len(est_np) > 0:
+                vals = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff)
+                f1_hist, roc_hist = M.track_roc_stats_from_values(vals, f1_hist, roc_hist, False)
+                f1_off, roc_off = M.track_roc_stats_from_values(vals, f1_off, roc_off, True)
+                dc_hist, dcdd_hist, daff_hist, plm_hist = M.track_deltacon_stats_from_values(
+                    vals, p, dc_hist, dcdd_hist, daff_hist, plm_hist)
+            else:
+                f1_hist, roc_hist = M.track_roc_stats(GC, est_np, f1_hist, roc_hist, remove_self_connections=False)
+                f1_off, roc_off = M.track_roc_stats(GC, est_np, f1_off, roc_off, remove_self_connections=True)
+                dc_hist, dcdd_hist, daff_hist, plm_hist = M.track_deltacon_stats(
+                    GC, est_np, p, dc_hist, dcdd_hist, daff_hist, plm_hist, deltaConEps, in_degree_coeff,
+                    out_degree_coeff)
         if nsup > 0:
             _, l1_hist = M.track_l1_stats(est_np, l1_hist)
-        cos_hist = M.track_cosine_stats([row[:nsup] for row in nolag_np], cos_hist, label_offset=0)
-        cos_unsup = M.track_cosine_stats([row[nsup:] for row in nolag_np], cos_unsup, label_offset=nsup)
+        cos_hist = M.track_cosine_stats_batched(nolag_np[:, :nsup], cos_hist, label_offset=0)
+        cos_unsup = M.track_cosine_stats_batched(nolag_np[:, nsup:], cos_unsup, label_offset=nsup)
 
         # ---- validation (:1416-1480)
         if nsup > 0:
@@ -160,16 +241,16 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
             else:
                 crit = sc_forecast * v_forecast
             if crit < best_loss:
-                best_loss, best_it, best_model = crit, it, copy.deepcopy(model)
+                best_loss, best_it, best_model = crit, it, _best_model(model, fused)
             elif (it - best_it) == lookback * check_every:
                 if verbose:
                     print("Stopping early")
                 break
         else:
-            best_it, best_model = it, copy.deepcopy(model)
+            best_it, best_model = it, _best_model(model, fused)
 
         if it % check_every == 0 and save_dir is not None:
-            save_checkpoint(model, save_dir, it, best_model, *[h[k] for k in HIST_KEYS], best_loss, best_it, f1_hist,
+            save_checkpoint(model, save_dir, it, _as_module(best_model), *[h[k] for k in HIST_KEYS], best_loss, best_it, f1_hist,
                             f1_off, roc_hist, roc_off, l1_hist, cos_hist, cos_unsup, dc_hist, dcdd_hist, daff_hist,
                             plm_hist, GC, X_val, cm_train=cm_train, cm_val=cm_val, save_plots=save_plots)
 

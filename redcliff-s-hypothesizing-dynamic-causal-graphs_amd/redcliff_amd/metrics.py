@@ -63,12 +63,19 @@ def _path_powers(A, kmax):
     return out
 
 
+def _approx_affinity(A, eps, kmax):
+    """metrics.py:142-160: S = I, then S = S + (1.*(eps**k)) * A^k in order (float64 S, the
+    terms in A's dtype)."""
+    S = np.eye(A.shape[0])
+    for k, Ak in enumerate(_path_powers(A, kmax), start=1):
+        S = S + (1. * (eps ** k) * Ak)
+    return S
+
+
 def deltaffinity(A1, A2, eps, max_path_length=None):
     n = A1.shape[0]
     kmax = n - 1 if max_path_length is None else max_path_length
-    S1 = np.eye(n) + sum((eps ** k) * Ak for k, Ak in enumerate(_path_powers(A1, kmax), start=1))
-    S2 = np.eye(n) + sum((eps ** k) * Ak for k, Ak in enumerate(_path_powers(A2, kmax), start=1))
-    return 1. / (1. + _matsusita(S1, S2))
+    return 1. / (1. + _matsusita(_approx_affinity(A1, eps, kmax), _approx_affinity(A2, eps, kmax)))
 
 
 def path_length_mse(A1, A2, max_path_length=None):
@@ -93,7 +100,7 @@ def track_roc_stats(GC, CURR_GC_EST, f1_hist, roc_hist, remove_self_connections=
         for s, ests in enumerate(CURR_GC_EST):
             for i, est in enumerate(ests[:len(GC)]):
                 true = _prep_true(GC[i], remove_self_connections)
-                e = np.asarray(est, dtype=np.float64)
+                e = np.array(est)  # the estimate's own dtype (float32), as the reference
                 if e.ndim == 3:
                     e = np.sum(e, axis=2)
                 if remove_self_connections:
@@ -132,7 +139,7 @@ def track_deltacon_stats(GC, CURR_GC_EST, num_chans, dc_hist, dcdd_hist, daff_hi
     for s, ests in enumerate(CURR_GC_EST):
         for i, est in enumerate(ests[:len(GC)]):
             true = _prep_true(GC[i], False)
-            e = np.asarray(est, dtype=np.float64)
+            e = np.array(est)
             if e.ndim == 3:
                 e = np.sum(e, axis=2)
             if np.max(np.sum(GC[i], axis=2)) != 0.:
@@ -203,4 +210,124 @@ def track_cosine_stats(CURR_GC_EST, hist, label_offset=0):
         n_samp += 1.
     for key in cur:
         hist[key].append(cur[key] / n_samp)
+    return hist
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU path (rc_metrics.hip, redcliff_gc_progress): the same per-(sample, graph) values computed
+# on the device in one launch, then accumulated over samples on the host exactly as the
+# reference's trackers accumulate them (python-float running sums, division by the sample
+# count, the length-mismatch rules of model_utils.py:63-84 / :136-158).
+
+def _truth_arrays(GC, G):
+    on = np.stack([_prep_true(np.asarray(GC[g], dtype=np.float64), False) for g in range(G)])
+    off = np.stack([_prep_true(np.asarray(GC[g], dtype=np.float64), True) for g in range(G)])
+    return np.ascontiguousarray(np.stack([on, off]), dtype=np.float64)
+
+
+def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.):
+    """est: float32 CUDA tensor (S, nE, p, p, Lt) of GC estimates; GC: true graphs (p, p, lags).
+    Returns float64 (S, G, 6 + p), G = min(nE, len(GC)): f1, roc_auc, f1 / roc_auc without
+    self-connections, deltacon0, deltacon0 with directed degrees, deltaffinity, path-length MSE
+    k = 1..p-1 -- the per-sample values the reference trackers sum."""
+    import ctypes
+    from . import _native as nat
+    S, nE, p, p2, Lt = est.shape
+    assert p == p2
+    G = min(nE, len(GC))
+    dev = est.device
+    est = est.to(torch.float32).contiguous()
+    truth = torch.from_numpy(_truth_arrays(GC, G)).to(dev)
+    eps_pow = torch.tensor([eps ** k for k in range(p)], dtype=torch.float64, device=dev)
+    out = torch.empty(S, G, 6 + p, dtype=torch.float64, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    nat.check(nat.lib().redcliff_gc_progress(S, nE, G, p, Lt, est.data_ptr(), truth.data_ptr(), eps_pow.data_ptr(),
+                                              float(in_degree_coeff), float(out_degree_coeff), out.data_ptr(), stream),
+              "gc_progress")
+    return out.cpu().numpy()
+
+
+def _running(vals):
+    """Per-graph running sums over samples in sample order (python floats), and the count."""
+    run = None
+    for s in range(vals.shape[0]):
+        row = [float(v) for v in vals[s]]
+        run = row if run is None else [a + b for a, b in zip(run, row)]
+    return (run or []), float(vals.shape[0])
+
+
+def track_roc_stats_from_values(vals, f1_hist, roc_hist, remove_self_connections=False):
+    """track_roc_stats with the device values (thresholds other than 0.0 are not on the device path)."""
+    col = 2 if remove_self_connections else 0
+    for thresh in f1_hist.keys():
+        if thresh != 0.0:
+            raise ValueError("device GC-progress metrics cover the fit's threshold 0.0 only")
+        f1_run, n = _running(vals[:, :, col])
+        roc_run, _ = _running(vals[:, :, col + 1])
+        if len(f1_hist[thresh]) != len(f1_run):
+            if len(f1_run) == 1 and len(f1_hist[thresh]) > 1:
+                for i in range(len(f1_hist[thresh])):
+                    f1_hist[thresh][i].append(f1_run[0] / n)
+                    roc_hist[thresh][i].append(roc_run[0] / n)
+                continue
+            assert len(f1_hist[thresh]) < len(f1_run)
+        for i in range(len(f1_hist[thresh])):
+            f1_hist[thresh][i].append(f1_run[i] / n)
+            roc_hist[thresh][i].append(roc_run[i] / n)
+    return f1_hist, roc_hist
+
+
+def track_deltacon_stats_from_values(vals, num_chans, dc_hist, dcdd_hist, daff_hist, plm_hist):
+    """track_deltacon_stats with the device values."""
+    dc, n = _running(vals[:, :, 4])
+    dcdd, _ = _running(vals[:, :, 5])
+    daff, _ = _running(vals[:, :, 6])
+    p = vals.shape[2] - 6
+    plm = {pl: _running(vals[:, :, 6 + pl])[0] for pl in range(1, min(num_chans, p))}
+    if len(dc_hist) != len(dc):
+        if len(dc) == 1 and len(dc_hist) > 1:
+            for i in range(len(dc_hist)):
+                dc_hist[i].append(dc[0] / n)
+                dcdd_hist[i].append(dcdd[0] / n)
+                daff_hist[i].append(daff[0] / n)
+            return dc_hist, dcdd_hist, daff_hist, plm_hist
+        assert len(dc_hist) < len(dc)
+        for i in range(len(dc_hist)):
+            dc_hist[i].append(dc[i] / n)
+            dcdd_hist[i].append(dcdd[i] / n)
+            daff_hist[i].append(daff[i] / n)
+        return dc_hist, dcdd_hist, daff_hist, plm_hist
+    for i in range(len(dc_hist)):
+        dc_hist[i].append(dc[i] / n)
+        dcdd_hist[i].append(dcdd[i] / n)
+        daff_hist[i].append(daff[i] / n)
+        for pl in plm.keys():
+            plm_hist[pl][i].append(plm[pl][i] / n)
+    return dc_hist, dcdd_hist, daff_hist, plm_hist
+
+
+def track_cosine_stats_batched(est, hist, label_offset=0):
+    """track_cosine_stats on a stacked (S, K, ...) array in one vectorised pass (float64, as
+    compute_cosine_similarity above)."""
+    a = np.asarray(est, dtype=np.float64)
+    S, K = a.shape[0], a.shape[1]
+    if K < 2 or S == 0:
+        return hist
+    flat = a.reshape(S, K, -1)
+    flat = flat / flat.max(axis=2, keepdims=True)
+    with np.errstate(invalid="ignore"):
+        nrm = np.linalg.norm(flat, axis=2)
+    nrm = np.where(np.isfinite(nrm), nrm, -1.)
+    nrm = np.maximum(nrm, 1e-8)
+    dots = np.einsum("ski,sli->skl", flat, flat)
+    cur = {}
+    for i1 in range(K):
+        for i2 in range(i1 + 1, K):
+            v = dots[:, i1, i2] / (nrm[:, i1] * nrm[:, i2])
+            tot = 0.
+            for x in v:
+                tot += float(x)
+            cur["%dand%d" % (i1 + label_offset, i2 + label_offset)] = tot
+    for key in cur:
+        hist[key].append(cur[key] / float(S))
     return hist

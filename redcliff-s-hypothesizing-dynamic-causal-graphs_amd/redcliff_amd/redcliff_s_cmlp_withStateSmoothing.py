@@ -248,6 +248,19 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         G = self.factor_score_embedder.GC(threshold=threshold, combine_node_feature_edges=combine)
         return G.view(self.num_series, self.num_series, 1)
 
+    def _conditional_gc_stack(self, gc_est_mode, X, threshold, ignore_lag, comb):
+        """The conditional GC estimates of every window as one (B, K, p, p, L') tensor: the
+        reference's per-(sample, factor) products (:481-498, :565-580) as one broadcast (the
+        same element-wise operations, so the same values)."""
+        ls = min(self.gen_lag, self.embed_lag)
+        w, _ = self.factor_score_embedder(torch.transpose(X[:, -self.embed_lag:, :], 1, 2))
+        fg = torch.stack(self._factor_gcs(threshold, ignore_lag))  # (K, p, p, L')
+        est = w[:, :, None, None, None] * fg[None]
+        if gc_est_mode == "conditional_factor_fixed_embedder":
+            eg = self._embedder_gc(threshold, comb)
+            est = est + eg if ignore_lag else est[..., -ls:] + eg[:, :, -ls:]
+        return est
+
     def GC(self, gc_est_mode, X=None, threshold=True, ignore_lag=True, combine_wavelet_representations=False,
            rank_wavelets=False):
         """The nine GC estimate modes of ...withStateSmoothing.py:415-620 (DGCNN embedder)."""
@@ -275,16 +288,8 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                 return [[g[:, :, -ls:] + eg[:, :, -ls:] for g in fg]]
             return [[g + eg for g in fg]]
         if gc_est_mode in ("conditional_factor_exclusive", "conditional_factor_fixed_embedder"):
-            w, _ = self.factor_score_embedder(torch.transpose(X[:, -self.embed_lag:, :], 1, 2))
-            fg = self._factor_gcs(threshold, ignore_lag)
-            out = [[w[b, k] * fg[k] for k in range(w.size(1))] for b in range(w.size(0))]
-            if gc_est_mode == "conditional_factor_exclusive":
-                return out
-            eg = self._embedder_gc(threshold, comb)
-            for b in range(X.size(0)):
-                for k in range(self.num_factors_nK):
-                    out[b][k] = out[b][k] + eg if ignore_lag else out[b][k][:, :, -ls:] + eg[:, :, -ls:]
-            return out
+            est = self._conditional_gc_stack(gc_est_mode, X, threshold, ignore_lag, comb)
+            return [[est[b, k] for k in range(est.size(1))] for b in range(est.size(0))]
         raise ValueError("GC EST MODE == " + str(gc_est_mode) + " IS NOT SUPPORTED")
 
     # ------------------------------------------------------------------ loss (values)

@@ -1,0 +1,82 @@
+"""Where the wall-clock of a whole REDCLIFF-S fit() goes (fits/hour): training steps vs
+per-epoch GC-progress metrics vs validation vs model snapshots.  Synthetic data of the bench
+configs; prints one JSON line."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "redcliff-s-hypothesizing-dynamic-causal-graphs_amd"))
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="d4ic")
+    ap.add_argument("--epochs", type=int, default=6)
+    ap.add_argument("--train-batches", type=int, default=40)
+    args = ap.parse_args()
+    import redcliff_amd
+    from redcliff_amd import fit_loop
+    c = bench.CONFIGS[args.config]
+    B = c["B"]
+    m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).cuda()
+    oA, oB = bench.adam_pair(m, c)
+    X, Y = bench.synth(c, args.train_batches * B, seed=1)
+    Xv, Yv = bench.synth(c, 8 * B, seed=2)
+    train = [(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)]
+    val = [(Xv[i:i + B], Yv[i:i + B]) for i in range(0, Xv.shape[0], B)]
+    rng = np.random.RandomState(3)
+    true_gc = [(rng.rand(c["p"], c["p"], 2) > 0.7).astype(np.float64) for _ in range(c["K"])]
+
+    times = {}
+
+    def wrap(owner, name, key):
+        f = getattr(owner, name)
+
+        def g(*a, **k):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r = f(*a, **k)
+            torch.cuda.synchronize()
+            times[key] = times.get(key, 0.0) + time.perf_counter() - t
+            return r
+        setattr(owner, name, g)
+        return f
+
+    saved = [(fit_loop.M, n, wrap(fit_loop.M, n, n)) for n in
+             ("track_roc_stats", "track_deltacon_stats", "track_l1_stats", "track_cosine_stats", "track_gc_progress")
+             if hasattr(fit_loop.M, n)]
+    saved.append((fit_loop.copy, "deepcopy", wrap(fit_loop.copy, "deepcopy", "deepcopy")))
+    eng_cls = type(m.engine())
+    saved.append((eng_cls, "run_steps", wrap(eng_cls, "run_steps", "train_steps")))
+    for n in ("run_values", "cache_dataset", "forward_outputs", "gc_norms", "bn_stats"):
+        saved.append((eng_cls, n, wrap(eng_cls, n, "eng." + n)))
+    saved.append((fit_loop, "_best_model", wrap(fit_loop, "_best_model", "best_model_snapshot")))
+    cls = type(m)
+    saved.append((cls, "validate_training", wrap(cls, "validate_training", "validate")))
+    saved.append((cls, "GC", wrap(cls, "GC", "GC")))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.fit(None, train, oA, oB, c["L"], 1, 1, args.epochs, val, lookback=args.epochs, check_every=1, verbose=0,
+          GC=true_gc, stopping_criteria_forecast_coeff=10., stopping_criteria_factor_coeff=100.,
+          stopping_criteria_cosSim_coeff=1.)
+    torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    for owner, name, f in saved:
+        setattr(owner, name, f)
+    out = {"config": args.config, "epochs": args.epochs, "train_batches": args.train_batches, "B": B,
+           "fit_s": round(total, 4), "per_epoch_ms": round(1e3 * total / args.epochs, 2),
+           "breakdown_ms_per_epoch": dict((k, round(1e3 * v / args.epochs, 2)) for k, v in sorted(times.items()))}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -253,6 +253,67 @@ def run_fit():
     print("wrote fit_trace")
 
 
+METRIC_CASES = {
+    # (S samples, K estimates, G true graphs, nsup histories, p, L lags of the estimates, true lags)
+    "a": dict(S=3, K=3, G=3, nsup=3, p=5, L=2, lags=2, seed=31, ties=False, edge=False),
+    "b": dict(S=4, K=4, G=4, nsup=4, p=10, L=4, lags=2, seed=32, ties=True, edge=False),
+    "c": dict(S=2, K=3, G=3, nsup=2, p=12, L=9, lags=3, seed=33, ties=False, edge=False),
+    "d": dict(S=2, K=2, G=2, nsup=2, p=6, L=3, lags=2, seed=34, ties=True, edge=True),
+}
+
+
+def run_metrics():
+    """The reference's per-epoch GC-progress trackers (general_utils/model_utils.py:18-209) on
+    seeded estimates: one tracking call each, histories stored per case."""
+    mu = REF.model_utils
+    out = {}
+    for name, c in METRIC_CASES.items():
+        rng = np.random.RandomState(c["seed"])
+        S, K, G, nsup, p, L = c["S"], c["K"], c["G"], c["nsup"], c["p"], c["L"]
+        est = (rng.rand(S, K, p, p, L) - 0.15).astype(np.float32)
+        if c["ties"]:
+            est = (np.round(est * 4.) / 4.).astype(np.float32)
+        gc = (rng.rand(G, p, p, c["lags"]) > 0.6).astype(np.float64)
+        if c["edge"]:
+            gc[0] = 0.                                  # unknown truth: roc 0.5, no normalisation
+            est[0, 1] = -np.abs(est[0, 1]) - 0.1         # all-negative estimate (max < 0)
+            est[1, 0, :, :, 0] = 0.                      # exact zeros
+        nolag = (rng.rand(S + 3, K, p, p, 1) - 0.2).astype(np.float32)
+        cur = [[torch.from_numpy(est[s, k].copy()) for k in range(K)] for s in range(S)]
+        GC = [gc[g] for g in range(G)]
+        f1, roc = {0.0: [[] for _ in range(nsup)]}, {0.0: [[] for _ in range(nsup)]}
+        f1o, roco = {0.0: [[] for _ in range(nsup)]}, {0.0: [[] for _ in range(nsup)]}
+        mu.track_receiver_operating_characteristic_stats_for_redcliff_models(GC, cur, f1, roc, remove_self_connections=False)
+        mu.track_receiver_operating_characteristic_stats_for_redcliff_models(GC, cur, f1o, roco, remove_self_connections=True)
+        dc, dcdd, daff = [[] for _ in range(nsup)], [[] for _ in range(nsup)], [[] for _ in range(nsup)]
+        plm = {pl: [[] for _ in range(nsup)] for pl in range(1, p)}
+        mu.track_deltacon0_related_stats_for_redcliff_models(GC, cur, p, dc, dcdd, daff, plm, deltaConEps=0.1,
+                                                             in_degree_coeff=1., out_degree_coeff=0.5)
+        l1 = [[] for _ in range(nsup)]
+        mu.track_l1_norm_stats_of_gc_ests_from_redcliff_models([[e.numpy() for e in row] for row in cur], l1)
+        cos = {"%dand%d" % (i, j): [] for i in range(K) for j in range(K) if i < j}
+        mu.track_cosine_similarity_stats_of_gc_ests_from_redcliff_models(
+            [[nolag[s, k] for k in range(K)] for s in range(S + 3)], cos, label_offset=0)
+        pre = "%s/" % name
+        out[pre + "est"] = est
+        out[pre + "gc"] = gc
+        out[pre + "nolag"] = nolag
+        out[pre + "meta"] = np.asarray(json.dumps(c))
+        out[pre + "f1"] = np.asarray([h[0] for h in f1[0.0]], dtype=np.float64)
+        out[pre + "roc"] = np.asarray([h[0] for h in roc[0.0]], dtype=np.float64)
+        out[pre + "f1_off"] = np.asarray([h[0] for h in f1o[0.0]], dtype=np.float64)
+        out[pre + "roc_off"] = np.asarray([h[0] for h in roco[0.0]], dtype=np.float64)
+        out[pre + "dc"] = np.asarray([h[0] for h in dc], dtype=np.float64)
+        out[pre + "dcdd"] = np.asarray([h[0] for h in dcdd], dtype=np.float64)
+        out[pre + "daff"] = np.asarray([h[0] for h in daff], dtype=np.float64)
+        out[pre + "plm"] = np.asarray([[plm[pl][i][0] if plm[pl][i] else np.nan for i in range(nsup)]
+                                       for pl in range(1, p)], dtype=np.float64)
+        out[pre + "l1"] = np.asarray([float(h[0]) for h in l1], dtype=np.float64)
+        out[pre + "cos"] = np.asarray([float(cos[k][0]) for k in sorted(cos)], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "gc_metrics.npz"), **out)
+    print("wrote gc_metrics")
+
+
 BASE = dict(seed=0, emb="DGCNN", p=6, L=3, K=3, nsup=3, h=8, F=5, n=3, H=7, eh=0, S=1, sigmoid=False,
             smoothing_class=True, gc_mode="conditional_factor_fixed_embedder",
             fwd_mode="apply_factor_weights_after_sim_completion",
@@ -293,3 +354,5 @@ if __name__ == "__main__":
         run_prox()
     if not only or "fit_trace" in only:
         run_fit()
+    if not only or "gc_metrics" in only:
+        run_metrics()
