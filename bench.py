@@ -119,6 +119,9 @@ def cpu_baseline(c, seconds):
                       % (n, c["B"], dt, threads)}
 
 
+PMC_CONFIG = "d4ic"  # the configuration scripts/profile_pmc.sh collects the counters on
+
+
 def pmc_traffic(kernel_name, launches_hint=None):
     """HBM bytes per launch of ``kernel_name`` from committed rocprofv3 PMC summaries
     (profiles/*pmc*.csv), FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE."""
@@ -299,7 +302,8 @@ def main():
                  "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final", "fac_mix": "k_fac_mix"}[dom]
         roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
-                "traffic": pmc_traffic(kname), "avg_launch_us": round(avg_ms * 1e3, 2),
+                "traffic": pmc_traffic(kname) if args.config == PMC_CONFIG else None,
+                "avg_launch_us": round(avg_ms * 1e3, 2),
                 "algorithmic_flops_per_launch": flops,
                 "kernel_avg_us": dict((k, round(v[0] * 1e3, 2)) for k, v in ktimes.items())}
     cpu = None
