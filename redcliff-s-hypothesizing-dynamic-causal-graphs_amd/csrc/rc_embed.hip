@@ -321,15 +321,28 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
     auto sW = rc_seg<1>(nbc * K, [&](int e) { return wraw[(int64_t)bw0 * K + e]; }, [&](int e, float v) { wrl[e] = v; });
     auto sL = rc_seg<1>(nbc * K, [&](int e) { return lab_on ? c.lab[r * c.labr + (c.row0 + bw0) * K + e] : 0.f; },
                         [&](int e, float v) { labl[e] = v; });
-    auto sD = rc_seg<1>(nbc * K, [&](int e) {
-      const int s = dK.div(e), k = e - s * K;
-      float g = 0.f;
-      if (fac_grad) {
-#pragma unroll 4
-        for (int j = 0; j < p; ++j) g += dwp[((int64_t)j * d.Bmax + bw0 + s) * K + k];
+    // factor-side dL/dw of the sub-block's windows (sum of the p channel partials): four lanes
+    // per (window, factor) item over every 4th channel; the first 64 items' loads are issued
+    // here and summed after the staging pass, so the two latencies overlap
+    const int ditem = tid >> 2, dg = tid & 3, nitem = nbc * K;
+    float dv[16];
+    auto dw_load = [&](int i0) {
+      const int it2 = i0 + ditem, sw = dK.div(it2), kk = it2 - sw * K;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {  // p <= 64
+        const int j = dg + 4 * u;
+        dv[u] = (fac_grad && it2 < nitem && j < p) ? dwp[((int64_t)j * d.Bmax + bw0 + sw) * K + kk] : 0.f;
       }
-      return g;
-    }, [&](int e, float v) { dwl[e] = v; });
+    };
+    auto dw_store = [&](int i0) {
+      float t = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t += dv[u];
+      t += __shfl_xor(t, 1);
+      t += __shfl_xor(t, 2);
+      if (dg == 0 && i0 + ditem < nitem) dwl[i0 + ditem] = t;
+    };
+    dw_load(0);
     __syncthreads();  // the previous sub-block is done with the LDS tiles
     if (it == 0) {
       rc_stage_all(
@@ -346,7 +359,12 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
             const int i = dp.div(e), cc = e - i * p;
             return S[((int64_t)i * p + node) * p + cc];
           }, [&](int e, float v) { Srow[e] = v; }),
-          sR, sT, sX, sF1, sW, sL, sD);
+          sR, sT, sX, sF1, sW, sL);
+      dw_store(0);
+      for (int i0 = RC_BLOCK / 4; i0 < nitem; i0 += RC_BLOCK / 4) {
+        dw_load(i0);
+        dw_store(i0);
+      }
       __syncthreads();
       if (tid < n) {
         float t = 0.f;
@@ -354,7 +372,12 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
         rs[tid] = t;
       }
     } else {
-      rc_stage_all(sR, sT, sX, sF1, sW, sL, sD);
+      rc_stage_all(sR, sT, sX, sF1, sW, sL);
+      dw_store(0);
+      for (int i0 = RC_BLOCK / 4; i0 < nitem; i0 += RC_BLOCK / 4) {
+        dw_load(i0);
+        dw_store(i0);
+      }
       __syncthreads();
     }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 34);
@@ -541,7 +564,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
   float* dWi = ws + c.wo.dWi + (int64_t)node * n * F * H;
   float* gfc1 = ws + c.wo.gfc1;
   const int64_t pout = (int64_t)node * nch + ch;
-  rc_stage<4>(head_grads ? pst : ofs_h, [&](int e) {
+  rc_stage<8>(head_grads ? pst : ofs_h, [&](int e) {
     float t = 0.f;
     for (int w0 = 0; w0 < nbw; w0 += 8) {
       float v[8];

@@ -25,7 +25,6 @@ namespace {
 
 #define MF_BT 64   // windows per forward tile (2 row blocks of 32)
 #define MF_QC 32   // contraction chunk per staging step (16 MFMA k-steps)
-#define MB_QT 128  // dW0 columns per backward tile
 #define MB_BC 32   // windows per backward staging step
 
 __device__ inline float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -51,16 +50,21 @@ __global__ __launch_bounds__(RC_BLOCK) void k_xwin(StepCtx c) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Forward GEMM.  grid (ceil(K*p/2), ceil(B/64), R); 4 waves: wave w owns rows 32*(w&1) of the
-// 64-row tile and network kj0 + (w>>1), one 32x32 accumulator.  The next chunk's operands are
-// loaded into registers while the current chunk's 16 MFMA k-steps run from LDS.
-// Epilogue: a = relu(z + b0) -> ws.a (backward), y = sum_u W1[u] a[u] + b1 -> ws.y chunk 0,
-// squared group norms gq[kj][q] = sum_u W0[u][q]^2 (first row block), W1 snapshot.
+// Forward GEMM.  Column blocks cb = (network kj, 32-unit hidden block ub), nUB = ceil(h/32) per
+// network; grid (ceil(K*p*nUB/2), ceil(B/64), R); 4 waves: wave w owns rows 32*(w&1) of the
+// 64-row tile and column block 2*blockIdx.x + (w>>1), one 32x32 accumulator.  The next chunk's
+// operands are loaded into registers while the current chunk's 16 MFMA k-steps run from LDS.
+// Epilogue: a = relu(z + b0) -> ws.a (backward), partial y_ub = sum_{u in ub} W1[u] a[u]
+// (+ b1 in block 0) -> ws.y slot ub, squared group norms gq[ub][kj][q] = sum_{u in ub} W0[u][q]^2
+// (first row block), W1 snapshot.
+__device__ inline int mf_nub(const RedcliffDims& d) { return (d.h + 31) / 32; }
+
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
   const RedcliffDims& d = c.d;
   const int r = blockIdx.z;
-  const int kj0 = blockIdx.x * 2, b0 = blockIdx.y * MF_BT;
-  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p;
+  const int cb0 = blockIdx.x * 2, b0 = blockIdx.y * MF_BT;
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p, nUB = mf_nub(d);
+  const int NB = KP * nUB;
   const float* P = c.fac + r * c.fs;
   float* ws = c.ws + r * c.wss;
   const float* Xw = ws + c.wo.xw;
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
   const int nb = min(MF_BT, c.B - b0);
 
   __shared__ float Xs[MF_BT][MF_QC + 1];
-  __shared__ float Ws[64][MF_QC + 1];  // [net*32 + u][q]
+  __shared__ float Ws[64][MF_QC + 1];  // [blk*32 + u][q]
 
   // staging maps: X 64x32 = 512 float4 (2 per thread); W 64x32 = 2048 floats (8 per thread)
   float4 xr[2];
@@ -82,8 +86,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int e = tid + i * RC_BLOCK, uu = e >> 5, qq = e & 31;
-      const int kj = kj0 + (uu >> 5), u = uu & 31, q = q0 + qq;
-      wr[i] = (kj < KP && u < h && q < Q) ? P[c.fo.W0 + ((int64_t)kj * h + u) * Q + q] : 0.f;
+      const int cb = cb0 + (uu >> 5), kj = cb / nUB, u = (cb - kj * nUB) * 32 + (uu & 31), q = q0 + qq;
+      wr[i] = (cb < NB && u < h && q < Q) ? P[c.fo.W0 + ((int64_t)kj * h + u) * Q + q] : 0.f;
     }
   };
   auto store = [&]() {
@@ -112,15 +116,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
     store();
     __syncthreads();
     if (q0 + MF_QC < Qp) load(q0 + MF_QC);
-    if (blockIdx.y == 0 && tid < 64) {  // GC group norms of this chunk (pre-update weights)
-      const int kj = kj0 + (tid >> 5), q = q0 + (tid & 31);
-      if (kj < KP && q < Q) {
+    if (blockIdx.y == 0 && tid < 64) {  // GC group norms of this chunk (pre-update weights), per block
+      const int cb = cb0 + (tid >> 5), q = q0 + (tid & 31);
+      if (cb < NB && q < Q) {
+        const int kj = cb / nUB, ub = cb - kj * nUB;
         float sq = 0.f;
         for (int u = 0; u < 32; ++u) {
           const float w = Ws[(tid >> 5) * 32 + u][tid & 31];
           sq += w * w;
         }
-        ws[c.wo.gq + (int64_t)kj * Q + q] = sq;
+        ws[c.wo.gq + ((int64_t)ub * KP + kj) * Q + q] = sq;
       }
     }
 #pragma unroll
@@ -131,13 +136,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
     }
   }
   // ---- epilogue
-  const int kj = kj0 + (wv >> 1), u = lane & 31;
-  if (kj >= KP) return;
+  const int cb = cb0 + (wv >> 1);
+  if (cb >= NB) return;
+  const int kj = cb / nUB, ub = cb - kj * nUB, u = ub * 32 + (lane & 31);
   const int k = kj / p, j = kj - k * p;
   const bool uv = u < h;
   const float bu = uv ? P[c.fo.b0 + (int64_t)kj * h + u] : 0.f;
   const float w1 = uv ? P[c.fo.W1 + (int64_t)kj * h + u] : 0.f;
-  const float b1 = P[c.fo.b1 + kj];
+  const float b1 = ub == 0 ? P[c.fo.b1 + kj] : 0.f;
   if (blockIdx.y == 0 && (wv & 1) == 0 && lane < 32 && uv) ws[c.wo.w1 + (int64_t)kj * h + u] = w1;
   const int nU = rc_nuchunk(d);
 #pragma unroll
@@ -148,8 +154,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
     float ys = w1 * a;
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);  // within the 32-lane half
-    if ((lane & 31) < nU && b < c.B)  // chunk 0 holds the sum, the other hidden-chunk slots 0
-      ws[c.wo.y + (((int64_t)(lane & 31) * d.Bmax + b) * K + k) * p + j] = (lane & 31) == 0 ? ys + b1 : 0.f;
+    if (b < c.B) {
+      const int l = lane & 31;
+      // slot ub holds this block's partial; block 0 also clears the slots past nUB
+      if (l == 0) ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = ys + b1;
+      else if (ub == 0 && l >= nUB && l < nU) ws[c.wo.y + (((int64_t)l * d.Bmax + b) * K + k) * p + j] = 0.f;
+    }
   }
 }
 
@@ -197,9 +207,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
+  const int nUB = mf_nub(d);
   for (int e = tid; e < B * K; e += RC_BLOCK) {
     const int b = e / K, kk = e - b * K;
-    ybuf[e] = ws[c.wo.y + ((int64_t)b * K + kk) * p + j];
+    float yv = ws[c.wo.y + ((int64_t)b * K + kk) * p + j];
+    for (int ub = 1; ub < nUB; ++ub) yv += ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + kk) * p + j];
+    ybuf[e] = yv;
   }
   __syncthreads();
   float fsum = 0.f;
@@ -232,7 +245,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 17);
   // ---- group norms G[kj][c][t], G0[kj][c] (cmlp.py:147-167) from the forward's squared norms
   for (int e = tid; e < Q; e += RC_BLOCK) {
-    const float sq = ws[c.wo.gq + (int64_t)kj * Q + e];
+    float sq = ws[c.wo.gq + (int64_t)kj * Q + e];
+    for (int ub = 1; ub < nUB; ++ub) sq += ws[c.wo.gq + ((int64_t)ub * K * p + kj) * Q + e];
     sqs[e] = sq;
     Gs[e] = sqrtf(sq);
     ws[c.wo.G + (int64_t)kj * Q + e] = Gs[e];
@@ -357,15 +371,21 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
 }
 
 // ------------------------------------------------------------------------------------------
-// dW0 GEMM + adjacency-L1 term + Adam.  grid (ceil(K*p/2), ceil(Q/128), R); wave w owns
-// network kj0 + (w&1) and dW0 columns [q0 + 64*(w>>1), +64) as two 32x32 accumulators
-// (rows = hidden units).  The batch is the contraction: chunks of 32 windows, dZ built on
-// the fly from the forward's activations, dL/dy and the W1 snapshot.
+// dW0 GEMM + adjacency-L1 term + Adam.  NBW column blocks (network kj, 32-unit block ub) per
+// workgroup and QT = 256 / NBW dW0 columns: grid (ceil(K*p*nUB/NBW), ceil(Q/QT), R).
+// NBW = 2 (long contractions, QT = 128): wave w owns block 2*bx + (w&1) and columns
+// [q0 + 64*(w>>1), +64); NBW = 4 (p*L <= 64, QT = 64): wave w owns block 4*bx + w and all 64
+// columns -- two 32x32 accumulators either way (rows = the block's hidden units).  The batch is
+// the contraction: chunks of 32 windows, dZ built on the fly from the forward's activations,
+// dL/dy and the W1 snapshot.
+template <int NBW>
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
+  constexpr int QT = 256 / NBW, Q4 = QT / 4;
   const RedcliffDims& d = c.d;
   const int r = blockIdx.z;
-  const int kj0 = blockIdx.x * 2, q0 = blockIdx.y * MB_QT;
-  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p, B = c.B;
+  const int cb0 = blockIdx.x * NBW, q0 = blockIdx.y * QT;
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p, B = c.B, nUB = mf_nub(d);
+  const int NB = KP * nUB;
   float* P = c.fac + r * c.fs;
   float* PM = c.facM + r * c.fs;
   float* PV = c.facV + r * c.fs;
@@ -375,24 +395,24 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 
-  __shared__ float Zs[2][MB_BC][33];      // dZ[net][b][u]
-  __shared__ float Xs[MB_BC][MB_QT + 4];  // Xw[b][q0 + .]
-  __shared__ float w1s[64];
+  __shared__ float Zs[NBW][MB_BC][33];  // dZ[blk][b][u]
+  __shared__ float Xs[MB_BC][QT + 4];    // Xw[b][q0 + .]
+  __shared__ float w1s[NBW * 32];
 
-  if (tid < 64) {
-    const int kj = kj0 + (tid >> 5), u = tid & 31;
-    w1s[tid] = (kj < KP && u < h) ? ws[c.wo.w1 + (int64_t)kj * h + u] : 0.f;
+  if (tid < NBW * 32) {
+    const int cb = cb0 + (tid >> 5), kj = cb / nUB, u = (cb - kj * nUB) * 32 + (tid & 31);
+    w1s[tid] = (cb < NB && u < h) ? ws[c.wo.w1 + (int64_t)kj * h + u] : 0.f;
   }
-  // staging maps: dZ 2x32x32 = 2048 (8 per thread: net, b, u); X 32x128 = 1024 float4 (4 per thread)
-  float zr[8];
-  float4 xr[4];
+  // staging maps: dZ NBW x 32 x 32 (4 NBW per thread: blk, b, u); X 32 x QT (QT / 32 float4 per thread)
+  float zr[4 * NBW];
+  float4 xr[QT / 32];
   auto load = [&](int bb0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31, u = e & 31;
-      const int kj = kj0 + net, b = bb0 + bb;
+    for (int i = 0; i < 4 * NBW; ++i) {
+      const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31;
+      const int cb = cb0 + net, kj = cb / nUB, u = (cb - kj * nUB) * 32 + (e & 31), b = bb0 + bb;
       float v = 0.f;
-      if (kj < KP && u < h && b < B) {
+      if (cb < NB && u < h && b < B) {
         const float av = ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u];
         const float dy = ws[c.wo.dyl + (int64_t)kj * d.Bmax + b];
         v = av > 0.f ? dy : 0.f;
@@ -400,21 +420,21 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
       zr[i] = v;  // times w1[u] at store time
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * RC_BLOCK, bb = e >> 5, c4 = (e & 31) * 4;
+    for (int i = 0; i < QT / 32; ++i) {
+      const int e = tid + i * RC_BLOCK, bb = e / Q4, c4 = (e % Q4) * 4;
       const int b = bb0 + bb, q = q0 + c4;
       xr[i] = (b < B && q < Qp) ? ld4(Xw + (int64_t)b * Qp + q) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 4 * NBW; ++i) {
       const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31, u = e & 31;
       Zs[net][bb][u] = zr[i] * w1s[net * 32 + u];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * RC_BLOCK, bb = e >> 5, c4 = (e & 31) * 4;
+    for (int i = 0; i < QT / 32; ++i) {
+      const int e = tid + i * RC_BLOCK, bb = e / Q4, c4 = (e % Q4) * 4;
       Xs[bb][c4] = xr[i].x;
       Xs[bb][c4 + 1] = xr[i].y;
       Xs[bb][c4 + 2] = xr[i].z;
@@ -424,9 +444,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
 
   // The epilogue's operands (W0, Adam moments, adjacency-L1 terms) are loaded before the
   // contraction, so their latency overlaps the matrix-core work.
-  const int net = wv & 1, qh = 64 * (wv >> 1), kh = lane >> 5, l31 = lane & 31;
-  const int kj = kj0 + net;
-  const bool kin = kj < KP;
+  const int net = NBW == 2 ? (wv & 1) : wv, qh = NBW == 2 ? 64 * (wv >> 1) : 0, kh = lane >> 5, l31 = lane & 31;
+  const int cbw = cb0 + net, kin = cbw < NB;
+  const int kj = kin ? cbw / nUB : 0, ub0 = kin ? (cbw - kj * nUB) * 32 : 0;
   const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
   const bool adam = !(c.flags & RC_GRAD_ONLY);
@@ -444,7 +464,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
     gn = (adj_grad && qin) ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int u = mf_row(reg, lane);
+      const int u = ub0 + mf_row(reg, lane);
       const bool in = qin && u < h;
       const int64_t idx = (int64_t)u * Q + q;
       pw[reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
@@ -457,7 +477,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
     if (!kin || q >= Q) return;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int u = mf_row(reg, lane);
+      const int u = ub0 + mf_row(reg, lane);
       if (u >= h) continue;
       const int64_t idx = (int64_t)u * Q + q;
       float g = acc[reg];
@@ -472,14 +492,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
       }
     }
   };
-#ifndef RC_EXP_NOEPI
   epi_load(0);
-#endif
 
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
-#ifndef RC_EXP_NOMFMA
   load(0);
   for (int bb0 = 0; bb0 < B; bb0 += MB_BC) {
     __syncthreads();
@@ -495,15 +512,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
       acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, x1, acc1, 0, 0, 0);
     }
   }
-#endif
   // ---- epilogue: + adjacency term through the group norms, then Adam (or store the gradient)
-#ifdef RC_EXP_NOEPI
-  if (kin && acc0[0] == 12345.f && acc1[0] == 12345.f) W0[0] = 0.f;  // keep the contraction live
-#else
   epi_store(0, acc0);
   epi_load(1);
   epi_store(1, acc1);
-#endif
 }
 
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
@@ -513,15 +525,18 @@ size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
 
 }  // namespace
 
-// Path choice: the matrix-core path needs one 32-column block per network (h <= 32) and pays
-// off once the contraction is long; REDCLIFF_FAC_PATH=mfma|vector overrides (tests, tuning).
+// Path choice: the matrix-core path (32-unit hidden blocks, h <= 128) pays off once the
+// contraction is long (the stress config) or many replicas share the launch (packed grid
+// search: D4IC R = 32 runs 4.2 M -> 5.5 M windows/s, while a single D4IC fit is faster on the
+// latency-shaped vector kernels, 1.31 M vs 0.92 M).  REDCLIFF_FAC_PATH=mfma|vector overrides
+// (tests, tuning).
 bool rc_fac_use_mfma(const RedcliffDims& d) {
   const char* v = getenv("REDCLIFF_FAC_PATH");  // read per call: tests switch paths in-process
   const int env = !v ? 0 : (!strcmp(v, "mfma") ? 1 : (!strcmp(v, "vector") ? 2 : 0));
-  if (d.h > 32) return false;
+  if (d.h > 128) return false;
   if (env == 1) return true;
   if (env == 2) return false;
-  return d.p * d.L >= 256;
+  return (d.p * d.L >= 256 && d.h <= 32) || d.R >= 8;
 }
 
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
@@ -530,7 +545,8 @@ int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
   hipLaunchKernelGGL(k_xwin, dim3(c.B, d.R), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_xwin");
   if (e) return e;
-  hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((KP + 1) / 2, (c.B + MF_BT - 1) / MF_BT, d.R), dim3(RC_BLOCK), 0, s, c);
+  const int NB = KP * ((d.h + 31) / 32);
+  hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, d.R), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_fwd_mfma");
 }
 
@@ -546,7 +562,10 @@ int rc_launch_fac_mix(const StepCtx& c, hipStream_t s) {
 int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (!(c.flags & RC_STEP_B)) return 0;
-  const int KP = d.K * d.p, Q = d.p * d.L;
-  hipLaunchKernelGGL(k_fac_bwd_mfma, dim3((KP + 1) / 2, (Q + MB_QT - 1) / MB_QT, d.R), dim3(RC_BLOCK), 0, s, c);
+  const int NB = d.K * d.p * ((d.h + 31) / 32), Q = d.p * d.L;
+  if (Q <= 64)  // short contraction rows: four column blocks share one 64-column X tile
+    hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, d.R), dim3(RC_BLOCK), 0, s, c);
+  else
+    hipLaunchKernelGGL(k_fac_bwd_mfma<2>, dim3((NB + 1) / 2, (Q + 127) / 128, d.R), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_bwd_mfma");
 }

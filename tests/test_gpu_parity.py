@@ -187,10 +187,11 @@ def synth(cfg, N, seed):
 
 
 @pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1K4", "mfma"), ("C4", "mfma"),
-                                                                        ("C1K4", "embgemm"), ("C2", "embgemm")])
+                                                                        ("C2", "mfma"), ("C1K4", "embgemm"),
+                                                                        ("C2", "embgemm")])
 def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
     """path "mfma" forces the matrix-core factor kernels (rc_factor_mfma.hip, normally chosen
-    for p*L >= 256), "embgemm" the GEMM-shaped embedder (rc_embed_gemm.hip, normally chosen for
+    for p*L >= 256; C2's h=100 runs as four 32-unit hidden blocks per network), "embgemm" the GEMM-shaped embedder (rc_embed_gemm.hip, normally chosen for
     p >= 32) onto the published shapes."""
     if path == "mfma":
         monkeypatch.setenv("REDCLIFF_FAC_PATH", path)

@@ -1,7 +1,7 @@
 """Grid-search replicas packed into one launch (redcliff_amd.ReplicaPack)
 must reproduce R independent fits exactly: same kernels, the replica only moves to
 blockIdx.y, so parameters, BatchNorm buffers, Adam state and validation losses are
-compared bit for bit against the same models stepped one at a time."""
+compared bit for bit against the same models stepped one at a time on the same factor path."""
 import numpy as np
 import pytest
 import torch
@@ -48,7 +48,11 @@ def data(N, seed):
     return [(X[i:i + 64], Y[i:i + 64]) for i in range(0, N, 64)]
 
 
-def test_packed_replicas_match_independent_fits():
+@pytest.mark.parametrize("path", ["vector", "mfma"])
+def test_packed_replicas_match_independent_fits(path, monkeypatch):
+    """Both factor paths (the default picks the matrix cores for packs of >= 8 replicas, so the
+    path is pinned here to compare like with like)."""
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     from redcliff_amd import ReplicaPack
     train = data(64 * 2 + 24, seed=3)  # two full batches + a ragged one
     val = data(80, seed=4)
