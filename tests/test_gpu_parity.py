@@ -318,3 +318,45 @@ def test_fit_trace_matches_reference():
     f1 = np.asarray([[get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), true_gc[k].sum(axis=2))
                       for k, g in enumerate(row)] for row in arr])
     np.testing.assert_array_equal(f1, d["f1"])
+
+
+@pytest.mark.parametrize("name", ["dgcnn_d4ic", "dgcnn_c1"])
+def test_eval_pipeline_f1_identical_to_oracle(name):
+    """SURVEY 8(f) row 3 on the GPU model: eval_utils.get_model_gc_estimates (primary GC mode,
+    one sample, lagged, unthresholded) from the HIP model vs the oracle, then the
+    system-level statistics and the optimal-F1 thresholded graphs -- F1 and graphs must be
+    IDENTICAL (north_star), the continuous statistics within 1e-4 relative."""
+    from oracle.redcliff_oracle import OracleREDCLIFF
+    from redcliff_amd import evaluation as E
+    d, meta = load(name)
+    m = build(meta)
+    m.eval()
+    args, kw = ctor_args(meta)
+    torch.manual_seed(meta["seed"])
+    oracle = OracleREDCLIFF(*args, with_smoothing=meta["smoothing_class"], **kw)
+    oracle.eval()
+    Xb, _ = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    K, p = meta["K"], meta["p"]
+    got = E.get_model_gc_estimates(m, "REDCLIFF_S_CMLP", K, X=Xb[:1, :Lm, :].cuda())
+    with torch.no_grad():
+        want = E.get_model_gc_estimates(oracle, "REDCLIFF_S_CMLP", K, X=Xb[:1, :Lm, :])
+    assert len(got) == len(want) == K
+    for k in range(K):
+        assert_close("gc%d" % k, got[k], want[k], RTOL, 1e-5)
+    rng = np.random.RandomState(3)
+    trus = []
+    for _ in range(K):
+        t = np.zeros((p, p, 2))
+        t[..., 0] = rng.rand(p, p) < 0.3
+        t[0, 1, 0], t[1, 0, 0] = 1.0, 0.0
+        trus.append(t)
+    with np.errstate(all="ignore"):
+        sg = E.system_level_factor_stats(got, trus, sort_unsupervised_ests=True)
+        sw = E.system_level_factor_stats(want, trus, sort_unsupervised_ests=True)
+    for key in ("cos_sim", "mse", "roc_auc", "T_cos_sim", "dir_deltacon0", "deltaffinity"):
+        assert_close(key, sg[key], sw[key], 1e-4, 1e-6)
+    rg = E.batched_graph_f1(np.stack(got), np.stack(trus))
+    rw = E.batched_graph_f1(np.stack(want), np.stack(trus))
+    assert np.array_equal(rg["f1"], rw["f1"]), (rg["f1"], rw["f1"])
+    assert np.array_equal(rg["graphs"], rw["graphs"])
