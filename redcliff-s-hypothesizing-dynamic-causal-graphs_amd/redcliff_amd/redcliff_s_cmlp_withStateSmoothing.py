@@ -271,6 +271,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             return self._generic().GC(gc_est_mode, Xd, threshold, ignore_lag, combine_wavelet_representations)
         if self.factor_score_embedder_type != "DGCNN":
             raise NotImplementedError("GC on the fused path is implemented for the DGCNN embedder")
+        self.engine()  # binds the embedder to this model's kernels (a fresh / loaded model may call GC first)
         ls = min(self.gen_lag, self.embed_lag)
         comb = combine_wavelet_representations
         if gc_est_mode == "fixed_factor_exclusive":
