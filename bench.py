@@ -60,6 +60,34 @@ def flops_per_window(c):
                 total=fac_fwd + fac_bwd + emb_fwd + emb_bwd + pen)
 
 
+
+def roofline_of(ktimes, fl, windows_per_launch, with_traffic):
+    """Roofline object of the dominant kernel: algorithmic FLOPs per launch (SURVEY 8(d)
+    per-window counts x the windows one launch processes) / its average HIP-event duration.
+    Timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch)
+    or the GEMM embedder's forward chain; on the matrix-core path "fac_fwd" = k_xwin +
+    k_fac_fwd_mfma, "fac_mix" = k_fac_mix, "fac_bwd" = k_fac_bwd_mfma.  With two kernel chains
+    on two streams the slots overlap in time (the step is shorter than their sum)."""
+    fl = dict(fl)
+    mfma = ktimes.get("fac_mix", (0, 0))[1] > 0
+    if mfma:  # k_fac_mix carries the penalty terms, k_fac_bwd_mfma the dW0 contraction
+        fl["fac_mix"] = fl["pen"]
+        fl["fac_bwd"] -= fl["pen"]
+    elif ktimes.get("fac_fwd", (0, 0))[1] == 0:
+        fl["emb_fwd"] += fl["fac_fwd"]
+    dom = max((k for k in ktimes if k in fl and k != "supports"), key=lambda k: ktimes[k][0])
+    avg_ms = ktimes[dom][0]
+    flops = fl.get(dom, 0) * windows_per_launch
+    achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_mfma", "fac_bwd": "k_fac_bwd_mfma" if mfma else "k_fac_bwd",
+             "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final", "fac_mix": "k_fac_mix"}[dom]
+    return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
+            "traffic": pmc_traffic(kname) if with_traffic else None,
+            "avg_launch_us": round(avg_ms * 1e3, 2),
+            "algorithmic_flops_per_launch": flops,
+            "kernel_avg_us": dict((k, round(v[0] * 1e3, 2)) for k, v in ktimes.items())}
+
 def synth(c, N, seed):
     rng = np.random.RandomState(seed)
     X = rng.randn(N, c["T"], c["p"]).astype(np.float32)
@@ -184,7 +212,7 @@ def run_grid(c, args, dev, rank, dist):
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    return el, R
+    return el, R, steps
 
 
 def main():
@@ -257,7 +285,7 @@ def main():
     # with different seeds / coefficients / learning rates, stepped together on this GPU
     grid = None
     if args.replicas > 1:
-        grid_elapsed, R = run_grid(c, args, dev, rank, dist)
+        grid_elapsed, R, grid_steps_fn = run_grid(c, args, dev, rank, dist)
         gsteps = args.grid_steps
         grid = {"replicas_per_gpu": R, "steps": gsteps,
                 "windows_per_s": round(world * R * gsteps * B / grid_elapsed, 1),
@@ -282,30 +310,16 @@ def main():
             dist.destroy_process_group()
         return
     fl = flops_per_window(c)
-    roof = None
-    if ktimes:
-        # timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch)
-        # or the GEMM embedder's forward chain; on the matrix-core path "fac_fwd" = k_xwin +
-        # k_fac_fwd_mfma, "fac_mix" = k_fac_mix, "fac_bwd" = k_fac_bwd_mfma.  With two kernel
-        # chains on two streams the slots overlap in time (the step is shorter than their sum).
-        mfma = ktimes.get("fac_mix", (0, 0))[1] > 0
-        if mfma:  # k_fac_mix carries the penalty terms, k_fac_bwd_mfma the dW0 contraction
-            fl["fac_mix"] = fl["pen"]
-            fl["fac_bwd"] -= fl["pen"]
-        elif ktimes.get("fac_fwd", (0, 0))[1] == 0:
-            fl["emb_fwd"] += fl["fac_fwd"]
-        dom = max((k for k in ktimes if k in fl and k != "supports"), key=lambda k: ktimes[k][0])
-        avg_ms = ktimes[dom][0]
-        flops = fl.get(dom, 0) * B
-        achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-        kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_mfma", "fac_bwd": "k_fac_bwd_mfma" if mfma else "k_fac_bwd",
-                 "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final", "fac_mix": "k_fac_mix"}[dom]
-        roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
-                "traffic": pmc_traffic(kname) if args.config == PMC_CONFIG else None,
-                "avg_launch_us": round(avg_ms * 1e3, 2),
-                "algorithmic_flops_per_launch": flops,
-                "kernel_avg_us": dict((k, round(v[0] * 1e3, 2)) for k, v in ktimes.items())}
+    roof = roofline_of(ktimes, fl, B, args.config == PMC_CONFIG) if ktimes else None
+    if grid is not None and not args.no_kernel_times:
+        # the same kernel-level roofline for the packed launch: one launch carries R * B windows
+        nat.kernel_timing(True)
+        grid_steps_fn(min(args.grid_steps, 20), 3)
+        torch.cuda.synchronize()
+        gkt = nat.kernel_times()
+        nat.kernel_timing(False)
+        gkt = dict((k, (ms / n if n else 0.0, n)) for k, (ms, n) in gkt.items())
+        grid["roofline"] = roofline_of(gkt, flops_per_window(c), grid["replicas_per_gpu"] * B, False)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(c, args.cpu_seconds)
