@@ -225,7 +225,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--replicas", type=int, default=32, help="grid-search replicas packed per GPU (1: skip)")
-    ap.add_argument("--grid-steps", type=int, default=50)
+    ap.add_argument("--grid-steps", type=int, default=100)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -1,6 +1,7 @@
 // rc_capi.hip -- extern "C" entry points of libredcliff_hip.so (see include/redcliff_hip.h).
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -52,7 +53,9 @@ int aux_stream(AuxStream** out) {
     // factor chain's long matrix-core launches fill the CUs it leaves idle
     int least = 0, greatest = 0;
     e = rc_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-    if (!e) e = rc_check(hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, least), "hipStreamCreateWithPriority");
+    const char* pv = getenv("REDCLIFF_AUX_PRIO");  // tuning knob: low (default) | normal | high
+    const int prio = !pv ? least : (!strcmp(pv, "high") ? greatest : (!strcmp(pv, "normal") ? (least + greatest) / 2 : least));
+    if (!e) e = rc_check(hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, prio), "hipStreamCreateWithPriority");
     for (int i = 0; i < 3 && !e; ++i) e = rc_check(hipEventCreateWithFlags(&a.ev[i], hipEventDisableTiming), "hipEventCreate");
     if (e) return e;
   }
@@ -62,6 +65,7 @@ int aux_stream(AuxStream** out) {
 
 // `to` waits for everything enqueued on `from` so far
 int stream_wait(hipStream_t to, hipStream_t from, hipEvent_t ev) {
+  if (to == from) return 0;  // single-stream step (REDCLIFF_FORK=0)
   int e = rc_check(hipEventRecord(ev, from), "hipEventRecord");
   return e ? e : rc_check(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent");
 }
@@ -239,9 +243,16 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   // forward, then (after the mixing) dW0 + Adam, which overlaps the embedder backward; joined
   // at the end.  Otherwise everything runs on s.
   const bool fork = fac && (egemm || mfma);
-  AuxStream* aux = nullptr;
+  static AuxStream none;  // single-stream step: null events, stream_wait(s, s) is a no-op
+  AuxStream* aux = &none;
   hipStream_t sf = s;
-  if (fork) {
+  // A single fit is latency-bound: the factor chain on a second stream fills idle CUs (C5 201K ->
+  // 233K windows/s).  Packed replicas (R >= 8) already fill the chip and the two chains only
+  // compete for it: one stream is faster there (D4IC R=32 grid 6.61M -> 6.78M windows/s).
+  // REDCLIFF_FORK=0 / 1 overrides (tuning).
+  const char* fv = getenv("REDCLIFF_FORK");
+  const bool two = fv ? strcmp(fv, "0") != 0 : c.d.R < 8;
+  if (fork && two) {
     if ((e = aux_stream(&aux))) return e;
     sf = aux->s;
     if ((e = stream_wait(sf, s, aux->ev[0]))) return e;
