@@ -9,6 +9,8 @@
 // 64x64 output tile per 256-thread workgroup, 4x4 outputs per thread, K staged through LDS in
 // steps of 16; each output is an in-order fmaf chain over k (deterministic).
 #pragma once
+#include <cstdlib>
+
 #include "rc_common.h"
 
 #define RC_GEMM_T 64
@@ -40,30 +42,36 @@ inline RcGemm rc_gemm_args(int ta, int tb, int M, int N, int K, const float* A, 
   return g;
 }
 
+// TT x TT output tile per 256-thread workgroup (TT = 64: 4x4 outputs per thread; TT = 32:
+// 2x2, four times the workgroups for short / skinny products).  Each output is the same
+// in-order fmaf chain over k whatever the tile, so both variants give identical bits.
+template <int TT>
 __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
+  constexpr int TP = TT / 16;           // outputs per thread along each tile dimension
+  constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
   rc_critical_priority();
   const int bz = blockIdx.z;
   const float* A = g.A + bz * g.sA;
   const float* B = g.B + bz * g.sB;
   float* C = g.C + bz * g.sC;
-  const int n0 = blockIdx.x * RC_GEMM_T, m0 = blockIdx.y * RC_GEMM_T;
+  const int n0 = blockIdx.x * TT, m0 = blockIdx.y * TT;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const RcDiv dkb(g.Kblk);
-  __shared__ float As[RC_GEMM_K][RC_GEMM_T + 4];  // As[k][m]
-  __shared__ float Bs[RC_GEMM_K][RC_GEMM_T + 4];  // Bs[k][n]
-  float acc[4][4];
+  __shared__ float As[RC_GEMM_K][TT + 4];  // As[k][m]
+  __shared__ float Bs[RC_GEMM_K][TT + 4];  // Bs[k][n]
+  float acc[TP][TP];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TP; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    for (int j = 0; j < TP; ++j) acc[i][j] = 0.f;
   // the next K step's operands are loaded into registers while the current step multiplies
-  float av[4], bv[4];
+  float av[NL], bv[NL];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = tid + r * RC_BLOCK;  // 1024 elements of each 16x64 tile
+    for (int r = 0; r < NL; ++r) {
+      const int e = tid + r * RC_BLOCK;  // 16 x TT elements of each tile
       int kk, mm;
-      if (g.ta) { kk = e >> 6; mm = e & 63; } else { mm = e >> 4; kk = e & 15; }
+      if (g.ta) { kk = e / TT; mm = e % TT; } else { mm = e >> 4; kk = e & 15; }
       const int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
       if (gm < g.M && gk < g.K) {
@@ -73,7 +81,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
       }
       av[r] = v;
       int kb2, nb;
-      if (g.tb) { nb = e >> 4; kb2 = e & 15; } else { kb2 = e >> 6; nb = e & 63; }
+      if (g.tb) { nb = e >> 4; kb2 = e & 15; } else { kb2 = e / TT; nb = e % TT; }
       const int gn = n0 + nb, gk2 = k0 + kb2;
       float w = 0.f;
       if (gn < g.N && gk2 < g.K) {
@@ -87,34 +95,34 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   if (g.K > 0) load(0);
   for (int k0 = 0; k0 < g.K; k0 += RC_GEMM_K) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < NL; ++r) {
       const int e = tid + r * RC_BLOCK;
-      if (g.ta) As[e >> 6][e & 63] = av[r]; else As[e & 15][e >> 4] = av[r];
-      if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e >> 6][e & 63] = bv[r];
+      if (g.ta) As[e / TT][e % TT] = av[r]; else As[e & 15][e >> 4] = av[r];
+      if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e / TT][e % TT] = bv[r];
     }
     __syncthreads();
     if (k0 + RC_GEMM_K < g.K) load(k0 + RC_GEMM_K);
 #pragma unroll
     for (int kk = 0; kk < RC_GEMM_K; ++kk) {
-      float a[4], b[4];
+      float a[TP], b[TP];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+      for (int i = 0; i < TP; ++i) a[i] = As[kk][ty * TP + i];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+      for (int j = 0; j < TP; ++j) b[j] = Bs[kk][tx * TP + j];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TP; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+        for (int j = 0; j < TP; ++j) acc[i][j] += a[i] * b[j];
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int gm = m0 + ty * 4 + i;
+  for (int i = 0; i < TP; ++i) {
+    const int gm = m0 + ty * TP + i;
     if (gm >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gn = n0 + tx * 4 + j;
+    for (int j = 0; j < TP; ++j) {
+      const int gn = n0 + tx * TP + j;
       if (gn >= g.N) continue;
       float* cp = C + (int64_t)gm * g.ldc + gn;
       float v = g.beta == 0.f ? g.alpha * acc[i][j] : g.alpha * acc[i][j] + g.beta * *cp;
@@ -128,7 +136,20 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
 inline int rc_gemm_launch(const RcGemm& g, int batch, hipStream_t s, const char* what) {
   if (g.M <= 0 || g.N <= 0 || batch <= 0) return 0;
   if (batch > 65535) { rc_set_error("%s: batch %d > 65535", what, batch); return REDCLIFF_ELIMIT; }
-  dim3 grid((g.N + RC_GEMM_T - 1) / RC_GEMM_T, (g.M + RC_GEMM_T - 1) / RC_GEMM_T, batch);
-  hipLaunchKernelGGL(k_rc_gemm, grid, dim3(RC_BLOCK), 0, s, g);
+  // fewer than two 64x64 tiles per CU: 32x32 tiles (more workgroups in flight to hide the
+  // operand latency of these short products).  REDCLIFF_GEMM_TILE=64|32 overrides (tuning).
+  static const int tile_env = [] {
+    const char* v = getenv("REDCLIFF_GEMM_TILE");
+    return v ? atoi(v) : 0;
+  }();
+  const int64_t t64 = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * batch;
+  const bool small = tile_env == 32 || (tile_env != 64 && t64 < 512);
+  if (small) {
+    dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, batch);
+    hipLaunchKernelGGL(k_rc_gemm<32>, grid, dim3(RC_BLOCK), 0, s, g);
+  } else {
+    dim3 grid((g.N + RC_GEMM_T - 1) / RC_GEMM_T, (g.M + RC_GEMM_T - 1) / RC_GEMM_T, batch);
+    hipLaunchKernelGGL(k_rc_gemm<RC_GEMM_T>, grid, dim3(RC_BLOCK), 0, s, g);
+  }
   return rc_check(hipGetLastError(), what);
 }
