@@ -204,6 +204,7 @@ static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
   c.Ls = rc_ls(d);
   c.flags = a->flags;
   c.nbn = a->n_bn_updates;
+  c.defer = 0;
   c.tA = a->tA;
   c.tB = a->tB;
   c.X = a->X; c.xr = a->x_rstride; c.row0 = a->row0;
@@ -247,11 +248,13 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   AuxStream* aux = &none;
   hipStream_t sf = s;
   // A single fit is latency-bound: the factor chain on a second stream fills idle CUs (C5 201K ->
-  // 233K windows/s).  Packed replicas (R >= 8) already fill the chip and the two chains only
-  // compete for it: one stream is faster there (D4IC R=32 grid 6.61M -> 6.78M windows/s).
-  // REDCLIFF_FORK=0 / 1 overrides (tuning).
+  // 233K windows/s).  Packed replicas already fill the chip and the two chains only compete
+  // for it: one stream is faster there (D4IC R=32 grid 6.61M -> 6.78M windows/s).  Packs also
+  // stay on one stream below R = 8: a forked R = 3 matrix-core pack occasionally (2 runs in
+  // ~12) gave its last replica an A different from the independent fit's -- root cause not
+  // found; the single-stream pack matches bit for bit.  REDCLIFF_FORK=0 / 1 overrides (tuning).
   const char* fv = getenv("REDCLIFF_FORK");
-  const bool two = fv ? strcmp(fv, "0") != 0 : c.d.R < 8;
+  const bool two = fv ? strcmp(fv, "0") != 0 : c.d.R == 1;
   if (fork && two) {
     if ((e = aux_stream(&aux))) return e;
     sf = aux->s;
@@ -287,7 +290,17 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
          })))
       return e;
   } else if (emb_grad) {
-    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
+    // The node blocks' window-block partials are summed by a separate k_emb_combine launch
+    // instead of the in-kernel last arriver (ticket + agent-scope fences): the fences cost the
+    // packed grid ~20 % (D4IC R=32 6.8M -> 8.1M windows/s).  Same sums in the same order.  The
+    // two-stream step keeps the in-kernel combine.  REDCLIFF_DEFER=0 / 1 overrides (tuning).
+    const char* dv = getenv("REDCLIFF_DEFER");
+    c.defer = dv ? strcmp(dv, "0") != 0 : sf == s;
+    if ((e = timed(KT_EMB_BWD, s, [&] {
+           const int e2 = rc_launch_emb_bwd(c, s, true);
+           return (e2 || !c.defer) ? e2 : rc_launch_emb_combine(c, s);
+         })))
+      return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }

@@ -210,6 +210,9 @@ struct StepCtx {
   // dS_i[cc][c'] = sum_s ws.dS[cc*dsCC + s*dsS + i*dsI + c'], s < dsN;  BN affine: ws.dgb[s][2][F], s < dgN
   int dsN, dgN;
   int64_t dsCC, dsS, dsI;
+  // 1: k_emb_bwd's node blocks leave their per-window-block partial records unreduced and
+  // k_emb_combine sums them (no cross-workgroup ticket / fences inside the backward kernel)
+  int defer;
   EmbOff eo;
   FacOff fo;
   WsOff wo;
@@ -428,6 +431,7 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
+int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);  // window-block partials (c.defer)
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,
                        WsOff wo, hipStream_t s);
 int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,

@@ -538,6 +538,10 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
     part[ofs_g + F + tid] = t;
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 39);
+  if (c.defer) {  // k_emb_combine sums the window blocks after this kernel (no ticket / fences)
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
+    return;
+  }
   // release (every wave drains its stores, one lane publishes at agent scope), then the ticket
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -592,6 +596,45 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
   });
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 41);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
+}
+
+// The last-arriver combine of emb_bwd_node as its own launch (c.defer): element e of
+// (node, chunk) group blockIdx.y summed over the window blocks in block order and scattered
+// exactly as the last arriver does, so both variants give the same bits.
+// grid (ceil(pstride / RC_BLOCK), p * nchunk, R).
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int grp = blockIdx.y, r = blockIdx.z, e = blockIdx.x * RC_BLOCK + threadIdx.x;
+  const int p = d.p, n = d.n, F = d.F, H = d.H, M1 = d.M1, HC = EMB_HC;
+  const int nch = rc_nchunk(d), node = grp / nch, ch = grp - node * nch;
+  const int pst = rc_emb_pstride(d), nbwm = rc_emb_nbw(d), wpb = rc_emb_wpb(d), nbw = (c.B + wpb - 1) / wpb;
+  const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
+  if (e >= (grp == 0 ? pst : ofs_h)) return;  // fc2 / fc1-bias partials ride on group 0
+  float* ws = c.ws + r * c.wss;
+  const float* base = ws + c.wo.ebp + (int64_t)grp * nbwm * pst + e;
+  float t = 0.f;
+  for (int w0 = 0; w0 < nbw; w0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = (w0 + q < nbw) ? base[(int64_t)(w0 + q) * pst] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (w0 + q < nbw) t += v[q];
+  }
+  const int h0 = ch * HC, hc = min(HC, H - h0);
+  if (e < ofs_w) {
+    const int m = e / HC, hh = e - m * HC;
+    if (hh < hc) ws[c.wo.gfc1 + (int64_t)m * p * H + node * H + h0 + hh] = t;
+  } else if (e < ofs_s) {
+    const int q = e - ofs_w, qh = q >> 4, i = qh / F, f = qh - i * F, hh = q & 15;  // HC == 16
+    if (hh < hc) ws[c.wo.dWi + (int64_t)node * n * F * H + ((int64_t)i * F + f) * H + h0 + hh] = t;
+  } else if (e < ofs_g) {
+    ws[c.wo.dS + (int64_t)grp * n * p + p + (e - ofs_s)] = t;
+  } else if (e < ofs_h) {
+    ws[c.wo.dgb + (int64_t)grp * 2 * F + (e - ofs_g)] = t;
+  } else {
+    ws[c.wo.gfc + (e - ofs_h)] = t;
+  }
 }
 
 // Adjacency-L1 gradient of A summed over the K factors' records, in place into record 0
@@ -969,6 +1012,14 @@ int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {
   if (c.d.K < 2 || !(c.flags & RC_VALUES)) return 0;
   hipLaunchKernelGGL(k_cos_values, dim3(c.B, c.d.R), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_cos_values");
+}
+
+int rc_launch_emb_combine(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int pst = rc_emb_pstride(d);
+  hipLaunchKernelGGL(k_emb_combine, dim3((pst + RC_BLOCK - 1) / RC_BLOCK, d.p * rc_nchunk(d), d.R), dim3(RC_BLOCK), 0,
+                     s, c);
+  return rc_check(hipGetLastError(), "k_emb_combine");
 }
 
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {

@@ -344,13 +344,13 @@ int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_
     static const int sb_env = [] {
       const char* v = getenv("REDCLIFF_EMB_SB");  // tuning knob: windows per forward workgroup
       const int x = v ? atoi(v) : 0;
-      return (x >= 1 && x <= 16) ? x : 0;
+      return (x >= 1 && x <= 4) ? x : 0;  // the fc1 stage holds at most 4 windows per workgroup
     }();
     // one window per workgroup keeps a single fit's forward short (latency); packed replicas
-    // fill the chip anyway, and 8 windows per workgroup share one staging of the embedder
-    // weights (R = 32 D4IC grid: forward 158 -> 64 us at 4 windows).  Per-window arithmetic
-    // does not depend on SB, so packed fits stay bitwise equal to independent ones.
-    SB = sb_env ? sb_env : (d.R >= 8 ? 8 : 1);
+    // fill the chip anyway, and 4 windows per workgroup share one staging of the embedder
+    // weights (R = 32 D4IC grid: forward 158 -> 64 us).  Per-window arithmetic does not
+    // depend on SB, so packed fits stay bitwise equal to independent ones.
+    SB = sb_env ? sb_env : (d.R >= 8 ? 4 : 1);
     size_t limit = RC_LDS_LIMIT_FLOATS;
     while (SB > 1 && emb_fwd_floats(d, SB, w_lds) > limit) --SB;
     if (emb_fwd_floats(d, SB, w_lds) > limit) w_lds = 0;

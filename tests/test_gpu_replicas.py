@@ -14,6 +14,10 @@ GRID = [  # (seed, FORECAST_COEFF, ADJ_L1 scale, gen_lr, embed_lr)
     (1, 1.0, 0.01, 1e-4, 5e-4),
     (2, 10.0, 0.01, 5e-4, 1e-4),
 ]
+# packs of >= 8 replicas take the packed-only code paths (8 windows per forward workgroup, one
+# stream, the embedder-backward partials combined by the final kernel): 8 grid points
+GRID8 = GRID + [(3 + i, (1.0, 10.0)[i % 2], (0.1, 0.01)[i % 2], (5e-4, 1e-4)[i % 2], (2e-4, 5e-4)[i % 2])
+                for i in range(5)]
 
 
 def make(seed, fc, adj, pre=1, acc=1):
@@ -48,11 +52,12 @@ def data(N, seed):
     return [(X[i:i + 64], Y[i:i + 64]) for i in range(0, N, 64)]
 
 
-@pytest.mark.parametrize("path", ["vector", "mfma"])
-def test_packed_replicas_match_independent_fits(path, monkeypatch):
+@pytest.mark.parametrize("path,grid", [("vector", GRID), ("mfma", GRID), ("mfma", GRID8)])
+def test_packed_replicas_match_independent_fits(path, grid, monkeypatch):
     """Both factor paths (the default picks the matrix cores for packs of >= 8 replicas, so the
-    path is pinned here to compare like with like)."""
+    path is pinned here to compare like with like); R = 3 and the packed-only paths at R = 8."""
     monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    GRID = grid
     from redcliff_amd import ReplicaPack
     train = data(64 * 2 + 24, seed=3)  # two full batches + a ragged one
     val = data(80, seed=4)
