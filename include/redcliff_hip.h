@@ -213,12 +213,12 @@ int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt
 
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()
- * synchronises them and returns per-kernel totals (ids 0..6: supports, emb_fwd, fac_fwd,
- * fac_bwd, emb_bwd, emb_final, fac_mix).  Returns the number of kernel ids.
- * When the step splits into two kernel chains (GEMM-shaped embedder and / or matrix-core factor
- * path), the factor chain runs on an internal second stream (one per host thread and device)
- * forked from and joined back into `stream` with events, so stream ordering for the caller is
- * unchanged. */
+ * synchronises them and returns per-kernel totals (ids 0..7: supports, emb_fwd, fac_fwd,
+ * fac_bwd, emb_bwd, emb_final, fac_mix, emb_combine).  Returns the number of kernel ids.
+ * When a single fit (R == 1) splits into two kernel chains (GEMM-shaped embedder and / or
+ * matrix-core factor path), the factor chain runs on an internal second stream (one per host
+ * thread and device) forked from and joined back into `stream` with events, so stream
+ * ordering for the caller is unchanged.  Packed replicas run on `stream` only. */
 int redcliff_kernel_timing(int32_t enable);
 int redcliff_kernel_times(double* total_ms, int64_t* counts, int32_t n);
 

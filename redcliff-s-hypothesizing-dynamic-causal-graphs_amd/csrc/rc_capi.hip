@@ -9,7 +9,7 @@
 
 // ---- optional per-kernel HIP-event timing (bench / profiling only) -------------------------
 namespace {
-enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_FAC_MIX, KT_N };
+enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_FAC_MIX, KT_EMB_COMB, KT_N };
 struct TimedLaunch {
   int id;
   hipEvent_t a, b;
@@ -296,11 +296,8 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     // two-stream step keeps the in-kernel combine.  REDCLIFF_DEFER=0 / 1 overrides (tuning).
     const char* dv = getenv("REDCLIFF_DEFER");
     c.defer = dv ? strcmp(dv, "0") != 0 : sf == s;
-    if ((e = timed(KT_EMB_BWD, s, [&] {
-           const int e2 = rc_launch_emb_bwd(c, s, true);
-           return (e2 || !c.defer) ? e2 : rc_launch_emb_combine(c, s);
-         })))
-      return e;
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
+    if (c.defer && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }
@@ -331,7 +328,7 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
 // Per-kernel timing: while enabled every launch of redcliff_train_step is bracketed by
 // HIP events on its stream.  redcliff_kernel_times() waits for the recorded events,
 // adds the elapsed milliseconds per kernel (ids: supports, emb_fwd, fac_fwd, fac_bwd,
-// emb_bwd, emb_final, fac_mix) into total_ms[]/counts[] and clears the record.
+// emb_bwd, emb_final, fac_mix, emb_combine) into total_ms[]/counts[] and clears the record.
 int redcliff_kernel_timing(int32_t enable) {
   g_timing = enable != 0;
   return 0;

@@ -33,7 +33,7 @@ EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_b
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
             "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm",
             "redcliff_gc_progress")
-KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix")
+KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine")
 
 
 class Dims(ctypes.Structure):
