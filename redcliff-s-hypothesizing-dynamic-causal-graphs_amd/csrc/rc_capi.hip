@@ -293,11 +293,18 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     // The node blocks' window-block partials are summed by a separate k_emb_combine launch
     // instead of the in-kernel last arriver (ticket + agent-scope fences): the fences cost the
     // packed grid ~20 % (D4IC R=32 6.8M -> 8.1M windows/s).  Same sums in the same order.  The
-    // two-stream step keeps the in-kernel combine.  REDCLIFF_DEFER=0 / 1 overrides (tuning).
+    // two-stream step uses it too: a matrix-core pack of 8 once gave one replica an A different
+    // from its forked independent fit, whose in-kernel ticket combine is the only cross-workgroup
+    // handshake on that path (root cause not isolated); the launch costs ~5 us there.
+    // defer 2: k_emb_final reads the partials in place (same order, no combine launch) --
+    // measured slower for the single fit (k_emb_final 10 -> 20.5 us: p * nbw dependent loads
+    // per element on its critical path), +1 % on the R = 32 grid, so not the default.
+    // REDCLIFF_DEFER=0 / 1 / 2 overrides (tuning).
     const char* dv = getenv("REDCLIFF_DEFER");
-    c.defer = dv ? strcmp(dv, "0") != 0 : sf == s;
+    c.defer = dv ? atoi(dv) : 1;
+    if (c.defer < 0 || c.defer > 2) c.defer = 1;
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
-    if (c.defer && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
+    if (c.defer == 1 && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }

@@ -757,6 +757,32 @@ __global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const flo
   supports_lds(sm, sm + p * P, ws + r * wss + wo.S, sm + (d.n + 1) * p * P, p, d.n);
 }
 
+// Window-block partials of k_emb_bwd read in place by k_emb_final (c.defer == 2): element
+// off of (node, chunk) group grp summed over the window blocks in block order -- the sum
+// k_emb_combine forms, so the fused read and the separate launch give the same bits.
+struct EmbWbSum {
+  const float* base;
+  int pst, nbw, nbwm;
+  __device__ EmbWbSum(const StepCtx& c, const float* ws)
+      : base(ws + c.wo.ebp), pst(rc_emb_pstride(c.d)), nbwm(rc_emb_nbw(c.d)) {
+    const int wpb = rc_emb_wpb(c.d);
+    nbw = (c.B + wpb - 1) / wpb;
+  }
+  __device__ float operator()(int grp, int off) const {
+    const float* b = base + (int64_t)grp * nbwm * pst + off;
+    float t = 0.f;
+    for (int w0 = 0; w0 < nbw; w0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = (w0 + q < nbw) ? b[(int64_t)(w0 + q) * pst] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (w0 + q < nbw) t += v[q];
+    }
+    return t;
+  }
+};
+
 // ------------------------------------------------------------------------------------------
 // K4: embedder optimizer finalisation.  Workgroups [1, nw] apply Adam to W_i, fc2, fc1 bias,
 // BN affine (reducing per-node partials in fixed order); workgroup 0 handles the
@@ -778,6 +804,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   const RcAdamScalars as = rc_adam_scalars(c.hyp[r].A, c.tA);
   const int nFH = n * F * H, nfc = K * M1 + K + M1, nf1 = M1 * p * H;
   const int total = nFH + nfc + 2 * F + nf1;
+  // c.defer == 2: the node blocks' window-block partials are summed here (no combine launch);
+  // record layout of emb_bwd_node: fc1 chunk | W_i chunk | dS rows i >= 1 | dgamma dbeta | head
+  const bool fused = c.defer == 2;
+  const int HC = EMB_HC, nch = rc_nchunk(d);
+  const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 0);
   // workgroup 0 is the adjacency workgroup (the longest; dispatched first), 1..nw the parameters
   if (blockIdx.x > 0) {
@@ -786,7 +817,36 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     if (e >= total) return;
     float g = 0.f;
     int64_t idx;
-    if (e < nFH) {
+    if (fused) {
+      const EmbWbSum wbs(c, ws);
+      if (e < nFH) {  // W_i[i][f][h]: node cc's record of chunk h / HC
+        const int ih = e / H, h = e - ih * H, off = ofs_w + ih * HC + h % HC, ch = h / HC;
+        for (int cc = 0; cc < p; ++cc) g += wbs(cc * nch + ch, off);
+        idx = c.eo.gcW + e;
+      } else if (e < nFH + nfc) {
+        const int q = e - nFH;
+        g = wbs(0, ofs_h + q);
+        if (q < K * M1) idx = c.eo.fc2W + q;
+        else if (q < K * M1 + K) idx = c.eo.fc2b + (q - K * M1);
+        else idx = c.eo.fc1b + (q - K * M1 - K);
+      } else if (e < nFH + nfc + 2 * F) {
+        const int q = e - nFH - nfc;
+        const int which = q / F, f = q - which * F;
+        float g4[4] = {0.f, 0.f, 0.f, 0.f};
+        int pt = 0;
+        for (; pt + 3 < c.dgN; pt += 4)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) g4[u] += wbs(pt + u, ofs_g + which * F + f);
+        for (; pt < c.dgN; ++pt) g4[0] += wbs(pt, ofs_g + which * F + f);
+        g = (g4[0] + g4[1]) + (g4[2] + g4[3]);
+        idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
+      } else {  // fc1 weight [m][node * H + h]
+        const int q = e - nFH - nfc - 2 * F, pH = p * H;
+        const int m = q / pH, rem = q - m * pH, node = rem / H, h = rem - node * H;
+        g = wbs(node * nch + h / HC, m * HC + h % HC);
+        idx = c.eo.fc1W + q;
+      }
+    } else if (e < nFH) {
 #pragma unroll 8
       for (int cc = 0; cc < p; ++cc) g += ws[c.wo.dWi + (int64_t)cc * nFH + e];
       idx = c.eo.gcW + e;
@@ -859,7 +919,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
         rc_seg<NR>((n - 1) * pp2, [&](int e) {
           const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
           float t = 0.f;
-          for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
+          if (fused) {
+            const EmbWbSum wbs(c, ws);
+            for (int chk = 0; chk < nch; ++chk) t += wbs(cc * nch + chk, ofs_s + (i - 1) * p + cp);
+          } else {
+            for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
+          }
           return t;
         }, [&](int e, float v) { dSw[at(e)] = v; }),
         // adjacency-L1 gradient (summed over the factors by k_emb_bwd's reduce workgroups)

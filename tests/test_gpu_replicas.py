@@ -102,3 +102,25 @@ def test_pack_rejects_mixed_shapes_and_phases():
     pack.run_epoch(0, ds)
     with pytest.raises(RuntimeError, match="different training phases"):
         pack.run_epoch(1, ds)
+
+
+@pytest.mark.parametrize("variant", ["0", "1"])
+def test_window_block_combine_variants_bitwise(variant, monkeypatch):
+    """The embedder-backward window-block partials can be summed by the last-arriving workgroup
+    (REDCLIFF_DEFER=0), a separate k_emb_combine launch (1, the default) or read in
+    place by k_emb_final (2): same sums in the same order, so the fits agree bit for bit (ragged
+    last batch included)."""
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
+    train = data(64 * 2 + 24, seed=5)
+    fits = {}
+    for v in ("2", variant):
+        monkeypatch.setenv("REDCLIFF_DEFER", v)
+        m = make(0, 10.0, 0.1)
+        oA, oB = opts(m, 5e-4, 2e-4)
+        for epoch in (0, 1, 2, 3):
+            for bi, (Xb, Yb) in enumerate(train):
+                m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+        torch.cuda.synchronize()
+        fits[v] = {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
+    for k, want in fits[variant].items():
+        np.testing.assert_array_equal(fits["2"][k], want, err_msg=k)
