@@ -229,8 +229,9 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
 // gradients and (node 0, chunk 0) the fc2 / fc1-bias gradients.  The windows are walked in
 // LDS sub-blocks of BC (register accumulators carry over), so large p*F windows keep the
 // partial records few.  The partials of the nbw window blocks of one (node, chunk) are
-// combined in fixed order by the block that arrives last (agent-scope release / ticket /
-// acquire, cdna_hip_programming.md §6 Guideline 16).  The first sub-block's inputs and the
+// combined in fixed order by k_emb_combine (c.defer == 1, the default), by k_emb_final in
+// place (2), or by the block that arrives last (0: agent-scope release / ticket / acquire,
+// cdna_hip_programming.md §6 Guideline 16).  The first sub-block's inputs and the
 // fixed operands are staged by one multi-segment pass (one memory latency for everything).
 template <bool MULTI>
 __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, int WPB, float* sm) {
