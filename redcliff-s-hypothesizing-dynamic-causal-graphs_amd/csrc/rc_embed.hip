@@ -769,18 +769,53 @@ struct EmbWbSum {
     const int wpb = rc_emb_wpb(c.d);
     nbw = (c.B + wpb - 1) / wpb;
   }
-  __device__ float operator()(int grp, int off) const {
-    const float* b = base + (int64_t)grp * nbwm * pst + off;
-    float t = 0.f;
-    for (int w0 = 0; w0 < nbw; w0 += 8) {
-      float v[8];
+  __device__ float operator()(int grp, int off) const { return nodes(grp, 1, 1, off); }
+  // Sum over u < nn, in order, of the window-block sums of group grp0 + u * gs: the combined
+  // records added one after another, as k_emb_final adds them.  Four groups x eight window
+  // blocks of loads are in flight at once (one memory round per 4 groups for nbw <= 8).
+  __device__ float nodes(int grp0, int gs, int nn, int off) const {
+    float g = 0.f;
+    for (int u0 = 0; u0 < nn; u0 += 4) {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int w0 = 0; w0 < nbw; w0 += 8) {
+        float v[4][8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = (w0 + q < nbw) ? b[(int64_t)(w0 + q) * pst] : 0.f;
+        for (int u = 0; u < 4; ++u) {
+          const float* b = base + (int64_t)(grp0 + (u0 + u) * gs) * nbwm * pst + off;
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (w0 + q < nbw) t += v[q];
+          for (int q = 0; q < 8; ++q) v[u][q] = (u0 + u < nn && w0 + q < nbw) ? b[(int64_t)(w0 + q) * pst] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (w0 + q < nbw) t[u] += v[u][q];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u0 + u < nn) g += t[u];
     }
-    return t;
+    return g;
+  }
+  // the four chains of consecutive groups grp0 .. grp0 + 3 (BatchNorm affine partials)
+  __device__ void four(int grp0, int off, float* g4) const {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int w0 = 0; w0 < nbw; w0 += 8) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* b = base + (int64_t)(grp0 + u) * nbwm * pst + off;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[u][q] = (w0 + q < nbw) ? b[(int64_t)(w0 + q) * pst] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (w0 + q < nbw) t[u] += v[u][q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) g4[u] += t[u];
   }
 };
 
@@ -822,7 +857,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       const EmbWbSum wbs(c, ws);
       if (e < nFH) {  // W_i[i][f][h]: node cc's record of chunk h / HC
         const int ih = e / H, h = e - ih * H, off = ofs_w + ih * HC + h % HC, ch = h / HC;
-        for (int cc = 0; cc < p; ++cc) g += wbs(cc * nch + ch, off);
+        g = wbs.nodes(ch, nch, p, off);
         idx = c.eo.gcW + e;
       } else if (e < nFH + nfc) {
         const int q = e - nFH;
@@ -835,9 +870,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
         const int which = q / F, f = q - which * F;
         float g4[4] = {0.f, 0.f, 0.f, 0.f};
         int pt = 0;
-        for (; pt + 3 < c.dgN; pt += 4)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) g4[u] += wbs(pt + u, ofs_g + which * F + f);
+        for (; pt + 3 < c.dgN; pt += 4) wbs.four(pt, ofs_g + which * F + f, g4);
         for (; pt < c.dgN; ++pt) g4[0] += wbs(pt, ofs_g + which * F + f);
         g = (g4[0] + g4[1]) + (g4[2] + g4[3]);
         idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
@@ -921,8 +954,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
           const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
           float t = 0.f;
           if (fused) {
-            const EmbWbSum wbs(c, ws);
-            for (int chk = 0; chk < nch; ++chk) t += wbs(cc * nch + chk, ofs_s + (i - 1) * p + cp);
+            t = EmbWbSum(c, ws).nodes(cc * nch, 1, nch, ofs_s + (i - 1) * p + cp);
           } else {
             for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
           }
