@@ -165,6 +165,16 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
  * back from a step run with RC_STORE_OUTPUTS. */
 int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out);
 
+/* Verification mode (tests only; no reference counterpart): with floats > 0 every workspace
+ * region laid out afterwards is followed by a guard band of that many floats, the last band
+ * also closing replica R-1's slice.  A test fills the bands with a NaN pattern; a write past
+ * a region's end changes a band, a read past it puts NaN into the results.  0 = production
+ * layout.  Returns the previous setting.  Process-wide: set it before sizing workspaces. */
+int redcliff_debug_guard_bands(int32_t floats);
+/* (start, size) pairs, in floats, of the regions of one replica's workspace slice in layout
+ * order (out[2i], out[2i+1]); returns the region count. */
+int redcliff_workspace_regions(const RedcliffDims* d, int64_t* out, int32_t n_pairs);
+
 /* Stand-alone forward of K cMLPs (models/cmlp.py:90-101) on B windows Xwin[r][B][L][p]
  * (x_rstride floats between replicas).  Per replica (ws_rstride floats) the workspace
  * receives a[K][p][B][h] | y[nU][B][K][p] | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h];

@@ -72,6 +72,7 @@ int stream_wait(hipStream_t to, hipStream_t from, hipEvent_t ev) {
 }  // namespace
 
 static thread_local char g_err[512] = "";
+int rc_ws_guard_floats = 0;
 
 void rc_set_error(const char* fmt, ...) {
   va_list ap;
@@ -139,6 +140,30 @@ int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_out && i < nv; ++i) out[i] = v[i];
   return nv;
+}
+
+// Verification mode: guard bands of `floats` floats after every workspace region (0 = off,
+// the production layout).  Affects workspaces sized / laid out after the call.  Returns the
+// previous setting.
+int redcliff_debug_guard_bands(int32_t floats) {
+  const int prev = rc_ws_guard_floats;
+  rc_ws_guard_floats = floats < 0 ? 0 : (floats > 4096 ? 4096 : floats);
+  return prev;
+}
+
+// (start, size) in floats of every region of one replica's workspace slice, in layout order;
+// with guard bands on, region i's band is [start + size, start + size + guard).  Returns the
+// number of regions.
+int redcliff_workspace_regions(const RedcliffDims* d, int64_t* out, int32_t n_pairs) {
+  if (check_dims(d) != 0) return REDCLIFF_EINVAL;
+  int64_t ext[2 * RC_WS_MAX_REGIONS];
+  int nr = 0;
+  rc_ws_off(*d, ext, &nr);
+  for (int i = 0; i < nr && i < n_pairs; ++i) {
+    out[2 * i] = ext[2 * i];
+    out[2 * i + 1] = ext[2 * i + 1];
+  }
+  return nr;
 }
 
 int redcliff_bn_batch_stats(const RedcliffDims* d, const float* X, int64_t x_rstride, int64_t N, int32_t B,
@@ -249,10 +274,10 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   hipStream_t sf = s;
   // A single fit is latency-bound: the factor chain on a second stream fills idle CUs (C5 201K ->
   // 233K windows/s).  Packed replicas already fill the chip and the two chains only compete
-  // for it: one stream is faster there (D4IC R=32 grid 6.61M -> 6.78M windows/s).  Packs also
-  // stay on one stream below R = 8: a forked R = 3 matrix-core pack occasionally (2 runs in
-  // ~12) gave its last replica an A different from the independent fit's -- root cause not
-  // found; the single-stream pack matches bit for bit.  REDCLIFF_FORK=0 / 1 overrides (tuning).
+  // for it: one stream is faster there (D4IC R=32 grid 6.61M -> 6.78M windows/s).  Forked and
+  // single-stream steps give the same bits (tests/test_gpu_forked.py); the intermittent A
+  // mismatch once blamed on the fork was a missing barrier in k_emb_final's adjacency
+  // workgroup, which concurrent work only made likelier.  REDCLIFF_FORK=0 / 1 overrides (tuning).
   const char* fv = getenv("REDCLIFF_FORK");
   const bool two = fv ? strcmp(fv, "0") != 0 : c.d.R == 1;
   if (fork && two) {
@@ -292,10 +317,8 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   } else if (emb_grad) {
     // The node blocks' window-block partials are summed by a separate k_emb_combine launch
     // instead of the in-kernel last arriver (ticket + agent-scope fences): the fences cost the
-    // packed grid ~20 % (D4IC R=32 6.8M -> 8.1M windows/s).  Same sums in the same order.  The
-    // two-stream step uses it too: a matrix-core pack of 8 once gave one replica an A different
-    // from its forked independent fit, whose in-kernel ticket combine is the only cross-workgroup
-    // handshake on that path (root cause not isolated); the launch costs ~5 us there.
+    // packed grid ~20 % (D4IC R=32 6.8M -> 8.1M windows/s).  Same sums in the same order, so
+    // every variant gives the same bits (tests/test_gpu_replicas.py, tests/test_gpu_forked.py).
     // defer 2: k_emb_final reads the partials in place (same order, no combine launch) --
     // measured slower for the single fit (k_emb_final 10 -> 20.5 us: p * nbw dependent loads
     // per element on its critical path), +1 % on the R = 32 grid, so not the default.

@@ -129,48 +129,66 @@ inline int64_t rc_align64(int64_t x) { return (x + 63) & ~(int64_t)63; }
 // layer-0 contraction length p*L rounded up to the MFMA staging chunk
 __host__ __device__ inline int rc_qpad(const RedcliffDims& d) { return (d.p * d.L + 31) & ~31; }
 
-inline WsOff rc_ws_off(const RedcliffDims& d) {
+// Verification mode (redcliff_debug_guard_bands): every workspace region is followed by a
+// guard band of this many floats, the last one doubling as the band after replica R-1, so a
+// test can fill the bands with a NaN pattern and find any write past a region's end (the band
+// changes) or read past it (NaN reaches the results).  0 in production.
+extern int rc_ws_guard_floats;
+#define RC_WS_MAX_REGIONS 40
+
+// Region layout of one replica's workspace slice.  ext (optional) receives (start, size) of
+// every region in layout order; *next its count.
+inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next = nullptr) {
   WsOff o;
   int64_t x = 0;
+  int nr = 0;
+  const int64_t G = rc_ws_guard_floats;
+  auto put = [&](int64_t& field, int64_t n) {
+    field = x;
+    if (ext && nr < RC_WS_MAX_REGIONS) { ext[2 * nr] = x; ext[2 * nr + 1] = n; }
+    ++nr;
+    x = rc_align64(x + n + G);
+  };
   const int64_t B = d.Bmax, p = d.p, K = d.K;
-  o.T = x; x = rc_align64(x + B * d.n * p * d.F);
-  o.R = x; x = rc_align64(x + B * p * d.H);
-  o.f1 = x; x = rc_align64(x + B * d.M1);
-  o.w = x; x = rc_align64(x + B * K);
-  o.a = x; x = rc_align64(x + K * p * B * d.h);
-  o.y = x; x = rc_align64(x + (int64_t)rc_nuchunk(d) * B * K * p);
-  o.G = x; x = rc_align64(x + K * p * p * d.L);
-  o.G0 = x; x = rc_align64(x + K * p * p);
-  o.w1 = x; x = rc_align64(x + K * p * d.h);
-  o.gq = x; x = rc_align64(x + (int64_t)rc_nuchunk(d) * K * p * p * d.L);
-  o.ebp = x; x = rc_align64(x + (int64_t)p * rc_nchunk(d) * rc_emb_nbw(d) * rc_emb_pstride(d));
-  o.ecnt = x; x = rc_align64(x + p * rc_nchunk(d));
-  o.gfc1 = x; x = rc_align64(x + (int64_t)d.M1 * p * d.H);
-  o.dwp = x; x = rc_align64(x + p * B * K);
-  o.dAadj = x; x = rc_align64(x + K * p * p);
-  o.dWi = x; x = rc_align64(x + p * d.n * d.F * d.H);
-  o.dS = x; x = rc_align64(x + (rc_nchunk(d) > 64 ? rc_nchunk(d) : 64) * d.n * p * p);
-  o.dgb = x; x = rc_align64(x + p * rc_nchunk(d) * 2 * d.F);
-  o.S = x; x = rc_align64(x + d.n * p * p);
-  o.dZ = x; x = rc_align64(x + p * B * d.H);
-  o.amat = x; x = rc_align64(x + 8 * p * p);
-  o.lossp = x; x = rc_align64(x + p + K * p + 8);
-  o.xsim = x; x = rc_align64(x + B * p);
-  o.gfc = x; x = rc_align64(x + K * d.M1 + K + d.M1);
-  o.xw = x; x = rc_align64(x + B * rc_qpad(d));
-  o.dyl = x; x = rc_align64(x + K * p * B);
-  o.dgs = x; x = rc_align64(x + K * p * p * d.L);
-  o.f1p = x; x = rc_align64(x + 64 * B * d.M1);
-  o.edf1 = x; x = rc_align64(x + B * d.M1);
-  o.edT = x; x = rc_align64(x + B * p * d.n * d.F);
-  o.edX = x; x = rc_align64(x + B * p * d.F);
-  o.eAf = x; x = rc_align64(x + p * p * d.n);
-  o.edr = x; x = rc_align64(x + B * K);
-  o.cosb = x; x = rc_align64(x + 2 * B);
+  put(o.T, B * d.n * p * d.F);
+  put(o.R, B * p * d.H);
+  put(o.f1, B * d.M1);
+  put(o.w, B * K);
+  put(o.a, K * p * B * d.h);
+  put(o.y, (int64_t)rc_nuchunk(d) * B * K * p);
+  put(o.G, K * p * p * d.L);
+  put(o.G0, K * p * p);
+  put(o.w1, K * p * d.h);
+  put(o.gq, (int64_t)rc_nuchunk(d) * K * p * p * d.L);
+  put(o.ebp, (int64_t)p * rc_nchunk(d) * rc_emb_nbw(d) * rc_emb_pstride(d));
+  put(o.ecnt, p * rc_nchunk(d));
+  put(o.gfc1, (int64_t)d.M1 * p * d.H);
+  put(o.dwp, p * B * K);
+  put(o.dAadj, K * p * p);
+  put(o.dWi, p * d.n * d.F * d.H);
+  put(o.dS, (rc_nchunk(d) > 64 ? rc_nchunk(d) : 64) * d.n * p * p);
+  put(o.dgb, p * rc_nchunk(d) * 2 * d.F);
+  put(o.S, d.n * p * p);
+  put(o.dZ, p * B * d.H);
+  put(o.amat, 8 * p * p);
+  put(o.lossp, p + K * p + 8);
+  put(o.xsim, B * p);
+  put(o.gfc, K * d.M1 + K + d.M1);
+  put(o.xw, B * rc_qpad(d));
+  put(o.dyl, K * p * B);
+  put(o.dgs, K * p * p * d.L);
+  put(o.f1p, 64 * B * d.M1);
+  put(o.edf1, B * d.M1);
+  put(o.edT, B * p * d.n * d.F);
+  put(o.edX, B * p * d.F);
+  put(o.eAf, p * p * d.n);
+  put(o.edr, B * K);
+  put(o.cosb, 2 * B);
 #ifdef RC_TRACE
   x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
 #endif
   o.total = x;
+  if (next) *next = nr < RC_WS_MAX_REGIONS ? nr : RC_WS_MAX_REGIONS;
   return o;
 }
 

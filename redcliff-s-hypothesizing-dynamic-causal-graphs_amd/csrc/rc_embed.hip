@@ -942,6 +942,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       vreg[u] = in ? V[c.eo.A + e] : 0.f;
     }
     RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 49);
+#ifdef RC_PROBE_DELAY
+    // race probe (scripts/race_probe.py): waves >= 1 store their staged operands late, as they
+    // do when their loads come back later than wave 0's (e.g. under a concurrent kernel chain)
+    if ((tid >> 6) >= 1)
+      for (int i = 0; i < 64; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
     rc_stage_all(
         rc_seg<NR>(pp2, [&](int e) { return A[e]; }, [&](int e, float v) {
           const int q = at(e);
@@ -962,6 +968,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
         }, [&](int e, float v) { dSw[at(e)] = v; }),
         // adjacency-L1 gradient (summed over the factors by k_emb_bwd's reduce workgroups)
         rc_seg<NR>(adjL1 ? pp2 : 0, [&](int e) { return ws[c.wo.dAadj + e]; }, [&](int e, float v) { Sl[at(e)] = v; }));
+#ifndef RC_PROBE_NO_BARRIER
+    // Every LDS operand above was stored by the thread that loaded it; the row sums below read
+    // whole rows, i.e. entries other waves stored.  Without this barrier a wave whose staging
+    // loads returned early read relu(A) rows another wave had not stored yet (stale LDS), and
+    // A's Adam step used a wrong D^-1/2 for those rows and columns: the intermittent A mismatch
+    // of round 1 ("Root cause of the round-1 A mismatch").
+    __syncthreads();
+#endif
     RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 50);
     for (int e = tid; e < pp2; e += RC_BLOCK) dL[at(e)] = 0.f;
     lds_rowsum(p, [&](int i, int j) { return Ar[i * P + j]; },

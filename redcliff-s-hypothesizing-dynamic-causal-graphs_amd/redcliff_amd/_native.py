@@ -32,7 +32,7 @@ EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_b
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
             "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm",
-            "redcliff_gc_progress")
+            "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine")
 
 
@@ -115,6 +115,8 @@ def lib():
                                 ctypes.c_int32, _vp]
     L.redcliff_gc_progress.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp]
+    L.redcliff_debug_guard_bands.argtypes = [ctypes.c_int32]
+    L.redcliff_workspace_regions.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(_i64), ctypes.c_int32]
     for name in EXPORTED[2:]:
         if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count"):
             getattr(L, name).restype = ctypes.c_int
@@ -136,6 +138,21 @@ def workspace_layout(dims):
     if n < 0:
         check(n, "workspace_layout")
     return dict(zip(WS_REGIONS, [int(v) for v in out]))
+
+
+def workspace_regions(dims):
+    """[(start, size)] in floats of one replica's workspace regions (layout order)."""
+    out = (_i64 * 80)()
+    n = lib().redcliff_workspace_regions(ctypes.byref(dims), out, 40)
+    if n < 0:
+        check(n, "workspace_regions")
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+
+def guard_bands(floats):
+    """Verification mode: guard bands of `floats` floats after every workspace region laid out
+    from now on (0 = production layout).  Returns the previous setting."""
+    return int(lib().redcliff_debug_guard_bands(int(floats)))
 
 
 def kernel_timing(enable):

@@ -12,10 +12,20 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libredcliff_hip.so")
 TRACE_LIB = os.path.join(LIB_DIR, "libredcliff_hip_trace.so")  # -DRC_TRACE: per-phase wall-clock marks
 ARCH = os.environ.get("REDCLIFF_OFFLOAD_ARCH", "gfx950")
+# Diagnostic variants (scripts/race_probe.py): the round-1 A-mismatch race made reproducible by
+# delaying waves >= 1 of k_emb_final's adjacency workgroup, with and without the fixing barrier.
+VARIANTS = {
+    "probe_fixed": ["-DRC_PROBE_DELAY"],
+    "probe_nobarrier": ["-DRC_PROBE_DELAY", "-DRC_PROBE_NO_BARRIER"],
+}
 
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def variant_path(name):
+    return os.path.join(LIB_DIR, "libredcliff_hip_%s.so" % name)
 
 
 def _stale(lib=LIB):
@@ -26,25 +36,53 @@ def _stale(lib=LIB):
     return any(os.path.getmtime(s) > t for s in deps)
 
 
+def _compile(lib, defines, verbose):
+    """One object per translation unit, compiled in parallel, then one link."""
+    from concurrent.futures import ThreadPoolExecutor
+    import tempfile
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    base = [hipcc, "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-I" + INCLUDE, "-I" + CSRC] + list(defines)
+    with tempfile.TemporaryDirectory(prefix="rc_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(s) + ".o") for s in sources()]
+        cmds = [base + ["-c", s, "-o", o] for s, o in zip(sources(), objs)]
+        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+        with ThreadPoolExecutor(jobs) as ex:
+            for cmd in cmds:
+                if verbose:
+                    print(" ".join(cmd))
+            list(ex.map(subprocess.check_call, cmds))
+        # -Bsymbolic: the library's own calls bind inside it, so a diagnostic variant can be loaded
+        # next to the production library without either resolving into the other
+        link = [hipcc, "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-Wl,-Bsymbolic"] + objs + ["-o", lib + ".tmp"]
+        if verbose:
+            print(" ".join(link))
+        subprocess.check_call(link)
+    os.replace(lib + ".tmp", lib)
+    return lib
+
+
 def build(force=False, verbose=False, trace=False):
     """Build the HIP shared library if it is missing or older than its sources.
     trace=True builds the phase-timing variant (scripts/phase_trace.py) instead."""
     lib = TRACE_LIB if trace else LIB
     if not force and not _stale(lib):
         return lib
-    os.makedirs(LIB_DIR, exist_ok=True)
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + INCLUDE, "-I" + CSRC]
-    if trace:
-        cmd.append("-DRC_TRACE")
-    cmd += sources() + ["-o", lib + ".tmp"]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
-    os.replace(lib + ".tmp", lib)
-    return lib
+    return _compile(lib, ["-DRC_TRACE"] if trace else [], verbose)
+
+
+def build_variant(name, force=False, verbose=False):
+    """Build one of the diagnostic VARIANTS (not part of the product)."""
+    lib = variant_path(name)
+    if not force and not _stale(lib):
+        return lib
+    return _compile(lib, VARIANTS[name], verbose)
 
 
 if __name__ == "__main__":
     import sys
-    print(build(force=True, verbose=True, trace="--trace" in sys.argv))
+    if "--variants" in sys.argv:
+        for v in VARIANTS:
+            print(build_variant(v, force=True, verbose=True))
+    else:
+        print(build(force=True, verbose=True, trace="--trace" in sys.argv))

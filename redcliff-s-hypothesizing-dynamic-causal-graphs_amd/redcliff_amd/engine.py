@@ -408,6 +408,12 @@ class FitEngine:
                       "train_steps")
             self._after(flags, nbn, len(rows_a))
 
+    def plan_steps(self, kind, X, lab, stats, d, rows, sizes, oA, oB):
+        """A prepared epoch of one update kind: the argument block, batch order and statistics
+        are built once; ``StepPlan.run()`` launches the epoch with only the Adam step numbers
+        refreshed (the host cost of one epoch is one C call)."""
+        return StepPlan(self, kind, X, lab, stats, d, rows, sizes, oA, oB)
+
     def run_values(self, X, lab, d, rows, sizes, train_bn=False, stats=None, confusion=True):
         """validate_training body over consecutive batches; returns (acc[8], confusion)."""
         self.ensure_bound()
@@ -457,6 +463,43 @@ class FitEngine:
         nat.check(nat.lib().redcliff_gc_norms(ctypes.byref(d), ptr(self.fac), self.fac.numel(), ptr(G), ptr(G0),
                                               _stream()), "gc_norms")
         return G, G0
+
+
+class StepPlan:
+    """One update kind over a fixed batch sequence (an epoch of fit(), or a bench run), with
+    everything but the Adam step numbers resolved up front.  Valid while the model's
+    parameters stay bound to this engine (fit loops and the bench do not rebind them)."""
+
+    def __init__(self, eng, kind, X, lab, stats, d, rows, sizes, oA, oB):
+        eng.ensure_bound()
+        self.eng = eng
+        self.flags, self.nbn = flags_for(kind, eng.nsup)
+        if self.flags & nat.STEP_A:
+            eng.bind_optimizer("A", oA)
+        if self.flags & nat.STEP_B:
+            eng.bind_optimizer("B", oB)
+        self.stats = stats.contiguous() if (stats is not None and self.flags & nat.BN_TRAIN) else None
+        self.X, self.lab = X, lab  # keep the buffers alive
+        self.a = eng._args(d, self.flags, self.nbn, X, lab, self.stats)
+        self.rows = np.ascontiguousarray(rows, dtype=np.int64)
+        self.sizes = np.ascontiguousarray(sizes, dtype=np.int32)
+        self.n = len(self.rows)
+        self._rows_p = self.rows.ctypes.data_as(ctypes.c_void_p)
+        self._sizes_p = self.sizes.ctypes.data_as(ctypes.c_void_p)
+        self._fn = nat.lib().redcliff_train_steps
+        self._bn_step = 2 * eng.F
+
+    def run(self, stream=None):
+        eng, a = self.eng, self.a
+        stA, stB = eng.opt["A"], eng.opt["B"]
+        a.tA = (stA["t"] + 1) if stA else 1
+        a.tB = (stB["t"] + 1) if stB else 1
+        a.flags = self.flags | (0 if eng.supports_fresh else nat.REFRESH_SUPPORTS)
+        rc = self._fn(ctypes.byref(a), self.n, self._rows_p, self._sizes_p, self._bn_step,
+                      stream if stream is not None else _stream())
+        if rc != 0:
+            nat.check(rc, "train_steps (plan)")
+        eng._after(self.flags, self.nbn, self.n)
 
 
 def _stream():

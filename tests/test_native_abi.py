@@ -61,6 +61,27 @@ def test_workspace_layout_and_validation():
     assert L.redcliff_workspace_bytes(ctypes.byref(bad)) == 0
 
 
+def test_guard_band_layout():
+    """Verification layout (redcliff_debug_guard_bands): every region is followed by its own band,
+    bands never overlap the next region, and the last band closes the replica's slice."""
+    from redcliff_amd import _native as nat
+    d = c1_dims()
+    plain = nat.workspace_regions(d)
+    assert len(plain) == 34 and nat.workspace_layout(d)["total"] >= plain[-1][0] + plain[-1][1]
+    prev = nat.guard_bands(64)
+    try:
+        regs = nat.workspace_regions(d)
+        total = nat.workspace_layout(d)["total"]
+        assert [n for _, n in regs] == [n for _, n in plain]
+        for (s, n), (s2, _) in zip(regs, regs[1:]):
+            assert s % 64 == 0 and s + n + 64 <= s2
+        assert regs[-1][0] + regs[-1][1] + 64 <= total
+        assert nat.lib().redcliff_workspace_bytes(ctypes.byref(d)) == 4 * total
+    finally:
+        nat.guard_bands(prev)
+    assert nat.workspace_regions(d) == plain
+
+
 def test_train_step_rejects_null_arguments():
     from redcliff_amd import _native as nat
     L = nat.lib()
