@@ -9,14 +9,24 @@ Default workload = BASELINE.json configs[1]: REDCLIFF-S w/ state smoothing, D4IC
 windows of 21 steps, labels (N, K, 1)); D4IC itself is not in the image, so the windows
 are synthetic with the same shapes.
 
-    python bench.py [--gpus N --steps K --warmup W]      (N>1: one rank per GPU via torchrun)
+    python bench.py [--gpus N --steps K --warmup W] [--mode fit|dp]
 
-Multi-GPU: every rank runs an independent fit (grid-search replicas shard one per GPU,
-no collective); value = all windows processed / max-over-ranks time ("scaling": "weak").
+--gpus N > 1 without a torch.distributed launcher: this process starts N ranks itself
+(torch.distributed.run, 127.0.0.1) before touching the GPU and exits with their status.
+
+mode "fit" (default): every rank runs an independent fit (grid-search replicas shard one per
+GPU, no collective); value = all windows processed / max-over-ranks time ("scaling": "weak").
+The same line carries the packed grid search (R fits per launch, windows/s and fits/hour)
+and, at N = 1, the north-star ratio config (10 channels / 5 lags / 4 factors) with its own
+CPU baseline.
+mode "dp": BASELINE configs[3] -- one TST-shaped fit data-parallel over the N ranks (shards of
+every global batch, one RCCL all-reduce of the flat gradient per update).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,6 +39,7 @@ sys.path.insert(0, os.path.join(ROOT, "redcliff-s-hypothesizing-dynamic-causal-g
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense FP32 (vector == f32 MFMA rate), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+METRIC = "cMLP-factor fwd+bwd windows/sec/GPU; grid-search fits/hour on 8 GPUs"
 
 CONFIGS = {
     # BASELINE.json configs[1]: D4IC-shaped, 4 factors (train/REDCLIFF_S_CMLP_Smooth_d4IC_BSCgs4ParsimSmo0_cached_args.txt)
@@ -39,6 +50,7 @@ CONFIGS = {
     "c1k4": dict(p=10, L=5, K=4, nsup=4, h=25, F=16, n=3, H=100, B=128, T=100, label_T=100, lrA=5e-4, lrB=5e-4,
                  workload="REDCLIFF-S cMLP w/ state smoothing, synthetic sVAR (p=10, gen_lag=5, K=4, h=25, "
                           "DGCNN F=16/3 layers/100 hidden), combined-phase batch_update, B=128"),
+    # BASELINE.json configs[3]: TST-shaped (region averages), data-parallel
     "c4": dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, B=128, T=150, label_T=150, lrA=5e-4, lrB=5e-4,
                workload="REDCLIFF-S TST-shaped (p=12, gen_lag=4, K=9, nsup=3, h=25, DGCNN 16/3/100), B=128"),
     # BASELINE.json configs[4]: scaled synthetic stress (large grouped contraction)
@@ -60,8 +72,7 @@ def flops_per_window(c):
                 total=fac_fwd + fac_bwd + emb_fwd + emb_bwd + pen)
 
 
-
-def roofline_of(ktimes, fl, windows_per_launch, with_traffic):
+def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg):
     """Roofline object of the dominant kernel: algorithmic FLOPs per launch (SURVEY 8(d)
     per-window counts x the windows one launch processes) / its average HIP-event duration.
     Timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch)
@@ -83,10 +94,11 @@ def roofline_of(ktimes, fl, windows_per_launch, with_traffic):
              "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final", "fac_mix": "k_fac_mix"}[dom]
     return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
-            "traffic": pmc_traffic(kname) if with_traffic else None,
+            "traffic": pmc_traffic(kname, traffic_cfg) if traffic_cfg else None,
             "avg_launch_us": round(avg_ms * 1e3, 2),
             "algorithmic_flops_per_launch": flops,
             "kernel_avg_us": dict((k, round(v[0] * 1e3, 2)) for k, v in ktimes.items())}
+
 
 def synth(c, N, seed):
     rng = np.random.RandomState(seed)
@@ -103,20 +115,23 @@ def synth(c, N, seed):
     return torch.from_numpy(X), torch.from_numpy(Y)
 
 
-def build_model(cls, c, seed):
-    K, p = c["K"], c["p"]
+def coeffs(K, p, forecast=10.0, adj=0.1):
     denom = sum(float(i) for i in range(1, K)) if K > 1 else 1.0
-    coeff = {"FORECAST_COEFF": 10.0, "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0 / denom,
-             "FACTOR_WEIGHT_L1_COEFF": 1e-3, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0,
-             "ADJ_L1_REG_COEFF": 0.1 / K / np.sqrt(p * p - 1.0), "DAGNESS_REG_COEFF": 0.0,
-             "DAGNESS_LAG_COEFF": 0.0, "DAGNESS_NODE_COEFF": 0.0}
+    return {"FORECAST_COEFF": forecast, "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0 / denom,
+            "FACTOR_WEIGHT_L1_COEFF": 1e-3, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0,
+            "ADJ_L1_REG_COEFF": adj / K / np.sqrt(p * p - 1.0), "DAGNESS_REG_COEFF": 0.0,
+            "DAGNESS_LAG_COEFF": 0.0, "DAGNESS_NODE_COEFF": 0.0}
+
+
+def build_model(cls, c, seed, pre=1, acc=1, **cw):
+    K, p = c["K"], c["p"]
     eargs = [("num_features_per_node", c["F"]), ("num_graph_conv_layers", c["n"]), ("num_hidden_nodes", c["H"]),
              ("sigmoid_eccentricity_coeff", 10.0)]
     torch.manual_seed(seed)
-    return cls(p, c["L"], [c["h"]], c["F"], [0], c["L"], 1, K, c["nsup"], coeff, False, "DGCNN", eargs,
+    return cls(p, c["L"], [c["h"]], c["F"], [0], c["L"], 1, K, c["nsup"], coeffs(K, p, **cw), False, "DGCNN", eargs,
                "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
-               training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=1,
-               num_acclimation_epochs=1)
+               training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=pre,
+               num_acclimation_epochs=acc)
 
 
 def adam_pair(m, c):
@@ -125,10 +140,14 @@ def adam_pair(m, c):
     return oA, oB
 
 
+def cpu_threads():
+    return int(os.environ.get("REDCLIFF_CPU_THREADS", min(16, os.cpu_count() or 1)))
+
+
 def cpu_baseline(c, seconds):
     """The oracle (CPU restatement keeping the reference's op structure) on the host cores."""
     from oracle.redcliff_oracle import OracleREDCLIFF
-    threads = int(os.environ.get("REDCLIFF_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     m = build_model(OracleREDCLIFF, c, seed=0)
     oA, oB = adam_pair(m, c)
@@ -141,35 +160,89 @@ def cpu_baseline(c, seconds):
         m.batch_update(2, n, Xb, Yb, oA, oB, 1)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n * c["B"] / dt, 2), "unit": "windows/s", "cores": threads, "kind": "port",
+    return {"value": round(n * c["B"] / dt, 2), "unit": "windows/s", "cores": threads,
+            "host_cpu_count": os.cpu_count(), "kind": "port",
             "sample": "%d combined-phase batch_updates of B=%d (%.1f s) with oracle/redcliff_oracle.py "
-                      "(reference op structure: per-sample loops, autograd, torch.optim.Adam) on %d threads"
-                      % (n, c["B"], dt, threads)}
+                      "(reference op structure: per-sample loops, autograd, torch.optim.Adam) on %d threads "
+                      "(os.cpu_count() = %s on this host)" % (n, c["B"], dt, threads, os.cpu_count())}
 
 
-PMC_CONFIG = "d4ic"  # the configuration scripts/profile_pmc.sh collects the counters on
-
-
-def pmc_traffic(kernel_name, launches_hint=None):
+def pmc_traffic(kernel_name, cfg):
     """HBM bytes per launch of ``kernel_name`` from committed rocprofv3 PMC summaries
-    (profiles/*pmc*.csv), FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE."""
+    (profiles/*pmc_<cfg>*counter_collection*.csv, else the round-1 ones for d4ic):
+    FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE."""
     import csv
     import glob
-    fetch, write = None, None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*counter_collection*.csv"))):
-        vals = {}
-        with open(path) as f:
-            for row in csv.DictReader(f):
-                if kernel_name not in row.get("Kernel_Name", ""):
-                    continue
-                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-        if "FETCH_SIZE" in vals:
-            fetch = float(np.mean(vals["FETCH_SIZE"]))
-        if "WRITE_SIZE" in vals:
-            write = float(np.mean(vals["WRITE_SIZE"]))
-    if fetch is None or write is None:
-        return None
-    return (2.0 * fetch + write) * 1024.0  # counters are in KiB
+    pats = [os.path.join(ROOT, "profiles", "*pmc_%s_*counter_collection*.csv" % cfg)]
+    if cfg == "d4ic":
+        pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
+    for pat in pats:
+        fetch, write = None, None
+        for path in sorted(glob.glob(pat)):
+            vals = {}
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if kernel_name not in row.get("Kernel_Name", ""):
+                        continue
+                    vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+            if "FETCH_SIZE" in vals:
+                fetch = float(np.mean(vals["FETCH_SIZE"]))
+            if "WRITE_SIZE" in vals:
+                write = float(np.mean(vals["WRITE_SIZE"]))
+        if fetch is not None and write is not None:
+            return (2.0 * fetch + write) * 1024.0  # counters are in KiB
+    return None
+
+
+# --------------------------------------------------------------------------- timing helpers
+def timed(fn, dist, dev):
+    """fn() bracketed by barrier + synchronize on both sides; max over ranks."""
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def single_fit(c, args, dev, rank, nbatch=32):
+    """One independent fit: model, optimizers, device-resident batches; returns the engine,
+    a plan factory for n steps starting at batch `start` (built outside any timed region)."""
+    import redcliff_amd
+    B = c["B"]
+    model = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=rank).to(dev)
+    oA, oB = adam_pair(model, c)
+    X, Y = synth(c, nbatch * B, seed=100 + rank)
+    eng = model.engine()
+    ds = eng.cache_dataset([(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)])
+    d = eng.workspace(ds["Bmax"], ds["T"])
+
+    def plan(nsteps, start):
+        idx = (np.arange(nsteps) + start) % nbatch
+        stats = ds["stats"][torch.as_tensor(idx, device=dev)].contiguous()
+        return eng.plan_steps("combined", ds["X"], ds["lab"], stats, d, ds["rows"][idx], ds["sizes"][idx], oA, oB)
+
+    return eng, plan
+
+
+def kernel_times_of(run):
+    from redcliff_amd import _native as nat
+    nat.kernel_timing(True)
+    run()
+    torch.cuda.synchronize()
+    kt = nat.kernel_times()
+    nat.kernel_timing(False)
+    return dict((k, (ms / n if n else 0.0, n)) for k, (ms, n) in kt.items())
 
 
 def run_grid(c, args, dev, rank, dist):
@@ -179,10 +252,9 @@ def run_grid(c, args, dev, rank, dist):
     R = args.replicas
     models, opts = [], []
     for i in range(R):
-        m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=1000 * rank + i).to(dev)
+        m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=1000 * rank + i,
+                        forecast=(10.0, 1.0)[i % 2], adj=(0.1, 0.01)[(i // 2) % 2]).to(dev)
         # vary what the reference grid varies (train/...gsSmooth1.py:278-309): lrs and coefficients
-        m.FORECAST_COEFF = (10.0, 1.0)[i % 2]
-        m.ADJ_L1_REG_COEFF = (0.1, 0.01)[(i // 2) % 2] / K / np.sqrt(p * p - 1.0)
         cc = dict(c, lrA=(5e-4, 1e-4)[(i // 4) % 2], lrB=(5e-4, 1e-4)[(i // 8) % 2])
         models.append(m)
         opts.append(adam_pair(m, cc))
@@ -193,26 +265,178 @@ def run_grid(c, args, dev, rank, dist):
 
     def steps(n, start):
         idx = (np.arange(n) + start) % nbatch
-        pack.run_steps(["combined"], ds, ds["rows"][idx], ds["sizes"][idx],
-                       ds["stats"][torch.as_tensor(idx, device=dev)].contiguous())
+        st = ds["stats"][torch.as_tensor(idx, device=dev)].contiguous()
+        return lambda: pack.run_steps(["combined"], ds, ds["rows"][idx], ds["sizes"][idx], st)
 
-    steps(5, 0)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    steps(args.grid_steps, 5)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    steps(5, 0)()
+    el = timed(steps(args.grid_steps, 5), dist, dev)
     return el, R, steps
+
+
+def fits_per_hour(c, args, dev, rank, dist, world):
+    """Whole grid-search fits (the reference's unit of work: one SLURM task = one fit,
+    train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:125-160) packed R per GPU:
+    ReplicaPack.fit over a fixed-epoch schedule (pretrain, acclimation, combined epochs;
+    per-epoch GC tracking, validation and best-model bookkeeping per replica)."""
+    import redcliff_amd
+    R, E = args.fit_replicas, args.fit_epochs
+    pre, acc = max(1, E // 5), max(1, E // 10)
+    ntr, nva = args.fit_train_batches, 2
+    models, opts = [], []
+    for i in range(R):
+        m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=5000 * rank + i, pre=pre, acc=acc,
+                        forecast=(10.0, 1.0)[i % 2], adj=(0.1, 0.01)[(i // 2) % 2]).to(dev)
+        models.append(m)
+        opts.append(adam_pair(m, dict(c, lrA=(5e-4, 2e-4)[(i // 4) % 2], lrB=(5e-4, 1e-4)[(i // 8) % 2])))
+    X, Y = synth(c, (ntr + nva) * c["B"], seed=300 + rank)
+    B = c["B"]
+    train = [(X[i:i + B], Y[i:i + B]) for i in range(0, ntr * B, B)]
+    val = [(X[i:i + B], Y[i:i + B]) for i in range(ntr * B, (ntr + nva) * B, B)]
+    rng = np.random.RandomState(7)
+    true_gc = [(rng.rand(c["p"], c["p"], c["L"]) < 0.2).astype(np.float64) for _ in range(c["K"])]
+    pack = redcliff_amd.ReplicaPack(models, opts)
+
+    def fit():
+        pack.fit(None, train, val, max_iter=E, lookback=10 ** 6, check_every=10 ** 6, GC=true_gc)
+
+    el = timed(fit, dist, dev)
+    return {"replicas_per_gpu": R, "epochs_per_fit": E, "train_windows": ntr * B, "val_windows": nva * B,
+            "seconds": round(el, 3), "value": round(world * R * 3600.0 / el, 1), "unit": "fits/hour",
+            "note": "fixed-epoch D4IC-shaped fits (%d pretrain, %d acclimation, %d combined epochs), early stopping "
+                    "disabled so every fit does the same work; per-epoch GC tracking + validation on the GPU"
+                    % (pre, acc, E - pre - acc)}
+
+
+# --------------------------------------------------------------------------- modes
+def mode_fit(args, dev, rank, world, dist):
+    from redcliff_amd import _native as nat  # noqa: F401
+    c = CONFIGS[args.config]
+    B = c["B"]
+    eng, plan = single_fit(c, args, dev, rank)
+    plan(args.warmup, 0).run()
+    p_timed = plan(args.steps, args.warmup)
+    elapsed = timed(p_timed.run, dist, dev)
+    value = world * args.steps * B / elapsed
+
+    out = {"metric": METRIC, "value": round(value, 1), "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (D4IC/sVAR-shaped windows; datasets not in image)",
+           "config": {"workload": c["workload"], "global_batch": B * world, "windows_per_step_per_gpu": B,
+                      "parallelism": "replicas%d (one independent fit per GPU, no collective)" % world,
+                      "ranks": world, "flops_per_window": flops_per_window(c)["total"]}}
+
+    ktimes = None if args.no_kernel_times else kernel_times_of(plan(min(args.steps, 100), 7).run)
+
+    grid = None
+    if args.replicas > 1:
+        gel, R, gsteps = run_grid(c, args, dev, rank, dist)
+        gv = world * R * args.grid_steps * B / gel
+        grid = {"replicas_per_gpu": R, "steps": args.grid_steps, "windows_per_s": round(gv, 1),
+                "ms_per_step": round(1e3 * gel / args.grid_steps, 4), "speedup_vs_single_fit": round(gv / value, 2),
+                "note": "R independent fits (grid points) per GPU, each B=%d windows per step; one launch per kernel "
+                        "for all R" % B}
+        if not args.no_kernel_times:
+            gkt = kernel_times_of(gsteps(min(args.grid_steps, 20), 3))
+            grid["roofline"] = roofline_of(gkt, flops_per_window(c), R * B, "%s_r%d" % (args.config, R))
+    fph = None
+    if args.fit_replicas > 0:
+        fph = fits_per_hour(c, args, dev, rank, dist, world)
+
+    ns = None
+    if world == 1 and not args.no_north_star and args.config != "c1k4":
+        cn = CONFIGS["c1k4"]
+        _, nplan = single_fit(cn, args, dev, rank)
+        nplan(args.warmup, 0).run()
+        nsteps = max(args.steps, 50)
+        nel = timed(nplan(nsteps, args.warmup).run, None, dev)
+        ns = {"workload": cn["workload"], "windows_per_s": round(nsteps * cn["B"] / nel, 1),
+              "ms_per_step": round(1e3 * nel / nsteps, 4), "steps": nsteps, "target_gpu_over_cpu": 50.0}
+
+    if rank != 0:
+        return None
+    if ktimes:
+        out["roofline"] = roofline_of(ktimes, flops_per_window(c), B, args.config)
+    out["grid_search"] = grid
+    out["fits_per_hour"] = fph
+    if not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds)
+        out["gpu_over_cpu"] = round(value / world / out["cpu_baseline"]["value"], 1)
+        if ns is not None:
+            ns["cpu_baseline"] = cpu_baseline(CONFIGS["c1k4"], args.cpu_seconds * 2.0 / 3.0)
+            ns["gpu_over_cpu"] = round(ns["windows_per_s"] / ns["cpu_baseline"]["value"], 1)
+    out["north_star_config"] = ns
+    return out
+
+
+def mode_dp(args, dev, rank, world, dist):
+    """BASELINE configs[3]: one TST-shaped fit sharded over the ranks (DataParallelFit)."""
+    import redcliff_amd
+    from redcliff_amd.data_parallel import DataParallelFit
+    c = dict(CONFIGS["c4"], B=args.dp_batch)
+    B = c["B"]
+    model = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).to(dev)
+    oA, oB = adam_pair(model, c)
+    nbatch = 16
+    X, Y = synth(c, nbatch * B, seed=100)  # every rank holds the whole (identical) data set
+    dp = DataParallelFit(model, oA, oB)
+    ds = dp.cache_dataset([(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)])
+    epoch = model.num_pretrain_epochs + model.num_acclimation_epochs  # combined phase
+
+    def run(n, start):
+        return lambda: [dp._step("combined", ds, (start + i) % nbatch) for i in range(n)]
+
+    run(args.warmup, 0)()
+    elapsed = timed(run(args.steps, args.warmup), dist, dev)
+    del epoch
+    if rank != 0:
+        return None
+    value = args.steps * B / elapsed
+    return {"metric": METRIC, "value": round(value, 1), "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (TST/LFP-shaped windows; recordings not in image)",
+            "config": {"workload": c["workload"].replace("B=128", "global B=%d" % B), "global_batch": B,
+                       "windows_per_step_per_gpu": B / world, "ranks": world,
+                       "parallelism": "dp%d (RCCL all-reduce of %d gradient floats per update)"
+                                      % (world, dp.PA + dp.PB)}}
+
+
+def mode_plumbing(args, rank, world, dist):
+    """No GPU visible (the build container): check the rank plumbing only -- launch, backend,
+    world size, barrier-bracketed timing with the max over ranks.  No throughput is claimed."""
+    if dist:
+        dist.barrier()
+        t = torch.tensor([1.0])
+        dist.all_reduce(t)
+        assert int(t.item()) == world
+    if rank != 0:
+        return None
+    return {"metric": METRIC, "value": None, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True,
+            "scaling": "strong" if args.mode == "dp" else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "none: no GPU visible, rank plumbing check only (backend %s)" % ("gloo" if dist else "none"),
+            "config": {"workload": CONFIGS["c4" if args.mode == "dp" else args.config]["workload"], "ranks": world,
+                       "parallelism": ("dp%d" if args.mode == "dp" else "replicas%d") % world}}
+
+
+# --------------------------------------------------------------------------- launch
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """Start n ranks of this script through torch.distributed.run (127.0.0.1), before any GPU
+    call in this process, and return their exit status."""
+    argv = [a for a in sys.argv[1:]]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -220,122 +444,58 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--mode", default="fit", choices=("fit", "dp"))
     ap.add_argument("--config", default="d4ic", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-times", action="store_true")
+    ap.add_argument("--no-north-star", action="store_true")
     ap.add_argument("--replicas", type=int, default=32, help="grid-search replicas packed per GPU (1: skip)")
     ap.add_argument("--grid-steps", type=int, default=100)
+    ap.add_argument("--fit-replicas", type=int, default=32, help="packed whole fits for fits/hour (0: skip)")
+    ap.add_argument("--fit-epochs", type=int, default=40)
+    ap.add_argument("--fit-train-batches", type=int, default=8)
+    ap.add_argument("--dp-batch", type=int, default=128, help="global batch of --mode dp")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cuda = torch.cuda.is_available()
     dist = None
-    if world > 1:
+    if world > 1 or args.mode == "dp":
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        backend = "nccl" if cuda else "gloo"  # nccl is RCCL on ROCm; gloo only for the CPU plumbing check
+        if cuda:
+            torch.cuda.set_device(local)
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            dist.init_process_group(backend, rank=0, world_size=1)
+        else:
+            dist.init_process_group(backend)
+        seen = dist.get_world_size()
+        if seen != world or (args.gpus > 1 and seen != args.gpus):
+            raise SystemExit("%s world size %d != --gpus %d / WORLD_SIZE %d" % (backend, seen, args.gpus, world))
+        world = seen
+    if not cuda:
+        out = mode_plumbing(args, rank, world, dist)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     if world == 1:
         import __graft_entry__
         __graft_entry__.build()  # no-op when the in-tree library is up to date
-    import redcliff_amd
-    from redcliff_amd import _native as nat
-
-    c = CONFIGS[args.config]
-    B = c["B"]
-    # independent fit per rank (grid-search replica): its own seed and its own data
-    model = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=rank).to(dev)
-    oA, oB = adam_pair(model, c)
-    nbatch = 32
-    X, Y = synth(c, nbatch * B, seed=100 + rank)
-    loader = [(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)]
-    eng = model.engine()
-    ds = eng.cache_dataset(loader)
-    d = eng.workspace(ds["Bmax"], ds["T"])
-
-    def run(nsteps, start):
-        idx = (np.arange(nsteps) + start) % nbatch
-        stats = ds["stats"][torch.as_tensor(idx, device=dev)].contiguous()
-        eng.run_steps(["combined"], ds["X"], ds["lab"], stats, d, ds["rows"][idx], ds["sizes"][idx], oA, oB)
-
-    run(args.warmup, 0)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps, args.warmup)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    windows = world * args.steps * B
-    value = windows / elapsed
-
-    # grid-search replicas packed into one launch: R fits of the same shape
-    # with different seeds / coefficients / learning rates, stepped together on this GPU
-    grid = None
-    if args.replicas > 1:
-        grid_elapsed, R, grid_steps_fn = run_grid(c, args, dev, rank, dist)
-        gsteps = args.grid_steps
-        grid = {"replicas_per_gpu": R, "steps": gsteps,
-                "windows_per_s": round(world * R * gsteps * B / grid_elapsed, 1),
-                "ms_per_step": round(1e3 * grid_elapsed / gsteps, 4),
-                "speedup_vs_single_fit": round((world * R * gsteps * B / grid_elapsed) / value, 2),
-                "note": "R independent fits (grid points) per GPU, each B=%d windows per step; one launch per kernel "
-                        "for all R" % B}
-
-    # per-kernel device time over the same kind of steps (HIP events on the launch stream)
-    ktimes = None
-    if not args.no_kernel_times:
-        nat.kernel_timing(True)
-        nk = min(args.steps, 100)
-        run(nk, 7)
-        torch.cuda.synchronize()
-        kt = nat.kernel_times()
-        nat.kernel_timing(False)
-        ktimes = dict((k, (ms / n if n else 0.0, n)) for k, (ms, n) in kt.items())
-
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
-    fl = flops_per_window(c)
-    roof = roofline_of(ktimes, fl, B, args.config == PMC_CONFIG) if ktimes else None
-    if grid is not None and not args.no_kernel_times:
-        # the same kernel-level roofline for the packed launch: one launch carries R * B windows
-        nat.kernel_timing(True)
-        grid_steps_fn(min(args.grid_steps, 20), 3)
-        torch.cuda.synchronize()
-        gkt = nat.kernel_times()
-        nat.kernel_timing(False)
-        gkt = dict((k, (ms / n if n else 0.0, n)) for k, (ms, n) in gkt.items())
-        grid["roofline"] = roofline_of(gkt, flops_per_window(c), grid["replicas_per_gpu"] * B, False)
-    cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(c, args.cpu_seconds)
-    out = {
-        "metric": "cMLP-factor fwd+bwd windows/sec/GPU; grid-search fits/hour on 8 GPUs",
-        "value": round(value, 1), "unit": "windows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic (D4IC/sVAR-shaped windows; datasets not in image)",
-        "config": {"workload": c["workload"], "global_batch": B * world, "windows_per_step_per_gpu": B,
-                   "parallelism": "replicas%d (one independent fit per GPU, no collective)" % world,
-                   "flops_per_window": fl["total"]},
-        "roofline": roof, "cpu_baseline": cpu, "grid_search": grid,
-    }
-    if cpu:
-        out["gpu_over_cpu"] = round(value / world / cpu["value"], 1)
-    print(json.dumps(out), flush=True)
+    out = (mode_dp if args.mode == "dp" else mode_fit)(args, dev, rank, world, dist)
+    if out is not None:
+        print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 3
+#define REDCLIFF_ABI_VERSION 4
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -123,6 +123,14 @@ typedef struct RedcliffStepArgs {
   int32_t B_global;
   int32_t pad_;
   float* grad_emb; float* grad_fac;  /* RC_GRAD_ONLY outputs, same layout/stride as emb / fac */
+  /* Packed grid-search fits (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:125-160,
+   * one fit per grid point): the replicas this call steps, a strictly increasing HOST array of
+   * n_replicas indices < R (at most 256).  A replica that stopped early (the per-fit rule of
+   * ...withStateSmoothing.py:1483-1559) is left out: its parameters, Adam state, BatchNorm
+   * statistics and accumulators are not touched and its workgroups are not launched.
+   * NULL = all R replicas.  n_replicas == 0 launches nothing. */
+  const int32_t* replicas; int32_t n_replicas;
+  int32_t pad2_;
 } RedcliffStepArgs;
 
 int redcliff_abi_version(void);

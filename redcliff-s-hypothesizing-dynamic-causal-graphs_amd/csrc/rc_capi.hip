@@ -220,6 +220,25 @@ static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
     return REDCLIFF_EINVAL;
   }
   memset(&c, 0, sizeof(c));
+  if (a->replicas) {
+    if (a->n_replicas < 0 || a->n_replicas > RC_MAX_ACTIVE || a->n_replicas > d.R) {
+      rc_set_error("active replica list of %d entries (at most min(R=%d, %d))", a->n_replicas, d.R, RC_MAX_ACTIVE);
+      return REDCLIFF_ELIMIT;
+    }
+    for (int i = 0; i < a->n_replicas; ++i) {
+      const int r = a->replicas[i];
+      if (r < 0 || r >= d.R || (i > 0 && r <= a->replicas[i - 1])) {
+        rc_set_error("active replica list must be strictly increasing indices < R=%d (entry %d = %d)", d.R, i, r);
+        return REDCLIFF_EINVAL;
+      }
+      c.rmap[i] = (uint8_t)r;
+    }
+    c.nrep = a->n_replicas;
+    c.rident = 0;
+  } else {
+    c.nrep = d.R;
+    c.rident = 1;
+  }
   c.d = d;
   c.B = a->B;
   c.Bg = a->B_global ? a->B_global : a->B;
@@ -254,6 +273,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   StepCtx c;
   int e = make_ctx(a, c);
   if (e) return e;
+  if (c.nrep == 0) return 0;  // every replica of the pack has stopped
   hipStream_t s = (hipStream_t)stream;
   const int fl = a->flags;
   const bool emb_grad = fl & RC_STEP_A;

@@ -8,6 +8,7 @@
 #define RC_TRACE_FLOATS 32768  // trace builds: u64 timing slots at the end of the workspace (8 kernels x 2048)
 #define RC_LDS_LIMIT_FLOATS 16384  // 64 KiB of dynamic LDS per workgroup (several workgroups per CU)
 #define RC_LDS_MAX_FLOATS 40960    // 160 KiB: the whole CU's LDS, used only when a tile needs it (large p)
+#define RC_MAX_ACTIVE 256          // longest active-replica list of one launch (RedcliffStepArgs.replicas)
 
 // Offsets (in floats) inside one replica's packed embedder parameters.
 struct EmbOff {
@@ -234,7 +235,15 @@ struct StepCtx {
   EmbOff eo;
   FacOff fo;
   WsOff wo;
+  // replicas this launch processes: grid index i (blockIdx.y / .z) -> replica rc_rep(c, i).
+  // rident: all R in order; else the active list of a packed fit whose stopped replicas
+  // (early stopping, ...withStateSmoothing.py:1483-1559) drop out of every grid.
+  int nrep, rident;
+  uint8_t rmap[RC_MAX_ACTIVE];
 };
+
+__host__ __device__ inline int rc_rep(const StepCtx& c, int i) { return c.rident ? i : (int)c.rmap[i]; }
+inline int rc_rep_host(const StepCtx& c, int i) { return rc_rep(c, i); }
 
 // ---------------------------------------------------------------------------------------------
 // Workgroup timing (trace builds, -DRC_TRACE): thread 0 of workgroup x < 1024 of replica 0

@@ -76,7 +76,7 @@ __device__ inline float draw_value(const StepCtx& c, int r, int k, float raw, fl
 // LDS and one thread per pair combines the four waves in order.
 __global__ __launch_bounds__(RC_BLOCK) void k_cos_values(StepCtx c) {
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, b = blockIdx.x, K = d.K, p = d.p, pp2 = p * p;
+  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x, K = d.K, p = d.p, pp2 = p * p;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* G0 = ws + c.wo.G0;
@@ -605,7 +605,7 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
 // grid (ceil(pstride / RC_BLOCK), p * nchunk, R).
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
   const RedcliffDims& d = c.d;
-  const int grp = blockIdx.y, r = blockIdx.z, e = blockIdx.x * RC_BLOCK + threadIdx.x;
+  const int grp = blockIdx.y, r = rc_rep(c, blockIdx.z), e = blockIdx.x * RC_BLOCK + threadIdx.x;
   const int p = d.p, n = d.n, F = d.F, H = d.H, M1 = d.M1, HC = EMB_HC;
   const int nch = rc_nchunk(d), node = grp / nch, ch = grp - node * nch;
   const int pst = rc_emb_pstride(d), nbwm = rc_emb_nbw(d), wpb = rc_emb_wpb(d), nbw = (c.B + wpb - 1) / wpb;
@@ -657,7 +657,7 @@ __device__ void emb_bwd_dadj(const StepCtx& c, int r, int blk) {
 template <bool MULTI>
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   extern __shared__ float sm[];
-  const int r = blockIdx.y;
+  const int r = rc_rep(c, blockIdx.y);
   const int nch = rc_nchunk(c.d);
   const int nbw = (c.B + WPB - 1) / WPB;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
@@ -830,7 +830,7 @@ template <int NR>
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y;
+  const int r = rc_rep(c, blockIdx.y);
   const int p = d.p, n = d.n, F = d.F, H = d.H, K = d.K, M1 = d.M1;
   float* E = c.emb + r * c.es;
   float* Mm = c.embM + r * c.es;
@@ -1111,25 +1111,25 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   if (WPB > BC) {
     int e = rc_lds_optin(k_emb_bwd<true>, lds, "k_emb_bwd LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_bwd<true>, dim3(nnode + head + nred, d.R), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
+    hipLaunchKernelGGL(k_emb_bwd<true>, dim3(nnode + head + nred, c.nrep), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
   } else {
     int e = rc_lds_optin(k_emb_bwd<false>, lds, "k_emb_bwd LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head + nred, d.R), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
+    hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head + nred, c.nrep), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
   }
   return rc_check(hipGetLastError(), "k_emb_bwd");
 }
 
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {
   if (c.d.K < 2 || !(c.flags & RC_VALUES)) return 0;
-  hipLaunchKernelGGL(k_cos_values, dim3(c.B, c.d.R), dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_cos_values, dim3(c.B, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_cos_values");
 }
 
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int pst = rc_emb_pstride(d);
-  hipLaunchKernelGGL(k_emb_combine, dim3((pst + RC_BLOCK - 1) / RC_BLOCK, d.p * rc_nchunk(d), d.R), dim3(RC_BLOCK), 0,
+  hipLaunchKernelGGL(k_emb_combine, dim3((pst + RC_BLOCK - 1) / RC_BLOCK, d.p * rc_nchunk(d), c.nrep), dim3(RC_BLOCK), 0,
                      s, c);
   return rc_check(hipGetLastError(), "k_emb_combine");
 }
@@ -1143,11 +1143,11 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   if (d.p * d.p <= 4 * RC_BLOCK) {
     int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + 1, d.R), dim3(RC_BLOCK), lds, s, c, nw);
+    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw);
   } else {
     int e = rc_lds_optin(k_emb_final<16>, lds, "k_emb_final LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, d.R), dim3(RC_BLOCK), lds, s, c, nw);
+    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw);
   }
   return rc_check(hipGetLastError(), "k_emb_final");
 }

@@ -31,7 +31,7 @@ __host__ __device__ inline int lemb_wpw(const RedcliffDims& d) { return 64 / d.K
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, b = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x;
   const int p = d.p, F = d.F, n = d.n;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, b = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x;
   const int M1 = d.M1, K = d.K;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
@@ -142,7 +142,7 @@ __device__ inline float lemb_draw(const StepCtx& c, int r, int k, float raw, flo
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y;
+  const int r = rc_rep(c, blockIdx.y);
   const int K = d.K, M1 = d.M1, p = d.p, B = c.B;
   const int WPW = lemb_wpw(d), b0 = blockIdx.x * WPW;
   const float* E = c.emb + r * c.es;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_gfc(StepCtx c, int ngfc) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, K = d.K, M1 = d.M1, B = c.B, p = d.p, n = d.n;
+  const int r = rc_rep(c, blockIdx.y), K = d.K, M1 = d.M1, B = c.B, p = d.p, n = d.n;
   float* ws = c.ws + r * c.wss;
   const int tid = threadIdx.x;
   if ((int)blockIdx.x >= ngfc) {
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_gfc(StepCtx c, int ngfc) {
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, s = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y), s = blockIdx.x;
   const int p = d.p, F = d.F;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -278,7 +278,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dsred(StepCtx c, int nds) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, p = d.p, n = d.n;
+  const int r = rc_rep(c, blockIdx.y), p = d.p, n = d.n;
   const int64_t pp2 = (int64_t)p * p;
   const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
   if (e >= (n - 1) * pp2) return;
@@ -340,10 +340,11 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F;
   if (F > 64 || M1 > 64) { rc_set_error("GEMM embedder: F <= 64 and M1 <= 64 required"); return REDCLIFF_ELIMIT; }
-  hipLaunchKernelGGL(k_lemb_prep, dim3(B, d.R), dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_lemb_prep, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_lemb_prep");
   const int nsp = fc1_splits(d), Ks = p * H / nsp;
-  for (int r = 0; r < d.R && !e; ++r) {
+  for (int i = 0; i < c.nrep && !e; ++i) {
+    const int r = rc_rep_host(c, i);
     float* ws = c.ws + r * c.wss;
     const float* E = c.emb + r * c.es;
     float* T = ws + c.wo.T;
@@ -361,7 +362,7 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
                                     ws + c.wo.f1p, M1, (int64_t)d.Bmax * M1), nsp, s, "emb fc1");
   }
   if (e) return e;
-  hipLaunchKernelGGL(k_lemb_head, dim3(B, d.R), dim3(RC_BLOCK), 0, s, c, nsp);
+  hipLaunchKernelGGL(k_lemb_head, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
   return rc_check(hipGetLastError(), "k_lemb_head");
 }
 
@@ -369,15 +370,16 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F, pH = (int64_t)p * H;
-  hipLaunchKernelGGL(k_lemb_dhead, dim3((B + lemb_wpw(d) - 1) / lemb_wpw(d), d.R), dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_lemb_dhead, dim3((B + lemb_wpw(d) - 1) / lemb_wpw(d), c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_lemb_dhead");
   if (!e) {
     const int ngfc = (d.K * M1 + d.K + M1 + 63) / 64, naf = (p * p * n + RC_BLOCK - 1) / RC_BLOCK;
-    hipLaunchKernelGGL(k_lemb_gfc, dim3(ngfc + naf, d.R), dim3(RC_BLOCK), 0, s, c, ngfc);
+    hipLaunchKernelGGL(k_lemb_gfc, dim3(ngfc + naf, c.nrep), dim3(RC_BLOCK), 0, s, c, ngfc);
     e = rc_check(hipGetLastError(), "k_lemb_gfc");
   }
   const int nds = ds_splits(B), wps = B / nds;
-  for (int r = 0; r < d.R && !e; ++r) {
+  for (int i = 0; i < c.nrep && !e; ++i) {
+    const int r = rc_rep_host(c, i);
     float* ws = c.ws + r * c.wss;
     const float* E = c.emb + r * c.es;
     const float* T = ws + c.wo.T;
@@ -417,9 +419,9 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
   if (e) return e;
   const int ndr = (int)(((int64_t)(n - 1) * p * p + RC_BLOCK - 1) / RC_BLOCK);
   if (n > 1) {
-    hipLaunchKernelGGL(k_lemb_dsred, dim3(ndr, d.R), dim3(RC_BLOCK), 0, s, c, nds);
+    hipLaunchKernelGGL(k_lemb_dsred, dim3(ndr, c.nrep), dim3(RC_BLOCK), 0, s, c, nds);
     if ((e = rc_check(hipGetLastError(), "k_lemb_dsred"))) return e;
   }
-  hipLaunchKernelGGL(k_lemb_bn, dim3(c.dgN, d.R), dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_lemb_bn, dim3(c.dgN, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_lemb_bn");
 }

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   // nUl x nQ workgroups per network (1 x 1 when there is no factor update)
   const RedcliffDims& d = c.d;
   const int nU = rc_nuchunk(d);
-  const int r = blockIdx.y;
+  const int r = rc_rep(c, blockIdx.y);
   const int kj = blockIdx.x / (nUl * nQ);
   const int rem0 = blockIdx.x - kj * nUl * nQ;
   const int uc = rem0 / nQ, qc = rem0 - uc * nQ;
@@ -397,7 +397,7 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   // without a factor update only the lead workgroup of each network has work
   const int nUl = (c.flags & RC_STEP_B) ? rc_nuchunk(d) : 1;
-  hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, d.R), dim3(RC_BLOCK), lds, s, c, nUl, nQ);
+  hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ);
   return rc_check(hipGetLastError(), "k_fac_bwd");
 }
 
@@ -412,6 +412,8 @@ extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const f
   if (d->p > 64 || d->h > 128 || d->L > 64) { rc_set_error("factor_forward: dims outside kernel limits"); return REDCLIFF_ELIMIT; }
   StepCtx c;
   memset(&c, 0, sizeof(c));
+  c.nrep = d->R;
+  c.rident = 1;
   c.d = *d;
   c.d.Bmax = B;
   c.d.T = d->L;

@@ -33,7 +33,7 @@ __device__ inline float4 ld4(const float* p) { return *reinterpret_cast<const fl
 // Window transpose: Xw[b][c*L + t] = X[row0 + b][Lmax - L + t][c], zero-padded to Qp columns.
 // grid (B, R); reads one contiguous L*p window, writes one Xw row.
 __global__ __launch_bounds__(RC_BLOCK) void k_xwin(StepCtx c) {
-  const int r = blockIdx.y, b = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x;
   const RedcliffDims& d = c.d;
   const int L = d.L, p = d.p, Q = p * L, Qp = rc_qpad(d);
   const float* src = c.X + r * c.xr + ((c.row0 + b) * d.T + (c.Lmax - L)) * p;
@@ -61,7 +61,7 @@ __device__ inline int mf_nub(const RedcliffDims& d) { return (d.h + 31) / 32; }
 
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.z;
+  const int r = rc_rep(c, blockIdx.z);
   const int cb0 = blockIdx.x * 2, b0 = blockIdx.y * MF_BT;
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p, nUB = mf_nub(d);
   const int NB = KP * nUB;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
 //   output-layer / hidden-bias gradients + Adam (b0, W1, b1).
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y, kj = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y), kj = blockIdx.x;
   const int p = d.p, h = d.h, K = d.K, L = d.L, Q = p * L, B = c.B;
   const int k = kj / p, j = kj - k * p;
   float* P = c.fac + r * c.fs;
@@ -382,7 +382,7 @@ template <int NBW>
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
   constexpr int QT = 256 / NBW, Q4 = QT / 4;
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.z;
+  const int r = rc_rep(c, blockIdx.z);
   const int cb0 = blockIdx.x * NBW, q0 = blockIdx.y * QT;
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), KP = K * p, B = c.B, nUB = mf_nub(d);
   const int NB = KP * nUB;
@@ -542,11 +542,11 @@ bool rc_fac_use_mfma(const RedcliffDims& d) {
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int KP = d.K * d.p;
-  hipLaunchKernelGGL(k_xwin, dim3(c.B, d.R), dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_xwin, dim3(c.B, c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_xwin");
   if (e) return e;
   const int NB = KP * ((d.h + 31) / 32);
-  hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, d.R), dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_fwd_mfma");
 }
 
@@ -555,7 +555,7 @@ int rc_launch_fac_mix(const StepCtx& c, hipStream_t s) {
   const int KP = d.K * d.p;
   const size_t lds = fac_mix_lds(d, c.Ls);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor mixing: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  hipLaunchKernelGGL(k_fac_mix, dim3(KP, d.R), dim3(RC_BLOCK), lds, s, c);
+  hipLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c);
   return rc_check(hipGetLastError(), "k_fac_mix");
 }
 
@@ -564,8 +564,8 @@ int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s) {
   if (!(c.flags & RC_STEP_B)) return 0;
   const int NB = d.K * d.p * ((d.h + 31) / 32), Q = d.p * d.L;
   if (Q <= 64)  // short contraction rows: four column blocks share one 64-column X tile
-    hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, d.R), dim3(RC_BLOCK), 0, s, c);
+    hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
   else
-    hipLaunchKernelGGL(k_fac_bwd_mfma<2>, dim3((NB + 1) / 2, (Q + 127) / 128, d.R), dim3(RC_BLOCK), 0, s, c);
+    hipLaunchKernelGGL(k_fac_bwd_mfma<2>, dim3((NB + 1) / 2, (Q + 127) / 128, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_bwd_mfma");
 }

@@ -28,7 +28,7 @@ __device__ inline int fq_tile(const RedcliffDims& d) { return d.p * d.L <= FQ_MA
 // Embedder forward of windows [bx*SB, bx*SB + SB).
 __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float* sm) {
   const RedcliffDims& d = c.d;
-  const int r = blockIdx.y;
+  const int r = rc_rep(c, blockIdx.y);
   const int b0 = bx * SB;
   const int nb = min(SB, c.B - b0);
   if (nb <= 0) return;
@@ -238,7 +238,7 @@ __device__ void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
   const RedcliffDims& d = c.d;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 0);
   const int nU = rc_nuchunk(d);
-  const int r = blockIdx.y, kj = bx / nU, uc = bx - kj * nU;
+  const int r = rc_rep(c, blockIdx.y), kj = bx / nU, uc = bx - kj * nU;
   const int p = d.p, h = d.h, K = d.K;
   const int k = kj / p, j = kj - k * p;
   const int Q = p * d.L, QT = fq_tile(d), QP = QT + 1;
@@ -370,7 +370,7 @@ int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_
   lds *= sizeof(float);
   int e = lds_optin(k_forward, lds, "k_forward LDS");
   if (e) return e;
-  hipLaunchKernelGGL(k_forward, dim3(nemb + nfac, d.R), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb);
+  hipLaunchKernelGGL(k_forward, dim3(nemb + nfac, c.nrep), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb);
   return rc_check(hipGetLastError(), "k_forward");
 }
 

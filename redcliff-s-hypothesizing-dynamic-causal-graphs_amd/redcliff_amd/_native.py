@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
@@ -68,7 +68,8 @@ class StepArgs(ctypes.Structure):
                 ("hyper", _vp),
                 ("ws", _vp), ("ws_bytes", ctypes.c_size_t),
                 ("acc", _vp), ("confusion", _vp),
-                ("B_global", ctypes.c_int32), ("pad_", ctypes.c_int32), ("grad_emb", _vp), ("grad_fac", _vp)]
+                ("B_global", ctypes.c_int32), ("pad_", ctypes.c_int32), ("grad_emb", _vp), ("grad_fac", _vp),
+                ("replicas", _vp), ("n_replicas", ctypes.c_int32), ("pad2_", ctypes.c_int32)]
 
 
 def adam_hyper(lr, betas, eps, weight_decay):

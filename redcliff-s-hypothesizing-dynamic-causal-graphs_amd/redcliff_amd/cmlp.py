@@ -23,7 +23,18 @@ class MLP(nn.Module):
         self.layers = nn.ModuleList([first] + [nn.Conv1d(a, b, 1) for a, b in zip(widths[:-1], widths[1:])])
 
     def forward(self, X):
-        # one network == a cMLP with a single channel output; route through the grouped kernel
+        """X (B, T, p) -> (B, T - lag + 1, 1) (models/cmlp.py:29-35).  Without gradients: the
+        grouped factor kernel (one network == a one-output cMLP); with gradients: the generic
+        HIP-GEMM path (a graph through redcliff_gemm)."""
+        from . import autograd as AG
+        params = [t for layer in self.layers for t in (layer.weight, layer.bias)]
+        if AG.grad_needed([X] + params):
+            from .generic import mlp_group
+            kernels.require_gpu(X, "MLP.forward")
+            L = self.layers[0].weight.shape[2]
+            B, T, p = X.shape
+            win = AG._windows(X.to(torch.float32), L)
+            return mlp_group([self], win).view(B, T - L + 1, 1)
         return kernels.single_network_forward(self, X)
 
 
@@ -42,8 +53,10 @@ class cMLP(nn.Module):
         self.networks = nn.ModuleList([MLP(self.num_series, lag, hidden) for _ in range(self.num_series)])
 
     def forward(self, X):
-        """X (batch, T, p) -> (batch, T - lag + 1, p) (models/cmlp.py:90-101)."""
-        return kernels.cmlp_forward([self], X)[0]
+        """X (batch, T, p) -> (batch, T - lag + 1, p) (models/cmlp.py:90-101); a graph tensor when
+        gradients are requested (fused kernel forward, HIP-GEMM backward: redcliff_amd.autograd)."""
+        from . import autograd as AG
+        return AG.cmlp_forward([self], X)[0]
 
     def perform_prox_update_on_GC_weights(self, lam, lr, penalty):
         """In-place GL / GSGL / H proximal step on layer-0 weights (models/cmlp.py:117-144)."""
@@ -53,6 +66,7 @@ class cMLP(nn.Module):
         """Group norms of layer-0 weights: (p, p) or (p, p, lag) (models/cmlp.py:147-203)."""
         if rank_wavelets:
             raise NotImplementedError("rank_wavelets needs wavelet_level != None")
-        G, G0 = kernels.cmlp_gc_norms([self])
+        from . import autograd as AG
+        G, G0 = AG.group_norms([self]) if not threshold else kernels.cmlp_gc_norms([self])
         out = G0[0] if ignore_lag else G[0]
         return (out > 0).int() if threshold else out

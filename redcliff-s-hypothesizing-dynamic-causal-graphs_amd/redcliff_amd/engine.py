@@ -103,6 +103,7 @@ class FitEngine:
         self.hyper_key = None
         self.hyper_dev = None
         self.supports_fresh = False
+        self._a_version = -1
         self.dataset_cache = {}
         self.pack = None  # ReplicaPack this fit belongs to (redcliff_amd.replicas), if any
         self.pack_index = None
@@ -349,7 +350,21 @@ class FitEngine:
         return ds
 
     # ------------------------------------------------------------------ step launch
+    def _fresh_state(self):
+        """Pick up changes made outside the kernels: an optimizer stepped by torch (its shared
+        step tensor moved) and an adjacency A modified by a torch op (A's version counter, shared
+        with the packed buffer it views, moved) -- the supports must then be rebuilt."""
+        for g in ("A", "B"):
+            st = self.opt[g]
+            if st is not None:
+                tv = int(float(st["step"]))
+                if tv != st["t"]:
+                    st["t"] = tv
+        if self.supports_fresh and self.dgcnn.A._version != self._a_version:
+            self.supports_fresh = False
+
     def _args(self, d, flags, nbn, X, lab, stats):
+        self._fresh_state()
         a = nat.StepArgs()
         a.d = d
         a.flags = flags | (0 if self.supports_fresh else nat.REFRESH_SUPPORTS)
@@ -377,8 +392,12 @@ class FitEngine:
         a.confusion = self.conf.data_ptr()
         return a
 
-    def _after(self, flags, nbn, nsteps):
+    def _mark_fresh(self):
         self.supports_fresh = True
+        self._a_version = self.dgcnn.A._version
+
+    def _after(self, flags, nbn, nsteps):
+        self._mark_fresh()
         if flags & nat.STEP_A:
             self.opt["A"]["t"] += nsteps
         if flags & nat.STEP_B:
@@ -428,7 +447,7 @@ class FitEngine:
         nat.check(nat.lib().redcliff_train_steps(ctypes.byref(a), len(rows_a), rows_a.ctypes.data_as(ctypes.c_void_p),
                                                  sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * self.F, _stream()),
                   "validate")
-        self.supports_fresh = True
+        self._mark_fresh()
         return self.acc.cpu().numpy(), self.conf.cpu().numpy().reshape(max(self.nsup, 1), max(self.nsup, 1))
 
     def forward_outputs(self, X, train_bn, bn_updates):
@@ -443,7 +462,7 @@ class FitEngine:
         a.B = B
         a.row0 = 0
         nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "forward")
-        self.supports_fresh = True
+        self._mark_fresh()
         if train_bn and bn_updates:
             self.dgcnn.BN1.num_batches_tracked.add_(bn_updates)
         o = self.ws_off
@@ -452,6 +471,21 @@ class FitEngine:
         y = self.ws[o["y"]:o["y"] + nU * d.Bmax * self.K * self.p].view(nU, d.Bmax, self.K, self.p)[:, :B].sum(0)
         xs = self.ws[o["xsim"]:o["xsim"] + B * self.p].view(B, self.p).clone()
         return w, y, xs
+
+    def embed_raw(self, X):
+        """Raw embedder outputs w (B, K) of windows X (B, T >= Lmax, p) with the BatchNorm running
+        statistics (eval mode): the embedder launch alone (no factor networks, no step)."""
+        self.ensure_bound()
+        X = X.to(self.device, torch.float32).contiguous()
+        B, T, _ = X.shape
+        d = self.workspace(B, T)
+        a = self._args(d, 0, 0, X, None, None)
+        a.B = B
+        a.row0 = 0
+        nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "embed")
+        self._mark_fresh()
+        o = self.ws_off
+        return self.ws[o["w"]:o["w"] + B * self.K].view(B, self.K).clone()
 
     def gc_norms(self):
         """(G (K,p,p,L), G0 (K,p,p)) of the current factor weights."""
@@ -491,6 +525,7 @@ class StepPlan:
 
     def run(self, stream=None):
         eng, a = self.eng, self.a
+        eng._fresh_state()
         stA, stB = eng.opt["A"], eng.opt["B"]
         a.tA = (stA["t"] + 1) if stA else 1
         a.tB = (stB["t"] + 1) if stB else 1

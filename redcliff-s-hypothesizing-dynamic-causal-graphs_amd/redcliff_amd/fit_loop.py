@@ -1,16 +1,19 @@
 """REDCLIFF-S ``fit`` (models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647) on the fused engine.
 
-Per epoch: one ``redcliff_train_steps`` call runs every batch of the (device-resident)
-training set; the embedder confusion matrix accumulates on the GPU; GC progress is
-tracked on the first validation batch (<= 40 windows, host metrics as in the reference);
-validation runs as one more kernel call; early stopping, best-model snapshots,
-checkpoints and ``restore_parameters`` follow the reference's rules, including its
-parity hazards:
+Per epoch: one prepared ``redcliff_train_steps`` call runs every batch of the (device-resident)
+training set; the embedder confusion matrix accumulates on the GPU; GC progress is tracked on
+the first validation batch (<= 40 windows: ONE embedder launch, the group norms, one
+broadcast, one metrics launch); validation runs as one more kernel call; early stopping,
+best-model snapshots, checkpoints and ``restore_parameters`` follow the reference's rules,
+including its parity hazards:
   * stopping is evaluated only after pretrain + acclimation epochs, with an equality test
     ``it - best_it == lookback * check_every``; before that best_model is refreshed every epoch;
   * GC tracking slices the SAMPLE list to num_supervised_factors;
   * restore_parameters restores parameters only (BatchNorm running statistics stay).
 The resume typo of the reference (redcliff_s_cmlp.py:1237) is not reproduced.
+
+The per-fit bookkeeping lives in ``FitTracker`` so that a packed grid search
+(``ReplicaPack.fit``, redcliff_amd.replicas) applies exactly the same rules to every replica.
 """
 import copy
 import os
@@ -25,6 +28,20 @@ from .engine import phase_of_epoch
 HIST_KEYS = ["avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
              "avg_fw_smoothing_penalty", "avg_adj_penalty", "avg_dagness_reg_loss", "avg_dagness_lag_loss",
              "avg_dagness_node_loss", "avg_combo_loss"]
+CM_KEYS = ("acc", "tpr", "tnr", "fpr", "fnr")
+
+
+def standalone_copy(model):
+    """deepcopy of `model` whose parameters and buffers are compact clones of their own values.
+    A packed replica's parameters are views of the pack's [R][...] storage (and a single fit's
+    of its engine's buffers); a plain deepcopy / torch.save would carry the whole storage."""
+    memo = {}
+    with torch.no_grad():
+        for prm in model.parameters():
+            memo[id(prm)] = torch.nn.Parameter(prm.detach().clone(), requires_grad=prm.requires_grad)
+        for buf in model.buffers():
+            memo[id(buf)] = buf.detach().clone()
+    return copy.deepcopy(model, memo)
 
 
 class ParamSnapshot:
@@ -34,15 +51,17 @@ class ParamSnapshot:
     costs more than the epoch's training steps.  ``materialize()`` builds the module the reference
     would hold (checkpoints); ``restore_into`` is restore_parameters (parameters only)."""
 
-    def __init__(self, model):
+    def __init__(self, model, emb=None, fac=None, bn=None):
         eng = model.engine()
         eng.ensure_bound()
         self.model = model
         with torch.no_grad():
-            self.emb = eng.emb.clone()
-            self.fac = eng.fac.clone()
-            bn = eng.dgcnn.BN1
-            self.bn = (bn.running_mean.clone(), bn.running_var.clone(), bn.num_batches_tracked.clone())
+            self.emb = eng.emb.clone() if emb is None else emb
+            self.fac = eng.fac.clone() if fac is None else fac
+            if bn is None:
+                b = eng.dgcnn.BN1
+                bn = (b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone())
+            self.bn = bn
 
     def _slices(self, model):
         """name -> (flat buffer, offset, numel) of every packed parameter of `model` (the fit's model)."""
@@ -65,7 +84,7 @@ class ParamSnapshot:
         eng.invalidate()  # A changed: the Chebyshev supports are recomputed before the next use
 
     def materialize(self):
-        m = copy.deepcopy(self.model)
+        m = standalone_copy(self.model)
         sl = self._slices(self.model)
         with torch.no_grad():
             for name, prm in m.named_parameters():
@@ -76,6 +95,15 @@ class ParamSnapshot:
             bn.running_var.copy_(self.bn[1])
             bn.num_batches_tracked.copy_(self.bn[2])
         return m
+
+
+def _compact_optimizer_state(opt):
+    """opt.state_dict() with every tensor cloned: the engine's Adam moments are views of its
+    (or a pack's) flat buffers, which must not be serialised whole."""
+    sd = opt.state_dict()
+    sd["state"] = dict((k, dict((kk, vv.detach().clone() if torch.is_tensor(vv) else vv) for kk, vv in v.items()))
+                       for k, v in sd["state"].items())
+    return sd
 
 
 def _best_model(model, fused):
@@ -100,6 +128,151 @@ def _confusion(cm):
     return _confusion_rates(cm)
 
 
+class FitTracker:
+    """Histories and stopping rule of ONE fit (...withStateSmoothing.py:1316-1559,
+    general_utils/model_utils.py:18-209 trackers).  Fed once per epoch with the train confusion
+    matrix, the GC-progress inputs and the validation values; decides improve / stop."""
+
+    def __init__(self, model, GC, deltaConEps, in_degree_coeff, out_degree_coeff, sc_forecast, sc_factor, sc_cos,
+                 lookback, check_every):
+        self.model = model
+        self.GC = GC
+        self.eps, self.cin, self.cout = deltaConEps, in_degree_coeff, out_degree_coeff
+        self.sc_forecast, self.sc_factor, self.sc_cos = sc_forecast, sc_factor, sc_cos
+        self.lookback, self.check_every = lookback, check_every
+        nsup, K, p = model.num_supervised_factors, model.num_factors_nK, model.num_chans
+        self.nsup, self.K, self.p = nsup, K, p
+        thresholds = [0.0]
+        self.h = dict((k, []) for k in HIST_KEYS)
+        self.f1_hist = {t: [[] for _ in range(nsup)] for t in thresholds}
+        self.f1_off = {t: [[] for _ in range(nsup)] for t in thresholds}
+        self.roc_hist = {t: [[] for _ in range(nsup)] for t in thresholds}
+        self.roc_off = {t: [[] for _ in range(nsup)] for t in thresholds}
+        self.cm_train = dict((k, []) for k in CM_KEYS)
+        self.cm_val = dict((k, []) for k in CM_KEYS)
+        self.l1_hist = [[] for _ in range(nsup)]
+        self.cos_hist = {"%dand%d" % (i, j): [] for i in range(nsup) for j in range(nsup) if i < j}
+        self.cos_unsup = {"%dand%d" % (i, j): [] for i in range(nsup, K) for j in range(nsup, K) if i < j}
+        self.dc_hist = [[] for _ in range(nsup)]
+        self.dcdd_hist = [[] for _ in range(nsup)]
+        self.daff_hist = [[] for _ in range(nsup)]
+        self.plm_hist = {pl: [[] for _ in range(nsup)] for pl in range(1, p)}
+        self.best_it, self.best_loss, self.best_model, self.iter_start = None, np.inf, None, 0
+        self.stopped_at = None
+
+    def resume(self, fused):
+        """resume_training_from_checkpoint was called (...withStateSmoothing.py:1229-1277)."""
+        m = self.model
+        if not hasattr(m, "chkpt_best_it"):
+            return 0
+        self.best_model = _best_model(m, fused)
+        self.iter_start = m.chkpt_best_it + 1
+        for k in HIST_KEYS:
+            self.h[k] = list(getattr(m, "chkpt_" + k))[:self.iter_start]
+        self.best_loss, self.best_it = m.chkpt_best_loss, m.chkpt_best_it
+        return self.iter_start
+
+    def train_confusion(self, cm):
+        if self.nsup > 0:
+            TPR, TNR, FPR, FNR, ACC = _confusion(cm)
+            for key, v in zip(CM_KEYS, (ACC, TPR, TNR, FPR, FNR)):
+                self.cm_train[key].append(v)
+
+    def gc_progress(self, est_np, nolag_np, vals):
+        """est_np: [nsup samples][K] lagged estimates (host); nolag_np (S, K, p, p, 1) lag-free
+        combined estimates; vals: device metric values (S, G, 6 + p) or None (host trackers)."""
+        GC, nsup = self.GC, self.nsup
+        if GC is not None and nsup > 0:
+            if vals is not None:
+                if len(est_np) > 0:
+                    self.f1_hist, self.roc_hist = M.track_roc_stats_from_values(vals, self.f1_hist, self.roc_hist, False)
+                    self.f1_off, self.roc_off = M.track_roc_stats_from_values(vals, self.f1_off, self.roc_off, True)
+                    self.dc_hist, self.dcdd_hist, self.daff_hist, self.plm_hist = M.track_deltacon_stats_from_values(
+                        vals, self.p, self.dc_hist, self.dcdd_hist, self.daff_hist, self.plm_hist)
+            else:
+                self.f1_hist, self.roc_hist = M.track_roc_stats(GC, est_np, self.f1_hist, self.roc_hist,
+                                                                remove_self_connections=False)
+                self.f1_off, self.roc_off = M.track_roc_stats(GC, est_np, self.f1_off, self.roc_off,
+                                                              remove_self_connections=True)
+                self.dc_hist, self.dcdd_hist, self.daff_hist, self.plm_hist = M.track_deltacon_stats(
+                    GC, est_np, self.p, self.dc_hist, self.dcdd_hist, self.daff_hist, self.plm_hist, self.eps,
+                    self.cin, self.cout)
+        if nsup > 0:
+            _, self.l1_hist = M.track_l1_stats(est_np, self.l1_hist)
+        self.cos_hist = M.track_cosine_stats_batched(nolag_np[:, :nsup], self.cos_hist, label_offset=0)
+        self.cos_unsup = M.track_cosine_stats_batched(nolag_np[:, nsup:], self.cos_unsup, label_offset=nsup)
+
+    def validation(self, vals):
+        """The tuple validate_training returns (with 5 one-entry confusion histories when supervised)."""
+        if self.nsup > 0:
+            for key, v in zip(CM_KEYS, vals[-5:]):
+                self.cm_val[key] = v
+            vals = vals[:-5]
+        vals = list(vals)
+        if not self.model._WITH_SMOOTHING:
+            vals = vals[:4] + [0.0] + vals[4:]
+        for k, v in zip(HIST_KEYS, vals):
+            self.h[k].append(v)
+        self._vf, self._vfac = vals[0], vals[1]
+
+    def step(self, it, snapshot):
+        """Early stopping (:1482-1559).  snapshot() makes the best-model copy; returns True when
+        the fit stops at this epoch."""
+        m = self.model
+        if it >= m.num_pretrain_epochs + m.num_acclimation_epochs:
+            with np.errstate(all="ignore"):
+                cos_mean = np.mean([self.cos_hist[key][-1] for key in self.cos_hist.keys()]) if self.cos_hist else np.nan
+            if self.nsup > 0:
+                crit = self.sc_factor * self._vfac + self.sc_forecast * self._vf + (
+                    self.sc_cos * cos_mean if self.nsup > 1 else 0.)
+            else:
+                crit = self.sc_forecast * self._vf
+            if crit < self.best_loss:
+                self.best_loss, self.best_it, self.best_model = crit, it, snapshot()
+            elif (it - self.best_it) == self.lookback * self.check_every:
+                self.stopped_at = it
+                return True
+        else:
+            self.best_it, self.best_model = it, snapshot()
+        return False
+
+    def checkpoint(self, save_dir, it, optimizers=None, save_plots=False):
+        save_checkpoint(self.model, save_dir, it, _as_module(self.best_model), *[self.h[k] for k in HIST_KEYS],
+                        self.best_loss, self.best_it, self.f1_hist, self.f1_off, self.roc_hist, self.roc_off,
+                        self.l1_hist, self.cos_hist, self.cos_unsup, self.dc_hist, self.dcdd_hist, self.daff_hist,
+                        self.plm_hist, self.GC, None, cm_train=self.cm_train, cm_val=self.cm_val,
+                        save_plots=save_plots, optimizers=optimizers)
+
+    def history(self):
+        return dict(self.h, best_loss=self.best_loss, best_it=self.best_it, f1score_histories=self.f1_hist,
+                    f1score_OffDiag_histories=self.f1_off, roc_auc_histories=self.roc_hist,
+                    roc_auc_OffDiag_histories=self.roc_off, gc_factor_l1_loss_histories=self.l1_hist,
+                    gc_factor_cosine_sim_histories=self.cos_hist,
+                    gc_factorUnsupervised_cosine_sim_histories=self.cos_unsup, deltacon0_histories=self.dc_hist,
+                    deltacon0_with_directed_degrees_histories=self.dcdd_hist,
+                    deltaffinity_histories=self.daff_hist, path_length_mse_histories=self.plm_hist,
+                    factor_score_train_history=self.cm_train, stopped_at=self.stopped_at)
+
+
+def conditional_gc_estimates(w, G, G0, A, nsup, ls, mode):
+    """The two GC-progress estimate stacks of fit() (:1366-1414) from the embedder weights
+    w (..., S, K) (post-sigmoid), the factor group norms G (..., K, p, p, L) / G0 (..., K, p, p)
+    and A (..., p, p) -- leading dims are replicas for a packed fit.  Element-wise the same
+    operations as GC(mode, X, threshold=False) (the reference's per-(sample, factor) products):
+      est   = lagged estimates of the first nsup samples, no abs on A   (..., nsup, K, p, p, ls)
+      nolag = lag-free estimates of all samples, combine=True (|A|)     (..., S, K, p, p, 1)."""
+    eg = A.transpose(-1, -2).unsqueeze(-1)  # (..., p, p, 1): DGCNN GC = A^T (models/dgcnn.py:47-61)
+    egc = torch.abs(A).transpose(-1, -2).unsqueeze(-1)
+    ws = w[..., :nsup, :, None, None, None]
+    wa = w[..., :, :, None, None, None]
+    est = ws * G.unsqueeze(-5)
+    nolag = wa * G0.unsqueeze(-1).unsqueeze(-5)
+    if mode == "conditional_factor_fixed_embedder":
+        est = est[..., -ls:] + eg.unsqueeze(-4).unsqueeze(-4)[..., -ls:]
+        nolag = nolag + egc.unsqueeze(-4).unsqueeze(-4)
+    return est, nolag
+
+
 def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
             deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path, sc_forecast, sc_factor, sc_cos,
             save_plots):
@@ -111,36 +284,25 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
         raise NotImplementedError("output_length must be 1")
     fused = model.fused_supported()
     eng = model.engine() if fused else None
-    nsup, K, p = model.num_supervised_factors, model.num_factors_nK, model.num_chans
-    thresholds = [0.0]
-    h = dict((k, []) for k in HIST_KEYS)
-    f1_hist = {t: [[] for _ in range(nsup)] for t in thresholds}
-    f1_off = {t: [[] for _ in range(nsup)] for t in thresholds}
-    roc_hist = {t: [[] for _ in range(nsup)] for t in thresholds}
-    roc_off = {t: [[] for _ in range(nsup)] for t in thresholds}
-    cm_train = dict((k, []) for k in ("acc", "tpr", "tnr", "fpr", "fnr"))
-    cm_val = dict((k, []) for k in ("acc", "tpr", "tnr", "fpr", "fnr"))
-    l1_hist = [[] for _ in range(nsup)]
-    cos_hist = {"%dand%d" % (i, j): [] for i in range(nsup) for j in range(nsup) if i < j}
-    cos_unsup = {"%dand%d" % (i, j): [] for i in range(nsup, K) for j in range(nsup, K) if i < j}
-    dc_hist = [[] for _ in range(nsup)]
-    dcdd_hist = [[] for _ in range(nsup)]
-    daff_hist = [[] for _ in range(nsup)]
-    plm_hist = {pl: [[] for _ in range(nsup)] for pl in range(1, p)}
-    best_it, best_loss, best_model, iter_start = None, np.inf, None, 0
-
-    if hasattr(model, "chkpt_best_it"):  # resume_training_from_checkpoint was called
-        best_model = _best_model(model, fused)
-        iter_start = model.chkpt_best_it + 1
-        for k in HIST_KEYS:
-            h[k] = list(getattr(model, "chkpt_" + k))[:iter_start]
-        best_loss, best_it = model.chkpt_best_loss, model.chkpt_best_it
+    nsup, p = model.num_supervised_factors, model.num_chans
+    tr = FitTracker(model, GC, deltaConEps, in_degree_coeff, out_degree_coeff, sc_forecast, sc_factor, sc_cos,
+                    lookback, check_every)
+    iter_start = tr.resume(fused)
+    ost = getattr(model, "chkpt_optimizer_state", None)
+    if ost is not None:  # this package's optimizer_state.pt next to the resumed checkpoint
+        oA.load_state_dict(ost["A"])
+        oB.load_state_dict(ost["B"])
+        if fused:
+            eng.opt = {"A": None, "B": None}  # re-bind: the kernels' moment buffers take the loaded state
+        del model.chkpt_optimizer_state
 
     if fused:
         train = eng.cache_dataset(X_train)
         val = eng.cache_dataset(X_val)
         d_train = eng.workspace(max(train["Bmax"], val["Bmax"]), train["T"])
+        plans = {}
     Lm = model.Lmax
+    ls = min(model.gen_lag, model.embed_lag)
 
     for it in range(iter_start, max_iter):
         if verbose:
@@ -153,126 +315,84 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
                                    running_factor_score_confusion_matrix=cm if nsup > 0 else None)
         else:
             eng.conf.zero_()
-            d_train = eng.workspace(train["Bmax"], train["T"])
-        if not fused:
-            pass
-        elif len(kinds) == 1:
-            eng.run_steps(kinds, train["X"], train["lab"], train["stats"], d_train, train["rows"], train["sizes"], oA, oB)
-        else:  # several updates per batch: batch-major order as in batch_update
-            F2 = train["stats"].shape[1] * train["stats"].shape[2]
-            for bi, (r, s) in enumerate(zip(train["rows"], train["sizes"])):
-                for kind in kinds:
-                    eng.run_steps([kind], train["X"], train["lab"], train["stats"][bi:bi + 1], d_train, [r], [s],
-                                  oA, oB)
-            del F2
-        model._set_module_modes(kinds[-1] if kinds else None)
-        if nsup > 0:
-            if fused:
+            if len(kinds) == 1:
+                key = kinds[0]
+                if key not in plans:
+                    plans[key] = eng.plan_steps(key, train["X"], train["lab"], train["stats"], d_train,
+                                                train["rows"], train["sizes"], oA, oB)
+                plans[key].run()
+            else:  # several updates per batch: batch-major order as in batch_update
+                for bi, (r, s) in enumerate(zip(train["rows"], train["sizes"])):
+                    for kind in kinds:
+                        eng.run_steps([kind], train["X"], train["lab"], train["stats"][bi:bi + 1], d_train, [r], [s],
+                                      oA, oB)
+            if nsup > 0:
                 cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
-            TPR, TNR, FPR, FNR, ACC = _confusion(cm)
-            for key, v in zip(("acc", "tpr", "tnr", "fpr", "fnr"), (ACC, TPR, TNR, FPR, FNR)):
-                cm_train[key].append(v)
+        model._set_module_modes(kinds[-1] if kinds else None)
+        tr.train_confusion(cm if nsup > 0 else None)
 
         # ---- GC progress on the first validation batch (:1366-1414)
         model.factor_score_embedder.eval()
         for f in model.factors:
             f.eval()
-        if fused:
-            nfirst = int(val["sizes"][0])
-            Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
-        else:
-            Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(), torch.float32)
-        # conditional GC modes on the fused path: estimates as stacked device tensors, metrics on
-        # the GPU (rc_metrics.hip); otherwise the host loops of the reference
         dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
             "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
         with torch.no_grad():
             if dev_metrics:
-                mode = model.primary_gc_est_mode
-                est_t = model._conditional_gc_stack(mode, Xv[:nsup], False, False, False)
-                nolag_np = model._conditional_gc_stack(mode, Xv, False, True, True).cpu().numpy()
+                nfirst = int(val["sizes"][0])
+                Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
+                w, _ = model._labels_from_w(eng.embed_raw(Xv))
+                G, G0 = eng.gc_norms()
+                est_t, nolag_t = conditional_gc_estimates(w, G, G0, eng.dgcnn.A.detach(), nsup, ls,
+                                                          model.primary_gc_est_mode)
+                vals = None
+                if GC is not None and nsup > 0 and est_t.shape[0] > 0:
+                    vals = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff)
                 est_host = est_t.cpu().numpy()
+                nolag_np = nolag_t.cpu().numpy()
                 est_np = [[est_host[s, k] for k in range(est_host.shape[1])] for s in range(est_host.shape[0])]
             else:
+                if fused:
+                    Xv = val["X"][:min(int(val["sizes"][0]), model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
+                else:
+                    Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(),
+                                                                                              torch.float32)
+                vals = None
                 est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
                 est_np = [[g.detach().cpu().numpy() for g in row] for row in est]
                 nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
                                  combine_wavelet_representations=True)
                 nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
-        if GC is not None and nsup > 0:
-            if dev_metrics and len(est_np) > 0:
-                vals = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff)
-                f1_hist, roc_hist = M.track_roc_stats_from_values(vals, f1_hist, roc_hist, False)
-                f1_off, roc_off = M.track_roc_stats_from_values(vals, f1_off, roc_off, True)
-                dc_hist, dcdd_hist, daff_hist, plm_hist = M.track_deltacon_stats_from_values(
-                    vals, p, dc_hist, dcdd_hist, daff_hist, plm_hist)
-            else:
-                f1_hist, roc_hist = M.track_roc_stats(GC, est_np, f1_hist, roc_hist, remove_self_connections=False)
-                f1_off, roc_off = M.track_roc_stats(GC, est_np, f1_off, roc_off, remove_self_connections=True)
-                dc_hist, dcdd_hist, daff_hist, plm_hist = M.track_deltacon_stats(
-                    GC, est_np, p, dc_hist, dcdd_hist, daff_hist, plm_hist, deltaConEps, in_degree_coeff,
-                    out_degree_coeff)
-        if nsup > 0:
-            _, l1_hist = M.track_l1_stats(est_np, l1_hist)
-        cos_hist = M.track_cosine_stats_batched(nolag_np[:, :nsup], cos_hist, label_offset=0)
-        cos_unsup = M.track_cosine_stats_batched(nolag_np[:, nsup:], cos_unsup, label_offset=nsup)
+        tr.gc_progress(est_np, nolag_np, vals)
 
         # ---- validation (:1416-1480)
         if nsup > 0:
-            vals = model.validate_training(X_val, output_length, model.num_series, [], [], [], [], [])
-            for key, v in zip(("acc", "tpr", "tnr", "fpr", "fnr"), vals[-5:]):
-                cm_val[key] = v
-            vals = vals[:-5]
+            tr.validation(model.validate_training(X_val, output_length, model.num_series, [], [], [], [], []))
         else:
-            vals = model.validate_training(X_val, output_length, model.num_series)
-        vals = list(vals)
-        if not model._WITH_SMOOTHING:
-            vals = vals[:4] + [0.0] + vals[4:]
-        for k, v in zip(HIST_KEYS, vals):
-            h[k].append(v)
-        v_forecast, v_factor = vals[0], vals[1]
+            tr.validation(model.validate_training(X_val, output_length, model.num_series))
 
         # ---- early stopping (:1482-1559)
-        if it >= model.num_pretrain_epochs + model.num_acclimation_epochs:
-            with np.errstate(all="ignore"):
-                cos_mean = np.mean([cos_hist[key][-1] for key in cos_hist.keys()]) if cos_hist else np.nan
-            if nsup > 0:
-                crit = sc_factor * v_factor + sc_forecast * v_forecast + (sc_cos * cos_mean if nsup > 1 else 0.)
-            else:
-                crit = sc_forecast * v_forecast
-            if crit < best_loss:
-                best_loss, best_it, best_model = crit, it, _best_model(model, fused)
-            elif (it - best_it) == lookback * check_every:
-                if verbose:
-                    print("Stopping early")
-                break
-        else:
-            best_it, best_model = it, _best_model(model, fused)
+        if tr.step(it, lambda: _best_model(model, fused)):
+            if verbose:
+                print("Stopping early")
+            break
 
         if it % check_every == 0 and save_dir is not None:
-            save_checkpoint(model, save_dir, it, _as_module(best_model), *[h[k] for k in HIST_KEYS], best_loss, best_it, f1_hist,
-                            f1_off, roc_hist, roc_off, l1_hist, cos_hist, cos_unsup, dc_hist, dcdd_hist, daff_hist,
-                            plm_hist, GC, X_val, cm_train=cm_train, cm_val=cm_val, save_plots=save_plots)
+            tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
 
-    restore_parameters(model, best_model)
+    restore_parameters(model, tr.best_model)
     if save_dir is not None:
-        torch.save(model, os.path.join(save_dir, "final_best_model.bin"))
+        torch.save(standalone_copy(model), os.path.join(save_dir, "final_best_model.bin"))
     if nsup > 0:
         final = model.validate_training(X_val, output_length, model.num_series, [], [], [], [], [])
         final_combo = final[-6]
     else:
         final_combo = model.validate_training(X_val, output_length, model.num_series)[-1]
     if verbose:
-        print("FINAL BEST (STOPPING CRITERIA) LOSS == ", best_loss, flush=True)
-        print("FINAL BEST (STOPPING CRITERIA) EPOCH == ", best_it, flush=True)
+        print("FINAL BEST (STOPPING CRITERIA) LOSS == ", tr.best_loss, flush=True)
+        print("FINAL BEST (STOPPING CRITERIA) EPOCH == ", tr.best_it, flush=True)
         print("FINAL VALIDATION COMBO LOSS == ", final_combo, flush=True)
-    model.fit_history = dict(h, best_loss=best_loss, best_it=best_it, f1score_histories=f1_hist,
-                             f1score_OffDiag_histories=f1_off, roc_auc_histories=roc_hist,
-                             roc_auc_OffDiag_histories=roc_off, gc_factor_l1_loss_histories=l1_hist,
-                             gc_factor_cosine_sim_histories=cos_hist,
-                             gc_factorUnsupervised_cosine_sim_histories=cos_unsup, deltacon0_histories=dc_hist,
-                             deltacon0_with_directed_degrees_histories=dcdd_hist, deltaffinity_histories=daff_hist,
-                             path_length_mse_histories=plm_hist, factor_score_train_history=cm_train)
+    model.fit_history = tr.history()
     return final_combo
 
 
@@ -283,11 +403,19 @@ def save_checkpoint(model, save_dir, it, best_model, avg_forecasting_loss, avg_f
                     roc_auc_OffDiag_histories, gc_factor_l1_loss_histories, gc_factor_cosine_sim_histories,
                     gc_factorUnsupervised_cosine_sim_histories, deltacon0_histories,
                     deltacon0_with_directed_degrees_histories, deltaffinity_histories, path_length_mse_histories,
-                    GC=None, X_vis=None, cm_train=None, cm_val=None, save_plots=False, **unused):
+                    GC=None, X_vis=None, cm_train=None, cm_val=None, save_plots=False, optimizers=None, **unused):
     """Writes the two files the reference's evaluation scripts and resume logic read
-    (...withStateSmoothing.py:936-990).  Plots (general_utils/plotting.py) are out of scope."""
+    (...withStateSmoothing.py:936-990).  Plots (general_utils/plotting.py) are out of scope.
+    The model is saved as a standalone copy (its own parameter storage, not the pack's).
+    With `optimizers` (fit passes its two Adams) a third file, optimizer_state.pt, holds their
+    state: the reference does not checkpoint it (redcliff_s_cmlp.py:245), so a resumed
+    reference fit restarts Adam; resume_training_from_checkpoint here picks the file up when
+    present, which makes a resumed fit continue exactly (tests/test_gpu_checkpoint.py)."""
     os.makedirs(save_dir, exist_ok=True)
-    torch.save(best_model, os.path.join(save_dir, "final_best_model.bin"))
+    torch.save(standalone_copy(best_model), os.path.join(save_dir, "final_best_model.bin"))
+    if optimizers is not None:
+        torch.save(dict(zip(("A", "B"), (_compact_optimizer_state(o) for o in optimizers))),
+                   os.path.join(save_dir, "optimizer_state.pt"))
     cm_train = cm_train or {}
     cm_val = cm_val or {}
     meta = {

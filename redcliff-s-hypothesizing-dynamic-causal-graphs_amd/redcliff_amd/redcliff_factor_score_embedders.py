@@ -3,8 +3,8 @@
 ``DGCNN_Embedder`` (the embedder of every published REDCLIFF-S run) is computed by the
 fused gfx950 kernels through the owning REDCLIFF model's FitEngine.  ``cEmbedder`` and
 the two "Vanilla" MLP classifiers keep the reference's parameter trees and seeded
-initialisation so checkpoints and seeds stay interchangeable; their training path is
-listed as a next row in DESIGN.md (the fused engine covers the DGCNN configuration).
+initialisation so checkpoints and seeds stay interchangeable; they run (forward, GC and
+training) on the generic HIP-GEMM path (redcliff_amd.generic).
 """
 import torch
 import torch.nn as nn
@@ -34,15 +34,28 @@ class DGCNN_Embedder(nn.Module):
         self.owner = None  # set by the REDCLIFF model: the engine that evaluates this embedder
 
     def forward(self, X, use_final_activation=True):
-        """(B, p, F) or (B, F, p) windows -> (factor weightings (B, K), class logits (B, nsup) | None)."""
-        if self.owner is None:
-            raise RuntimeError("DGCNN_Embedder is evaluated through its REDCLIFF_S_CMLP model (fused gfx950 path)")
+        """(B, p, F) or (B, F, p) windows -> (factor weightings (B, K), class logits (B, nsup) | None).
+        Inside a REDCLIFF model (the owner, re-attached after torch.load / deepcopy) the fused
+        embedder launch evaluates it; a stand-alone embedder runs the generic HIP-GEMM path.
+        Differentiable either way (redcliff_amd.autograd)."""
         assert X.dim() == 3
         if X.size(2) != self.num_features_per_node:  # (B, F, p) -> (B, p, F), as the reference (:369-371)
             assert X.size(1) == self.num_features_per_node
             X = torch.transpose(X, 1, 2)
+        owner = self.owner() if self.owner is not None else None
+        if owner is None:
+            from .autograd import standalone_dgcnn_forward
+            w = standalone_dgcnn_forward(self.dgcnn.dgcnn, X)
+            logits = None
+            if self.num_classes > 0:
+                logits = w[:, :self.num_classes]
+                if use_final_activation and self.use_sigmoid_restriction:
+                    logits = torch.sigmoid(logits)
+            if self.use_sigmoid_restriction:
+                w = torch.sigmoid(self.sigmoid_eccentricity_coeff * w)
+            return w, logits
         # X is (B, p, F) (nodes x features); the kernels read time-major windows (B, F, p)
-        return self.owner()._embed_windows(X.transpose(1, 2), use_final_activation)
+        return owner._embed_windows(X.transpose(1, 2), use_final_activation)
 
     def GC(self, threshold=True, combine_node_feature_edges=False):
         return self.dgcnn.GC(threshold=threshold, combine_node_feature_edges=combine_node_feature_edges)

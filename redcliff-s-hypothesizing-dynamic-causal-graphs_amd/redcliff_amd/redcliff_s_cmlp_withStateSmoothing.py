@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from . import _native as nat
+from . import autograd as AG
 from . import metrics as M
 from .cmlp import cMLP
 from .engine import FitEngine, phase_of_epoch, select_labels
@@ -126,6 +127,8 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                                            save_path=save_path) for _ in range(num_factors)])
         self.gen_model = nn.ModuleList([self.factor_score_embedder, self.factors])
         self._engine = None
+        if isinstance(self.factor_score_embedder, DGCNN_Embedder):
+            self.factor_score_embedder.owner = weakref.ref(self)
 
     # ------------------------------------------------------------------ plumbing
     def __getstate__(self):
@@ -133,6 +136,15 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         st["_engine"] = None
         st.pop("_generic_path", None)
         return st
+
+    def __setstate__(self, state):
+        """torch.load / deepcopy: re-attach the DGCNN embedder to this model, so
+        ``model.factor_score_embedder(x)`` (general_utils/misc.py:66,79) works on a loaded model;
+        the engine itself is created lazily on the first GPU call."""
+        super().__setstate__(state)
+        emb = self.__dict__.get("_modules", {}).get("factor_score_embedder")
+        if isinstance(emb, DGCNN_Embedder):
+            emb.owner = weakref.ref(self)
 
     @property
     def Lmax(self):
@@ -206,12 +218,13 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                 w = torch.sigmoid(emb.sigmoid_eccentricity_coeff * w)
             return w, logits
         eng = self.engine()
+        Xw = Xw.to(eng.device, torch.float32)
         B, F, p = Xw.shape
         pad = self.Lmax - F
         if pad > 0:
             Xw = torch.cat([torch.zeros(B, pad, p, device=Xw.device, dtype=Xw.dtype), Xw], 1)
         train = self.factor_score_embedder.training
-        w_raw, _, _ = eng.forward_outputs(Xw, train_bn=train, bn_updates=1)
+        w_raw = AG.embedder_forward(self, Xw.contiguous(), train)
         w, logits = self._labels_from_w(w_raw)
         if logits is not None and not use_final_activation and self.factor_score_embedder.use_sigmoid_restriction:
             logits = w_raw[:, :self.num_supervised_factors]
@@ -230,7 +243,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             raise ValueError("forward needs at least max(gen_lag, embed_lag) time steps")
         Xw = X[:, X.shape[1] - self.Lmax:, :].contiguous()
         train = self.factor_score_embedder.training
-        w_raw, y, xs = eng.forward_outputs(Xw, train_bn=train, bn_updates=1)
+        xs, y, w_raw = AG.fused_forward(self, Xw, train)  # a graph when gradients are requested
         w, logits = self._labels_from_w(w_raw)
         if logits is None:
             logits = w
@@ -239,7 +252,12 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
 
     # ------------------------------------------------------------------ GC
     def _factor_gcs(self, threshold, ignore_lag):
-        G, G0 = self.engine().gc_norms()
+        eng = self.engine()
+        W0s = [net.layers[0].weight for f in self.factors for net in f.networks]
+        if AG.grad_needed(W0s) and not threshold:
+            G, G0 = AG.group_norms(list(self.factors))  # differentiable (cmlp.py:147-167)
+        else:
+            G, G0 = eng.gc_norms()
         ests = [G0[k].view(self.num_series, self.num_series, 1) if ignore_lag else G[k]
                 for k in range(self.num_factors_nK)]
         return [(e > 0).int() for e in ests] if threshold else ests
@@ -296,17 +314,19 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
     # ------------------------------------------------------------------ loss (values)
     def compute_loss(self, conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
                      node_dag_scale=0.1, embedder_pretrain_loss=False, factor_pretrain_loss=False):
-        """Loss terms of ...withStateSmoothing.py:624-731.  On the fused configuration they are
-        values (the fused step produces the gradients); on the generic path they carry autograd."""
+        """Loss terms of ...withStateSmoothing.py:624-731.  A graph tensor whenever gradients are
+        enabled (the reference calls .backward() on it, :783): forward, GC and the embedder are
+        autograd Functions over the fused kernels (redcliff_amd.autograd); the fused
+        batch_update does not use this method (its backward is fused)."""
         if not self.fused_supported():
             dev = self._device()
             return self._generic().compute_loss(conditioning_X.to(dev, torch.float32), preds, targets.to(dev),
                                                 factor_scores, factor_labels, gc_est_mode,
                                                 embedder_pretrain_loss=embedder_pretrain_loss,
                                                 factor_pretrain_loss=factor_pretrain_loss)
-        with torch.no_grad():
-            return self._fused_loss_values(conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
-                                           embedder_pretrain_loss, factor_pretrain_loss)
+        dev = self._device()
+        return self._fused_loss_values(conditioning_X.to(dev, torch.float32), preds, targets.to(dev), factor_scores,
+                                       factor_labels, gc_est_mode, embedder_pretrain_loss, factor_pretrain_loss)
 
     def _fused_loss_values(self, conditioning_X, preds, targets, factor_scores, factor_labels, gc_est_mode,
                            embedder_pretrain_loss, factor_pretrain_loss):
@@ -324,21 +344,25 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             factor = factor + self.FACTOR_SCORE_COEFF * self.supervised_loss_fn(yhat[:, :nsup], lab[:, :nsup])
         fw_l1 = self.FACTOR_WEIGHT_L1_COEFF * (torch.norm(factor_scores[0], 1) - 1.)
         smooth = torch.zeros(1, device=dev)
-        cos_pen, adj = None, None
-        logw = [math.log(i + 2.) for i in range(gc_lagged[0][0].size(2))]
-        for b in range(len(gc)):
-            if len(gc[b]) > 1:
-                eye = torch.eye(self.num_series, device=dev).view(self.num_series, self.num_series, 1)
-                vs = [(g - eye).flatten() for g in gc[b]]
+        # the per-(sample, factor) loops of :696-715 over stacked estimates: one batched
+        # cosine per factor pair (values only: the reference's torch.Tensor(list) drops the
+        # gradient, general_utils/metrics.py:380) and one batched lag-weighted L1
+        g0 = torch.stack([torch.stack(list(row)) for row in gc])          # (B, K', p, p, 1)
+        gl = torch.stack([torch.stack(list(row)) for row in gc_lagged])   # (B, K', p, p, L')
+        cos_pen = None
+        if g0.shape[1] > 1:
+            eye = torch.eye(self.num_series, device=dev).view(1, self.num_series, self.num_series, 1)
+            v = (g0.detach() - eye).flatten(2)
+            pairs = [(i, j) for i in range(v.shape[1]) for j in range(i + 1, v.shape[1])]
+            cs = torch.stack([torch.nn.functional.cosine_similarity(v[:, i], v[:, j], dim=1) for i, j in pairs], 1)
+            for row in cs.tolist():
                 tot = 0.
-                for i in range(len(vs)):
-                    for j in range(i + 1, len(vs)):
-                        tot += float(torch.nn.functional.cosine_similarity(vs[i].view(1, -1), vs[j].view(1, -1)))
-                v = self.FACTOR_COS_SIM_COEFF * tot
-                cos_pen = v if cos_pen is None else cos_pen + v
-            for G in gc_lagged[b]:
-                v = self.ADJ_L1_REG_COEFF * sum(lw * torch.sum(torch.abs(G[:, :, i])) for i, lw in enumerate(logw))
-                adj = v if adj is None else adj + v
+                for x in row:
+                    tot += x
+                val = self.FACTOR_COS_SIM_COEFF * tot
+                cos_pen = val if cos_pen is None else cos_pen + val
+        logw = torch.tensor([math.log(i + 2.) for i in range(gl.shape[-1])], device=dev, dtype=torch.float32)
+        adj = self.ADJ_L1_REG_COEFF * (torch.abs(gl).sum(dim=(2, 3)) * logw).sum()
         cos_t = None if cos_pen is None else torch.tensor(cos_pen, device=dev)
         if embedder_pretrain_loss:
             combo = factor + fw_l1 + smooth
@@ -353,13 +377,19 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
 
     def resume_training_from_checkpoint(self, training_meta_data_path):
         """...withStateSmoothing.py:209-251: histories of a previous run; fit() resumes at best_it+1.
-        (Optimizer state is not checkpointed, as in the reference.)"""
+        The reference does not checkpoint the optimizers (redcliff_s_cmlp.py:245) and restarts
+        Adam; when this package's save_checkpoint left optimizer_state.pt next to the metadata,
+        fit() loads it into its optimizers, so the resumed fit continues exactly."""
+        import os
         import pickle
         with open(training_meta_data_path, "rb") as f:
             meta = pickle.load(f)  # a file written by this package's (or the reference's) save_checkpoint
         self.chkpt_epoch = meta["epoch"]
         for k, v in meta.items():
             setattr(self, "chkpt_" + k, v)
+        opt_path = os.path.join(os.path.dirname(os.path.abspath(training_meta_data_path)), "optimizer_state.pt")
+        if os.path.exists(opt_path):
+            self.chkpt_optimizer_state = torch.load(opt_path, map_location=self._device(), weights_only=True)
 
     # ------------------------------------------------------------------ training step
     def batch_update(self, epoch_num, batch_num, X, Y, optimizerA, optimizerB, output_length, best_model=None,

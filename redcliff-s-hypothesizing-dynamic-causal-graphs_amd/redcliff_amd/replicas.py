@@ -9,20 +9,30 @@ carries the replica on blockIdx.y and every per-fit buffer (parameters, Adam mom
 BatchNorm running statistics, hyper-parameters, workspace, loss accumulators) is a row
 of an [R][...] tensor.  Replicas may differ in everything that is not a shape: seeds,
 coefficient dicts, learning rates / eps / weight decay of both optimizers, BatchNorm
-momentum.  They share the training windows (one dataset for the whole grid, as in the
-reference) and the update schedule of the step (phase flags, Adam step counters).
+momentum, stopping-criterion coefficients.  They share the training windows (one dataset
+for the whole grid, as in the reference) and the phase schedule (pretrain / acclimation
+epochs; ``grid_packs`` groups a grid by shape and schedule).
+
+``ReplicaPack.fit`` is the packed counterpart of ``fit()`` (...withStateSmoothing.py:
+1175-1647): every replica keeps its own histories, GC-progress trackers, best-epoch
+snapshot, checkpoints and early-stopping rule (redcliff_amd.fit_loop.FitTracker -- the very
+code the single fit runs); a replica that stops leaves the launch's active list, so its
+state freezes and its workgroups are no longer launched.
 
 Each model stays a normal drop-in module: its parameters and its optimizers' state are
 views of its pack row, so ``state_dict()``, ``GC()``, ``forward()`` and the single-fit
 methods keep working on it between packed epochs.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
 
 from . import _native as nat
+from . import metrics as M
 from .engine import _stream, flags_for, phase_of_epoch
+from .fit_loop import FitTracker, ParamSnapshot, conditional_gc_estimates, restore_parameters, standalone_copy
 
 
 class ReplicaPack:
@@ -63,6 +73,7 @@ class ReplicaPack:
         self.conf = torch.zeros(R, ns * ns, device=dev, dtype=torch.int32)
         self.ws = None
         self.ws_B = 0
+        self._plans = {}
         for r, (e, (oA, oB)) in enumerate(zip(self.engines, self.optimizers)):
             e.attach_pack(self, r)
             e.bind_optimizer("A", oA)
@@ -89,24 +100,41 @@ class ReplicaPack:
                 nat.check(-1, "workspace_bytes")
             self.ws = torch.zeros(nbytes // 4, device=self.device, dtype=torch.float32)
             self.ws_B = Bmax
+            self.ws_off = nat.workspace_layout(d)
         return self._dims(self.ws_B, T)
 
     def _hyper(self):
-        return torch.cat([e._hyper() for e in self.engines]).contiguous()
+        parts = [e._hyper() for e in self.engines]
+        key = tuple(e.hyper_key for e in self.engines)
+        if key != getattr(self, "_hyper_key", None):
+            self._hyper_cat = torch.cat(parts).contiguous()
+            self._hyper_key = key
+        return self._hyper_cat
 
-    def _args(self, d, flags, nbn, ds, stats):
-        e0 = self.engines[0]
+    def _active_list(self, active):
+        """(host int32 array or None, engines stepped)"""
+        if active is None:
+            return None, self.engines
+        act = np.ascontiguousarray(sorted(int(r) for r in active), dtype=np.int32)
+        return act, [self.engines[r] for r in act]
+
+    def _args(self, d, flags, nbn, ds, stats, active=None):
         a = nat.StepArgs()
         a.d = d
         a.flags = flags | nat.REFRESH_SUPPORTS  # the pack's workspace holds its own supports
         a.n_bn_updates = nbn
-        tA = set(e.opt["A"]["t"] for e in self.engines)
-        tB = set(e.opt["B"]["t"] for e in self.engines)
-        if len(tA) != 1 or len(tB) != 1:
-            raise RuntimeError("packed replicas must share their Adam step counters (same update schedule)")
-        a.tA, a.tB = tA.pop() + 1, tB.pop() + 1
+        act, engs = self._active_list(active)
+        # the stepped groups' Adam step numbers are shared by the launch (bias corrections); replicas
+        # that stopped early keep theirs and are not in the active list
+        ts = []
+        for g, bit in (("A", nat.STEP_A), ("B", nat.STEP_B)):
+            t = set(e.opt[g]["t"] for e in engs if e.opt[g] is not None) or {0}
+            if (flags & bit) and len(t) != 1:
+                raise RuntimeError("packed replicas must share their Adam step counters (same update schedule)")
+            ts.append(min(t) + 1)
+        a.tA, a.tB = ts
         a.X, a.x_rstride = ds["X"].data_ptr(), 0  # one dataset for the whole grid
-        a.labels, a.lab_rstride = ds["lab"].data_ptr(), 0
+        a.labels, a.lab_rstride = (ds["lab"].data_ptr() if ds.get("lab") is not None else None), 0
         a.bn_stats = stats.data_ptr() if stats is not None else None
         a.bn_stats_rstride = 0
         a.emb, a.emb_stride = self.emb.data_ptr(), self.emb.shape[1]
@@ -119,17 +147,20 @@ class ReplicaPack:
         a.ws, a.ws_bytes = self.ws.data_ptr(), self.ws.numel() * 4
         a.acc = self.acc.data_ptr()
         a.confusion = self.conf.data_ptr()
-        del e0
-        return a
+        if act is not None:
+            self._act_keep = act  # the host array must outlive the call
+            a.replicas = act.ctypes.data_as(ctypes.c_void_p)
+            a.n_replicas = len(act)
+        return a, engs
 
     def cache_dataset(self, loader):
         """Upload the (shared) training set once; see FitEngine.cache_dataset."""
         return self.engines[0].cache_dataset(loader)
 
     # ------------------------------------------------------------------ stepping
-    def run_steps(self, kinds, ds, rows=None, sizes=None, stats=None):
-        """Update kinds of one phase over consecutive batches of `ds` for all R replicas
-        (one redcliff_train_steps launch chain of R-replica kernels per kind)."""
+    def run_steps(self, kinds, ds, rows=None, sizes=None, stats=None, active=None):
+        """Update kinds of one phase over consecutive batches of `ds` for the active replicas
+        (all when None): one redcliff_train_steps launch chain of R-replica kernels per kind."""
         for e in self.engines:
             e.ensure_bound()
         rows = ds["rows"] if rows is None else rows
@@ -138,36 +169,38 @@ class ReplicaPack:
         d = self._workspace(max(int(ds["Bmax"]), 1), ds["T"])
         for kind in kinds:
             flags, nbn = flags_for(kind, self.engines[0].nsup)
-            a = self._args(d, flags, nbn, ds, stats if flags & nat.BN_TRAIN else None)
+            a, engs = self._args(d, flags, nbn, ds, stats if flags & nat.BN_TRAIN else None, active)
             rows_a = np.ascontiguousarray(rows, dtype=np.int64)
             sizes_a = np.ascontiguousarray(sizes, dtype=np.int32)
             nat.check(nat.lib().redcliff_train_steps(ctypes.byref(a), len(rows_a),
                                                      rows_a.ctypes.data_as(ctypes.c_void_p),
                                                      sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * self.engines[0].F,
                                                      _stream()), "packed train_steps")
-            for e in self.engines:
+            for e in engs:
                 e._after(flags, nbn, len(rows_a))
+            for e in self.engines:
                 e.supports_fresh = False  # the single-fit workspace's supports are stale now
 
-    def run_epoch(self, epoch, ds):
+    def run_epoch(self, epoch, ds, active=None):
         """The batch_update phase of `epoch` (...withStateSmoothing.py:741-759) over every batch
-        of `ds`, for all replicas.  All replicas must be in the same phase."""
-        kinds = [tuple(phase_of_epoch(m, epoch)) for m in self.models]
-        if len(set(kinds)) != 1:
+        of `ds`, for the active replicas.  All replicas must be in the same phase."""
+        idx = range(self.R) if active is None else active
+        kinds = [tuple(phase_of_epoch(self.models[r], epoch)) for r in idx]
+        if len(set(kinds)) > 1:
             raise RuntimeError("replicas are in different training phases at epoch %d: %s" % (epoch, kinds))
-        kinds = list(kinds[0])
+        kinds = list(kinds[0]) if kinds else []
         if len(kinds) <= 1:
-            self.run_steps(kinds, ds)
+            self.run_steps(kinds, ds, active=active)
         else:  # several updates per batch: batch-major order as in batch_update
             for bi, (r, s) in enumerate(zip(ds["rows"], ds["sizes"])):
                 for kind in kinds:
-                    self.run_steps([kind], ds, [r], [s], ds["stats"][bi:bi + 1])
-        for m in self.models:
-            m._set_module_modes(kinds[-1] if kinds else None)
+                    self.run_steps([kind], ds, [r], [s], ds["stats"][bi:bi + 1], active=active)
+        for r in idx:
+            self.models[r]._set_module_modes(kinds[-1] if kinds else None)
+        return kinds
 
-    def validate(self, ds):
-        """validate_training loss averages (:1650-1790) of every replica: array [R][7]
-        (forecast, factor, cos, fw_l1, smooth, adj, combo), plus confusion matrices [R][nsup][nsup]."""
+    def _values(self, ds, active=None):
+        """validate_training accumulators of the active replicas: raw acc [R][8], confusion."""
         for e in self.engines:
             e.ensure_bound()
         self.acc.zero_()
@@ -175,13 +208,227 @@ class ReplicaPack:
         e0 = self.engines[0]
         d = self._workspace(max(int(ds["Bmax"]), 1), ds["T"])
         flags = nat.VALUES | (nat.CONFUSION if e0.nsup > 0 else 0)
-        a = self._args(d, flags, 0, ds, None)
+        a, _ = self._args(d, flags, 0, ds, None, active)
         rows_a = np.ascontiguousarray(ds["rows"], dtype=np.int64)
         sizes_a = np.ascontiguousarray(ds["sizes"], dtype=np.int32)
         nat.check(nat.lib().redcliff_train_steps(ctypes.byref(a), len(rows_a), rows_a.ctypes.data_as(ctypes.c_void_p),
                                                  sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * e0.F, _stream()),
                   "packed validate")
-        acc = self.acc.cpu().numpy()
-        nb = np.maximum(acc[:, 7:8], 1.0)
         ns = max(e0.nsup, 1)
-        return acc[:, :7] / nb, self.conf.cpu().numpy().reshape(self.R, ns, ns)
+        return self.acc.cpu().numpy(), self.conf.cpu().numpy().reshape(self.R, ns, ns)
+
+    def validate(self, ds, active=None):
+        """validate_training loss averages (:1650-1790) of every replica: array [R][7]
+        (forecast, factor, cos, fw_l1, smooth, adj, combo), plus confusion matrices [R][nsup][nsup]."""
+        acc, conf = self._values(ds, active)
+        nb = np.maximum(acc[:, 7:8], 1.0)
+        return acc[:, :7] / nb, conf
+
+    def embed_raw(self, X, active=None):
+        """Raw embedder outputs [Ra][B][K] of windows X (B, T >= Lmax, p) for the active replicas
+        (BatchNorm running statistics): one embedder-only launch for all of them."""
+        X = X.to(self.device, torch.float32).contiguous()
+        B, T, _ = X.shape
+        d = self._workspace(max(B, 1), T)
+        ds = {"X": X, "lab": None}
+        a, _ = self._args(d, 0, 0, ds, None, active)
+        a.B, a.row0 = B, 0
+        nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "packed embed")
+        idx = list(range(self.R)) if active is None else sorted(active)
+        K = self.engines[0].K
+        o, tot = self.ws_off["w"], self.ws_off["total"]
+        ws = self.ws[:self.R * tot].view(self.R, tot)
+        return ws[idx, o:o + B * K].view(len(idx), B, K).clone()
+
+    def gc_norms(self):
+        """(G [R][K][p][p][L], G0 [R][K][p][p]) of every replica's factor weights (one launch)."""
+        e0 = self.engines[0]
+        d = nat.Dims(R=self.R, Bmax=1, T=e0.L, p=e0.p, L=e0.L, K=e0.K, h=e0.h, F=e0.L, n=1, H=1, M1=1, nsup=0,
+                     use_sigmoid=0, sigmoid_ecc=0.0)
+        G = torch.empty(self.R, e0.K, e0.p, e0.p, e0.L, device=self.device, dtype=torch.float32)
+        G0 = torch.empty(self.R, e0.K, e0.p, e0.p, device=self.device, dtype=torch.float32)
+        nat.check(nat.lib().redcliff_gc_norms(ctypes.byref(d), ctypes.c_void_p(self.fac.data_ptr()),
+                                              self.fac.shape[1], ctypes.c_void_p(G.data_ptr()),
+                                              ctypes.c_void_p(G0.data_ptr()), _stream()), "packed gc_norms")
+        return G, G0
+
+    # ------------------------------------------------------------------ packed fit
+    def fit(self, save_dir, X_train, X_val, max_iter, lookback=5, check_every=50, verbose=0, GC=None,
+            deltaConEps=0.1, in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=1.,
+            stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., output_length=1, save_plots=False):
+        """R fits of ``fit()`` (...withStateSmoothing.py:1175-1647) in one packed launch chain.
+
+        Every replica follows exactly the rules (and the host code, FitTracker) of a single fit:
+        its histories, its stopping criterion (per-model stopping_criteria_* may be given as
+        lists), best-epoch snapshot, checkpoints every check_every epochs (save_dir: a list of R
+        directories, or one root that gets replica_<r>/ sub-directories), restore_parameters and
+        final model file.  A stopped replica leaves the active list: nothing of it is launched
+        or updated afterwards.  Returns the final validation combo loss of every replica; each
+        model gets ``fit_history`` as a single fit would."""
+        if output_length != 1:
+            raise NotImplementedError("output_length must be 1")
+        R, models = self.R, self.models
+        for m in models:
+            if not m.fused_supported() or "Freeze" in m.training_mode:
+                raise NotImplementedError("packed fits cover the fused (published) configuration")
+        sched = set((m.num_pretrain_epochs, m.num_acclimation_epochs, m.training_mode) for m in models)
+        if len(sched) != 1:
+            raise ValueError("a pack shares its phase schedule (pretrain / acclimation epochs); group the grid "
+                             "with grid_packs(): %s" % sorted(sched))
+
+        def per(x):
+            return list(x) if isinstance(x, (list, tuple)) else [x] * R
+        scf, scfa, scc = per(stopping_criteria_forecast_coeff), per(stopping_criteria_factor_coeff), \
+            per(stopping_criteria_cosSim_coeff)
+        dirs = None
+        if save_dir is not None:
+            dirs = list(save_dir) if isinstance(save_dir, (list, tuple)) else \
+                [os.path.join(save_dir, "replica_%d" % r) for r in range(R)]
+        trackers = [FitTracker(m, GC, deltaConEps, in_degree_coeff, out_degree_coeff, scf[r], scfa[r], scc[r],
+                               lookback, check_every) for r, m in enumerate(models)]
+        e0, m0 = self.engines[0], models[0]
+        nsup, p, K = e0.nsup, e0.p, e0.K
+        Lm, ls = m0.Lmax, min(m0.gen_lag, m0.embed_lag)
+        train = self.cache_dataset(X_train)
+        val = self.cache_dataset(X_val)
+        self._workspace(max(int(train["Bmax"]), int(val["Bmax"]), 1), train["T"])
+        dev_metrics = 2 <= p <= 64 and m0.primary_gc_est_mode in ("conditional_factor_exclusive",
+                                                                   "conditional_factor_fixed_embedder")
+        if not dev_metrics:
+            raise NotImplementedError("packed fits track GC progress on the device (2 <= p <= 64, conditional modes)")
+        best = _PackBest(self)
+        active = list(range(R))
+        nfirst = min(int(val["sizes"][0]), m0.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING)
+        Xv = val["X"][:nfirst, :Lm, :]
+        for it in range(max_iter):
+            if not active:
+                break
+            if verbose:
+                print("ReplicaPack.fit: epoch %d, %d of %d replicas active" % (it, len(active), R), flush=True)
+            self.conf.zero_()
+            self.run_epoch(it, train, active)
+            cms = self.conf.cpu().numpy().reshape(R, max(nsup, 1), max(nsup, 1)) if nsup > 0 else None
+            for r in active:
+                trackers[r].train_confusion(cms[r] if nsup > 0 else None)
+                models[r].factor_score_embedder.eval()
+                for f in models[r].factors:
+                    f.eval()
+            # ---- GC progress of every active replica on the first validation batch (:1366-1414)
+            with torch.no_grad():
+                w_raw = self.embed_raw(Xv, active)  # (Ra, S, K)
+                emb0 = models[0].factor_score_embedder
+                w = torch.sigmoid(emb0.sigmoid_eccentricity_coeff * w_raw) if emb0.use_sigmoid_restriction else w_raw
+                G, G0 = self.gc_norms()
+                A = self.emb[:, :p * p].view(R, p, p)
+                ai = torch.as_tensor(active, device=self.device)
+                est_t, nolag_t = conditional_gc_estimates(w, G[ai], G0[ai], A[ai], nsup, ls, m0.primary_gc_est_mode)
+                vals = None
+                if GC is not None and nsup > 0 and est_t.shape[1] > 0:
+                    Ra, S = est_t.shape[0], est_t.shape[1]
+                    vals = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
+                                                in_degree_coeff, out_degree_coeff)
+                    vals = vals.reshape(Ra, S, *vals.shape[1:])
+                est_host = est_t.cpu().numpy()
+                nolag_host = nolag_t.cpu().numpy()
+            for i, r in enumerate(active):
+                eh = est_host[i]
+                est_np = [[eh[s, k] for k in range(eh.shape[1])] for s in range(eh.shape[0])]
+                trackers[r].gc_progress(est_np, nolag_host[i], None if vals is None else vals[i])
+            # ---- validation of every active replica (:1416-1480), one launch chain
+            acc, conf = self._values(val, active)
+            nb = float(val["len"])
+            for r in active:
+                hist = [[] for _ in range(5)] if nsup > 0 else [None] * 5
+                trackers[r].validation(models[r]._validation_tuple(acc[r], nb, conf[r], *hist))
+            # ---- early stopping, per replica (:1482-1559); snapshots copied in one batch
+            stopped = []
+            for r in active:
+                if trackers[r].step(it, lambda r=r: best.mark(r)):
+                    stopped.append(r)
+            best.copy_marked()
+            for r in stopped:
+                if verbose:
+                    print("ReplicaPack.fit: replica %d stops early at epoch %d" % (r, it), flush=True)
+            active = [r for r in active if r not in stopped]
+            if dirs is not None and it % check_every == 0:
+                for r in active:
+                    trackers[r].checkpoint(dirs[r], it, optimizers=self.optimizers[r], save_plots=save_plots)
+        # ---- restore best parameters, final files and validation (:1621-1647)
+        for r, m in enumerate(models):
+            restore_parameters(m, trackers[r].best_model)
+            if dirs is not None:
+                os.makedirs(dirs[r], exist_ok=True)
+                torch.save(standalone_copy(m), os.path.join(dirs[r], "final_best_model.bin"))
+        for e in self.engines:
+            e.supports_fresh = False
+        acc, conf = self._values(val)
+        nb = float(val["len"])
+        finals = []
+        for r, m in enumerate(models):
+            hist = [[] for _ in range(5)] if nsup > 0 else [None] * 5
+            v = m._validation_tuple(acc[r], nb, conf[r], *hist)
+            finals.append(v[-6] if nsup > 0 else v[-1])
+            m.fit_history = trackers[r].history()
+        return finals
+
+
+class _PackBest:
+    """Best-epoch snapshots of every replica of a pack: rows of [R][...] buffers, refreshed for
+    all improving replicas of an epoch with one indexed copy per buffer (instead of R model
+    deep-copies).  mark(r) returns the replica's ParamSnapshot (views of its rows)."""
+
+    def __init__(self, pack):
+        self.pack = pack
+        self.emb = torch.empty_like(pack.emb)
+        self.fac = torch.empty_like(pack.fac)
+        self.bn = torch.empty_like(pack.bn)
+        dev = pack.device
+        self.nbt = torch.zeros(pack.R, dtype=torch.long, device=dev)
+        self.marked = []
+
+    def mark(self, r):
+        self.marked.append(r)
+        return ParamSnapshot(self.pack.models[r], emb=self.emb[r], fac=self.fac[r],
+                             bn=(self.bn[0][r], self.bn[1][r], self.nbt[r]))
+
+    def copy_marked(self):
+        if not self.marked:
+            return
+        idx = torch.as_tensor(sorted(set(self.marked)), device=self.pack.device)
+        with torch.no_grad():
+            self.emb.index_copy_(0, idx, self.pack.emb.index_select(0, idx))
+            self.fac.index_copy_(0, idx, self.pack.fac.index_select(0, idx))
+            self.bn.index_copy_(1, idx, self.pack.bn.index_select(1, idx))
+            nbt = torch.stack([self.pack.models[int(r)].factor_score_embedder.dgcnn.dgcnn.BN1.num_batches_tracked
+                               for r in idx.tolist()])
+            self.nbt.index_copy_(0, idx, nbt.to(self.nbt.dtype))
+        self.marked = []
+
+
+def grid_packs(models_and_opts, max_replicas=64):
+    """Group grid points (model, (optimizerA, optimizerB)) into packs of identical shapes and
+    phase schedules (the reference grid varies embed_lag, graph-conv layers and the pretrain /
+    acclimation epochs, train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:278-309),
+    in the grid's own order, at most max_replicas per pack.  Returns [(models, optimizers)]."""
+    groups = {}
+    order = []
+    for m, o in models_and_opts:
+        e = m.engine()
+        key = ReplicaPack._shape(e) + (m.num_pretrain_epochs, m.num_acclimation_epochs, m.training_mode)
+        if key not in groups:
+            groups[key] = []
+            order.append(key)
+        groups[key].append((m, o))
+    out = []
+    for key in order:
+        g = groups[key]
+        for i in range(0, len(g), max_replicas):
+            chunk = g[i:i + max_replicas]
+            out.append(([m for m, _ in chunk], [o for _, o in chunk]))
+    return out
+
+
+def shard_grid(n_points, world, rank):
+    """Grid-point indices of rank `rank`: round-robin over the grid order, as SLURM array tasks
+    map onto nodes (train/...gsSmooth1.py:157-160: task i -> parameters_to_be_parallelized[i-1])."""
+    return list(range(rank, n_points, world))

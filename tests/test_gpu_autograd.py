@@ -1,0 +1,202 @@
+"""Autograd at the drop-in boundary (redcliff_amd.autograd).
+
+The reference's forward / GC / compute_loss return graph tensors and its own batch_update calls
+compute_loss(...).backward() (models/redcliff_s_cmlp_withStateSmoothing.py:731, 783); cMLP.forward
+(models/cmlp.py:90-101) and cMLP.GC (:147-203) are differentiable too.  Checked here against the
+CPU oracle's autograd on the golden scenarios:
+  * the fused compute_loss values (eval mode) against the reference's own eval/loss/* fixtures;
+  * torch.autograd.grad of the full batch_update loss (train mode: forward, the two GC calls of
+    compute_loss, every penalty) w.r.t. every parameter, and of the cMLP outputs / group norms
+    w.r.t. their weights and inputs, within 1e-4 relative;
+  * the BatchNorm running statistics advance as in the reference (3 evaluations per loss);
+  * DGCNN_Embedder.forward works on a torch.load-ed model (general_utils/misc.py:66,79)."""
+import copy
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_close, batches, ctor_args, load
+
+pytestmark = pytest.mark.gpu
+
+FUSED = ["dgcnn_c1", "dgcnn_d4ic", "dgcnn_partial_sigmoid", "dgcnn_unsup", "dgcnn_base", "dgcnn_feql"]
+
+
+def pair(name):
+    import redcliff_amd
+    from oracle.redcliff_oracle import OracleREDCLIFF
+    d, meta = load(name)
+    args, kw = ctor_args(meta)
+    torch.manual_seed(meta["seed"])
+    cls = redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing if meta["smoothing_class"] else redcliff_amd.REDCLIFF_S_CMLP
+    m = cls(*args, **kw).float().cuda()
+    torch.manual_seed(meta["seed"])
+    o = OracleREDCLIFF(*args, with_smoothing=meta["smoothing_class"], **kw)
+    return d, meta, m, o
+
+
+@pytest.mark.parametrize("name", FUSED)
+def test_compute_loss_matches_reference_fixtures(name):
+    """eval/loss/{combined,emb,fac}/* were written by the reference's compute_loss on batch 0."""
+    d, meta, m, _ = pair(name)
+    m.eval()
+    Xb, Yb = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    X = Xb.cuda()
+    with torch.no_grad():
+        x_sim, _, _, labels = m(X[:, :Lm, :])
+        tgt = X[:, Lm:Lm + meta["S"], :]
+        for flag in ("combined", "emb", "fac"):
+            combo, terms = m.compute_loss(X[:, :meta["F"], :], x_sim, tgt, labels, Yb.cuda(), meta["gc_mode"],
+                                          embedder_pretrain_loss=(flag == "emb"), factor_pretrain_loss=(flag == "fac"))
+            assert_close("%s/combo" % flag, float(combo), d["eval/loss/%s/combo" % flag], 1e-4, 1e-6)
+            for i, t in enumerate(terms):
+                want = d["eval/loss/%s/t%d" % (flag, i)]
+                if np.isnan(want):
+                    assert t is None, (flag, i)
+                else:
+                    assert_close("%s/t%d" % (flag, i), float(t), want, 1e-4, 1e-6)
+
+
+def _loss_and_grads(model, Xb, Yb, meta, dev):
+    Lm = max(meta["L"], meta["F"])
+    X = Xb.to(dev)
+    x_sim, _, _, labels = model(X[:, :Lm, :])
+    tgt = X[:, Lm:Lm + meta["S"], :]
+    combo, _ = model.compute_loss(X[:, :meta["F"], :], x_sim, tgt, labels, Yb.to(dev), meta["gc_mode"])
+    names = [n for n, _ in model.named_parameters() if not n.startswith("gen_model.")]
+    params = dict(model.named_parameters())
+    grads = torch.autograd.grad(combo, [params[n] for n in names], allow_unused=True)
+    return float(combo), dict((n, None if g is None else g.detach().cpu().numpy()) for n, g in zip(names, grads))
+
+
+@pytest.mark.parametrize("name", ["dgcnn_c1", "dgcnn_d4ic", "dgcnn_partial_sigmoid", "dgcnn_unsup"])
+def test_batch_update_loss_gradients_match_oracle(name):
+    d, meta, m, o = pair(name)
+    m.train()
+    o.train()
+    Xb, Yb = batches(d, meta)[0]
+    lm, gm = _loss_and_grads(m, Xb, Yb, meta, "cuda")
+    lo, go = _loss_and_grads(o, Xb, Yb, meta, "cpu")
+    assert_close("combo", lm, lo, 1e-4, 1e-6)
+    assert set(gm) == set(go)
+    for n in go:
+        if go[n] is None:
+            assert gm[n] is None or not np.any(gm[n]), n
+            continue
+        scale = max(1e-6, float(np.abs(go[n]).max()))
+        assert_close("grad/" + n, gm[n], go[n], 1e-4, 2e-5 * scale)
+    # three embedder evaluations (forward + two GC calls) advanced BatchNorm, as in the reference
+    bn_m = m.factor_score_embedder.dgcnn.dgcnn.BN1
+    bn_o = o.factor_score_embedder.dgcnn.dgcnn.BN1
+    assert int(bn_m.num_batches_tracked) == int(bn_o.num_batches_tracked) == 3
+    assert_close("running_mean", bn_m.running_mean.cpu().numpy(), bn_o.running_mean.detach().numpy(), 1e-4, 1e-6)
+    assert_close("running_var", bn_m.running_var.cpu().numpy(), bn_o.running_var.detach().numpy(), 1e-4, 1e-6)
+
+
+def test_external_training_loop_with_backward_and_torch_adam():
+    """compute_loss(...).backward() + torch.optim.Adam.step(), three times, tracks the oracle doing
+    the same; then a fused batch_update continues from that state (step counters, supports)."""
+    d, meta, m, o = pair("dgcnn_c1")
+    from oracle.redcliff_oracle import make_optimizers
+    hA, hB = make_optimizers(m, 5e-4, 1e-4, 1e-4, 5e-4, 1e-4, 1e-4)
+    oA, oB = make_optimizers(o, 5e-4, 1e-4, 1e-4, 5e-4, 1e-4, 1e-4)
+    Lm = max(meta["L"], meta["F"])
+    bs = batches(d, meta)
+    m.train()
+    o.train()
+    for Xb, Yb in bs[:3]:
+        for model, (A, B), dev in ((m, (hA, hB), "cuda"), (o, (oA, oB), "cpu")):
+            A.zero_grad()
+            B.zero_grad()
+            X = Xb.to(dev)
+            x_sim, _, _, labels = model(X[:, :Lm, :])
+            combo, _ = model.compute_loss(X[:, :meta["F"], :], x_sim, X[:, Lm:Lm + 1, :], labels, Yb.to(dev),
+                                          meta["gc_mode"])
+            combo.backward()
+            A.step()
+            B.step()
+    want = dict((k, v.detach().numpy()) for k, v in o.state_dict().items() if not k.startswith("gen_model."))
+    got = dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items() if not k.startswith("gen_model."))
+    for k in want:
+        scale = max(1.0, float(np.abs(want[k]).max()))
+        assert_close("torch-stepped/" + k, got[k], want[k], 2e-4, 5e-6 * scale)
+    # the fused step picks up torch's step counters and the moved adjacency
+    epoch = meta["pre"] + meta["acc"]
+    o.batch_update(epoch, 0, bs[0][0], bs[0][1], oA, oB, 1)
+    m.batch_update(epoch, 0, bs[0][0], bs[0][1], hA, hB, 1)
+    want = dict((k, v.detach().numpy()) for k, v in o.state_dict().items() if not k.startswith("gen_model."))
+    got = dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items() if not k.startswith("gen_model."))
+    for k in want:
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(want[k]), k
+            continue
+        scale = max(1.0, float(np.abs(want[k]).max()))
+        assert_close("fused-after-torch/" + k, got[k], want[k], 2e-4, 5e-6 * scale)
+
+
+def test_cmlp_forward_and_gc_gradients_match_oracle():
+    import redcliff_amd
+    from oracle.redcliff_oracle import OCMLP
+    torch.manual_seed(3)
+    net = redcliff_amd.cMLP(5, 4, [6]).cuda()
+    torch.manual_seed(3)
+    ref = OCMLP(5, 4, [6])
+    rng = np.random.RandomState(0)
+    X = torch.from_numpy(rng.randn(7, 12, 5).astype(np.float32))
+    Wy = torch.from_numpy(rng.randn(7, 9, 5).astype(np.float32))
+    Xg = X.cuda().requires_grad_(True)
+    Xo = X.clone().requires_grad_(True)
+    y = net(Xg)
+    yo = ref(Xo)
+    assert_close("fwd", y.detach().cpu().numpy(), yo.detach().numpy(), 1e-5, 1e-6)
+    pg = list(net.parameters())
+    po = list(ref.parameters())
+    g = torch.autograd.grad((y * Wy.cuda()).sum(), [Xg] + pg)
+    go = torch.autograd.grad((yo * Wy).sum(), [Xo] + po)
+    for i, (a, b) in enumerate(zip(g, go)):
+        assert_close("cmlp grad %d" % i, a.cpu().numpy(), b.numpy(), 1e-4, 1e-6)
+    for ign in (True, False):
+        G = net.GC(threshold=False, ignore_lag=ign)
+        Go = ref.GC(threshold=False, ignore_lag=ign)
+        Wg = torch.from_numpy(rng.randn(*Go.shape).astype(np.float32))
+        g = torch.autograd.grad((G * Wg.cuda()).sum(), pg, allow_unused=True)
+        go = torch.autograd.grad((Go * Wg).sum(), po, allow_unused=True)
+        for i, (a, b) in enumerate(zip(g, go)):
+            if b is None:
+                assert a is None or not a.abs().max().item()
+                continue
+            assert_close("gc grad %d ign%d" % (i, ign), a.cpu().numpy(), b.numpy(), 1e-4, 1e-6)
+    # MLP.forward (one network) with gradients
+    mlp = net.networks[2]
+    yo2 = ref.networks[2](Xo)
+    y2 = mlp(Xg)
+    assert_close("mlp fwd", y2.detach().cpu().numpy(), yo2.detach().numpy(), 1e-5, 1e-6)
+    a = torch.autograd.grad(y2.sum(), list(mlp.parameters()))
+    b = torch.autograd.grad(yo2.sum(), list(ref.networks[2].parameters()))
+    for i, (x1, x2) in enumerate(zip(a, b)):
+        assert_close("mlp grad %d" % i, x1.cpu().numpy(), x2.numpy(), 1e-4, 1e-6)
+
+
+def test_embedder_forward_on_loaded_model():
+    """general_utils/misc.py:66 calls model.factor_score_embedder(x) on a torch.load-ed model."""
+    d, meta, m, _ = pair("dgcnn_d4ic")
+    m.eval()
+    Xb, _ = batches(d, meta)[0]
+    x = Xb[:, :meta["F"], :].transpose(1, 2).cuda()  # (B, p, F), as misc.py feeds it
+    with torch.no_grad():
+        w_live, _ = m.factor_score_embedder(x)
+    buf = io.BytesIO()
+    torch.save(m, buf)
+    buf.seek(0)
+    m2 = torch.load(buf, weights_only=False)  # this package's own pickled module
+    with torch.no_grad():
+        w_loaded, _ = m2.factor_score_embedder(x)
+    np.testing.assert_array_equal(w_loaded.cpu().numpy(), w_live.cpu().numpy())
+    # a deep copy (best-model snapshots) too
+    m3 = copy.deepcopy(m)
+    with torch.no_grad():
+        w_copy, _ = m3.factor_score_embedder(x)
+    np.testing.assert_array_equal(w_copy.cpu().numpy(), w_live.cpu().numpy())

@@ -1,0 +1,75 @@
+"""Packed grid-search fit (ReplicaPack.fit, the fits/hour unit of BASELINE.metric) against R
+independent fit() calls (models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647, one SLURM task
+per grid point in the reference, train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:
+125-160).  Every replica must end bit-identical to its independent fit -- parameters, BatchNorm
+buffers, loss histories, best epoch, the epoch it stopped at -- including replicas that stop
+at different epochs (a stopped replica leaves the launch's active list)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_replicas import data, make, opts
+
+pytestmark = pytest.mark.gpu
+
+# (seed, FORECAST_COEFF, ADJ_L1 scale, gen_lr, embed_lr, stopping forecast coeff, stopping factor coeff)
+GRID = [
+    (0, 10.0, 0.1, 5e-4, 2e-4, 10.0, 100.0),
+    (1, 1.0, 0.01, 1e-3, 1e-3, 1.0, 100.0),
+    (2, 10.0, 0.01, 5e-4, 1e-4, 10.0, 1.0),
+    (3, 1.0, 0.1, 2e-3, 5e-4, 10.0, 10.0),
+]
+HKEYS = ("avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
+         "avg_adj_penalty", "avg_combo_loss")
+
+
+def true_graphs(K, p, L, seed=11):
+    rng = np.random.RandomState(seed)
+    return [(rng.rand(p, p, L) < 0.3).astype(np.float64) for _ in range(K)]
+
+
+@pytest.mark.parametrize("path", ["vector", "mfma"])
+def test_pack_fit_bitwise_equals_independent_fits(path, monkeypatch, tmp_path):
+    from redcliff_amd import ReplicaPack
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    train = data(64 * 2 + 24, seed=3)
+    val = data(96, seed=4)
+    gc = true_graphs(4, 10, 4)
+    kw = dict(lookback=1, check_every=1, GC=gc, deltaConEps=0.1)
+    max_iter = 9
+    solo = []
+    for s, fc, adj, lrB, lrA, scf, scfa in GRID:
+        m = make(s, fc, adj)
+        oA, oB = opts(m, lrB, lrA)
+        m.fit(None, train, oA, oB, 4, 1, 1, max_iter, val, verbose=0, stopping_criteria_forecast_coeff=scf,
+              stopping_criteria_factor_coeff=scfa, stopping_criteria_cosSim_coeff=1., **kw)
+        torch.cuda.synchronize()
+        solo.append(m)
+    packed = [make(s, fc, adj) for s, fc, adj, _, _, _, _ in GRID]
+    pack = ReplicaPack(packed, [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA, _, _) in zip(packed, GRID)])
+    finals = pack.fit(str(tmp_path), train, val, max_iter, verbose=0,
+                      stopping_criteria_forecast_coeff=[g[5] for g in GRID],
+                      stopping_criteria_factor_coeff=[g[6] for g in GRID], stopping_criteria_cosSim_coeff=1., **kw)
+    torch.cuda.synchronize()
+    stops = []
+    for r, (a, b) in enumerate(zip(solo, packed)):
+        ha, hb = a.fit_history, b.fit_history
+        assert hb["best_it"] == ha["best_it"], r
+        assert hb["stopped_at"] == ha["stopped_at"], r
+        stops.append(ha["stopped_at"])
+        for k in HKEYS:
+            assert hb[k] == ha[k], "replica %d %s" % (r, k)
+        for k in ("f1score_histories", "roc_auc_histories", "deltacon0_histories"):
+            assert hb[k] == ha[k], "replica %d %s" % (r, k)
+        sa, sb = a.state_dict(), b.state_dict()
+        for k in sa:
+            np.testing.assert_array_equal(sb[k].cpu().numpy(), sa[k].cpu().numpy(), err_msg="replica %d %s" % (r, k))
+        # the final model file holds this replica's own parameters only
+        f = os.path.join(str(tmp_path), "replica_%d" % r, "final_best_model.bin")
+        nparam = sum(t.numel() for t in b.parameters())
+        assert os.path.getsize(f) < 4 * nparam * 1.5 + 2 ** 20
+    assert len(finals) == len(GRID)
+    print("stop epochs:", stops)
+    assert any(s is not None for s in stops), "no replica stopped early: the active-list path went untested"
