@@ -1047,36 +1047,37 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
 }
 
-// BatchNorm batch statistics for consecutive batches.  grid (nbatch, R).
+// BatchNorm batch statistics for consecutive batches: one workgroup per (batch, feature),
+// grid (nbatch, F, R).  Two double-precision passes over the batch's B*p values of that
+// feature (the second pass re-reads them from L2), as torch's batch_norm statistics.
 __global__ __launch_bounds__(RC_BLOCK) void k_bn_stats(RedcliffDims d, const float* X, int64_t xr, int64_t N,
                                                        int B, double* st, int64_t str) {
-  const int r = blockIdx.y, bi = blockIdx.x;
+  const int r = blockIdx.z, bi = blockIdx.x, f = blockIdx.y;
   const int64_t b0 = (int64_t)bi * B;
   const int nb = (int)((N - b0) < B ? (N - b0) : B);
   const int p = d.p, F = d.F;
   const int Lmax = rc_lmax(d);
-  const float* Xr = X + r * xr;
+  const float* Xf = X + r * xr + (b0 * d.T + (Lmax - F + f)) * p;
+  const int64_t rs = (int64_t)d.T * p;  // one window (row of the data set) to the next
   __shared__ double red[8];
   const int cnt = nb * p;
-  for (int f = 0; f < F; ++f) {
-    double s = 0.0;
-    for (int e = threadIdx.x; e < cnt; e += RC_BLOCK) {
-      const int b = e / p, cc = e - b * p;
-      s += Xr[((b0 + b) * d.T + (Lmax - F + f)) * p + cc];
-    }
-    const double mean = rc_block_sum_d(s, red) / (double)cnt;
-    double q = 0.0;
-    for (int e = threadIdx.x; e < cnt; e += RC_BLOCK) {
-      const int b = e / p, cc = e - b * p;
-      const double v = Xr[((b0 + b) * d.T + (Lmax - F + f)) * p + cc] - mean;
-      q += v * v;
-    }
-    const double var = rc_block_sum_d(q, red) / (double)cnt;
-    if (threadIdx.x == 0) {
-      double* o = st + r * str + (int64_t)bi * 2 * F;
-      o[f] = mean;
-      o[F + f] = var;
-    }
+  double s = 0.0;
+  for (int e = threadIdx.x; e < cnt; e += RC_BLOCK) {
+    const int b = e / p, cc = e - b * p;
+    s += Xf[b * rs + cc];
+  }
+  const double mean = rc_block_sum_d(s, red) / (double)cnt;
+  double q = 0.0;
+  for (int e = threadIdx.x; e < cnt; e += RC_BLOCK) {
+    const int b = e / p, cc = e - b * p;
+    const double v = Xf[b * rs + cc] - mean;
+    q += v * v;
+  }
+  const double var = rc_block_sum_d(q, red) / (double)cnt;
+  if (threadIdx.x == 0) {
+    double* o = st + r * str + (int64_t)bi * 2 * F;
+    o[f] = mean;
+    o[F + f] = var;
   }
 }
 
@@ -1164,6 +1165,6 @@ int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, floa
 int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,
                        hipStream_t s) {
   const int nbatch = (int)((N + B - 1) / B);
-  hipLaunchKernelGGL(k_bn_stats, dim3(nbatch, d.R), dim3(RC_BLOCK), 0, s, d, X, xr, N, B, st, str);
+  hipLaunchKernelGGL(k_bn_stats, dim3(nbatch, d.F, d.R), dim3(RC_BLOCK), 0, s, d, X, xr, N, B, st, str);
   return rc_check(hipGetLastError(), "k_bn_stats");
 }

@@ -342,9 +342,13 @@ class FitEngine:
         lab = torch.cat(ys, 0).to(self.device, torch.float32).contiguous()
         rows = np.cumsum([0] + sizes[:-1]).astype(np.int64)
         d = self.workspace(max(sizes), Xall.shape[1])
-        stats = [self.bn_stats(d, Xall[r:r + s], s, s) for r, s in zip(rows, sizes)]
+        if all(s == sizes[0] for s in sizes[:-1]) and sizes[-1] <= sizes[0]:
+            # consecutive equal batches (a ragged last one allowed): one launch for all of them
+            stats = self.bn_stats(d, Xall, int(Xall.shape[0]), sizes[0])
+        else:
+            stats = torch.cat([self.bn_stats(d, Xall[r:r + s], s, s) for r, s in zip(rows, sizes)], 0)
         ds = {"X": Xall, "lab": lab, "rows": rows, "sizes": np.asarray(sizes, dtype=np.int32),
-              "stats": torch.cat(stats, 0).contiguous(), "T": int(Xall.shape[1]), "Bmax": max(sizes),
+              "stats": stats.contiguous(), "T": int(Xall.shape[1]), "Bmax": max(sizes),
               "len": len(sizes), "loader": loader}
         self.dataset_cache[key] = ds
         return ds

@@ -7,6 +7,7 @@ re-association of batch reductions); thresholded graphs / F1 identical.
 All compute goes through libredcliff_hip.so (the tests fail if it is not loaded).
 """
 import copy
+import os
 
 import numpy as np
 import pytest
@@ -145,6 +146,8 @@ def test_cmlp_gc_prox_forward_match_reference():
 
 # --------------------------------------------------------------------------- vs the oracle at real sizes
 CONFIGS = {
+    # configs[0] C1: p=10, L=gen_lag=5, K=2, h=25, DGCNN F=16 / 3 layers / 100 hidden, B=128
+    "C1": dict(p=10, L=5, K=2, nsup=2, h=25, F=16, n=3, H=100, B=128, T=100, label_T=100),
     # C1 north-star ratio config: p=10, L=5, K=4, h=25, DGCNN F=16 / 3 layers / 100 hidden, B=128
     "C1K4": dict(p=10, L=5, K=4, nsup=4, h=25, F=16, n=3, H=100, B=128, T=100, label_T=100),
     # C2 D4IC-shaped: p=10, L=4, K=4, h=100, F=20, 2 layers, 30 hidden, labels (N, K, 1), T=21
@@ -152,8 +155,8 @@ CONFIGS = {
     # C4 TST-shaped: p=12, L=4, K=9 (3 supervised), h=25, F=16, 3 layers, 100 hidden, T=150
     "C4": dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, B=128, T=150, label_T=150),
 }
-# C5 stress: p=64, L=20, K=8, h=25, F=64, 3 layers, 100 hidden (B=32 keeps the oracle to seconds)
-C5 = dict(p=64, L=20, K=8, nsup=8, h=25, F=64, n=3, H=100, B=32, T=128, label_T=128)
+# C5 stress: p=64, L=20, K=8, h=25, F=64, 3 layers, 100 hidden
+C5 = dict(p=64, L=20, K=8, nsup=8, h=25, F=64, n=3, H=100, B=128, T=128, label_T=128)
 
 
 def oracle_and_hip(cfg, seed=0):
@@ -188,7 +191,7 @@ def synth(cfg, N, seed):
     return torch.from_numpy(X), torch.from_numpy(Y)
 
 
-@pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1K4", "mfma"), ("C4", "mfma"),
+@pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1", "mfma"), ("C1K4", "mfma"), ("C4", "mfma"),
                                                                         ("C2", "mfma"), ("C1K4", "embgemm"),
                                                                         ("C2", "embgemm")])
 def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
@@ -232,19 +235,87 @@ def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
     np.testing.assert_array_equal(b > 0, a > 0)
 
 
-def test_stress_config_vs_oracle():
-    """C5 (BASELINE configs[4]): p=64, L=20, K=8 -- one step of each phase vs the oracle.
+def _oracle_fp64(o):
+    """A float64 copy of an oracle model (same initial values, exactly widened)."""
+    return copy.deepcopy(o).double()
 
-    At this size the layer-0 contraction is p*L = 1280 long and a step evaluates B*K*p*h =
-    0.4M relu gates and B*K*p*p*L = 21M adjacency-L1 signs.  Any other fp32 summation order
-    (the oracle's MKL conv vs the kernels') flips the odd near-tie gate; a flipped gate changes
-    the gradient of a whole hidden unit's layer-0 row, and Adam's eps-normalised update turns
-    that into a weight change of up to ~lr.  The check is therefore: every tensor within the
-    usual tolerance except at most 5% of its elements, and those within 3*lr per Adam step;
-    the validation losses within 1e-3 relative; GC tensors within 5e-3 relative (a flipped
-    unit moves a group norm by ~0.2%) and the thresholded GC graphs identical."""
-    cfg = C5
+
+class _Float64Default:
+    def __enter__(self):
+        self.prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.float64)
+
+    def __exit__(self, *exc):
+        torch.set_default_dtype(self.prev)
+
+
+class _FlipNearTies:
+    """Run the float64 oracle with every near-tie DECISION of the path taken the other way.
+
+    The path has data-dependent discrete decisions: the ReLU gates of the graph convolution,
+    fc1 and the factor hidden layers, and the sign of every term of the fw-L1 and lag-weighted
+    adjacency-L1 norms (the gradient of |v| is sign(v)).  Where a decision's argument is within
+    fp32 rounding of zero (|v| <= tau * max|v| of its tensor), any fp32 implementation -- the
+    reference's own CPU path included -- may take either branch, and the branch moves the Adam
+    update of the affected weights by up to ~lr (eps-normalised steps).  This context patches
+    torch.relu / F.relu / the L1 torch.norm so that every such decision is flipped; the
+    difference between this run and the plain float64 run bounds what tie resolution alone can
+    change.  ``self.flipped`` counts the flipped decisions."""
+
+    def __init__(self, tau=1e-7):
+        self.tau, self.flipped = tau, {"relu": 0, "l1": 0}
+
+    def _near(self, z, kind):
+        zz = z.detach().abs()
+        m = (zz <= self.tau * zz.max()) & (zz > 0) if zz.numel() else zz > 0
+        self.flipped[kind] += int(m.sum())
+        return m
+
+    def __enter__(self):
+        import torch.nn.functional as F_
+        self.saved = (torch.relu, F_.relu, torch.norm)
+        relu0, norm0 = torch.relu, torch.norm
+
+        def relu(z, inplace=False):
+            gate = (z.detach() > 0) ^ self._near(z, "relu")
+            return z * gate.to(z.dtype)
+
+        def norm(x, p="fro", dim=None, keepdim=False, out=None, dtype=None):
+            if p == 1 and dim is None and not keepdim:
+                s = torch.sign(x.detach())
+                s = torch.where(self._near(x, "l1"), -s, s)
+                return (x * s).sum()
+            return norm0(x, p, dim, keepdim, out, dtype)
+
+        torch.relu, F_.relu, torch.norm = relu, relu, norm
+        return self
+
+    def __exit__(self, *exc):
+        import torch.nn.functional as F_
+        torch.relu, F_.relu, torch.norm = self.saved
+
+
+def test_stress_config_error_budget_vs_fp64():
+    """C5 (BASELINE configs[4]): p=64, L=20, K=8, B=128 -- the pretrain -> acclimate -> combined
+    schedule, judged against the SAME oracle run in float64 from the same initial values and
+    inputs.  Error budget, element-wise for every parameter / buffer, validation loss and GC value:
+
+        |HIP - fp64| <= |oracle_fp32 - fp64| + |fp64_tieflip - fp64| + 1e-4 |fp64| + 1e-7
+
+    i.e. the HIP path may not be further from the exact result than the reference's own fp32
+    arithmetic is, plus what resolving the near-tie decisions the other way moves (a float64
+    run with every ReLU gate / L1 sign within fp32 rounding of zero flipped, _FlipNearTies),
+    plus the north-star 1e-4 relative.  Why the tie term is needed: at this size a step takes
+    0.8 M embedder gates, 0.8 M factor gates and 67 M adjacency-L1 signs, so a few of them sit
+    within fp32 rounding of zero (the float64 run has a graph-conv pre-activation of 5e-8 in
+    hidden column 0 in the combined step); the fp32 oracle and the HIP kernels resolve such
+    ties independently, and a tie taken the other way moves that column's eps-normalised Adam
+    update by up to ~lr.  The thresholded GC graphs must equal the float64 graphs."""
+    cfg = dict(C5, B=128)
+    dump = {} if os.environ.get("REDCLIFF_C5_DUMP") else None
     o, m = oracle_and_hip(cfg)
+    o64 = _oracle_fp64(o)
+    o64f = _oracle_fp64(o)
     X, Y = synth(cfg, cfg["B"], seed=5)
     from oracle.redcliff_oracle import make_optimizers
     lr = 5e-4
@@ -253,33 +324,67 @@ def test_stress_config_vs_oracle():
     for epoch in (0, 1, 2):
         o.batch_update(epoch, 0, X, Y, oA, oB, 1)
         m.batch_update(epoch, 0, X, Y, hA, hB, 1)
-    want = dict((k, v.detach().numpy()) for k, v in o.state_dict().items() if not k.startswith("gen_model."))
-    got = dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items() if not k.startswith("gen_model."))
-    for k in want:
-        if k.endswith("num_batches_tracked"):
-            assert int(got[k]) == int(want[k]), k
+    with _Float64Default():
+        dA, dB = make_optimizers(o64, lr, 1e-4, 1e-4, lr, 1e-4, 1e-4)
+        for epoch in (0, 1, 2):
+            o64.batch_update(epoch, 0, X.double(), Y.double(), dA, dB, 1)
+        fA, fB = make_optimizers(o64f, lr, 1e-4, 1e-4, lr, 1e-4, 1e-4)
+        with _FlipNearTies() as flip:
+            for epoch in (0, 1, 2):
+                o64f.batch_update(epoch, 0, X.double(), Y.double(), fA, fB, 1)
+    print("near-tie decisions flipped in the float64 tie run: %s" % flip.flipped)
+    fails = []
+    n_tie = [0]
+
+    def budget(tag, hip, o32, o64_, tie):
+        h, a, x, t = (np.asarray(v, np.float64) for v in (hip, o32, o64_, tie))
+        plain = np.abs(a - x) + 1e-4 * np.abs(x) + 1e-7
+        over = np.abs(h - x) - (plain + np.abs(t - x))
+        n_tie[0] += int((np.abs(h - x) > plain).sum())
+        n = int((over > 0).sum())
+        if n:
+            i = int(np.argmax(over))
+            fails.append("%s: %d/%d entries outside the fp64 error budget (worst excess %.3e at fp64 %.6e: "
+                         "HIP %.6e, oracle fp32 %.6e, tie-flipped fp64 %.6e)" % (
+                             tag, n, x.size, over.max(), x.flat[i], h.flat[i], a.flat[i], t.flat[i]))
+        if dump is not None and not tag.startswith("factors."):
+            dump[tag] = np.stack([h, a, x, t]).astype(np.float64)
+
+    s64, s64f, s32, got = o64.state_dict(), o64f.state_dict(), o.state_dict(), m.state_dict()
+    for k in s64:
+        if k.startswith("gen_model."):
             continue
-        g, w = got[k].astype(np.float64), want[k].astype(np.float64)
-        err = np.abs(g - w)
-        bad = err > 5e-6 * max(1.0, np.abs(w).max()) + 2e-4 * np.abs(w)
-        assert bad.mean() <= 0.05, "%s: %d/%d elements off" % (k, int(bad.sum()), w.size)
-        assert err.max() <= 3 * lr * 2, "%s: max err %.3e beyond what a flipped gate can explain" % (k, err.max())
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(s64[k]) == int(s32[k]), k
+            continue
+        budget(k, got[k].detach().cpu().numpy(), s32[k].detach().numpy(), s64[k].detach().numpy(),
+               s64f[k].detach().numpy())
     Xv, Yv = synth(cfg, 40, seed=9)
     ov = o.validate([(Xv, Yv)])
+    with _Float64Default():
+        ov64 = o64.validate([(Xv.double(), Yv.double())])
+        ov64f = o64f.validate([(Xv.double(), Yv.double())])
     hv = m.validate_training([(Xv, Yv)], 1, cfg["p"], *[[] for _ in range(5)])
     for i, k in enumerate(["forecast", "factor", "cos", "fw_l1", "smooth", "adj"]):
-        assert_close("val/" + k, hv[i], ov[k], 1e-3, 1e-6)
-    o.eval()
-    m.eval()
+        budget("val/" + k, hv[i], ov[k], ov64[k], ov64f[k])
+    for mod in (o, o64, o64f, m):
+        mod.eval()
     Lm = max(cfg["L"], cfg["F"])
+    gcs = []
     with torch.no_grad():
-        go = o.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm], threshold=False, ignore_lag=True)
-        gm = m.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm].cuda(), threshold=False, ignore_lag=True)
-    a = np.stack([np.stack([g.numpy() for g in row]) for row in go])
-    b = np.stack([np.stack([g.cpu().numpy() for g in row]) for row in gm])
-    assert_close("GC", b, a, 5e-3, 1e-5)
-    clear = np.abs(a) > 1e-5  # thresholded graph (GC > 0) identical wherever the sign is not a tie
-    np.testing.assert_array_equal((b > 0)[clear], (a > 0)[clear])
+        gcs.append(m.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm].cuda(), threshold=False, ignore_lag=True))
+        gcs.append(o.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm], threshold=False, ignore_lag=True))
+        with _Float64Default():
+            for mod in (o64, o64f):
+                gcs.append(mod.GC("conditional_factor_fixed_embedder", X=Xv[:8, :Lm].double(), threshold=False,
+                                  ignore_lag=True))
+    b, a, x, t = [np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in gc]) for gc in gcs]
+    budget("GC", b, a, x, t)
+    print("entries outside the plain budget, inside the tie-resolution term: %d" % n_tie[0])
+    if dump is not None:
+        np.savez_compressed(os.environ["REDCLIFF_C5_DUMP"], **dict((k, v) for k, v in dump.items() if v[0].size < 2e4))
+    assert not fails, "\n".join(fails)
+    np.testing.assert_array_equal(b > 0, x > 0)
 
 
 def test_fit_trace_matches_reference():
