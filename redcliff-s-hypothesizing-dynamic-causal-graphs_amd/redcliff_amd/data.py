@@ -23,11 +23,26 @@ generator and the normalised window set that feeds ``fit`` with device-resident 
   reaches ~1.6 k samples/s), the normalised windows are materialised once and moved to
   HBM; ``batches`` then yields the DataLoader's batch sequence as views.
 
+* ``NormalizedRecordingDirectory`` reads the reference's subset-pickle directories:
+  ``kind="dream4"`` restates data/dream4_datasets.py:18-157 (NormalizedDREAM4Dataset: files
+  named ``subset_*``, no grid-search cut) and ``kind="lfp"`` restates
+  data/local_field_potential_datasets.py:18-187 (NormalizedLocalFieldPotentialDataset: files
+  named ``*_subset*``, optional region averaging :118-132 applied before the statistics and
+  to every item, the grid-search tenth :109-112); ``kind="synthetic"`` is
+  NormalizedSyntheticWVARDataset's file filter.  Each file is unpickled once (the reference
+  re-opens a file per sample in the statistics pass and per item), the statistics keep the
+  reference's operation order on the arrays as stored, and the same shuffle / cut / item
+  arithmetic applies; ``*_train_test_split`` mirror the loaders' ``train`` / ``validation``
+  split (:168-189 / :198-219).
+
 Per-edge activations are integer codes (``ACT_*``) instead of lambdas; the curation
 script's two patterns are identity and ``[min(x, 0), max(x, 0)]`` per lag
 (data/currate_sVARwInnovativeContinuousGaussianNoise_data_etNL.py:272-275).
 """
+import os
+import pickle
 import random
+import shutil
 
 import numpy as np
 import torch
@@ -161,9 +176,13 @@ class NormalizedWindowSet:
     recordings: sequence of (T, D) float64 arrays (the reference's ``sample[0]``, file
     order); labels: matching (K, T) arrays.  Attributes mirror the reference:
     ``channel_means`` (1, D) float64 numpy, ``channel_std_devs`` (1, D) float64 torch,
-    ``data`` = the kept recording indices after the shuffle / grid-search cut."""
+    ``data`` = the kept recording indices after the shuffle / grid-search cut.
+    ``grid_fraction`` is the grid-search cut (4: the synthetic quarter, 10: the LFP tenth,
+    None: no cut, DREAM4); ``fortran_sums`` reproduces the synthetic recordings' memory layout
+    in the statistics (the reference stores ``curr_samp.T``), False sums the arrays as given."""
 
-    def __init__(self, recordings, labels, shuffle=True, shuffle_seed=0, grid_search=True):
+    def __init__(self, recordings, labels, shuffle=True, shuffle_seed=0, grid_search=True, grid_fraction=4,
+                 fortran_sums=True):
         self.recordings = [np.asarray(r) for r in recordings]
         self.labels = [np.asarray(y) for y in labels]
         accepted = [i for i, r in enumerate(self.recordings) if not np.isnan(np.sum(r))]
@@ -171,23 +190,24 @@ class NormalizedWindowSet:
             raise ValueError("no finite recordings")
         T, D = self.recordings[accepted[0]].shape
         self.num_time_steps, self.num_chans = T, D
+        lay = np.asfortranarray if fortran_sums else (lambda a: a)
         summed = None
         for i in accepted:                       # synthetic_datasets.py:66-73 (sequential sum)
             summed = self.recordings[i] if summed is None else summed + self.recordings[i]
         n = len(accepted)
         # the reference's synthetic recordings are ``curr_samp.T`` (Fortran-ordered, kept
         # by pickle) and numpy's reduction order follows the memory layout: sum the same way
-        self.channel_means = (np.sum(np.asfortranarray(summed), axis=0) / (1. * n * T)).reshape(1, D)
+        self.channel_means = (np.sum(lay(summed), axis=0) / (1. * n * T)).reshape(1, D)
         sq = None
         for i in accepted:                       # :89-104
             d2 = (self.recordings[i] - self.channel_means) ** 2.
             sq = d2 if sq is None else sq + d2
-        self.channel_std_devs = torch.from_numpy(np.sqrt(np.sum(np.asfortranarray(sq), axis=0) / (1. * n * T))).reshape(1, D)
+        self.channel_std_devs = torch.from_numpy(np.sqrt(np.sum(lay(sq), axis=0) / (1. * n * T))).reshape(1, D)
         self.data = list(accepted)
         if shuffle:
             random.Random(shuffle_seed).shuffle(self.data)
-        if grid_search:
-            self.data = self.data[:len(self.data) // 4]
+        if grid_search and grid_fraction:
+            self.data = self.data[:len(self.data) // grid_fraction]
 
     def __len__(self):
         return len(self.data)
@@ -213,3 +233,104 @@ class NormalizedWindowSet:
         device-resident views."""
         X, Y = self.materialize(device, dtype)
         return [(X[i:i + batch_size], Y[i:i + batch_size]) for i in range(0, X.shape[0], batch_size)]
+
+
+# --------------------------------------------------------------------------- subset-pickle directories
+_FILE_FILTERS = {
+    "dream4": lambda x: "subset_" in x,                      # dream4_datasets.py:38
+    "lfp": lambda x: "_subset" in x,                         # local_field_potential_datasets.py:40
+    "synthetic": lambda x: "_subset" in x or "subset_" in x,  # synthetic_datasets.py:41
+}
+_GRID_FRACTION = {"dream4": None, "lfp": 10, "synthetic": 4}
+
+
+def average_regions(signal, average_region_map):
+    """local_field_potential_datasets.py:118-132: (T, C) -> (T, R) float64, region r the mean of
+    its listed channels, regions in the map's key order."""
+    out = np.zeros((signal.shape[0], len(average_region_map)))
+    for i, name in enumerate(average_region_map.keys()):
+        out[:, i] = np.mean(signal[:, average_region_map[name]], axis=1)
+    return out
+
+
+def _load_subset_file(path):
+    """One subset file of the reference's curated data sets: a pickled list of
+    (x (T, C), y, ...) samples written by the user's data-curation scripts."""
+    with open(path, "rb") as fh:
+        return pickle.load(fh)
+
+
+class NormalizedRecordingDirectory(NormalizedWindowSet):
+    """The reference's per-directory normalised data sets (DREAM4, LFP, synthetic subsets).
+
+    ``file_order`` overrides ``os.listdir(data_path)`` (the reference's file order, which is the
+    filesystem's); the remaining arguments follow the reference constructors.  Only the
+    ``"original"`` signal format is on the fitting path (directed-spectrum / flattened formats
+    feed other model families)."""
+
+    def __init__(self, data_path, kind="dream4", shuffle=True, shuffle_seed=0, grid_search=True,
+                 average_region_map=None, signal_format="original", file_order=None):
+        if kind not in _FILE_FILTERS:
+            raise ValueError("kind must be one of %s" % sorted(_FILE_FILTERS))
+        if signal_format != "original":
+            raise NotImplementedError("signal_format %r is not on the REDCLIFF-S fitting path" % signal_format)
+        if average_region_map is not None and kind != "lfp":
+            raise ValueError("average_region_map applies to LFP data sets only")
+        names = list(os.listdir(data_path)) if file_order is None else list(file_order)
+        self.files = [x for x in names if _FILE_FILTERS[kind](x) and ".pkl" in x and "metadata" not in x]
+        self.data_path, self.kind, self.average_region_map = data_path, kind, average_region_map
+        recs, labs, self.sources = [], [], []
+        x_ind, y_ind = 0, (3 if kind == "synthetic" else 1)
+        for name in self.files:
+            for j, smp in enumerate(_load_subset_file(os.path.join(data_path, name))):
+                x = np.asarray(smp[x_ind])
+                if kind == "synthetic" and x.ndim > 2:
+                    x = x[0]
+                if average_region_map is not None:
+                    x = average_regions(x, average_region_map)
+                recs.append(x)
+                labs.append(np.asarray(smp[y_ind]))
+                self.sources.append((os.path.join(data_path, name), j))
+        super().__init__(recs, labs, shuffle=shuffle, shuffle_seed=shuffle_seed, grid_search=grid_search,
+                         grid_fraction=_GRID_FRACTION[kind], fortran_sums=False)
+
+    def source(self, index):
+        """(file path, position in file) of item ``index`` -- the reference's ``data[index]``."""
+        return self.sources[self.data[index]]
+
+
+def _split_dirs(data_root_path, train_portion, name_filter):
+    """The loaders' one-time train / validation split of a root directory's subset files
+    (dream4_datasets.py:168-183, local_field_potential_datasets.py:198-213): the first
+    train_portion of os.listdir's subset files are copied to ``train``, the rest to ``validation``."""
+    train_path, val_path = os.path.join(data_root_path, "train"), os.path.join(data_root_path, "validation")
+    if not os.path.exists(train_path):
+        assert not os.path.exists(val_path)
+        os.mkdir(train_path)
+        os.mkdir(val_path)
+        files = [x for x in os.listdir(data_root_path) if name_filter(x) and ".pkl" in x]
+        cut = int(train_portion * len(files))
+        for f in files[:cut]:
+            shutil.copy(os.path.join(data_root_path, f), os.path.join(train_path, f))
+        for f in files[cut:]:
+            shutil.copy(os.path.join(data_root_path, f), os.path.join(val_path, f))
+    return train_path, val_path
+
+
+def load_normalized_DREAM4_data_train_test_split(data_root_path, batch_size, shuffle=True, shuffle_seed=0,
+                                                 train_portion=0.8, grid_search=True, device=None):
+    """dream4_datasets.py:168-189 -> (train batches, validation batches), device-resident."""
+    tp, vp = _split_dirs(data_root_path, train_portion, lambda x: "subset_" in x)
+    return tuple(NormalizedRecordingDirectory(p, "dream4", shuffle, shuffle_seed, grid_search).batches(batch_size, device)
+                 for p in (tp, vp))
+
+
+def load_normalized_lfp_data_train_test_split(data_root_path, batch_size, shuffle=True, shuffle_seed=0,
+                                              train_portion=0.8, grid_search=True, average_region_map=None,
+                                              device=None):
+    """local_field_potential_datasets.py:198-219 -> (train batches, validation batches).  The
+    reference copies files whose names contain ``subset_`` here but its data set then reads only
+    ``*_subset*`` names (:40 vs :207); both filters are kept as written."""
+    tp, vp = _split_dirs(data_root_path, train_portion, lambda x: "subset_" in x)
+    return tuple(NormalizedRecordingDirectory(p, "lfp", shuffle, shuffle_seed, grid_search, average_region_map)
+                 .batches(batch_size, device) for p in (tp, vp))

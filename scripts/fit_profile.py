@@ -36,6 +36,19 @@ def main():
     rng = np.random.RandomState(3)
     true_gc = [(rng.rand(c["p"], c["p"], 2) > 0.7).astype(np.float64) for _ in range(c["K"])]
 
+    # unwrapped fit first (the breakdown's synchronising wrappers serialise host and device)
+    m0 = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).cuda()
+    oA0, oB0 = bench.adam_pair(m0, c)
+    m0.fit(None, train, oA0, oB0, c["L"], 1, 1, 2, val, lookback=2, check_every=1, verbose=0, GC=true_gc)  # warm-up
+    m0 = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).cuda()
+    oA0, oB0 = bench.adam_pair(m0, c)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m0.fit(None, train, oA0, oB0, c["L"], 1, 1, args.epochs, val, lookback=args.epochs, check_every=1, verbose=0,
+           GC=true_gc, stopping_criteria_forecast_coeff=10., stopping_criteria_factor_coeff=100.,
+           stopping_criteria_cosSim_coeff=1.)
+    torch.cuda.synchronize()
+    unwrapped = time.perf_counter() - t0
     times = {}
 
     def wrap(owner, name, key):
@@ -52,12 +65,18 @@ def main():
         return f
 
     saved = [(fit_loop.M, n, wrap(fit_loop.M, n, n)) for n in
-             ("track_roc_stats", "track_deltacon_stats", "track_l1_stats", "track_cosine_stats", "track_gc_progress")
+             ("track_roc_stats", "track_deltacon_stats", "track_l1_stats", "track_cosine_stats", "track_gc_progress",
+              "gc_progress_values", "track_roc_stats_from_values", "track_deltacon_stats_from_values",
+              "track_cosine_stats_batched")
              if hasattr(fit_loop.M, n)]
     saved.append((fit_loop.copy, "deepcopy", wrap(fit_loop.copy, "deepcopy", "deepcopy")))
     eng_cls = type(m.engine())
     saved.append((eng_cls, "run_steps", wrap(eng_cls, "run_steps", "train_steps")))
-    for n in ("run_values", "cache_dataset", "forward_outputs", "gc_norms", "bn_stats"):
+    from redcliff_amd import engine as engmod
+    saved.append((engmod.StepPlan, "run", wrap(engmod.StepPlan, "run", "train_steps(plan)")))
+    saved.append((fit_loop.FitTracker, "gc_progress", wrap(fit_loop.FitTracker, "gc_progress", "tracker.gc_progress")))
+    saved.append((fit_loop.FitTracker, "step", wrap(fit_loop.FitTracker, "step", "tracker.step")))
+    for n in ("run_values", "cache_dataset", "forward_outputs", "gc_norms", "bn_stats", "embed_raw"):
         saved.append((eng_cls, n, wrap(eng_cls, n, "eng." + n)))
     saved.append((fit_loop, "_best_model", wrap(fit_loop, "_best_model", "best_model_snapshot")))
     cls = type(m)
@@ -74,6 +93,7 @@ def main():
         setattr(owner, name, f)
     out = {"config": args.config, "epochs": args.epochs, "train_batches": args.train_batches, "B": B,
            "fit_s": round(total, 4), "per_epoch_ms": round(1e3 * total / args.epochs, 2),
+           "unwrapped_fit_s": round(unwrapped, 4), "unwrapped_per_epoch_ms": round(1e3 * unwrapped / args.epochs, 2),
            "breakdown_ms_per_epoch": dict((k, round(1e3 * v / args.epochs, 2)) for k, v in sorted(times.items()))}
     print(json.dumps(out), flush=True)
 
