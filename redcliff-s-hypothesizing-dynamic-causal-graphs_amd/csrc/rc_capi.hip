@@ -321,7 +321,17 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if ((e = timed(KT_FAC_MIX, s, [&] { return rc_launch_fac_mix(c, s); }))) return e;
     if ((e = stream_wait(sf, s, aux->ev[0]))) return e;  // dW0 needs the mixing's dL/dy
     if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf); }))) return e;
-  } else if (fac) {
+  }
+  // Merged backward (vector factor path + fused embedder, one stream, training without loss
+  // values): factor and embedder backward in one launch, the embedder workgroups waiting only
+  // for the factor-lead workgroups' dL/dw / dL/dA records (k_bwd_merged), when its grid fits the
+  // chip at once (rc_bwd_merged_grid: D4IC 0.097 -> 0.083 ms per step).  REDCLIFF_MERGE=0 / 1
+  // forces the two launches / the merged one (same bits).
+  const char* mv = getenv("REDCLIFF_MERGE");
+  const char* dv0 = getenv("REDCLIFF_DEFER");
+  const bool merged = fac && !mfma && !fork && !egemm && emb_grad && !(fl & RC_VALUES) && !(dv0 && strcmp(dv0, "1") != 0) &&
+                      (mv ? strcmp(mv, "0") != 0 : rc_bwd_merged_grid(c) > 0);
+  if (!mfma && fac && !merged) {
     if (fork && (e = stream_wait(sf, s, aux->ev[1]))) return e;  // the mixing needs the embedder output w
     if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf); }))) return e;
     if (fork && (e = stream_wait(s, sf, aux->ev[0]))) return e;
@@ -334,6 +344,10 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
            return e2 ? e2 : rc_launch_emb_bwd(c, s, false);
          })))
       return e;
+  } else if (merged) {
+    c.defer = 1;
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_bwd_merged(c, s); }))) return e;
+    if ((e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (emb_grad) {
     // The node blocks' window-block partials are summed by a separate k_emb_combine launch
     // instead of the in-kernel last arriver (ticket + agent-scope fences): the fences cost the

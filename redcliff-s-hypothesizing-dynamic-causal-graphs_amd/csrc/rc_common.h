@@ -31,7 +31,8 @@ struct WsOff {
   int64_t w1;     // [K][p][h]         pre-update snapshot of the factor output weights
   int64_t gq;     // [nU][K][p][p*L]   squared layer-0 group norms, partial over hidden chunks
   int64_t ebp;    // [p*nch][nbw][pst] embedder-backward partials per (node, chunk, window block)
-  int64_t ecnt;   // [p*nch]           arrival counters of those blocks (u32, self-resetting)
+  int64_t ecnt;   // [p*nch + 1]       arrival counters of those blocks (u32, self-resetting); the last
+                  //                   slot counts published factor-lead workgroups (k_bwd_merged)
   int64_t gfc1;   // [M1][p*H]         fc1 weight gradient (combined by the node blocks)
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
@@ -162,7 +163,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.w1, K * p * d.h);
   put(o.gq, (int64_t)rc_nuchunk(d) * K * p * p * d.L);
   put(o.ebp, (int64_t)p * rc_nchunk(d) * rc_emb_nbw(d) * rc_emb_pstride(d));
-  put(o.ecnt, p * rc_nchunk(d));
+  put(o.ecnt, p * rc_nchunk(d) + 1);  // + the merged backward's factor-lead counter
   put(o.gfc1, (int64_t)d.M1 * p * d.H);
   put(o.dwp, p * B * K);
   put(o.dAadj, K * p * p);
@@ -279,6 +280,37 @@ inline int rc_rep_host(const StepCtx& c, int i) { return rc_rep(c, i); }
 
 // ---------------------------------------------------------------------------------------------
 // device helpers
+
+// Producer / consumer hand-off between workgroups of ONE launch (k_bwd_merged): every producer
+// workgroup drains its stores, one lane releases them at agent scope (all XCDs) and counts
+// itself in; a consumer's lane 0 polls the count (agent-scope loads, s_sleep between polls),
+// acquires, and the workgroup proceeds.  Producers have lower workgroup ids than their consumers
+// and never wait, so they are dispatched first and finish (no co-residency assumption); the
+// poll is bounded all the same, so a missing producer cannot hang the GPU.
+__device__ inline void rc_publish(unsigned* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ inline void rc_wait_count(const unsigned* cnt, unsigned target) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++spins < (1u << 24))
+      __builtin_amdgcn_s_sleep(2);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// the merged backward's factor-lead counter of replica slice `ws`
+__device__ inline unsigned* rc_fac_lead_cnt(const StepCtx& c, float* ws) {
+  return reinterpret_cast<unsigned*>(ws + c.wo.ecnt) + c.d.p * ((c.d.H + EMB_HC - 1) / EMB_HC);
+}
+
 __device__ inline float rc_wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -458,7 +490,9 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
-int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);  // window-block partials (c.defer)
+int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);
+int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s);  // factor + embedder backward, one launch
+int rc_bwd_merged_grid(const StepCtx& c);                    // its grid, 0 when not worth it  // window-block partials (c.defer)
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,
                        WsOff wo, hipStream_t s);
 int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,

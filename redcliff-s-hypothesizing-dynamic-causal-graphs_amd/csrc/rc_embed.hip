@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "rc_common.h"
+#include "rc_fac_bwd.h"
 
 namespace {
 
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_cos_values(StepCtx c) {
 // ------------------------------------------------------------------------------------------
 // K3 head workgroup (launched only for loss values / the confusion matrix): the
 // coefficient-normalised loss terms of validate_training and the factor-score confusion.
-__device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
+__device__ __forceinline__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
   const RedcliffDims& d = c.d;
   const int K = d.K, B = c.B, p = d.p, nsup = d.nsup;
   const float* E = c.emb + r * c.es;
@@ -234,7 +235,8 @@ __device__ void emb_bwd_head(const StepCtx& c, int r, float* sm) {
 // cdna_hip_programming.md §6 Guideline 16).  The first sub-block's inputs and the
 // fixed operands are staged by one multi-segment pass (one memory latency for everything).
 template <bool MULTI>
-__device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, int WPB, float* sm) {
+__device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, int WPB, float* sm,
+                             const unsigned* wait_cnt = nullptr, unsigned wait_target = 0) {
   const RedcliffDims& d = c.d;
   const int K = d.K, M1 = d.M1, B = c.B, p = d.p, H = d.H, F = d.F, n = d.n;
   const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC, HP = EMB_HC + 1;
@@ -343,7 +345,10 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
       t += __shfl_xor(t, 2);
       if (dg == 0 && i0 + ditem < nitem) dwl[i0 + ditem] = t;
     };
-    dw_load(0);
+    // merged launch: the factor-side partials come from the same launch's factor-lead workgroups;
+    // stage everything else first, then wait for them
+    const bool wait_now = wait_cnt != nullptr && it == 0;
+    if (!wait_now) dw_load(0);
     __syncthreads();  // the previous sub-block is done with the LDS tiles
     if (it == 0) {
       rc_stage_all(
@@ -361,6 +366,10 @@ __device__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, 
             return S[((int64_t)i * p + node) * p + cc];
           }, [&](int e, float v) { Srow[e] = v; }),
           sR, sT, sX, sF1, sW, sL);
+      if (wait_now) {
+        rc_wait_count(wait_cnt, wait_target);
+        dw_load(0);
+      }
       dw_store(0);
       for (int i0 = RC_BLOCK / 4; i0 < nitem; i0 += RC_BLOCK / 4) {
         dw_load(i0);
@@ -640,7 +649,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
 
 // Adjacency-L1 gradient of A summed over the K factors' records, in place into record 0
 // (fixed order, every load in flight at once: K <= 16).
-__device__ void emb_bwd_dadj(const StepCtx& c, int r, int blk) {
+__device__ __forceinline__ void emb_bwd_dadj(const StepCtx& c, int r, int blk) {
   const int pp2 = c.d.p * c.d.p, e = blk * RC_BLOCK + threadIdx.x;
   if (e >= pp2) return;
   float* dA = c.ws + r * c.wss + c.wo.dAadj;
@@ -671,6 +680,52 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int 
     const int grp = blockIdx.x / nbw, wb = blockIdx.x - grp * nbw;
     emb_bwd_node<MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
   }
+}
+
+// Merged backward launch (vector factor path + fused embedder, training steps without loss
+// values): the factor backward and the embedder backward in ONE grid instead of two dependent
+// launches.  The embedder backward needs only the factor-side dL/dw partials and the
+// adjacency-L1 dL/dA records, which the K*p factor-lead workgroups (mixing, forecast residual,
+// adjacency L1) write early; the rest of the factor backward (dW0 / Adam) is independent of
+// it.  Workgroup order: [K*p factor leads][embedder node / head / dA-reduce workgroups][the
+// other factor workgroups]; node and reduce workgroups wait on the leads' published count
+// (rc_wait_count), everything else runs free.  Same arithmetic in the same order as the two
+// launches, so the results are bit-identical (tests/test_gpu_replicas.py).
+template <bool MULTI>
+__global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int nQ, int nnode, int head, int nred,
+                                                         int BC, int WPB) {
+  extern __shared__ float sm[];
+  const int r = rc_rep(c, blockIdx.y);
+  unsigned* cnt = rc_fac_lead_cnt(c, c.ws + r * c.wss);
+  const int KP = c.d.K * c.d.p;
+  const int bx = blockIdx.x;
+  const int nemb = nnode + head + nred;
+  const int e = bx - KP;
+  if (e >= 0 && e < nemb) {
+    if (e >= nnode + head) {
+      rc_wait_count(cnt, KP);
+      emb_bwd_dadj(c, r, e - nnode - head);
+    } else if (e == nnode) {
+      emb_bwd_head(c, r, sm);
+    } else {
+      const int nch = rc_nchunk(c.d), nbw = (c.B + WPB - 1) / WPB;
+      const int grp = e / nbw, wb = e - grp * nbw;
+      emb_bwd_node<MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm, cnt, (unsigned)KP);
+    }
+    return;
+  }
+  // factor workgroups: the K*p leads first (ids [0, K*p)), the rest after the embedder's
+  int kj, uc = 0, qc = 0;
+  if (e < 0) {
+    kj = bx;
+  } else {
+    const int f = e - nemb, per = nUl * nQ - 1;
+    kj = f / per;
+    const int rem = f - kj * per + 1;
+    uc = rem / nQ;
+    qc = rem - uc * nQ;
+  }
+  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, r, sm, e < 0 ? cnt : nullptr);
 }
 
 // ---- adjacency algebra for p <= 64 in one workgroup, operands in LDS with row stride P = p + 1
@@ -1119,6 +1174,62 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
     hipLaunchKernelGGL(k_emb_bwd<false>, dim3(nnode + head + nred, c.nrep), dim3(RC_BLOCK), lds, s, c, nnode, head, BC, WPB);
   }
   return rc_check(hipGetLastError(), "k_emb_bwd");
+}
+
+// Workgroups of the merged launch, or 0 when it should not be used: the embedder side must be
+// the single-sub-block variant (the multi-sub-block one needs 256 VGPRs), and the whole grid
+// must fit the chip at once at the merged kernel's occupancy (174 VGPRs: 2 workgroups of 256
+// lanes per CU) -- otherwise the factor body's register budget throttles the embedder
+// workgroups and the two launches are faster (C1(K=4): 81 us merged vs 29 + 41 us).
+int rc_bwd_merged_grid(const StepCtx& c) {
+  const RedcliffDims& d = c.d;
+  if (rc_emb_wpb(d) > rc_emb_bc(d)) return 0;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  const int Q = d.p * d.L;
+  const int nQ = (c.flags & RC_STEP_B) ? (Q + FB_QT - 1) / FB_QT : 1;
+  const int nUl = (c.flags & RC_STEP_B) ? rc_nuchunk(d) : 1;
+  const int WPB = rc_emb_wpb(d);
+  const int nnode = d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB);
+  const int head = (c.flags & RC_CONFUSION) ? 1 : 0;
+  const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
+  const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
+  const int grid = d.K * d.p * nUl * nQ + nnode + head + nred;
+  return (int64_t)grid * c.nrep <= 2 * (int64_t)cus ? grid : 0;
+}
+
+// The merged backward (k_bwd_merged); requires the deferred combine (c.defer == 1) and no
+// loss values (the head's loss sums read the factor leads' records).
+int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  if (c.defer != 1 || (c.flags & RC_VALUES)) { rc_set_error("merged backward: needs defer == 1 and no values"); return REDCLIFF_EINVAL; }
+  const size_t le = rc_emb_bwd_lds(d), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
+  const size_t lds = le > lf ? le : lf;
+  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("merged backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  const int Q = d.p * d.L;
+  const int nQ = (c.flags & RC_STEP_B) ? (Q + FB_QT - 1) / FB_QT : 1;
+  const int nUl = (c.flags & RC_STEP_B) ? rc_nuchunk(d) : 1;
+  const int BC = rc_emb_bc(d), WPB = rc_emb_wpb(d);
+  const int nnode = d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB);
+  const int head = (c.flags & RC_CONFUSION) ? 1 : 0;
+  const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
+  const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
+  const int KP = d.K * d.p;
+  const int grid = KP * nUl * nQ + nnode + head + nred;
+  if (WPB > BC) {
+    int e = rc_lds_optin(k_bwd_merged<true>, lds, "k_bwd_merged LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_bwd_merged<true>, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, nnode, head, nred, BC, WPB);
+  } else {
+    int e = rc_lds_optin(k_bwd_merged<false>, lds, "k_bwd_merged LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_bwd_merged<false>, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, nnode, head, nred, BC, WPB);
+  }
+  return rc_check(hipGetLastError(), "k_bwd_merged");
 }
 
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {

@@ -14,377 +14,17 @@
 #include <cstring>
 
 #include "rc_common.h"
+#include "rc_fac_bwd.h"
 
 namespace {
 
-#define FB_BT 128   // windows per backward tile (the whole batch at B <= 128)
-#define FB_QT 64    // dW0 columns per backward tile
-
-__device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
-  const int L = c.d.L;
-  const int ch = dL.div(q), t = q - ch * L;
-  return X[((c.row0 + b) * c.d.T + (c.Lmax - L + t)) * c.d.p + ch];
-}
-
-// ------------------------------------------------------------------------------------------
-// K2b: mixing, forecast loss, adjacency L1, backward and Adam.  grid (K*p*nU*nQ, R):
-// workgroup (network kj, hidden chunk uc, dW0 column tile qc).  The cheap per-window work
-// (x_sim, residual, dL/dy, adjacency-L1 signs) is recomputed by every workgroup of a network;
-// its outputs (dL/dw partials, loss values, dL/dA) are written by the (uc, qc) = (0, 0) one.
-// Latency structure: every global operand of the workgroup -- predictions, embedder outputs,
-// target, group-norm partials, A column, the chunk's activations, the window tile and the
-// Adam state of the parameters it updates -- is requested in ONE staging pass at the start;
-// the rest is LDS / register work and one store pass.
-__host__ __device__ inline int fb_tsz(const RedcliffDims& d) {
-  const int a = d.Bmax > RC_BLOCK ? d.Bmax : RC_BLOCK, b = d.p * d.L;
-  return a > b ? a : b;
-}
-
-__device__ inline void rc_adam_pre(const StepCtx& c, float* P, float* M, float* V, float* G, int64_t idx, float g,
-                                   const RcAdamScalars& s, float pp, float mm, float vv) {
-  if (c.flags & RC_GRAD_ONLY) {
-    G[idx] = g;
-    return;
-  }
-  rc_adam(pp, mm, vv, g, s);
-  P[idx] = pp; M[idx] = mm; V[idx] = vv;
-}
-
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ) {
   // nUl x nQ workgroups per network (1 x 1 when there is no factor update)
-  const RedcliffDims& d = c.d;
-  const int nU = rc_nuchunk(d);
-  const int r = rc_rep(c, blockIdx.y);
+  extern __shared__ float sm[];
   const int kj = blockIdx.x / (nUl * nQ);
   const int rem0 = blockIdx.x - kj * nUl * nQ;
   const int uc = rem0 / nQ, qc = rem0 - uc * nQ;
-  const bool lead = (uc == 0 && qc == 0);
-  const int p = d.p, h = d.h, K = d.K, L = d.L;
-  const int k = kj / p, j = kj - k * p;
-  const int Q = p * L;
-  const int u0 = uc * FAC_UC, q0 = qc * FB_QT;
-  float* P = c.fac + r * c.fs;
-  float* PM = c.facM + r * c.fs;
-  float* PV = c.facV + r * c.fs;
-  float* GF = c.gF + r * c.fs;
-  const float* E = c.emb + r * c.es;
-  float* ws = c.ws + r * c.wss;
-  const float* X = c.X + r * c.xr;
-  const RedcliffReplicaHyper& hy = c.hyp[r];
-  const int tid = threadIdx.x;
-  const int B = c.B;
-  const RcDiv dL(d.L), dK(K);
-  const bool sig = d.use_sigmoid;
-  const float ecc = d.sigmoid_ecc;
-  const bool fgrad = (c.flags & RC_STEP_B) || (c.flags & RC_STEP_A);
-  const bool adj_grad = fgrad && (c.flags & RC_LOSS_ADJ);
-  const bool values = c.flags & RC_VALUES;
-  const bool stepB = c.flags & RC_STEP_B;
-  const bool tgt = c.flags & (RC_LOSS_FORECAST | RC_VALUES);
-  const int Ls = c.Ls;
-  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 0);
-
-  extern __shared__ float sm[];
-  float* ybuf = sm;                        // [Bmax][K]  per-factor predictions
-  float* wrl = ybuf + d.Bmax * K;          // [Bmax][K]  raw embedder outputs
-  float* xt = wrl + d.Bmax * K;            // [Bmax]     forecast target X[:, Lmax, j]
-  float* dyl = xt + d.Bmax;                // [Bmax]     dL/dy_bk
-  float* wk = dyl + d.Bmax;                // [Bmax]     w_bk (post-sigmoid)
-  float* sqs = wk + d.Bmax;                // [Q]        squared group norms
-  float* Gs = sqs + Q;                     // [Q]
-  float* dGs = Gs + Q;                     // [Q]
-  float* Acol = dGs + Q;                   // [p]
-  float* lwt = Acol + p;                   // [L]
-  float* red = lwt + L;                    // [16]
-  float* rA = red + 16;                    // [2*RC_BLOCK] reduction partials
-  float* rB = rA + RC_BLOCK;
-  float* tpart = rB + RC_BLOCK;            // [fb_tsz]  lead's window partials, then dL/dA items
-  float* awl = tpart + fb_tsz(d);          // [FB_BT][17] chunk activations / dZ
-  float* Xs = awl + FB_BT * (FAC_UC + 1);  // [FB_BT][FB_QT+1] window tile
-  float* w1s = Xs + FB_BT * (FB_QT + 1);   // [FAC_UC] W1 snapshot of the chunk
-
-  // ---- one staging pass for everything the workgroup reads
-  const int tq = tid & 15, tu = tid >> 4;
-  const int64_t kjW0 = c.fo.W0 + (int64_t)kj * h * Q;
-  float pw[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f}, pv[4] = {0.f, 0.f, 0.f, 0.f};
-  float sb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s1[3] = {0.f, 0.f, 0.f};
-  const bool gonly = c.flags & RC_GRAD_ONLY;
-  if (stepB && !gonly) {  // Adam state of the parameters this thread updates
-    if (u0 + tu < h)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int q = q0 + tq + 16 * jj;
-        if (q < Q) {
-          const int64_t idx = kjW0 + (int64_t)(u0 + tu) * Q + q;
-          pw[jj] = P[idx]; pm[jj] = PM[idx]; pv[jj] = PV[idx];
-        }
-      }
-    if (qc == 0 && tid < FAC_UC && u0 + tid < h) {
-      const int64_t ib = c.fo.b0 + (int64_t)kj * h + u0 + tid, iw = c.fo.W1 + (int64_t)kj * h + u0 + tid;
-      sb[0] = P[ib]; sb[1] = PM[ib]; sb[2] = PV[ib];
-      sb[3] = P[iw]; sb[4] = PM[iw]; sb[5] = PV[iw];
-    }
-    if (qc == 0 && uc == 0 && tid == 0) {
-      const int64_t i1 = c.fo.b1 + kj;
-      s1[0] = P[i1]; s1[1] = PM[i1]; s1[2] = PV[i1];
-    }
-  }
-  const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
-  const float* W1snap = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by the forward
-  const int64_t ys_ = (int64_t)d.Bmax * K * p;
-  const int nb0 = min(B, FB_BT);
-  rc_stage_all(
-      rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order)
-        const int b = dK.div(e), kk = e - b * K;
-        const float* yp = ws + c.wo.y + ((int64_t)b * K + kk) * p + j;
-        float v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = q < nU ? yp[q * ys_] : 0.f;
-        float yv = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (q < nU) yv += v[q];
-        return yv;
-      }, [&](int e, float v) { ybuf[e] = v; }),
-      rc_seg<4>(B * K, [&](int e) { return ws[c.wo.w + e]; }, [&](int e, float v) { wrl[e] = v; }),
-      rc_seg<1>(tgt ? B : 0, [&](int b) { return X[((c.row0 + b) * d.T + c.Lmax) * p + j]; },
-                [&](int b, float v) { xt[b] = v; }),
-      rc_seg<1>(Q, [&](int e) {
-        float sq = 0.f;
-        for (int q = 0; q < nU; ++q) sq += ws[c.wo.gq + ((int64_t)q * K * p + kj) * Q + e];
-        return sq;
-      }, [&](int e, float v) { sqs[e] = v; }),
-      rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }),
-      rc_seg<1>(stepB ? FAC_UC : 0, [&](int e) { return u0 + e < h ? W1snap[u0 + e] : 0.f; },
-                [&](int e, float v) { w1s[e] = v; }),
-      rc_seg<8>(stepB ? nb0 * FAC_UC : 0, [&](int e) {
-        const int bb = e >> 4, uu = e & 15;
-        return u0 + uu < h ? aw[(int64_t)bb * h + u0 + uu] : 0.f;
-      }, [&](int e, float v) { awl[(e >> 4) * (FAC_UC + 1) + (e & 15)] = v; }),
-      rc_seg<32>(stepB ? nb0 * FB_QT : 0, [&](int e) {
-        const int bb = e >> 6, qq = e & 63;
-        return q0 + qq < Q ? xwin(c, dL, X, bb, q0 + qq) : 0.f;
-      }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
-  for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
-  __syncthreads();
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
-
-  // ---- part 1: mixture x_sim = sum_k w_k y_k, forecast residual, dL/dy and dL/dw (forecast)
-  const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
-  float fsum = 0.f;
-  for (int b = tid; b < B; b += RC_BLOCK) {
-    const float* wr = wrl + b * K;
-    float xs = 0.f;
-    for (int kk = 0; kk < K; ++kk) {
-      const float we = sig ? rc_sigmoid(ecc * wr[kk]) : wr[kk];
-      xs = (kk == 0) ? we * ybuf[b * K + kk] : xs + we * ybuf[b * K + kk];
-    }
-    const float res = tgt ? xs - xt[b] : 0.f;
-    const float wb = sig ? rc_sigmoid(ecc * wr[k]) : wr[k];
-    const float g = gscale * res;
-    wk[b] = wb;
-    dyl[b] = g * wb;
-    if (lead && fgrad && !adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = g * ybuf[b * K + k];
-    if (lead && adj_grad) tpart[b] = g * ybuf[b * K + k];  // forecast part, adjacency part added below
-    if (lead && k == 0) {
-      fsum += res * res;
-      ws[c.wo.xsim + (int64_t)b * p + j] = xs;
-    }
-  }
-  // ---- group norms G[kj][c][t] (cmlp.py:147-167)
-  for (int e = tid; e < Q; e += RC_BLOCK) {
-    const float g = sqrtf(sqs[e]);
-    Gs[e] = g;
-    dGs[e] = 0.f;
-    if (lead) ws[c.wo.G + (int64_t)kj * Q + e] = g;
-  }
-  if (values && lead && k == 0) {
-    const float t = rc_block_sum(fsum, red);
-    if (tid == 0) ws[c.wo.lossp + j] = t;
-  }
-  __syncthreads();
-  if (lead)
-    for (int cc = tid; cc < p; cc += RC_BLOCK) {
-      float sq = 0.f;
-      for (int t = 0; t < L; ++t) sq += sqs[cc * L + t];
-      ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
-    }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 17);
-
-  // ---- part 2: adjacency L1 of the conditional GC estimate  w_bk G_k[j][c][t] + A[c][j]
-  if (lead && (adj_grad || values)) {
-    // (window, channel slice) items: nsl slices of the p channels per window
-    const int nsl = B >= RC_BLOCK ? 1 : RC_BLOCK / B;
-    const int b = tid % B, sl = tid / B;
-    float t = 0.f, v = 0.f;
-    if (tid < nsl * B) {
-      const float wb = wk[b];
-      for (int cc = sl; cc < p; cc += nsl)
-        for (int i = 0; i < Ls; ++i) {
-          const float g = Gs[cc * L + (L - Ls + i)];
-          const float val = wb * g + Acol[cc];
-          t += lwt[i] * rc_sign(val) * g;
-          if (values) v += lwt[i] * fabsf(val);
-        }
-    }
-    for (int bb = tid + RC_BLOCK; bb < B; bb += RC_BLOCK) {  // B > 256: remaining windows, whole rows
-      const float wb = wk[bb];
-      float tb = 0.f;
-      for (int cc = 0; cc < p; ++cc)
-        for (int i = 0; i < Ls; ++i) {
-          const float g = Gs[cc * L + (L - Ls + i)];
-          const float val = wb * g + Acol[cc];
-          tb += lwt[i] * rc_sign(val) * g;
-          if (values) v += lwt[i] * fabsf(val);
-        }
-      if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + bb) * K + k] = tpart[bb] + hy.c_adj * tb;
-    }
-    rA[tid] = t;
-    __syncthreads();
-    if (adj_grad && tid < B && tid < RC_BLOCK) {
-      float s = 0.f;
-      for (int q = 0; q < nsl; ++q) s += rA[q * B + tid];
-      ws[c.wo.dwp + ((int64_t)j * d.Bmax + tid) * K + k] = tpart[tid] + hy.c_adj * s;
-    }
-    if (values) {
-      const float tv = rc_block_sum(v, red);
-      if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * tv;
-    }
-  }
-  if (adj_grad) {
-    // dL/dG[q] (q in the lag slice) and dL/dA[c][j]: items (q, window slice)
-    const int ni = p * Ls;
-    const int nsl = ni >= RC_BLOCK ? 1 : RC_BLOCK / ni;
-    const bool needA = lead && (c.flags & RC_STEP_A);
-    __syncthreads();
-    for (int it = tid; it < ni * nsl; it += RC_BLOCK) {
-      const int e = it % ni, sl = it / ni;
-      const int cc = e / Ls, i = e - cc * Ls;
-      const float g = Gs[cc * L + (L - Ls + i)];
-      float sw = 0.f, s1v = 0.f;
-      for (int b = sl; b < B; b += nsl) {
-        const float sg = rc_sign(wk[b] * g + Acol[cc]);
-        sw += sg * wk[b];
-        s1v += sg;
-      }
-      if (nsl == 1) {
-        dGs[cc * L + (L - Ls + i)] = hy.c_adj * lwt[i] * sw;
-        tpart[e] = hy.c_adj * lwt[i] * s1v;  // reused: the lead's window partials are consumed
-      } else {
-        rA[it] = sw;
-        rB[it] = s1v;
-      }
-    }
-    __syncthreads();
-    if (nsl > 1)
-      for (int e = tid; e < ni; e += RC_BLOCK) {
-        float sw = 0.f, s1v = 0.f;
-        for (int q = 0; q < nsl; ++q) {
-          sw += rA[q * ni + e];
-          s1v += rB[q * ni + e];
-        }
-        const int cc = e / Ls, i = e - cc * Ls;
-        dGs[cc * L + (L - Ls + i)] = hy.c_adj * lwt[i] * sw;
-        tpart[e] = hy.c_adj * lwt[i] * s1v;
-      }
-    __syncthreads();
-    if (needA)
-      for (int cc = tid; cc < p; cc += RC_BLOCK) {
-        float s = 0.f;
-        for (int i = 0; i < Ls; ++i) s += tpart[cc * Ls + i];
-        ws[c.wo.dAadj + ((int64_t)k * p + cc) * p + j] = s;  // d/dA[c][j]
-      }
-  }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 18);
-  if (!stepB) return;
-  __syncthreads();
-
-  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
-  // ---- part 3: over window tiles of FB_BT (one tile when B <= 128; the first is already staged)
-  const int uu = tid & 15, part = tid >> 4;  // 3a: 16 slices of the batch per hidden unit
-  float dW1u = 0.f, db0u = 0.f, db1 = 0.f;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int bt = 0; bt < B; bt += FB_BT) {
-    const int nb = min(FB_BT, B - bt);
-    if (bt > 0) {
-      __syncthreads();
-      rc_stage_all(
-          rc_seg<8>(nb * FAC_UC, [&](int e) {
-            const int bb = e >> 4, u = e & 15;
-            return u0 + u < h ? aw[(int64_t)(bt + bb) * h + u0 + u] : 0.f;
-          }, [&](int e, float v) { awl[(e >> 4) * (FAC_UC + 1) + (e & 15)] = v; }),
-          rc_seg<32>(nb * FB_QT, [&](int e) {
-            const int bb = e >> 6, qq = e & 63;
-            return q0 + qq < Q ? xwin(c, dL, X, bt + bb, q0 + qq) : 0.f;
-          }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
-      __syncthreads();
-    }
-    // 3a (column tile 0): output-layer / bias gradients of the chunk's hidden units
-    if (qc == 0) {
-      const float w1 = w1s[uu];
-      for (int bb = part; bb < nb; bb += 16) {
-        const float av = awl[bb * (FAC_UC + 1) + uu];
-        dW1u += dyl[bt + bb] * av;
-        db0u += av > 0.f ? dyl[bt + bb] * w1 : 0.f;
-      }
-      if (uc == 0)
-        for (int bb = tid; bb < nb; bb += RC_BLOCK) db1 += dyl[bt + bb];
-    }
-    __syncthreads();
-    // dZ = [a > 0] dL/dy W1 in place of the activations
-    for (int e = tid; e < nb * FAC_UC; e += RC_BLOCK) {
-      const int bb = e >> 4, u = e & 15;
-      const float av = awl[bb * (FAC_UC + 1) + u];
-      awl[bb * (FAC_UC + 1) + u] = av > 0.f ? dyl[bt + bb] * w1s[u] : 0.f;
-    }
-    __syncthreads();
-    // 3b: dW0 tile partial = dZ^T Xw
-#pragma unroll 8
-    for (int bb = 0; bb < nb; ++bb) {
-      const float zv = awl[bb * (FAC_UC + 1) + tu];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[jj] += zv * Xs[bb * (FB_QT + 1) + tq + 16 * jj];
-    }
-  }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 21);
-  if (qc == 0) {
-    rA[tid] = dW1u;
-    rB[tid] = db0u;
-    if (uc == 0) db1 = rc_block_sum(db1, red);
-    __syncthreads();
-    if (tid < 16 && u0 + tid < h) {
-      float g1 = 0.f, g0 = 0.f;
-      for (int s2 = 0; s2 < 16; ++s2) {
-        g1 += rA[s2 * 16 + tid];
-        g0 += rB[s2 * 16 + tid];
-      }
-      rc_adam_pre(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + u0 + tid, g0, as, sb[0], sb[1], sb[2]);
-      rc_adam_pre(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + u0 + tid, g1, as, sb[3], sb[4], sb[5]);
-    }
-    if (uc == 0 && tid == 0) rc_adam_pre(c, P, PM, PV, GF, c.fo.b1 + kj, db1, as, s1[0], s1[1], s1[2]);
-  }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 22);
-  // dW0 tile: + adjacency-L1 term through the group norms, then Adam
-  const int u = u0 + tu;
-  if (u < h) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int q = q0 + tq + 16 * jj;
-      if (q >= Q) continue;
-      const int64_t idx = kjW0 + (int64_t)u * Q + q;
-      float g = acc[jj];
-      if (adj_grad && Gs[q] > 0.f) g += dGs[q] * ((gonly ? P[idx] : pw[jj]) / Gs[q]);
-      rc_adam_pre(c, P, PM, PV, GF, idx, g, as, pw[jj], pm[jj], pv[jj]);
-    }
-  }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 23);
-  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 1);
-}
-
-int fac_bwd_lds_floats(const RedcliffDims& d) {
-  const int Q = d.p * d.L;
-  return 2 * d.Bmax * d.K + 3 * d.Bmax + 3 * Q + d.p + d.L + 16 + 2 * RC_BLOCK + fb_tsz(d) +
-         FB_BT * (FAC_UC + 1) + FB_BT * (FB_QT + 1) + FAC_UC;
+  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, rc_rep(c, blockIdx.y), sm, nullptr);
 }
 
 }  // namespace

@@ -319,6 +319,9 @@ size_t fac_fwd_floats(const RedcliffDims& d) {
 // grid (nemb + nfac, R): embedder blocks first, then factor blocks.
 __global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_lds, int nemb) {
   extern __shared__ float sm[];
+  // every step with an embedder forward re-arms the merged backward's factor-lead counter (the
+  // kernel boundary orders this store before k_bwd_merged's polls)
+  if (blockIdx.x == 0 && nemb > 0 && threadIdx.x == 0) *rc_fac_lead_cnt(c, c.ws + rc_rep(c, blockIdx.y) * c.wss) = 0u;
   if ((int)blockIdx.x < nemb)
     emb_fwd_body(c, blockIdx.x, SB, w_lds, sm);
   else

@@ -112,3 +112,35 @@ def test_forked_pack_bitwise_equals_single_stream_pack(monkeypatch, guard_bands)
     for r in range(len(GRID)):
         for k, want in states["0"][r].items():
             np.testing.assert_array_equal(states["1"][r][k], want, err_msg="replica %d %s" % (r, k))
+
+
+def run_vector(monkeypatch, merge, train, guarded, seed=0):
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
+    monkeypatch.setenv("REDCLIFF_MERGE", merge)
+    m = make(seed, 10.0, 0.1)
+    oA, oB = opts(m, 5e-4, 2e-4)
+    eng = m.engine()
+    eng.workspace(max(x.shape[0] for x, _ in train), train[0][0].shape[1])
+    armed = arm(eng.ws, eng.dims(eng.ws_dims[0], train[0][0].shape[1]), 1) if guarded else None
+    for epoch in (0, 1, 2, 3, 4):
+        for bi, (Xb, Yb) in enumerate(train):
+            m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+    torch.cuda.synchronize()
+    if guarded:
+        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s" % merge)
+    return {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
+
+
+def test_merged_backward_bitwise_equals_two_launches(monkeypatch, guard_bands):
+    """k_bwd_merged (factor and embedder backward in one launch, the embedder workgroups waiting
+    on the factor-lead workgroups' published records) against the two dependent launches
+    (REDCLIFF_MERGE=0): bit for bit through pretrain -> acclimate -> combined, ragged last
+    batch included, with every workspace guard band intact; then a second merged run (the
+    lead counter re-arms every step, so repeated steps see fresh records)."""
+    train = data(64 * 2 + 24, seed=5)
+    two = run_vector(monkeypatch, "0", train, True)
+    one = run_vector(monkeypatch, "1", train, True)
+    again = run_vector(monkeypatch, "1", train, False)
+    for k, want in two.items():
+        np.testing.assert_array_equal(one[k], want, err_msg=k)
+        np.testing.assert_array_equal(again[k], want, err_msg=k)

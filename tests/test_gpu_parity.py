@@ -416,8 +416,9 @@ def test_stress_config_error_budget_vs_fp64():
 
     with torch.no_grad():
         g_hip = gc_of(m, Xg.cuda())
+        g_runs = [gc_of(r_, Xg) for r_ in runs]
         with _Float64Default():
-            g64 = gc_of(o64, Xg.double())
+            g64, g64f = gc_of(o64, Xg.double()), gc_of(o64f, Xg.double())
     # GC extraction on the SAME parameters: the HIP model's final state loaded into the float64
     # oracle (the trajectory is judged above; this isolates the GC computation), 1e-4 relative
     o64h = _oracle_fp64(o0)
@@ -441,7 +442,14 @@ def test_stress_config_error_budget_vs_fp64():
     assert worst[0] <= max(2.0 * worst[1:].max(), 1e-2 * lr), "HIP path's worst excess beyond the reference's"
     assert gexcess.max() <= 0, "GC extraction differs from float64 on the same parameters"
     np.testing.assert_array_equal(g_hip > 0, g64h > 0)
-    np.testing.assert_array_equal(g_hip > 0, g64 > 0)  # the graphs of the float64 trajectory too
+    # the graphs of the float64 trajectory too, wherever the trajectory decides the sign: an
+    # entry whose float64 value is within the spread of the reference's own fp32 runs and of the
+    # tie-flipped run (x3) is undecidable at fp32 resolution
+    band = 3.0 * np.max(np.stack([np.abs(g - g64) for g in g_runs] + [np.abs(g64f - g64)]), axis=0) \
+        + 1e-6 * np.abs(g64).max()
+    decided = np.abs(g64) > band
+    print("trajectory graph entries decided at fp32 resolution: %d / %d" % (int(decided.sum()), decided.size))
+    np.testing.assert_array_equal((g_hip > 0)[decided], (g64 > 0)[decided])
 
 
 def test_fit_trace_matches_reference():
