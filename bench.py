@@ -81,17 +81,23 @@ def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg):
     on two streams the slots overlap in time (the step is shorter than their sum)."""
     fl = dict(fl)
     mfma = ktimes.get("fac_mix", (0, 0))[1] > 0
+    merged = False
     if mfma:  # k_fac_mix carries the penalty terms, k_fac_bwd_mfma the dW0 contraction
         fl["fac_mix"] = fl["pen"]
         fl["fac_bwd"] -= fl["pen"]
     elif ktimes.get("fac_fwd", (0, 0))[1] == 0:
         fl["emb_fwd"] += fl["fac_fwd"]
+        if ktimes.get("fac_bwd", (0, 0))[1] == 0 and ktimes.get("emb_bwd", (0, 0))[1] > 0:
+            # k_bwd_merged: the factor and embedder backward in one launch (emb_bwd slot)
+            merged = True
+            fl["emb_bwd"] += fl["fac_bwd"]
     dom = max((k for k in ktimes if k in fl and k != "supports"), key=lambda k: ktimes[k][0])
     avg_ms = ktimes[dom][0]
     flops = fl.get(dom, 0) * windows_per_launch
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_mfma", "fac_bwd": "k_fac_bwd_mfma" if mfma else "k_fac_bwd",
-             "emb_bwd": "k_emb_bwd", "emb_final": "k_emb_final", "fac_mix": "k_fac_mix"}[dom]
+             "emb_bwd": "k_bwd_merged" if merged else "k_emb_bwd", "emb_final": "k_emb_final",
+             "fac_mix": "k_fac_mix"}[dom]
     return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 6),
             "traffic": pmc_traffic(kname, traffic_cfg) if traffic_cfg else None,
@@ -168,22 +174,33 @@ def cpu_baseline(c, seconds):
 
 
 def pmc_traffic(kernel_name, cfg):
-    """HBM bytes per launch of ``kernel_name`` from committed rocprofv3 PMC summaries
-    (profiles/*pmc_<cfg>*counter_collection*.csv, else the round-1 ones for d4ic):
-    FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE."""
+    """HBM bytes per launch of ``kernel_name`` from committed rocprofv3 PMC summaries:
+    FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE.  cfg "<config>"
+    reads profiles/*pmc_<config>_*counter_collection*.csv and keeps the launches with the
+    SMALLEST grid (the single fit); "<config>_r<R>" (a packed grid search) reads the same passes
+    and keeps the LARGEST grid (the R-replica launches)."""
     import csv
     import glob
-    pats = [os.path.join(ROOT, "profiles", "*pmc_%s_*counter_collection*.csv" % cfg)]
-    if cfg == "d4ic":
+    import re
+    base, packed = (cfg.rsplit("_r", 1)[0], True) if "_r" in cfg else (cfg, False)
+    pats = [os.path.join(ROOT, "profiles", "r02_pmc_%s_*counter_collection*.csv" % base)]
+    if base == "d4ic" and not packed:
         pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
     for pat in pats:
         fetch, write = None, None
         for path in sorted(glob.glob(pat)):
-            vals = {}
+            rows = []
             with open(path) as f:
                 for row in csv.DictReader(f):
-                    if kernel_name not in row.get("Kernel_Name", ""):
-                        continue
+                    if re.search(r"(^|::)%s(<|\(|$)" % re.escape(kernel_name), row.get("Kernel_Name", "")):
+                        rows.append(row)
+            if not rows:
+                continue
+            gsz = [int(r_.get("Grid_Size", 0) or 0) for r_ in rows]
+            keep = max(gsz) if packed else min(gsz)
+            vals = {}
+            for row, g in zip(rows, gsz):
+                if g == keep:
                     vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
             if "FETCH_SIZE" in vals:
                 fetch = float(np.mean(vals["FETCH_SIZE"]))

@@ -93,6 +93,9 @@ inline FacOff rc_fac_off(const RedcliffDims& d) {
 __host__ __device__ inline int rc_nchunk(const RedcliffDims& d) { return (d.H + EMB_HC - 1) / EMB_HC; }
 // factor hidden units per factor-kernel workgroup
 #define FAC_UC 16
+// vector factor path: with p*L <= 64 (one dW0 column tile) the backward recomputes the hidden
+// activations from the window and W0 instead of the forward storing them (rc_fac_bwd.h)
+__host__ __device__ inline bool rc_fac_recompute(const RedcliffDims& d) { return d.p * d.L <= 64; }
 __host__ __device__ inline int rc_nuchunk(const RedcliffDims& d) { return (d.h + FAC_UC - 1) / FAC_UC; }
 
 // Embedder backward node blocks: BC windows each (16, fewer if the LDS tiles do not fit).
@@ -281,28 +284,45 @@ inline int rc_rep_host(const StepCtx& c, int i) { return rc_rep(c, i); }
 // ---------------------------------------------------------------------------------------------
 // device helpers
 
-// Producer / consumer hand-off between workgroups of ONE launch (k_bwd_merged): every producer
-// workgroup drains its stores, one lane releases them at agent scope (all XCDs) and counts
-// itself in; a consumer's lane 0 polls the count (agent-scope loads, s_sleep between polls),
-// acquires, and the workgroup proceeds.  Producers have lower workgroup ids than their consumers
-// and never wait, so they are dispatched first and finish (no co-residency assumption); the
-// poll is bounded all the same, so a missing producer cannot hang the GPU.
+// Producer / consumer hand-off between workgroups of ONE launch (k_bwd_merged), the write-through
+// form of cdna_hip_programming.md Guideline 16 (R1): every payload word is stored sc1 (agent-scope
+// relaxed atomic store: write-through to the device coherence point, so no release fence and no
+// L2 writeback), every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier, and
+// one lane counts the workgroup in with an agent-scope atomic.  A consumer's lane 0 polls the
+// count relaxed (s_sleep between polls, bounded), and EVERY load of the payload in the consumer is
+// an sc1 load (agent-scope relaxed atomic load), so no acquire fence / L1 invalidate is needed --
+// only a compiler barrier keeps the loads below the poll.  Producers have lower workgroup ids than
+// their consumers and never wait, so they are dispatched first and finish (no co-residency
+// assumption); the bounded poll means a missing producer cannot hang the GPU.
+__device__ inline void rc_store_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline float rc_load_sc1(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(reinterpret_cast<unsigned*>(const_cast<float*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// a payload store: sc1 inside the merged launch, plain otherwise (read by a later launch)
+__device__ inline void rc_store_payload(float* p, float v, bool sc1) {
+  if (sc1)
+    rc_store_sc1(p, v);
+  else
+    *p = v;
+}
+
 __device__ inline void rc_publish(unsigned* cnt) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ inline void rc_wait_count(const unsigned* cnt, unsigned target) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && ++spins < (1u << 24))
+    while (__hip_atomic_load(const_cast<unsigned*>(cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+           ++spins < (1u << 24))
       __builtin_amdgcn_s_sleep(2);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler barrier only: payload loads are sc1
   __syncthreads();
 }
 

@@ -334,7 +334,8 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
 #pragma unroll
       for (int u = 0; u < 16; ++u) {  // p <= 64
         const int j = dg + 4 * u;
-        dv[u] = (fac_grad && it2 < nitem && j < p) ? dwp[((int64_t)j * d.Bmax + bw0 + sw) * K + kk] : 0.f;
+        const float* q = dwp + ((int64_t)j * d.Bmax + bw0 + sw) * K + kk;
+        dv[u] = (fac_grad && it2 < nitem && j < p) ? (wait_cnt ? rc_load_sc1(q) : *q) : 0.f;
       }
     };
     auto dw_store = [&](int i0) {
@@ -649,14 +650,18 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
 
 // Adjacency-L1 gradient of A summed over the K factors' records, in place into record 0
 // (fixed order, every load in flight at once: K <= 16).
-__device__ __forceinline__ void emb_bwd_dadj(const StepCtx& c, int r, int blk) {
+__device__ __forceinline__ void emb_bwd_dadj(const StepCtx& c, int r, int blk, bool sc1 = false) {
   const int pp2 = c.d.p * c.d.p, e = blk * RC_BLOCK + threadIdx.x;
   if (e >= pp2) return;
   float* dA = c.ws + r * c.wss + c.wo.dAadj;
+  float v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    v[k] = k < c.d.K ? (sc1 ? rc_load_sc1(dA + (int64_t)k * pp2 + e) : dA[(int64_t)k * pp2 + e]) : 0.f;
   float t = 0.f;
 #pragma unroll
   for (int k = 0; k < 16; ++k)
-    if (k < c.d.K) t += dA[(int64_t)k * pp2 + e];
+    if (k < c.d.K) t += v[k];
   dA[e] = t;
 }
 
@@ -704,7 +709,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int
   if (e >= 0 && e < nemb) {
     if (e >= nnode + head) {
       rc_wait_count(cnt, KP);
-      emb_bwd_dadj(c, r, e - nnode - head);
+      emb_bwd_dadj(c, r, e - nnode - head, true);
     } else if (e == nnode) {
       emb_bwd_head(c, r, sm);
     } else {

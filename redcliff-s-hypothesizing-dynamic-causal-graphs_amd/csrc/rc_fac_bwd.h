@@ -53,6 +53,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const RedcliffDims& d = c.d;
   const int nU = rc_nuchunk(d);
   const bool lead = (uc == 0 && qc == 0);
+  const bool sc1 = publish != nullptr;  // payload read inside this launch: write-through stores
   (void)nUl;
   (void)nQ;
   const int p = d.p, h = d.h, K = d.K, L = d.L;
@@ -97,6 +98,12 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   float* awl = tpart + fb_tsz(d);          // [FB_BT][17] chunk activations / dZ
   float* Xs = awl + FB_BT * (FAC_UC + 1);  // [FB_BT][FB_QT+1] window tile
   float* w1s = Xs + FB_BT * (FB_QT + 1);   // [FAC_UC] W1 snapshot of the chunk
+  float* Wc = w1s + FAC_UC;                // [FAC_UC][FB_QT+1] the chunk's W0 rows (recompute)
+  float* bc0 = Wc + FAC_UC * (FB_QT + 1);  // [FAC_UC]          and its b0
+  // p*L <= FB_QT: the hidden activations are recomputed here from the window tile and the
+  // chunk's (pre-update) W0 rows -- the forward's exact fmaf chain, so the same bits -- instead of
+  // being written by the forward and read back (2 MB each way per D4IC step)
+  const bool recompute = rc_fac_recompute(d);
 
   // ---- one staging pass for everything the workgroup reads
   const int tq = tid & 15, tu = tid >> 4;
@@ -152,10 +159,16 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }),
       rc_seg<1>(stepB ? FAC_UC : 0, [&](int e) { return u0 + e < h ? W1snap[u0 + e] : 0.f; },
                 [&](int e, float v) { w1s[e] = v; }),
-      rc_seg<8>(stepB ? nb0 * FAC_UC : 0, [&](int e) {
+      rc_seg<8>(stepB && !recompute ? nb0 * FAC_UC : 0, [&](int e) {
         const int bb = e >> 4, uu = e & 15;
         return u0 + uu < h ? aw[(int64_t)bb * h + u0 + uu] : 0.f;
       }, [&](int e, float v) { awl[(e >> 4) * (FAC_UC + 1) + (e & 15)] = v; }),
+      rc_seg<4>(stepB && recompute ? FAC_UC * Q : 0, [&](int e) {
+        const int uu = e / Q, q = e - uu * Q;
+        return u0 + uu < h ? P[kjW0 + (int64_t)(u0 + uu) * Q + q] : 0.f;
+      }, [&](int e, float v) { Wc[(e / Q) * (FB_QT + 1) + e % Q] = v; }),
+      rc_seg<1>(stepB && recompute ? FAC_UC : 0, [&](int e) { return u0 + e < h ? P[c.fo.b0 + (int64_t)kj * h + u0 + e] : 0.f; },
+                [&](int e, float v) { bc0[e] = v; }),
       rc_seg<32>(stepB ? nb0 * FB_QT : 0, [&](int e) {
         const int bb = e >> 6, qq = e & 63;
         return q0 + qq < Q ? xwin(c, dL, X, bb, q0 + qq) : 0.f;
@@ -179,7 +192,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
     const float g = gscale * res;
     wk[b] = wb;
     dyl[b] = g * wb;
-    if (lead && fgrad && !adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = g * ybuf[b * K + k];
+    if (lead && fgrad && !adj_grad) rc_store_payload(ws + c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k, g * ybuf[b * K + k], sc1);
     if (lead && adj_grad) tpart[b] = g * ybuf[b * K + k];  // forecast part, adjacency part added below
     if (lead && k == 0) {
       fsum += res * res;
@@ -232,14 +245,14 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
           tb += lwt[i] * rc_sign(val) * g;
           if (values) v += lwt[i] * fabsf(val);
         }
-      if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + bb) * K + k] = tpart[bb] + hy.c_adj * tb;
+      if (adj_grad) rc_store_payload(ws + c.wo.dwp + ((int64_t)j * d.Bmax + bb) * K + k, tpart[bb] + hy.c_adj * tb, sc1);
     }
     rA[tid] = t;
     __syncthreads();
     if (adj_grad && tid < B && tid < RC_BLOCK) {
       float s = 0.f;
       for (int q = 0; q < nsl; ++q) s += rA[q * B + tid];
-      ws[c.wo.dwp + ((int64_t)j * d.Bmax + tid) * K + k] = tpart[tid] + hy.c_adj * s;
+      rc_store_payload(ws + c.wo.dwp + ((int64_t)j * d.Bmax + tid) * K + k, tpart[tid] + hy.c_adj * s, sc1);
     }
     if (values) {
       const float tv = rc_block_sum(v, red);
@@ -287,7 +300,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       for (int cc = tid; cc < p; cc += RC_BLOCK) {
         float s = 0.f;
         for (int i = 0; i < Ls; ++i) s += tpart[cc * Ls + i];
-        ws[c.wo.dAadj + ((int64_t)k * p + cc) * p + j] = s;  // d/dA[c][j]
+        rc_store_payload(ws + c.wo.dAadj + ((int64_t)k * p + cc) * p + j, s, sc1);  // d/dA[c][j]
       }
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 18);
@@ -300,12 +313,39 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const int uu = tid & 15, part = tid >> 4;  // 3a: 16 slices of the batch per hidden unit
   float dW1u = 0.f, db0u = 0.f, db1 = 0.f;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto recompute_a = [&](int nb) {  // a = relu(Xw W0^T + b0), rc_forward.hip's chain (q ascending)
+    // thread: windows {bp, bp + 64} x units 4*uq .. 4*uq+3 (FB_BT = 128 = 2 x 64, FAC_UC = 16 = 4 x 4):
+    // 6 LDS reads per 8 fmaf; every output keeps its own chain z = fmaf(x_q, w_q, z), q ascending
+    const int bp = tid >> 2, u4 = (tid & 3) * 4;
+    const float* x0 = Xs + bp * (FB_QT + 1);
+    const float* x1 = Xs + (bp + 64) * (FB_QT + 1);
+    const float* wr = Wc + u4 * (FB_QT + 1);
+    float z0[4] = {0.f, 0.f, 0.f, 0.f}, z1[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bp < nb) {
+      for (int q = 0; q < Q; ++q) {
+        const float a0 = x0[q], a1 = x1[q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float w = wr[i * (FB_QT + 1) + q];
+          z0[i] = fmaf(a0, w, z0[i]);
+          z1[i] = fmaf(a1, w, z1[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool uin = u0 + u4 + i < h;
+        awl[bp * (FAC_UC + 1) + u4 + i] = uin ? fmaxf(z0[i] + bc0[u4 + i], 0.f) : 0.f;
+        if (bp + 64 < nb) awl[(bp + 64) * (FAC_UC + 1) + u4 + i] = uin ? fmaxf(z1[i] + bc0[u4 + i], 0.f) : 0.f;
+      }
+    }
+    __syncthreads();
+  };
   for (int bt = 0; bt < B; bt += FB_BT) {
     const int nb = min(FB_BT, B - bt);
     if (bt > 0) {
       __syncthreads();
       rc_stage_all(
-          rc_seg<8>(nb * FAC_UC, [&](int e) {
+          rc_seg<8>(recompute ? 0 : nb * FAC_UC, [&](int e) {
             const int bb = e >> 4, u = e & 15;
             return u0 + u < h ? aw[(int64_t)(bt + bb) * h + u0 + u] : 0.f;
           }, [&](int e, float v) { awl[(e >> 4) * (FAC_UC + 1) + (e & 15)] = v; }),
@@ -315,6 +355,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
           }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
       __syncthreads();
     }
+    if (recompute) recompute_a(nb);
     // 3a (column tile 0): output-layer / bias gradients of the chunk's hidden units
     if (qc == 0) {
       const float w1 = w1s[uu];
@@ -380,7 +421,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
 inline int fac_bwd_lds_floats(const RedcliffDims& d) {
   const int Q = d.p * d.L;
   return 2 * d.Bmax * d.K + 3 * d.Bmax + 3 * Q + d.p + d.L + 16 + 2 * RC_BLOCK + fb_tsz(d) +
-         FB_BT * (FAC_UC + 1) + FB_BT * (FB_QT + 1) + FAC_UC;
+         FB_BT * (FAC_UC + 1) + FB_BT * (FB_QT + 1) + FAC_UC + FAC_UC * (FB_QT + 1) + FAC_UC;
 }
 
 

@@ -290,7 +290,7 @@ __device__ void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
       for (int qq = 0; qq < qn; ++qq) {
         const float wv = Ws[tu * QP + qq];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] += Xs[(tb + 16 * i) * QP + qq] * wv;
+        for (int i = 0; i < 8; ++i) acc[i] = fmaf(Xs[(tb + 16 * i) * QP + qq], wv, acc[i]);  // rc_fac_bwd.h recomputes this chain
       }
     }
     if (bc == 0 && tb == 0 && u < h) ws[c.wo.w1 + (int64_t)kj * h + u] = w1;
@@ -300,7 +300,7 @@ __device__ void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
       float ys = 0.f;
       if (u < h) {
         const float a = fmaxf(acc[i] + bu, 0.f);
-        if (b < c.B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+        if (b < c.B && !rc_fac_recompute(d)) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
         ys = w1 * a;
       }
 #pragma unroll

@@ -1,0 +1,56 @@
+"""Bitwise comparison of two library builds on the same fits (regression check for kernel
+changes that must not change any bit).
+
+    REDCLIFF_HIP_LIB=exp/lib_prev.so python scripts/compare_builds.py dump gpurun_out/prev.npz
+    python scripts/compare_builds.py dump gpurun_out/cur.npz
+    python scripts/compare_builds.py compare gpurun_out/prev.npz gpurun_out/cur.npz
+
+dump: D4IC- and C1(K=4)-shaped fits (vector factor path) through pretrain -> acclimate ->
+combined with a ragged last batch; every state_dict tensor is saved."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "redcliff-s-hypothesizing-dynamic-causal-graphs_amd"))
+
+
+def dump(path):
+    import bench
+    import redcliff_amd
+    out = {}
+    for cfg in ("d4ic", "c1k4", "c4"):
+        c = dict(bench.CONFIGS[cfg])
+        m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).cuda()
+        oA, oB = bench.adam_pair(m, c)
+        X, Y = bench.synth(c, 2 * c["B"] + 40, seed=3)
+        bs = [(X[i:i + c["B"]], Y[i:i + c["B"]]) for i in range(0, X.shape[0], c["B"])]
+        for epoch in (0, 1, 2, 3):
+            for bi, (Xb, Yb) in enumerate(bs):
+                m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+        torch.cuda.synchronize()
+        for k, v in m.state_dict().items():
+            if not k.startswith("gen_model."):
+                out["%s/%s" % (cfg, k)] = v.detach().cpu().numpy()
+    np.savez(path, **out)
+    print("dumped %d tensors to %s" % (len(out), path))
+
+
+def compare(a, b):
+    A, B = np.load(a), np.load(b)
+    assert set(A.files) == set(B.files)
+    bad = [k for k in A.files if not np.array_equal(A[k], B[k])]
+    for k in bad[:20]:
+        print("DIFF %s: max |d| %.3e" % (k, float(np.abs(A[k].astype(np.float64) - B[k]).max())))
+    print("%d / %d tensors differ" % (len(bad), len(A.files)))
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "dump":
+        dump(sys.argv[2])
+    else:
+        compare(sys.argv[2], sys.argv[3])
