@@ -187,27 +187,27 @@ def pmc_traffic(kernel_name, cfg):
     if base == "d4ic" and not packed:
         pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
     for pat in pats:
-        fetch, write = None, None
+        # every pass of the pattern (single-fit and grid passes share it): the launches with the
+        # smallest / largest grid over ALL of them, so a single-fit pass never stands in for the grid
+        rows = []
         for path in sorted(glob.glob(pat)):
-            rows = []
             with open(path) as f:
                 for row in csv.DictReader(f):
                     if re.search(r"(^|::)%s(<|\(|$)" % re.escape(kernel_name), row.get("Kernel_Name", "")):
                         rows.append(row)
-            if not rows:
+        if not rows:
+            continue
+        gsz = [int(r_.get("Grid_Size", 0) or 0) for r_ in rows]
+        vals = {}
+        for cname in ("FETCH_SIZE", "WRITE_SIZE"):
+            g_c = [g for row, g in zip(rows, gsz) if row["Counter_Name"] == cname]
+            if not g_c:
                 continue
-            gsz = [int(r_.get("Grid_Size", 0) or 0) for r_ in rows]
-            keep = max(gsz) if packed else min(gsz)
-            vals = {}
-            for row, g in zip(rows, gsz):
-                if g == keep:
-                    vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-            if "FETCH_SIZE" in vals:
-                fetch = float(np.mean(vals["FETCH_SIZE"]))
-            if "WRITE_SIZE" in vals:
-                write = float(np.mean(vals["WRITE_SIZE"]))
-        if fetch is not None and write is not None:
-            return (2.0 * fetch + write) * 1024.0  # counters are in KiB
+            keep = max(g_c) if packed else min(g_c)
+            vals[cname] = float(np.mean([float(row["Counter_Value"]) for row, g in zip(rows, gsz)
+                                         if row["Counter_Name"] == cname and g == keep]))
+        if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+            return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0  # counters are in KiB
     return None
 
 

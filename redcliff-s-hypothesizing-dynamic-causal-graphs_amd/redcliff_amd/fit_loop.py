@@ -16,6 +16,7 @@ The per-fit bookkeeping lives in ``FitTracker`` so that a packed grid search
 (``ReplicaPack.fit``, redcliff_amd.replicas) applies exactly the same rules to every replica.
 """
 import copy
+import gc
 import os
 import pickle as pkl
 
@@ -254,6 +255,108 @@ class FitTracker:
                     factor_score_train_history=self.cm_train, stopped_at=self.stopped_at)
 
 
+def _per_graph_appends(hists, run, n, G):
+    """The length rules of model_utils.py:63-84 / :136-158 for one fit's per-graph histories
+    (len(hists) = nsup lists) given its per-graph running sums run[G]: returns the values to
+    append and whether the lengths match (only then are the path-length histories appended)."""
+    L = len(hists)
+    if L != G:
+        if G == 1 and L > 1:
+            return [run[0] / n] * L, False
+        assert L < G
+    return [run[i] / n for i in range(L)], L == G
+
+
+def train_confusion_many(trackers, cms):
+    """FitTracker.train_confusion of several fits (cms [Ra][nsup][nsup] integer counts): the
+    confusion rates of all of them in one vectorised pass (exact: integer-valued sums)."""
+    if not trackers or trackers[0].nsup <= 0:
+        return
+    cm = np.asarray(cms, dtype=np.float64)
+    TP = np.diagonal(cm, axis1=1, axis2=2)
+    FP = cm.sum(axis=1) - TP
+    FN = cm.sum(axis=2) - TP
+    TN = cm.sum(axis=(1, 2))[:, None] - (FP + FN + TP)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rates = (TP / (TP + FN), TN / (TN + FP), FP / (FP + TN), FN / (TP + FN), (TP + TN) / (TP + FP + FN + TN))
+    TPR, TNR, FPR, FNR, ACC = rates
+    for i, t in enumerate(trackers):
+        for key, v in zip(CM_KEYS, (ACC, TPR, TNR, FPR, FNR)):
+            t.cm_train[key].append(v[i].copy())
+
+
+def gc_progress_many(trackers, est, nolag, vals):
+    """FitTracker.gc_progress (device-metrics path) of several fits at once -- a packed grid search
+    updates every replica's trackers in a few array operations instead of R python loops.
+
+    est (Ra, S, K, p, p, ls) float32 host array of the lagged estimates, nolag (Ra, Sn, K, p, p, 1),
+    vals (Ra, S, G, 6 + p) device metric values or None; trackers share GC, nsup, K and p.  Every
+    appended value is bit-identical to the per-fit trackers' (metrics.track_*): the reductions
+    keep their numpy order (per-row pairwise sums, einsum), and the reference's python-float
+    running sums over samples are left-to-right float64 cumulative sums."""
+    t0 = trackers[0]
+    GC, nsup, K = t0.GC, t0.nsup, t0.K
+    S = est.shape[1]
+    if S == 0:  # nothing to vectorise: keep the per-fit code (and its error behaviour)
+        for i, t in enumerate(trackers):
+            t.gc_progress([], nolag[i], None if vals is None else vals[i])
+        return
+    if GC is not None and nsup > 0 and vals is not None:
+        n = float(S)
+        run = np.cumsum(vals, axis=1)[:, -1]  # (Ra, G, C): _running over samples
+        G = run.shape[1]
+        pv = vals.shape[3] - 6
+        for i, t in enumerate(trackers):
+            for col, f1h, roch in ((0, t.f1_hist, t.roc_hist), (2, t.f1_off, t.roc_off)):
+                for thresh in f1h.keys():
+                    if thresh != 0.0:
+                        raise ValueError("device GC-progress metrics cover the fit's threshold 0.0 only")
+                    f1v, _ = _per_graph_appends(f1h[thresh], run[i, :, col].tolist(), n, G)
+                    rov, _ = _per_graph_appends(roch[thresh], run[i, :, col + 1].tolist(), n, G)
+                    for j in range(len(f1h[thresh])):
+                        f1h[thresh][j].append(f1v[j])
+                        roch[thresh][j].append(rov[j])
+            ri = run[i].tolist()
+            dcv, full = _per_graph_appends(t.dc_hist, [r[4] for r in ri], n, G)
+            dddv, _ = _per_graph_appends(t.dcdd_hist, [r[5] for r in ri], n, G)
+            dafv, _ = _per_graph_appends(t.daff_hist, [r[6] for r in ri], n, G)
+            for j in range(len(t.dc_hist)):
+                t.dc_hist[j].append(dcv[j])
+                t.dcdd_hist[j].append(dddv[j])
+                t.daff_hist[j].append(dafv[j])
+                if full:
+                    for pl in range(1, min(t.p, pv)):
+                        t.plm_hist[pl][j].append(ri[j][6 + pl] / n)
+    if nsup > 0:  # track_l1_stats over every (sample, factor) estimate
+        e = est.astype(np.float64)
+        mx = e.max(axis=(3, 4, 5), keepdims=True)
+        v = np.abs(e / mx).reshape(e.shape[0], S, K, -1).sum(axis=-1)
+        l1 = np.cumsum(v, axis=1)[:, -1] / float(S)  # (Ra, K)
+        for i, t in enumerate(trackers):
+            li = l1[i].tolist()
+            for j in range(len(t.l1_hist)):
+                t.l1_hist[j].append(li[j])
+    for lo, hi, attr in ((0, nsup, "cos_hist"), (nsup, K, "cos_unsup")):  # track_cosine_stats_batched
+        a = np.asarray(nolag[:, :, lo:hi], dtype=np.float64)
+        Ra, Sn, Kc = a.shape[0], a.shape[1], a.shape[2]
+        if Kc < 2 or Sn == 0:
+            continue
+        flat = a.reshape(Ra, Sn, Kc, -1)
+        flat = flat / flat.max(axis=3, keepdims=True)
+        with np.errstate(invalid="ignore"):
+            nrm = np.linalg.norm(flat, axis=3)
+        nrm = np.where(np.isfinite(nrm), nrm, -1.)
+        nrm = np.maximum(nrm, 1e-8)
+        dots = np.einsum("rski,rsli->rskl", flat, flat)
+        for i1 in range(Kc):
+            for i2 in range(i1 + 1, Kc):
+                cv = dots[:, :, i1, i2] / (nrm[:, :, i1] * nrm[:, :, i2])
+                tot = np.cumsum(np.concatenate([np.zeros((Ra, 1)), cv], axis=1), axis=1)[:, -1] / float(Sn)
+                key = "%dand%d" % (i1 + lo, i2 + lo)
+                for i, t in enumerate(trackers):
+                    getattr(t, attr)[key].append(float(tot[i]))
+
+
 def conditional_gc_estimates(w, G, G0, A, nsup, ls, mode):
     """The two GC-progress estimate stacks of fit() (:1366-1414) from the embedder weights
     w (..., S, K) (post-sigmoid), the factor group norms G (..., K, p, p, L) / G0 (..., K, p, p)
@@ -273,9 +376,30 @@ def conditional_gc_estimates(w, G, G0, A, nsup, ls, mode):
     return est, nolag
 
 
-def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
-            deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path, sc_forecast, sc_factor, sc_cos,
-            save_plots):
+def run_fit(*args):
+    """fit() on the fused engine (see _run_fit).  The host side of an epoch is python; the cyclic
+    garbage collector is paused for the fit (restored afterwards): its full passes over the model's
+    module tree land inside epochs."""
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        return _run_fit(*args)
+    finally:
+        if gc_was:
+            gc.enable()
+
+
+def _eval_modes(model):
+    """The module modes every fit epoch ends in: GC tracking and validate_training call .eval() on
+    the embedder and every factor (...withStateSmoothing.py:1366-1480)."""
+    model.factor_score_embedder.eval()
+    for f in model.factors:
+        f.eval()
+
+
+def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
+             deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path, sc_forecast, sc_factor, sc_cos,
+             save_plots):
     if "Freeze" in model.training_mode:
         raise NotImplementedError("Freeze* training modes are not on the fused path")
     if prior_factors_path is not None:
@@ -328,15 +452,17 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
                                       oA, oB)
             if nsup > 0:
                 cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
-        model._set_module_modes(kinds[-1] if kinds else None)
+        if not fused:  # the generic path's torch modules read their train/eval flags
+            model._set_module_modes(kinds[-1] if kinds else None)
         tr.train_confusion(cm if nsup > 0 else None)
 
-        # ---- GC progress on the first validation batch (:1366-1414)
-        model.factor_score_embedder.eval()
-        for f in model.factors:
-            f.eval()
+        # ---- GC progress on the first validation batch (:1366-1414).  The device-metrics path's
+        # launches take their BatchNorm mode from flags, so there the module flags are set once
+        # (_eval_modes: the state every epoch ends in) instead of three tree walks per epoch.
         dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
             "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
+        if not dev_metrics:
+            _eval_modes(model)
         with torch.no_grad():
             if dev_metrics:
                 nfirst = int(val["sizes"][0])
@@ -350,7 +476,6 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
                     vals = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff)
                 est_host = est_t.cpu().numpy()
                 nolag_np = nolag_t.cpu().numpy()
-                est_np = [[est_host[s, k] for k in range(est_host.shape[1])] for s in range(est_host.shape[0])]
             else:
                 if fused:
                     Xv = val["X"][:min(int(val["sizes"][0]), model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
@@ -363,10 +488,15 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
                 nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
                                  combine_wavelet_representations=True)
                 nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
-        tr.gc_progress(est_np, nolag_np, vals)
+        if dev_metrics:
+            gc_progress_many([tr], est_host[None], nolag_np[None], None if vals is None else vals[None])
+        else:
+            tr.gc_progress(est_np, nolag_np, vals)
 
         # ---- validation (:1416-1480)
-        if nsup > 0:
+        if fused:
+            tr.validation(model._validate_fused(X_val, nsup > 0))
+        elif nsup > 0:
             tr.validation(model.validate_training(X_val, output_length, model.num_series, [], [], [], [], []))
         else:
             tr.validation(model.validate_training(X_val, output_length, model.num_series))
@@ -378,8 +508,12 @@ def run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lo
             break
 
         if it % check_every == 0 and save_dir is not None:
+            if fused:
+                _eval_modes(model)
             tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
 
+    if fused:
+        _eval_modes(model)
     restore_parameters(model, tr.best_model)
     if save_dir is not None:
         torch.save(standalone_copy(model), os.path.join(save_dir, "final_best_model.bin"))

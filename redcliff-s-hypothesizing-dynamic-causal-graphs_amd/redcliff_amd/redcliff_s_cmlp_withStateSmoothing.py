@@ -442,16 +442,25 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             return self._validation_tuple(acc, 1.0, conf, factor_score_val_acc_history,
                                           factor_score_val_tpr_history, factor_score_val_tnr_history,
                                           factor_score_val_fpr_history, factor_score_val_fnr_history)
-        eng = self.engine()
         self.factor_score_embedder.eval()
         for f in self.factors:
             f.eval()
+        return self._validate_fused(X_val, False, factor_score_val_acc_history, factor_score_val_tpr_history,
+                                    factor_score_val_tnr_history, factor_score_val_fpr_history,
+                                    factor_score_val_fnr_history)
+
+    def _validate_fused(self, X_val, fresh_histories, *hists):
+        """validate_training on the fused engine without touching the module flags (fit() sets
+        them once); fresh_histories: five new confusion-history lists (fit's call)."""
+        eng = self.engine()
         ds = eng.cache_dataset(X_val)
         d = eng.workspace(ds["Bmax"], ds["T"])
         acc, conf = eng.run_values(ds["X"], ds["lab"], d, ds["rows"], ds["sizes"])
-        return self._validation_tuple(acc, float(ds["len"]), conf, factor_score_val_acc_history,
-                                      factor_score_val_tpr_history, factor_score_val_tnr_history,
-                                      factor_score_val_fpr_history, factor_score_val_fnr_history)
+        if fresh_histories:
+            hists = [[] for _ in range(5)]
+        elif not hists:
+            hists = [None] * 5
+        return self._validation_tuple(acc, float(ds["len"]), conf, *hists)
 
     def _validation_tuple(self, acc, nb, conf, acc_h, tpr_h, tnr_h, fpr_h, fnr_h):
         vals = [acc[nat_i] / nb for nat_i in range(7)]

@@ -24,6 +24,7 @@ views of its pack row, so ``state_dict()``, ``GC()``, ``forward()`` and the sing
 methods keep working on it between packed epochs.
 """
 import ctypes
+import gc
 import os
 
 import numpy as np
@@ -32,7 +33,8 @@ import torch
 from . import _native as nat
 from . import metrics as M
 from .engine import _stream, flags_for, phase_of_epoch
-from .fit_loop import FitTracker, ParamSnapshot, conditional_gc_estimates, restore_parameters, standalone_copy
+from .fit_loop import (FitTracker, ParamSnapshot, conditional_gc_estimates, gc_progress_many, restore_parameters,
+                       standalone_copy, train_confusion_many)
 
 
 class ReplicaPack:
@@ -74,6 +76,7 @@ class ReplicaPack:
         self.ws = None
         self.ws_B = 0
         self._plans = {}
+        self._bound_this_epoch = False  # fit(): parameter bindings checked once per epoch
         for r, (e, (oA, oB)) in enumerate(zip(self.engines, self.optimizers)):
             e.attach_pack(self, r)
             e.bind_optimizer("A", oA)
@@ -153,6 +156,11 @@ class ReplicaPack:
             a.n_replicas = len(act)
         return a, engs
 
+    def _ensure_bound(self):
+        if not self._bound_this_epoch:
+            for e in self.engines:
+                e.ensure_bound()
+
     def cache_dataset(self, loader):
         """Upload the (shared) training set once; see FitEngine.cache_dataset."""
         return self.engines[0].cache_dataset(loader)
@@ -161,8 +169,7 @@ class ReplicaPack:
     def run_steps(self, kinds, ds, rows=None, sizes=None, stats=None, active=None):
         """Update kinds of one phase over consecutive batches of `ds` for the active replicas
         (all when None): one redcliff_train_steps launch chain of R-replica kernels per kind."""
-        for e in self.engines:
-            e.ensure_bound()
+        self._ensure_bound()
         rows = ds["rows"] if rows is None else rows
         sizes = ds["sizes"] if sizes is None else sizes
         stats = ds["stats"] if stats is None else stats
@@ -181,7 +188,7 @@ class ReplicaPack:
             for e in self.engines:
                 e.supports_fresh = False  # the single-fit workspace's supports are stale now
 
-    def run_epoch(self, epoch, ds, active=None):
+    def run_epoch(self, epoch, ds, active=None, set_modes=True):
         """The batch_update phase of `epoch` (...withStateSmoothing.py:741-759) over every batch
         of `ds`, for the active replicas.  All replicas must be in the same phase."""
         idx = range(self.R) if active is None else active
@@ -195,14 +202,14 @@ class ReplicaPack:
             for bi, (r, s) in enumerate(zip(ds["rows"], ds["sizes"])):
                 for kind in kinds:
                     self.run_steps([kind], ds, [r], [s], ds["stats"][bi:bi + 1], active=active)
-        for r in idx:
-            self.models[r]._set_module_modes(kinds[-1] if kinds else None)
+        if set_modes:
+            for r in idx:
+                self.models[r]._set_module_modes(kinds[-1] if kinds else None)
         return kinds
 
     def _values(self, ds, active=None):
         """validate_training accumulators of the active replicas: raw acc [R][8], confusion."""
-        for e in self.engines:
-            e.ensure_bound()
+        self._ensure_bound()
         self.acc.zero_()
         self.conf.zero_()
         e0 = self.engines[0]
@@ -253,9 +260,21 @@ class ReplicaPack:
         return G, G0
 
     # ------------------------------------------------------------------ packed fit
-    def fit(self, save_dir, X_train, X_val, max_iter, lookback=5, check_every=50, verbose=0, GC=None,
-            deltaConEps=0.1, in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=1.,
-            stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., output_length=1, save_plots=False):
+    def fit(self, *args, **kwargs):
+        """R fits of ``fit()`` in one packed launch chain; see ``_fit``.  The host side of an epoch
+        is O(R) python, so the cyclic garbage collector is paused for the fit: its full passes
+        over R models' module trees cost as much as whole epochs (restored afterwards)."""
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            return self._fit(*args, **kwargs)
+        finally:
+            if gc_was:
+                gc.enable()
+
+    def _fit(self, save_dir, X_train, X_val, max_iter, lookback=5, check_every=50, verbose=0, GC=None,
+             deltaConEps=0.1, in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=1.,
+             stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., output_length=1, save_plots=False):
         """R fits of ``fit()`` (...withStateSmoothing.py:1175-1647) in one packed launch chain.
 
         Every replica follows exactly the rules (and the host code, FitTracker) of a single fit:
@@ -300,59 +319,65 @@ class ReplicaPack:
         active = list(range(R))
         nfirst = min(int(val["sizes"][0]), m0.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING)
         Xv = val["X"][:nfirst, :Lm, :]
-        for it in range(max_iter):
-            if not active:
-                break
-            if verbose:
-                print("ReplicaPack.fit: epoch %d, %d of %d replicas active" % (it, len(active), R), flush=True)
-            self.conf.zero_()
-            self.run_epoch(it, train, active)
-            cms = self.conf.cpu().numpy().reshape(R, max(nsup, 1), max(nsup, 1)) if nsup > 0 else None
-            for r in active:
-                trackers[r].train_confusion(cms[r] if nsup > 0 else None)
-                models[r].factor_score_embedder.eval()
-                for f in models[r].factors:
-                    f.eval()
-            # ---- GC progress of every active replica on the first validation batch (:1366-1414)
-            with torch.no_grad():
-                w_raw = self.embed_raw(Xv, active)  # (Ra, S, K)
-                emb0 = models[0].factor_score_embedder
-                w = torch.sigmoid(emb0.sigmoid_eccentricity_coeff * w_raw) if emb0.use_sigmoid_restriction else w_raw
-                G, G0 = self.gc_norms()
-                A = self.emb[:, :p * p].view(R, p, p)
-                ai = torch.as_tensor(active, device=self.device)
-                est_t, nolag_t = conditional_gc_estimates(w, G[ai], G0[ai], A[ai], nsup, ls, m0.primary_gc_est_mode)
-                vals = None
-                if GC is not None and nsup > 0 and est_t.shape[1] > 0:
-                    Ra, S = est_t.shape[0], est_t.shape[1]
-                    vals = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
-                                                in_degree_coeff, out_degree_coeff)
-                    vals = vals.reshape(Ra, S, *vals.shape[1:])
-                est_host = est_t.cpu().numpy()
-                nolag_host = nolag_t.cpu().numpy()
-            for i, r in enumerate(active):
-                eh = est_host[i]
-                est_np = [[eh[s, k] for k in range(eh.shape[1])] for s in range(eh.shape[0])]
-                trackers[r].gc_progress(est_np, nolag_host[i], None if vals is None else vals[i])
-            # ---- validation of every active replica (:1416-1480), one launch chain
-            acc, conf = self._values(val, active)
-            nb = float(val["len"])
-            for r in active:
-                hist = [[] for _ in range(5)] if nsup > 0 else [None] * 5
-                trackers[r].validation(models[r]._validation_tuple(acc[r], nb, conf[r], *hist))
-            # ---- early stopping, per replica (:1482-1559); snapshots copied in one batch
-            stopped = []
-            for r in active:
-                if trackers[r].step(it, lambda r=r: best.mark(r)):
-                    stopped.append(r)
-            best.copy_marked()
-            for r in stopped:
+        # The module train/eval flags -- which no fused launch reads -- are set once, to the state
+        # the reference leaves after every epoch (eval: GC tracking and validation call .eval()),
+        # before checkpoints and at the end, instead of walking R module trees twice per epoch.
+        try:
+            for it in range(max_iter):
+                if not active:
+                    break
                 if verbose:
-                    print("ReplicaPack.fit: replica %d stops early at epoch %d" % (r, it), flush=True)
-            active = [r for r in active if r not in stopped]
-            if dirs is not None and it % check_every == 0:
+                    print("ReplicaPack.fit: epoch %d, %d of %d replicas active" % (it, len(active), R), flush=True)
+                self._bound_this_epoch = False
+                self._ensure_bound()
+                self._bound_this_epoch = True
+                self.conf.zero_()
+                self.run_epoch(it, train, active, set_modes=False)
+                tr_act = [trackers[r] for r in active]
+                if nsup > 0:
+                    cms = self.conf.cpu().numpy().reshape(R, nsup, nsup)
+                    train_confusion_many(tr_act, cms[active])
+                # ---- GC progress of every active replica on the first validation batch (:1366-1414)
+                with torch.no_grad():
+                    w_raw = self.embed_raw(Xv, active)  # (Ra, S, K)
+                    emb0 = models[0].factor_score_embedder
+                    w = torch.sigmoid(emb0.sigmoid_eccentricity_coeff * w_raw) if emb0.use_sigmoid_restriction else w_raw
+                    G, G0 = self.gc_norms()
+                    A = self.emb[:, :p * p].view(R, p, p)
+                    ai = torch.as_tensor(active, device=self.device)
+                    est_t, nolag_t = conditional_gc_estimates(w, G[ai], G0[ai], A[ai], nsup, ls, m0.primary_gc_est_mode)
+                    vals = None
+                    if GC is not None and nsup > 0 and est_t.shape[1] > 0:
+                        Ra, S = est_t.shape[0], est_t.shape[1]
+                        vals = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
+                                                    in_degree_coeff, out_degree_coeff)
+                        vals = vals.reshape(Ra, S, *vals.shape[1:])
+                    est_host = est_t.cpu().numpy()
+                    nolag_host = nolag_t.cpu().numpy()
+                gc_progress_many(tr_act, est_host, nolag_host, vals)
+                # ---- validation of every active replica (:1416-1480), one launch chain
+                acc, conf = self._values(val, active)
+                nb = float(val["len"])
                 for r in active:
-                    trackers[r].checkpoint(dirs[r], it, optimizers=self.optimizers[r], save_plots=save_plots)
+                    hist = [[] for _ in range(5)] if nsup > 0 else [None] * 5
+                    trackers[r].validation(models[r]._validation_tuple(acc[r], nb, conf[r], *hist))
+                # ---- early stopping, per replica (:1482-1559); snapshots copied in one batch
+                stopped = []
+                for r in active:
+                    if trackers[r].step(it, lambda r=r: best.mark(r)):
+                        stopped.append(r)
+                best.copy_marked()
+                for r in stopped:
+                    if verbose:
+                        print("ReplicaPack.fit: replica %d stops early at epoch %d" % (r, it), flush=True)
+                active = [r for r in active if r not in stopped]
+                if dirs is not None and it % check_every == 0:
+                    _eval_modes(models)
+                    for r in active:
+                        trackers[r].checkpoint(dirs[r], it, optimizers=self.optimizers[r], save_plots=save_plots)
+        finally:
+            self._bound_this_epoch = False
+        _eval_modes(models)
         # ---- restore best parameters, final files and validation (:1621-1647)
         for r, m in enumerate(models):
             restore_parameters(m, trackers[r].best_model)
@@ -370,6 +395,15 @@ class ReplicaPack:
             finals.append(v[-6] if nsup > 0 else v[-1])
             m.fit_history = trackers[r].history()
         return finals
+
+
+def _eval_modes(models):
+    """The module modes every fit epoch ends in (GC tracking + validate_training call .eval() on
+    the embedder and every factor, ...withStateSmoothing.py:1366-1480)."""
+    for m in models:
+        m.factor_score_embedder.eval()
+        for f in m.factors:
+            f.eval()
 
 
 class _PackBest:
