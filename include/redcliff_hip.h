@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 4
+#define REDCLIFF_ABI_VERSION 5
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -228,6 +228,18 @@ int redcliff_gemm(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_
 int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt, const float* est,
                          const double* truth, const double* eps_pow, double in_degree_coeff, double out_degree_coeff,
                          double* out, void* stream);
+
+/* Per-epoch tracker statistics of fit() (replaces the host reductions of
+ * general_utils/model_utils.py:163-186 track_l1_stats and :189-209 track_cosine_stats, which the
+ * reference runs on float64 copies of every estimate):
+ *   est      float32 [n_l1_rows][l1_len]     lagged estimates, one (sample, factor) per row
+ *   l1_out   float64 [n_l1_rows]             sum |e / max(e)|
+ *   nolag    float32 [n_samples][K][row_len] lag-free estimates
+ *   dots_out float64 [n_samples][K][K]       upper triangle (i1 <= i2): sum (a / max a)(b / max b)
+ *                                            over rows i1, i2 (the diagonal: squared norms)
+ * One workgroup per row / pair, reductions in a fixed order independent of the launch size. */
+int redcliff_gc_track_stats(int32_t n_l1_rows, int64_t l1_len, const float* est, double* l1_out, int32_t n_samples,
+                            int32_t K, int64_t row_len, const float* nolag, double* dots_out, void* stream);
 
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()

@@ -18,7 +18,9 @@
 
 namespace {
 
-#define GP_NR 16  // matrix elements per thread: p * p <= GP_NR * RC_BLOCK
+#define GP_NT 1024  // threads per workgroup: 16 waves keep the LDS / FP64 latencies of one (sample,
+                    // graph) hidden (one workgroup per CU: 36 p^2 bytes of LDS at p = 64)
+#define GP_NR 4     // matrix elements per thread: p * p <= GP_NR * GP_NT
 
 // numpy's float32 pairwise sum of a contiguous run (loops_utils.h.src, n <= 128)
 __device__ inline float np_pairwise_f32(const float* a, int n) {
@@ -81,7 +83,7 @@ __device__ inline float gp_block_max(float v, float* red) {
   if (lane == 0) red[wv] = v;
   __syncthreads();
   float m = red[0];
-  for (int i = 1; i < RC_BLOCK / 64; ++i) m = fmaxf(m, red[i]);
+  for (int i = 1; i < GP_NT / 64; ++i) m = fmaxf(m, red[i]);
   __syncthreads();
   return m;
 }
@@ -91,7 +93,7 @@ __device__ inline float gp_block_max(float v, float* red) {
 // the right half.  Singular columns leave inf / nan, as numpy's inv would raise.
 __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
   const int tid = threadIdx.x, P2 = 2 * p;
-  for (int e = tid; e < p * p; e += RC_BLOCK) {
+  for (int e = tid; e < p * p; e += GP_NT) {
     const int i = e / p, j = e - i * p;
     Aug[i * P2 + p + j] = (i == j) ? 1.0 : 0.0;
   }
@@ -112,7 +114,7 @@ __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
     __syncthreads();
     const int piv = redi[0];
     if (piv != c)
-      for (int j = tid; j < P2; j += RC_BLOCK) {
+      for (int j = tid; j < P2; j += GP_NT) {
         const double t = Aug[c * P2 + j];
         Aug[c * P2 + j] = Aug[piv * P2 + j];
         Aug[piv * P2 + j] = t;
@@ -120,12 +122,12 @@ __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
     __syncthreads();
     const double inv = 1.0 / Aug[c * P2 + c];
     __syncthreads();
-    for (int j = tid; j < P2; j += RC_BLOCK) Aug[c * P2 + j] *= inv;
+    for (int j = tid; j < P2; j += GP_NT) Aug[c * P2 + j] *= inv;
     __syncthreads();
     // eliminate column c from every other row; the multipliers are read before any write
     if (tid < p) redd[tid] = Aug[tid * P2 + c];
     __syncthreads();
-    for (int e = tid; e < p * P2; e += RC_BLOCK) {
+    for (int e = tid; e < p * P2; e += GP_NT) {
       const int i = e / P2, j = e - i * P2;
       if (i != c) Aug[e] -= redd[i] * Aug[c * P2 + j];
     }
@@ -133,15 +135,21 @@ __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
   }
 }
 
-// ROC-AUC / F1 of one estimate variant: x (float32, prepared) against truth t (float64)
 struct GpRoc {
   double f1, auc;
 };
-__device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* redd) {
+// ROC-AUC / F1 of one estimate variant: x (float32, prepared) against truth t (float64).
+// ROC-AUC = Mann-Whitney count over (positive, negative) pairs; the positives' and negatives'
+// scores are first compacted into LDS (xp, xn: any order -- the counts are integers, exact in
+// double in any summation order), then every thread walks all negatives for its positives with
+// one broadcast LDS read per pair.
+__device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* redd, float* xp, float* xn, int* cnt) {
   const int tid = threadIdx.x;
   // F1 counts (get_f1_score): masks of x > 0, x == 0, t > 0, t == 0
-  double tp = 0., ppos = 0., pz = 0., tn = 0.;
-  for (int e = tid; e < pp; e += RC_BLOCK) {
+  double tp = 0., ppos = 0., pz = 0., tn = 0., nan = 0.;
+  if (tid < 2) cnt[tid] = 0;
+  __syncthreads();
+  for (int e = tid; e < pp; e += GP_NT) {
     const float x = xs[e];
     const double tv = t[e];
     const bool pp_ = x > 0.f, pn_ = x == 0.f, lp = tv > 0.0, ln = tv == 0.0;
@@ -149,45 +157,41 @@ __device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* red
     ppos += pp_ ? 1.0 : 0.0;
     pz += pn_ ? 1.0 : 0.0;
     tn += (pn_ && ln) ? 1.0 : 0.0;
+    nan += (x != x) ? 1.0 : 0.0;
+    // ROC-AUC labels int(t) (1 only where the normalised truth is 1)
+    const int lab = (int)tv;
+    if (lab == 1) xp[atomicAdd(&cnt[0], 1)] = x;
+    else if (lab == 0) xn[atomicAdd(&cnt[1], 1)] = x;
   }
   tp = rc_block_sum_d(tp, redd);
   ppos = rc_block_sum_d(ppos, redd);
   pz = rc_block_sum_d(pz, redd);
   tn = rc_block_sum_d(tn, redd);
+  nan = rc_block_sum_d(nan, redd);  // its barriers also publish xp / xn / cnt
   const float ftp = (float)tp, ffp = (float)(ppos - tp), ffn = (float)(pz - tn);
   const float prec = ftp / (ftp + ffp), rec = ftp / (ftp + ffn);
   GpRoc o;
   o.f1 = (prec + rec == 0.f) ? 0.0 : (double)((2.f * (prec * rec)) / (prec + rec));
-  // ROC-AUC: labels int(t) (1 only where the normalised truth is 1); ties count 1/2
-  double npos = 0., nneg = 0., cnt2 = 0., nan = 0.;
-  for (int e = tid; e < pp; e += RC_BLOCK) {
-    const int lab = (int)t[e];
-    npos += lab == 1 ? 1.0 : 0.0;
-    nneg += lab == 0 ? 1.0 : 0.0;
-    nan += (xs[e] != xs[e]) ? 1.0 : 0.0;
-    if (lab == 1) {
-      const float xi = xs[e];
-      double c2 = 0.;
-      for (int j = 0; j < pp; ++j)
-        if ((int)t[j] == 0) {
-          const float xj = xs[j];
-          c2 += xi > xj ? 2.0 : (xi == xj ? 1.0 : 0.0);
-        }
-      cnt2 += c2;
+  const int npos = cnt[0], nneg = cnt[1];
+  double cnt2 = 0.;
+  for (int a = tid; a < npos; a += GP_NT) {
+    const float xi = xp[a];
+    int c2 = 0;
+    for (int b = 0; b < nneg; ++b) {
+      const float xj = xn[b];
+      c2 += xi > xj ? 2 : (xi == xj ? 1 : 0);
     }
+    cnt2 += (double)c2;
   }
-  npos = rc_block_sum_d(npos, redd);
-  nneg = rc_block_sum_d(nneg, redd);
   cnt2 = rc_block_sum_d(cnt2, redd);
-  nan = rc_block_sum_d(nan, redd);
-  if (npos == 0.) o.auc = 0.5;  // the reference's guard (sum(labels) == 0)
-  else if (nneg == 0. || nan > 0.) o.auc = __builtin_nan("");  // sklearn raises
-  else o.auc = cnt2 / (2.0 * npos * nneg);
+  if (npos == 0) o.auc = 0.5;  // the reference's guard (sum(labels) == 0)
+  else if (nneg == 0 || nan > 0.) o.auc = __builtin_nan("");  // sklearn raises
+  else o.auc = cnt2 / (2.0 * (double)npos * (double)nneg);
   return o;
 }
 
 // grid (S * G); dynamic LDS 36 p^2 bytes (+ small statics)
-__global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, int p, int Lt, const float* est,
+__global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int p, int Lt, const float* est,
                                                           const double* truth, const double* eps_pow, double cin,
                                                           double cout, double* out) {
   const int s = blockIdx.x / G, g = blockIdx.x - s * G;
@@ -199,7 +203,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
   float* Ek = Ex + pp;                               // [pp] E^k
   float* En = Ek + pp;                               // [pp] E^(k+1)
   __shared__ double redd[64];
-  __shared__ float redf[8];
+  __shared__ float redf[GP_NT / 64];
+  __shared__ int cnt[2];
   __shared__ int redi[4];
   __shared__ double degT[64], degE[64];
 
@@ -208,7 +213,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
   float es[GP_NR];
 #pragma unroll
   for (int u = 0; u < GP_NR; ++u) {
-    const int e = tid + u * RC_BLOCK;
+    const int e = tid + u * GP_NT;
     es[u] = e < pp ? np_pairwise_f32(ep + (int64_t)e * Lt, Lt) : 0.f;
   }
   double* o = out + ((int64_t)s * G + g) * NM;
@@ -219,7 +224,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
     float mx = -INFINITY;
 #pragma unroll
     for (int u = 0; u < GP_NR; ++u) {
-      const int e = tid + u * RC_BLOCK;
+      const int e = tid + u * GP_NT;
       if (e < pp) {
         const int i = e / p;
         const float x = (v == 1 && e == i * p + i) ? 0.f : es[u];
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
     mx = gp_block_max(mx, redf);
 #pragma unroll
     for (int u = 0; u < GP_NR; ++u) {
-      const int e = tid + u * RC_BLOCK;
+      const int e = tid + u * GP_NT;
       if (e < pp) {
         const int i = e / p;
         float x = (v == 1 && e == i * p + i) ? 0.f : es[u];
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
       }
     }
     __syncthreads();
-    const GpRoc rr = gp_roc_f1(Ex, t, pp, redd);
+    const GpRoc rr = gp_roc_f1(Ex, t, pp, redd, Ek, En, cnt);
     if (tid == 0) {
       o[2 * v] = rr.f1;
       o[2 * v + 1] = rr.auc;
@@ -249,14 +254,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
   // ---- deltacon0 / with directed degrees (model_utils.py:90-160, metrics.py:136-216)
   const double* t0 = truth + (int64_t)g * pp;
   double tm_all = -INFINITY;
-  for (int e = tid; e < pp; e += RC_BLOCK) {
+  for (int e = tid; e < pp; e += GP_NT) {
     T[e] = t0[e];
     tm_all = fmax(tm_all, t0[e]);
   }
   float emx = -INFINITY;
 #pragma unroll
   for (int u = 0; u < GP_NR; ++u)
-    if (tid + u * RC_BLOCK < pp) emx = fmaxf(emx, es[u]);
+    if (tid + u * GP_NT < pp) emx = fmaxf(emx, es[u]);
   emx = gp_block_max(emx, redf);
   {
 #pragma unroll
@@ -265,7 +270,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
     if (lane == 0) redd[8 + wv] = tm_all;
     __syncthreads();
     double m = redd[8];
-    for (int i = 1; i < RC_BLOCK / 64; ++i) m = fmax(m, redd[8 + i]);
+    for (int i = 1; i < GP_NT / 64; ++i) m = fmax(m, redd[8 + i]);
     tm_all = m;
     __syncthreads();
   }
@@ -273,7 +278,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
   const bool tnorm = tm_all != 0.0;
 #pragma unroll
   for (int u = 0; u < GP_NR; ++u) {
-    const int e = tid + u * RC_BLOCK;
+    const int e = tid + u * GP_NT;
     if (e < pp) Ex[e] = tnorm ? es[u] / emx : es[u];
   }
   __syncthreads();
@@ -301,7 +306,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
     __syncthreads();
     for (int side = 0; side < 2; ++side) {
       // I + (eps^2) D - eps A
-      for (int e = tid; e < pp; e += RC_BLOCK) {
+      for (int e = tid; e < pp; e += GP_NT) {
         const int i = e / p, j = e - i * p;
         double mval;
         if (side == 0) {
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
       if (side == 0) {
 #pragma unroll
         for (int u = 0; u < GP_NR; ++u) {
-          const int e = tid + u * RC_BLOCK;
+          const int e = tid + u * GP_NT;
           if (e < pp) {
             const int i = e / p, j = e - i * p;
             sreg[u] = Aug[i * 2 * p + p + j];
@@ -329,7 +334,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
         double acc = 0.;
 #pragma unroll
         for (int u = 0; u < GP_NR; ++u) {
-          const int e = tid + u * RC_BLOCK;
+          const int e = tid + u * GP_NT;
           if (e < pp) {
             const int i = e / p, j = e - i * p;
             const double df = sqrt(sreg[u]) - sqrt(Aug[i * 2 * p + p + j]);
@@ -348,70 +353,159 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_progress(int S, int nE, int G, 
   __syncthreads();
 
   // ---- deltaffinity and path-length MSE over k = 1..p-1 (metrics.py:142-252)
+  // Thread layout of this section: column j = tid % p, rows r0, r0 + rpp, ... (rpp = GP_NT / p
+  // rows per pass, at most GP_NR passes), so a thread's outputs of A^k = A^(k-1) A share the
+  // column operand A[m][j] and run GP_NR independent fma chains (each output still sums over m
+  // in ascending order, as before).  Tk/Tn and Ek/En alternate instead of being copied back.
+  const int rpp = GP_NT / p, jc = tid % p, r0 = tid / p;
+  const bool act = r0 < rpp;
   double* Tk = Aug;
   double* Tn = Aug + pp;
   double sa1[GP_NR], sa2[GP_NR];
-  for (int e = tid; e < pp; e += RC_BLOCK) {
+  for (int e = tid; e < pp; e += GP_NT) {
     Tk[e] = T[e];
     Ek[e] = Ex[e];
   }
 #pragma unroll
-  for (int u = 0; u < GP_NR; ++u) {
-    const int e = tid + u * RC_BLOCK;
-    const int i = e / p, j = e - i * p;
-    sa1[u] = (e < pp && i == j) ? 1.0 : 0.0;
-    sa2[u] = sa1[u];
+  for (int v = 0; v < GP_NR; ++v) {
+    const int i = r0 + v * rpp;
+    sa1[v] = (act && i < p && i == jc) ? 1.0 : 0.0;
+    sa2[v] = sa1[v];
   }
   __syncthreads();
   for (int k = 1; k < p; ++k) {
     if (k > 1) {  // A^k = A^(k-1) A
-      for (int e = tid; e < pp; e += RC_BLOCK) {
-        const int i = e / p, j = e - i * p;
-        double a = 0.;
-        float b = 0.f;
-        for (int m = 0; m < p; ++m) {
-          a += Tk[i * p + m] * T[m * p + j];
-          b += Ek[i * p + m] * Ex[m * p + j];
+      if (act) {
+        double a[GP_NR];
+        float b[GP_NR];
+#pragma unroll
+        for (int v = 0; v < GP_NR; ++v) {
+          a[v] = 0.;
+          b[v] = 0.f;
         }
-        Tn[e] = a;
-        En[e] = b;
+        for (int m = 0; m < p; ++m) {
+          const double tm = T[m * p + jc];
+          const float xm = Ex[m * p + jc];
+#pragma unroll
+          for (int v = 0; v < GP_NR; ++v) {
+            const int i = r0 + v * rpp;
+            if (i < p) {
+              a[v] += Tk[i * p + m] * tm;
+              b[v] += Ek[i * p + m] * xm;
+            }
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < GP_NR; ++v) {
+          const int i = r0 + v * rpp;
+          if (i < p) {
+            Tn[i * p + jc] = a[v];
+            En[i * p + jc] = b[v];
+          }
+        }
       }
       __syncthreads();
-      for (int e = tid; e < pp; e += RC_BLOCK) {
-        Tk[e] = Tn[e];
-        Ek[e] = En[e];
-      }
-      __syncthreads();
+      double* tt = Tk;
+      Tk = Tn;
+      Tn = tt;
+      float* ff = Ek;
+      Ek = En;
+      En = ff;
     }
     const double ck = eps_pow[k];
     const float ckf = (float)ck;
     double se = 0.;
+    if (act) {
 #pragma unroll
-    for (int u = 0; u < GP_NR; ++u) {
-      const int e = tid + u * RC_BLOCK;
-      if (e < pp) {
-        const double tk = Tk[e];
-        const float ek = Ek[e];
-        sa1[u] = sa1[u] + ck * tk;
-        sa2[u] = sa2[u] + (double)(ckf * ek);
-        const double df = tk - (double)ek;
-        se += df * df;
+      for (int v = 0; v < GP_NR; ++v) {
+        const int i = r0 + v * rpp;
+        if (i < p) {
+          const double tk = Tk[i * p + jc];
+          const float ek = Ek[i * p + jc];
+          sa1[v] = sa1[v] + ck * tk;
+          sa2[v] = sa2[v] + (double)(ckf * ek);
+          const double df = tk - (double)ek;
+          se += df * df;
+        }
       }
     }
-    se = rc_block_sum_d(se, redd);
+    se = rc_block_sum_d(se, redd);  // its barriers also order this pass's reads before the next writes
     if (tid == 0) o[6 + k] = se / (double)pp;
   }
   double acc = 0.;
+  if (act) {
 #pragma unroll
-  for (int u = 0; u < GP_NR; ++u) {
-    const int e = tid + u * RC_BLOCK;
-    if (e < pp) {
-      const double df = sqrt(sa1[u]) - sqrt(sa2[u]);
-      acc += df * df;
+    for (int v = 0; v < GP_NR; ++v) {
+      const int i = r0 + v * rpp;
+      if (i < p) {
+        const double df = sqrt(sa1[v]) - sqrt(sa2[v]);
+        acc += df * df;
+      }
     }
   }
   const double dd = sqrt(rc_block_sum_d(acc, redd));
   if (tid == 0) o[6] = 1.0 / (1.0 + dd);
+}
+
+
+// ---- per-epoch tracker statistics (model_utils.py:163-209: track_l1_stats, track_cosine_stats)
+// The reference converts every estimate to float64 on the host and reduces it there; a packed
+// grid search would copy R x S x K full lagged estimates per epoch (tens of MB at p = 64).
+// Here one workgroup reduces one row (a fixed order: per-thread strided partial sums, wave tree,
+// waves in order -- independent of how many rows a launch holds), so a replica's values do not
+// depend on the pack it runs in.
+
+__device__ inline float gp_block_maxf(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wv] = v;
+  __syncthreads();
+  float m = red[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+  __syncthreads();
+  return m;
+}
+
+// grid (nrows): out[row] = sum_i |x_i / max(x)| in float64 over the n floats of the row
+__global__ __launch_bounds__(RC_BLOCK) void k_gc_l1(const float* x, int64_t n, double* out) {
+  const float* r = x + (int64_t)blockIdx.x * n;
+  __shared__ float redf[RC_BLOCK / 64];
+  __shared__ double redd[RC_BLOCK / 64];
+  float mx = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += RC_BLOCK) mx = fmaxf(mx, r[i]);
+  const double m = (double)gp_block_maxf(mx, redf);
+  double acc = 0.;
+  for (int64_t i = threadIdx.x; i < n; i += RC_BLOCK) acc += fabs((double)r[i] / m);
+  acc = rc_block_sum_d(acc, redd);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
+// grid (K(K+1)/2 pairs, nsamp): rows i1 <= i2 of sample s (K rows of n floats), each divided by its
+// own max in float64: out[s][i1][i2] = sum_e f1_e f2_e (the diagonal is the squared norm)
+__global__ __launch_bounds__(RC_BLOCK) void k_gc_dots(const float* x, int K, int64_t n, double* out) {
+  int q = blockIdx.x, i1 = 0;
+  while (q >= K - i1) {
+    q -= K - i1;
+    ++i1;
+  }
+  const int i2 = i1 + q;
+  const int s = blockIdx.y;
+  const float* a = x + ((int64_t)s * K + i1) * n;
+  const float* b = x + ((int64_t)s * K + i2) * n;
+  __shared__ float redf[RC_BLOCK / 64];
+  __shared__ double redd[RC_BLOCK / 64];
+  float ma = -INFINITY, mb = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += RC_BLOCK) {
+    ma = fmaxf(ma, a[i]);
+    mb = fmaxf(mb, b[i]);
+  }
+  const double da = (double)gp_block_maxf(ma, redf), db = (double)gp_block_maxf(mb, redf);
+  double acc = 0.;
+  for (int64_t i = threadIdx.x; i < n; i += RC_BLOCK) acc += ((double)a[i] / da) * ((double)b[i] / db);
+  acc = rc_block_sum_d(acc, redd);
+  if (threadIdx.x == 0) out[((int64_t)s * K + i1) * K + i2] = acc;
 }
 
 }  // namespace
@@ -432,7 +526,29 @@ extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p,
                            "k_gc_progress LDS");
     if (e) return e;
   }
-  hipLaunchKernelGGL(k_gc_progress, dim3(S * G), dim3(RC_BLOCK), lds, (hipStream_t)stream, S, nE, G, p, Lt, est, truth,
+  hipLaunchKernelGGL(k_gc_progress, dim3(S * G), dim3(GP_NT), lds, (hipStream_t)stream, S, nE, G, p, Lt, est, truth,
                      eps_pow, in_degree_coeff, out_degree_coeff, out);
   return rc_check(hipGetLastError(), "k_gc_progress");
+}
+
+extern "C" int redcliff_gc_track_stats(int32_t n_l1_rows, int64_t l1_len, const float* est, double* l1_out,
+                                       int32_t n_samples, int32_t K, int64_t row_len, const float* nolag,
+                                       double* dots_out, void* stream) {
+  if (n_l1_rows < 0 || n_samples < 0 || K < 1 || K > 64 || (n_l1_rows > 0 && (l1_len < 1 || !est || !l1_out)) ||
+      (n_samples > 0 && (row_len < 1 || !nolag || !dots_out))) {
+    rc_set_error("gc_track_stats: bad arguments (rows=%d len=%lld samples=%d K=%d row_len=%lld)", n_l1_rows,
+                 (long long)l1_len, n_samples, K, (long long)row_len);
+    return REDCLIFF_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (n_l1_rows > 0) {
+    hipLaunchKernelGGL(k_gc_l1, dim3(n_l1_rows), dim3(RC_BLOCK), 0, s, est, l1_len, l1_out);
+    const int e = rc_check(hipGetLastError(), "k_gc_l1");
+    if (e) return e;
+  }
+  if (n_samples > 0) {
+    hipLaunchKernelGGL(k_gc_dots, dim3(K * (K + 1) / 2, n_samples), dim3(RC_BLOCK), 0, s, nolag, K, row_len, dots_out);
+    return rc_check(hipGetLastError(), "k_gc_dots");
+  }
+  return 0;
 }

@@ -9,7 +9,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
@@ -32,7 +32,8 @@ EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_b
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
             "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm",
-            "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions")
+            "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions",
+            "redcliff_gc_track_stats")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine")
 
 
@@ -116,6 +117,8 @@ def lib():
                                 ctypes.c_int32, _vp]
     L.redcliff_gc_progress.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp]
+    L.redcliff_gc_track_stats.argtypes = [ctypes.c_int32, _i64, _vp, _vp, ctypes.c_int32, ctypes.c_int32, _i64, _vp,
+                                          _vp, _vp]
     L.redcliff_debug_guard_bands.argtypes = [ctypes.c_int32]
     L.redcliff_workspace_regions.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(_i64), ctypes.c_int32]
     for name in EXPORTED[2:]:

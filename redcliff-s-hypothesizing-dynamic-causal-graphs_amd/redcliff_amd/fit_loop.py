@@ -54,7 +54,8 @@ class ParamSnapshot:
 
     def __init__(self, model, emb=None, fac=None, bn=None):
         eng = model.engine()
-        eng.ensure_bound()
+        if emb is None or fac is None or bn is None:  # copies of the live buffers: bindings must be current
+            eng.ensure_bound()
         self.model = model
         with torch.no_grad():
             self.emb = eng.emb.clone() if emb is None else emb
@@ -285,23 +286,20 @@ def train_confusion_many(trackers, cms):
             t.cm_train[key].append(v[i].copy())
 
 
-def gc_progress_many(trackers, est, nolag, vals):
+def gc_progress_many(trackers, vals, l1, nrm, dots):
     """FitTracker.gc_progress (device-metrics path) of several fits at once -- a packed grid search
     updates every replica's trackers in a few array operations instead of R python loops.
 
-    est (Ra, S, K, p, p, ls) float32 host array of the lagged estimates, nolag (Ra, Sn, K, p, p, 1),
-    vals (Ra, S, G, 6 + p) device metric values or None; trackers share GC, nsup, K and p.  Every
-    appended value is bit-identical to the per-fit trackers' (metrics.track_*): the reductions
-    keep their numpy order (per-row pairwise sums, einsum), and the reference's python-float
-    running sums over samples are left-to-right float64 cumulative sums."""
+    vals (Ra, S, G, 6 + p) device metric values (redcliff_gc_progress) or None; l1 (Ra, S, K),
+    nrm (Ra, Sn, K), dots (Ra, Sn, K, K): the per-estimate statistics of metrics.gc_track_values
+    (device) or metrics.track_values_host; trackers share GC, nsup, K and p.  With the host
+    statistics every appended value is bit-identical to the per-fit trackers' (metrics.track_*):
+    the reference's python-float running sums over samples are left-to-right float64 cumulative
+    sums, the history length rules are model_utils.py:63-84 / :136-158."""
     t0 = trackers[0]
     GC, nsup, K = t0.GC, t0.nsup, t0.K
-    S = est.shape[1]
-    if S == 0:  # nothing to vectorise: keep the per-fit code (and its error behaviour)
-        for i, t in enumerate(trackers):
-            t.gc_progress([], nolag[i], None if vals is None else vals[i])
-        return
-    if GC is not None and nsup > 0 and vals is not None:
+    S = l1.shape[1]
+    if GC is not None and nsup > 0 and vals is not None and S > 0:
         n = float(S)
         run = np.cumsum(vals, axis=1)[:, -1]  # (Ra, G, C): _running over samples
         G = run.shape[1]
@@ -328,29 +326,23 @@ def gc_progress_many(trackers, est, nolag, vals):
                     for pl in range(1, min(t.p, pv)):
                         t.plm_hist[pl][j].append(ri[j][6 + pl] / n)
     if nsup > 0:  # track_l1_stats over every (sample, factor) estimate
-        e = est.astype(np.float64)
-        mx = e.max(axis=(3, 4, 5), keepdims=True)
-        v = np.abs(e / mx).reshape(e.shape[0], S, K, -1).sum(axis=-1)
-        l1 = np.cumsum(v, axis=1)[:, -1] / float(S)  # (Ra, K)
+        if S == 0:
+            raise IndexError("list index out of range")  # track_l1_stats on an empty sample list
+        l1m = np.cumsum(l1, axis=1)[:, -1] / float(S)  # (Ra, K)
         for i, t in enumerate(trackers):
-            li = l1[i].tolist()
+            li = l1m[i].tolist()
             for j in range(len(t.l1_hist)):
                 t.l1_hist[j].append(li[j])
+    Ra, Sn = dots.shape[0], dots.shape[1]
     for lo, hi, attr in ((0, nsup, "cos_hist"), (nsup, K, "cos_unsup")):  # track_cosine_stats_batched
-        a = np.asarray(nolag[:, :, lo:hi], dtype=np.float64)
-        Ra, Sn, Kc = a.shape[0], a.shape[1], a.shape[2]
-        if Kc < 2 or Sn == 0:
+        if hi - lo < 2 or Sn == 0:
             continue
-        flat = a.reshape(Ra, Sn, Kc, -1)
-        flat = flat / flat.max(axis=3, keepdims=True)
-        with np.errstate(invalid="ignore"):
-            nrm = np.linalg.norm(flat, axis=3)
-        nrm = np.where(np.isfinite(nrm), nrm, -1.)
-        nrm = np.maximum(nrm, 1e-8)
-        dots = np.einsum("rski,rsli->rskl", flat, flat)
-        for i1 in range(Kc):
-            for i2 in range(i1 + 1, Kc):
-                cv = dots[:, :, i1, i2] / (nrm[:, :, i1] * nrm[:, :, i2])
+        nr = nrm[:, :, lo:hi]
+        nr = np.where(np.isfinite(nr), nr, -1.)
+        nr = np.maximum(nr, 1e-8)
+        for i1 in range(hi - lo):
+            for i2 in range(i1 + 1, hi - lo):
+                cv = dots[:, :, lo + i1, lo + i2] / (nr[:, :, i1] * nr[:, :, i2])
                 tot = np.cumsum(np.concatenate([np.zeros((Ra, 1)), cv], axis=1), axis=1)[:, -1] / float(Sn)
                 key = "%dand%d" % (i1 + lo, i2 + lo)
                 for i, t in enumerate(trackers):
@@ -474,8 +466,7 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
                 vals = None
                 if GC is not None and nsup > 0 and est_t.shape[0] > 0:
                     vals = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff)
-                est_host = est_t.cpu().numpy()
-                nolag_np = nolag_t.cpu().numpy()
+                stats = M.gc_track_values(est_t, nolag_t)
             else:
                 if fused:
                     Xv = val["X"][:min(int(val["sizes"][0]), model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
@@ -489,7 +480,7 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
                                  combine_wavelet_representations=True)
                 nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
         if dev_metrics:
-            gc_progress_many([tr], est_host[None], nolag_np[None], None if vals is None else vals[None])
+            gc_progress_many([tr], None if vals is None else vals[None], *(x[None] for x in stats))
         else:
             tr.gc_progress(est_np, nolag_np, vals)
 

@@ -225,6 +225,23 @@ def _truth_arrays(GC, G):
     return np.ascontiguousarray(np.stack([on, off]), dtype=np.float64)
 
 
+_TRUTH_CACHE = []  # [(GC list object, its arrays' ids, G, p, eps, device, truth, eps_pow)]: a fit's constants
+
+
+def _device_truth(GC, G, p, eps, dev):
+    """The normalised true graphs and eps powers on the device, uploaded once per fit (same GC
+    list object and arrays) instead of once per epoch."""
+    ids = tuple(id(g) for g in GC)
+    for ent in _TRUTH_CACHE:
+        if ent[0] is GC and ent[1] == ids and ent[2:6] == (G, p, eps, dev):
+            return ent[6], ent[7]
+    truth = torch.from_numpy(_truth_arrays(GC, G)).to(dev)
+    eps_pow = torch.tensor([eps ** k for k in range(p)], dtype=torch.float64, device=dev)
+    _TRUTH_CACHE.insert(0, (GC, ids, G, p, eps, dev, truth, eps_pow))
+    del _TRUTH_CACHE[4:]
+    return truth, eps_pow
+
+
 def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.):
     """est: float32 CUDA tensor (S, nE, p, p, Lt) of GC estimates; GC: true graphs (p, p, lags).
     Returns float64 (S, G, 6 + p), G = min(nE, len(GC)): f1, roc_auc, f1 / roc_auc without
@@ -237,8 +254,7 @@ def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.
     G = min(nE, len(GC))
     dev = est.device
     est = est.to(torch.float32).contiguous()
-    truth = torch.from_numpy(_truth_arrays(GC, G)).to(dev)
-    eps_pow = torch.tensor([eps ** k for k in range(p)], dtype=torch.float64, device=dev)
+    truth, eps_pow = _device_truth(GC, G, p, eps, dev)
     out = torch.empty(S, G, 6 + p, dtype=torch.float64, device=dev)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     nat.check(nat.lib().redcliff_gc_progress(S, nE, G, p, Lt, est.data_ptr(), truth.data_ptr(), eps_pow.data_ptr(),
@@ -331,3 +347,54 @@ def track_cosine_stats_batched(est, hist, label_offset=0):
     for key in cur:
         hist[key].append(cur[key] / float(S))
     return hist
+
+
+# ---------------------------------------------------------------------------------------------
+# Tracker statistics of fit() (model_utils.py:163-209): the per-(sample, factor) L1 values of the
+# lagged estimates and the normalised dot products of the lag-free estimates, computed on the
+# device (redcliff_gc_track_stats) so only [S][K] / [Sn][K][K] values cross to the host; the
+# python-float bookkeeping (running sums over samples, pairs, history appends) is
+# fit_loop.gc_progress_many.  track_values_host is the same quantities in the reference's numpy
+# order (test oracle for the device values).
+
+def gc_track_values(est, nolag):
+    """est (..., S, K, p, p, Ls) and nolag (..., Sn, K, p, p, 1) float32 CUDA tensors ->
+    (l1 (..., S, K), nrm (..., Sn, K), dots (..., Sn, K, K)) float64 numpy (dots: upper triangle)."""
+    import ctypes
+    from . import _native as nat
+    dev = est.device
+    lead = est.shape[:-5]
+    S, K = est.shape[-5], est.shape[-4]
+    Sn = nolag.shape[-5]
+    est = est.to(torch.float32).contiguous()
+    nolag = nolag.to(torch.float32).contiguous()
+    nrow = int(np.prod(lead, dtype=np.int64)) * S * K
+    nsamp = int(np.prod(lead, dtype=np.int64)) * Sn
+    l1 = torch.zeros(max(nrow, 1), dtype=torch.float64, device=dev)
+    dots = torch.zeros(max(nsamp, 1), K, K, dtype=torch.float64, device=dev)
+    row = int(np.prod(est.shape[-3:]))
+    rown = int(np.prod(nolag.shape[-3:]))
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    nat.check(nat.lib().redcliff_gc_track_stats(nrow, row, est.data_ptr(), l1.data_ptr(), nsamp, K, rown,
+                                                nolag.data_ptr(), dots.data_ptr(), stream), "gc_track_stats")
+    l1 = l1.cpu().numpy()[:nrow].reshape(tuple(lead) + (S, K))
+    dots = dots.cpu().numpy()[:nsamp].reshape(tuple(lead) + (Sn, K, K))
+    nrm = np.sqrt(np.diagonal(dots, axis1=-2, axis2=-1))
+    return l1, nrm, dots
+
+
+def track_values_host(est, nolag):
+    """gc_track_values on host arrays, in the per-fit trackers' numpy order (track_l1_stats:
+    np.sum(np.abs(e / np.max(e))) per estimate; track_cosine_stats_batched: np.linalg.norm and
+    einsum of the max-normalised rows)."""
+    e = np.asarray(est, dtype=np.float64)
+    lead = e.shape[:-3]
+    mx = e.max(axis=(-3, -2, -1), keepdims=True)
+    l1 = np.abs(e / mx).reshape(lead + (-1,)).sum(axis=-1)
+    a = np.asarray(nolag, dtype=np.float64)
+    flat = a.reshape(a.shape[:-3] + (-1,))
+    flat = flat / flat.max(axis=-1, keepdims=True)
+    with np.errstate(invalid="ignore"):
+        nrm = np.linalg.norm(flat, axis=-1)
+    dots = np.einsum("...ki,...li->...kl", flat, flat)
+    return l1, nrm, dots

@@ -352,9 +352,8 @@ class ReplicaPack:
                         vals = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
                                                     in_degree_coeff, out_degree_coeff)
                         vals = vals.reshape(Ra, S, *vals.shape[1:])
-                    est_host = est_t.cpu().numpy()
-                    nolag_host = nolag_t.cpu().numpy()
-                gc_progress_many(tr_act, est_host, nolag_host, vals)
+                    stats = M.gc_track_values(est_t, nolag_t)
+                gc_progress_many(tr_act, vals, *stats)
                 # ---- validation of every active replica (:1416-1480), one launch chain
                 acc, conf = self._values(val, active)
                 nb = float(val["len"])

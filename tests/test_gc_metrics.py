@@ -115,3 +115,27 @@ def test_device_metrics_match_host_restatement(p, L, S, K):
                 daff=[x[0] for x in h[6]],
                 plm=np.asarray([[h[7][pl][i][0] for i in range(K)] for pl in range(1, p)]))
     _check("p%d" % p, dict(nsup=K, p=p), want, f1, roc, f1o, roco, dc, dcdd, daff, plm, 1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p,L,S,Sn,K,R", [(10, 4, 4, 40, 4, 3), (64, 20, 8, 40, 8, 1), (7, 3, 2, 5, 5, 2)])
+def test_device_tracker_stats_match_host(p, L, S, Sn, K, R):
+    """redcliff_gc_track_stats (per-estimate L1 values, normalised dot products of the lag-free
+    estimates; model_utils.py:163-209) vs the trackers' numpy reductions: the device sums in its
+    own fixed order, so 1e-12 relative; and the values of one replica do not depend on the
+    number of replicas in the launch (bitwise)."""
+    import torch
+    from redcliff_amd import metrics as M
+    rng = np.random.RandomState(p + L)
+    est = (rng.rand(R, S, K, p, p, L) - 0.05).astype(np.float32)
+    nolag = (rng.rand(R, Sn, K, p, p, 1) - 0.05).astype(np.float32)
+    got = M.gc_track_values(torch.from_numpy(est).cuda(), torch.from_numpy(nolag).cuda())
+    want = M.track_values_host(est, nolag)
+    for tag, g, w in zip(("l1", "nrm", "dots"), got, want):
+        if tag == "dots":
+            iu = np.triu_indices(K)
+            g, w = g[..., iu[0], iu[1]], w[..., iu[0], iu[1]]
+        np.testing.assert_allclose(g, w, rtol=1e-12, atol=0, err_msg=tag)
+    one = M.gc_track_values(torch.from_numpy(est[-1:]).cuda(), torch.from_numpy(nolag[-1:]).cuda())
+    for g, o in zip(got, one):
+        assert np.array_equal(g[-1:], o)

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from redcliff_amd import fit_loop
+from redcliff_amd import metrics as M
 
 
 def _tracker(p, K, nsup, GC):
@@ -50,7 +51,7 @@ def test_gc_progress_many_bitwise(p, K, nsup, nG, S, Sn, ls):
         for i, t in enumerate(solo):
             est_np = [[est[i, s, k] for k in range(K)] for s in range(S)]
             t.gc_progress(est_np, nolag[i], vals[i])
-        fit_loop.gc_progress_many(many, est, nolag, vals)
+        fit_loop.gc_progress_many(many, vals, *M.track_values_host(est, nolag))
         cms = rng.randint(0, 50, size=(Ra, max(nsup, 1), max(nsup, 1)))
         cms[0, 0] = 0  # an empty class: nan rates
         for i, t in enumerate(solo):
