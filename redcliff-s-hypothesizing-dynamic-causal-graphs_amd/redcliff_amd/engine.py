@@ -437,12 +437,24 @@ class FitEngine:
         refreshed (the host cost of one epoch is one C call)."""
         return StepPlan(self, kind, X, lab, stats, d, rows, sizes, oA, oB)
 
-    def run_values(self, X, lab, d, rows, sizes, train_bn=False, stats=None, confusion=True):
-        """validate_training body over consecutive batches; returns (acc[8], confusion)."""
+    VAL_GROUP = 7  # validation batches per replicated launch (R < 8 keeps the single fit's kernel paths)
+
+    def run_values(self, X, lab, d, rows, sizes, train_bn=False, stats=None, confusion=True, grouped=True, host=True):
+        """validate_training body over consecutive batches; returns (acc[8], confusion).
+        grouped=False: one launch chain per batch (the reference's loop, used by the tests).
+        host=False (eval mode): the per-batch device rows (acc [nb][8], confusion [nb][ns*ns]),
+        still on the device -- finish with values_from_rows after copying them back."""
         self.ensure_bound()
+        flags = nat.VALUES | (nat.CONFUSION if (confusion and self.nsup > 0) else 0)
+        rows = np.asarray(rows, dtype=np.int64)
+        sizes = np.asarray(sizes, dtype=np.int32)
+        if not host:
+            assert not train_bn
+            return self._run_values_grouped(X, lab, d, rows, sizes, flags, host=False)
+        if grouped and not train_bn and len(sizes) > 1:
+            return self._run_values_grouped(X, lab, d, rows, sizes, flags)
         self.acc.zero_()
         self.conf.zero_()
-        flags = nat.VALUES | (nat.CONFUSION if (confusion and self.nsup > 0) else 0)
         if train_bn:
             flags |= nat.BN_TRAIN
         a = self._args(d, flags, 0, X, lab, stats if train_bn else None)
@@ -453,6 +465,65 @@ class FitEngine:
                   "validate")
         self._mark_fresh()
         return self.acc.cpu().numpy(), self.conf.cpu().numpy().reshape(max(self.nsup, 1), max(self.nsup, 1))
+
+    def values_from_rows(self, accs, confs):
+        """(acc[8], confusion) of validate_training from the per-batch rows of run_values(host=False)
+        (host arrays): the batch loop's running sum, left to right in batch order."""
+        ns = max(self.nsup, 1)
+        return (np.cumsum(np.asarray(accs, dtype=np.float64), axis=0)[-1],
+                np.asarray(confs).reshape(-1, ns, ns).sum(axis=0).astype(np.int32))
+
+    def _run_values_grouped(self, X, lab, d, rows, sizes, flags, host=True):
+        """Eval-mode validation with the batches on the replica axis: a run of g <= VAL_GROUP
+        consecutive equal-size batches is ONE launch chain of g "replicas" that all read this
+        fit's parameters (parameter strides 0, window / label strides one batch) instead of g
+        dependent chains (validation updates nothing, so the batches are independent), and all
+        chains are enqueued before the one copy back.  Each batch's values land in its own
+        accumulator row as 0 + v (the batch loop adds v to the running sum); the rows are then
+        summed left to right in batch order, so the totals are bit-identical to the loop."""
+        ns = max(self.nsup, 1)
+        nb = len(sizes)
+        gmax = min(self.VAL_GROUP, nb)
+        dg = nat.Dims(**dict((f, getattr(d, f)) for f, _ in nat.Dims._fields_))
+        dg.R = gmax
+        key = (gmax, nb, d.Bmax, d.T)
+        vr = getattr(self, "_val_rep", None)
+        if vr is None or vr["key"] != key:
+            nbytes = nat.lib().redcliff_workspace_bytes(ctypes.byref(dg))
+            if nbytes == 0:
+                nat.check(-1, "workspace_bytes")
+            vr = {"key": key, "ws": torch.zeros(nbytes // 4, device=self.device, dtype=torch.float32),
+                  "acc": torch.zeros(nb, 8, device=self.device, dtype=torch.float64),
+                  "conf": torch.zeros(nb, ns * ns, device=self.device, dtype=torch.int32)}
+            self._val_rep = vr
+        rm = self.bn[0].unsqueeze(0).expand(gmax, self.F).contiguous()
+        rv = self.bn[1].unsqueeze(0).expand(gmax, self.F).contiguous()
+        hg = self._hyper().repeat(gmax)
+        vr["acc"].zero_()
+        vr["conf"].zero_()
+        a = self._args(dg, flags | nat.REFRESH_SUPPORTS, 0, X, lab, None)
+        a.emb_stride, a.fac_stride = 0, 0  # every "replica" reads this fit's parameters
+        a.bn_rm, a.bn_rv = rm.data_ptr(), rv.data_ptr()
+        a.hyper = hg.data_ptr()
+        a.ws, a.ws_bytes = vr["ws"].data_ptr(), vr["ws"].numel() * 4
+        i = 0
+        while i < nb:
+            g = 1
+            while (g < gmax and i + g < nb and sizes[i + g] == sizes[i]
+                   and rows[i + g] == rows[i] + g * int(sizes[i])):
+                g += 1
+            B = int(sizes[i])
+            a.d.R = g
+            a.B, a.row0 = B, int(rows[i])
+            a.x_rstride = B * d.T * self.p  # replica r = batch i + r
+            a.lab_rstride = B * self.K
+            a.acc = vr["acc"][i].data_ptr()
+            a.confusion = vr["conf"][i].data_ptr()
+            nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "validate (replicated batches)")
+            i += g
+        if not host:
+            return vr["acc"], vr["conf"]
+        return self.values_from_rows(vr["acc"].cpu().numpy(), vr["conf"].cpu().numpy())
 
     def forward_outputs(self, X, train_bn, bn_updates):
         """Embedder + factors + mixing on windows X (B, T>=Lmax, p): returns w_raw, y, xsim."""

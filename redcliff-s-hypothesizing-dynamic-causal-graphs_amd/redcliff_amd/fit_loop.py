@@ -420,6 +420,8 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
     Lm = model.Lmax
     ls = min(model.gen_lag, model.embed_lag)
 
+    dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
+        "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
     for it in range(iter_start, max_iter):
         if verbose:
             print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
@@ -442,55 +444,63 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
                     for kind in kinds:
                         eng.run_steps([kind], train["X"], train["lab"], train["stats"][bi:bi + 1], d_train, [r], [s],
                                       oA, oB)
-            if nsup > 0:
+            if nsup > 0 and not dev_metrics:
                 cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
         if not fused:  # the generic path's torch modules read their train/eval flags
             model._set_module_modes(kinds[-1] if kinds else None)
-        tr.train_confusion(cm if nsup > 0 else None)
 
-        # ---- GC progress on the first validation batch (:1366-1414).  The device-metrics path's
-        # launches take their BatchNorm mode from flags, so there the module flags are set once
-        # (_eval_modes: the state every epoch ends in) instead of three tree walks per epoch.
-        dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
-            "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
-        if not dev_metrics:
-            _eval_modes(model)
-        with torch.no_grad():
-            if dev_metrics:
+        if dev_metrics:
+            # The whole per-epoch evaluation on the device, ONE copy back: the train confusion
+            # matrix, GC progress on the first validation batch (:1366-1414: one embedder launch,
+            # the group norms, one broadcast, the metrics and tracker-statistics launches) and
+            # validation (:1416-1480, batches on the replica axis).  The launches take their
+            # BatchNorm mode from flags, so the module flags are set once (_eval_modes) instead
+            # of three tree walks per epoch.
+            with torch.no_grad():
+                conf_d = eng.conf.clone()
                 nfirst = int(val["sizes"][0])
                 Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
                 w, _ = model._labels_from_w(eng.embed_raw(Xv))
                 G, G0 = eng.gc_norms()
                 est_t, nolag_t = conditional_gc_estimates(w, G, G0, eng.dgcnn.A.detach(), nsup, ls,
                                                           model.primary_gc_est_mode)
-                vals = None
+                vals_d = None
                 if GC is not None and nsup > 0 and est_t.shape[0] > 0:
-                    vals = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff)
-                stats = M.gc_track_values(est_t, nolag_t)
-            else:
+                    vals_d = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff, host=False)
+                l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
+                acc_d, confv_d = eng.run_values(val["X"], val["lab"], d_train, val["rows"], val["sizes"], host=False)
+                got = M.fetch([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
+            cm, l1, dots, accs, confs = got[:5]
+            vals = got[5] if vals_d is not None else None
+            tr.train_confusion(cm.reshape(nsup, nsup) if nsup > 0 else None)
+            l1, nrm, dots = M.track_values_finish(l1, dots)
+            gc_progress_many([tr], None if vals is None else vals[None], l1[None], nrm[None], dots[None])
+            acc, confv = eng.values_from_rows(accs, confs)
+            hists = [[] for _ in range(5)] if nsup > 0 else [None] * 5
+            tr.validation(model._validation_tuple(acc, float(val["len"]), confv, *hists))
+        else:
+            tr.train_confusion(cm if nsup > 0 else None)
+            # ---- GC progress on the first validation batch (:1366-1414)
+            _eval_modes(model)
+            with torch.no_grad():
                 if fused:
                     Xv = val["X"][:min(int(val["sizes"][0]), model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
                 else:
                     Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(),
                                                                                               torch.float32)
-                vals = None
                 est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
                 est_np = [[g.detach().cpu().numpy() for g in row] for row in est]
                 nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
                                  combine_wavelet_representations=True)
                 nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
-        if dev_metrics:
-            gc_progress_many([tr], None if vals is None else vals[None], *(x[None] for x in stats))
-        else:
-            tr.gc_progress(est_np, nolag_np, vals)
-
-        # ---- validation (:1416-1480)
-        if fused:
-            tr.validation(model._validate_fused(X_val, nsup > 0))
-        elif nsup > 0:
-            tr.validation(model.validate_training(X_val, output_length, model.num_series, [], [], [], [], []))
-        else:
-            tr.validation(model.validate_training(X_val, output_length, model.num_series))
+            tr.gc_progress(est_np, nolag_np, None)
+            # ---- validation (:1416-1480)
+            if fused:
+                tr.validation(model._validate_fused(X_val, nsup > 0))
+            elif nsup > 0:
+                tr.validation(model.validate_training(X_val, output_length, model.num_series, [], [], [], [], []))
+            else:
+                tr.validation(model.validate_training(X_val, output_length, model.num_series))
 
         # ---- early stopping (:1482-1559)
         if tr.step(it, lambda: _best_model(model, fused)):

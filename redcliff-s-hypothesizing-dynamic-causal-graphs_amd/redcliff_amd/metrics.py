@@ -242,7 +242,7 @@ def _device_truth(GC, G, p, eps, dev):
     return truth, eps_pow
 
 
-def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.):
+def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1., host=True):
     """est: float32 CUDA tensor (S, nE, p, p, Lt) of GC estimates; GC: true graphs (p, p, lags).
     Returns float64 (S, G, 6 + p), G = min(nE, len(GC)): f1, roc_auc, f1 / roc_auc without
     self-connections, deltacon0, deltacon0 with directed degrees, deltaffinity, path-length MSE
@@ -260,7 +260,7 @@ def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.
     nat.check(nat.lib().redcliff_gc_progress(S, nE, G, p, Lt, est.data_ptr(), truth.data_ptr(), eps_pow.data_ptr(),
                                               float(in_degree_coeff), float(out_degree_coeff), out.data_ptr(), stream),
               "gc_progress")
-    return out.cpu().numpy()
+    return out.cpu().numpy() if host else out
 
 
 def _running(vals):
@@ -357,9 +357,10 @@ def track_cosine_stats_batched(est, hist, label_offset=0):
 # fit_loop.gc_progress_many.  track_values_host is the same quantities in the reference's numpy
 # order (test oracle for the device values).
 
-def gc_track_values(est, nolag):
+def gc_track_values(est, nolag, host=True):
     """est (..., S, K, p, p, Ls) and nolag (..., Sn, K, p, p, 1) float32 CUDA tensors ->
-    (l1 (..., S, K), nrm (..., Sn, K), dots (..., Sn, K, K)) float64 numpy (dots: upper triangle)."""
+    (l1 (..., S, K), nrm (..., Sn, K), dots (..., Sn, K, K)) float64 numpy (dots: upper triangle).
+    host=False: (l1, dots) still on the device (finish with track_values_finish)."""
     import ctypes
     from . import _native as nat
     dev = est.device
@@ -377,10 +378,28 @@ def gc_track_values(est, nolag):
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     nat.check(nat.lib().redcliff_gc_track_stats(nrow, row, est.data_ptr(), l1.data_ptr(), nsamp, K, rown,
                                                 nolag.data_ptr(), dots.data_ptr(), stream), "gc_track_stats")
-    l1 = l1.cpu().numpy()[:nrow].reshape(tuple(lead) + (S, K))
-    dots = dots.cpu().numpy()[:nsamp].reshape(tuple(lead) + (Sn, K, K))
-    nrm = np.sqrt(np.diagonal(dots, axis1=-2, axis2=-1))
-    return l1, nrm, dots
+    l1 = l1[:nrow].view(tuple(lead) + (S, K))
+    dots = dots[:nsamp].view(tuple(lead) + (Sn, K, K))
+    if not host:
+        return l1, dots
+    return track_values_finish(l1.cpu().numpy(), dots.cpu().numpy())
+
+
+def track_values_finish(l1, dots):
+    """(l1, nrm, dots) host arrays from the device statistics (nrm = sqrt of the diagonal)."""
+    return l1, np.sqrt(np.diagonal(dots, axis1=-2, axis2=-1)), dots
+
+
+def fetch(tensors):
+    """ONE device -> host copy of several small tensors (float64 / integer counts, exact as
+    float64): numpy arrays of their shapes (integers come back as int64)."""
+    flat = torch.cat([t.reshape(-1).to(torch.float64) for t in tensors]).cpu().numpy()
+    out, o = [], 0
+    for t in tensors:
+        a = flat[o:o + t.numel()].reshape(tuple(t.shape))
+        out.append(a if t.dtype == torch.float64 else a.astype(np.int64))
+        o += t.numel()
+    return out
 
 
 def track_values_host(est, nolag):

@@ -207,8 +207,9 @@ class ReplicaPack:
                 self.models[r]._set_module_modes(kinds[-1] if kinds else None)
         return kinds
 
-    def _values(self, ds, active=None):
-        """validate_training accumulators of the active replicas: raw acc [R][8], confusion."""
+    def _values(self, ds, active=None, host=True):
+        """validate_training accumulators of the active replicas: raw acc [R][8], confusion
+        (host=False: the device buffers, for one combined copy back)."""
         self._ensure_bound()
         self.acc.zero_()
         self.conf.zero_()
@@ -222,6 +223,8 @@ class ReplicaPack:
                                                  sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * e0.F, _stream()),
                   "packed validate")
         ns = max(e0.nsup, 1)
+        if not host:
+            return self.acc, self.conf
         return self.acc.cpu().numpy(), self.conf.cpu().numpy().reshape(self.R, ns, ns)
 
     def validate(self, ds, active=None):
@@ -334,11 +337,11 @@ class ReplicaPack:
                 self.conf.zero_()
                 self.run_epoch(it, train, active, set_modes=False)
                 tr_act = [trackers[r] for r in active]
-                if nsup > 0:
-                    cms = self.conf.cpu().numpy().reshape(R, nsup, nsup)
-                    train_confusion_many(tr_act, cms[active])
-                # ---- GC progress of every active replica on the first validation batch (:1366-1414)
+                # ---- the per-epoch evaluation of every active replica on the device, ONE copy
+                # back: train confusion, GC progress on the first validation batch (:1366-1414),
+                # validation (:1416-1480, one launch chain)
                 with torch.no_grad():
+                    conf_d = self.conf.clone()
                     w_raw = self.embed_raw(Xv, active)  # (Ra, S, K)
                     emb0 = models[0].factor_score_embedder
                     w = torch.sigmoid(emb0.sigmoid_eccentricity_coeff * w_raw) if emb0.use_sigmoid_restriction else w_raw
@@ -346,16 +349,21 @@ class ReplicaPack:
                     A = self.emb[:, :p * p].view(R, p, p)
                     ai = torch.as_tensor(active, device=self.device)
                     est_t, nolag_t = conditional_gc_estimates(w, G[ai], G0[ai], A[ai], nsup, ls, m0.primary_gc_est_mode)
-                    vals = None
-                    if GC is not None and nsup > 0 and est_t.shape[1] > 0:
-                        Ra, S = est_t.shape[0], est_t.shape[1]
-                        vals = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
-                                                    in_degree_coeff, out_degree_coeff)
-                        vals = vals.reshape(Ra, S, *vals.shape[1:])
-                    stats = M.gc_track_values(est_t, nolag_t)
-                gc_progress_many(tr_act, vals, *stats)
-                # ---- validation of every active replica (:1416-1480), one launch chain
-                acc, conf = self._values(val, active)
+                    Ra, S = est_t.shape[0], est_t.shape[1]
+                    vals_d = None
+                    if GC is not None and nsup > 0 and S > 0:
+                        vals_d = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
+                                                      in_degree_coeff, out_degree_coeff, host=False)
+                    l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
+                    acc_d, confv_d = self._values(val, active, host=False)
+                    got = M.fetch([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
+                cms, l1, dots, acc, conf = got[:5]
+                vals = got[5].reshape(Ra, S, *got[5].shape[1:]) if vals_d is not None else None
+                if nsup > 0:
+                    train_confusion_many(tr_act, cms.reshape(R, nsup, nsup)[active])
+                gc_progress_many(tr_act, vals, *M.track_values_finish(l1, dots))
+                ns = max(nsup, 1)
+                conf = conf.reshape(R, ns, ns)
                 nb = float(val["len"])
                 for r in active:
                     hist = [[] for _ in range(5)] if nsup > 0 else [None] * 5

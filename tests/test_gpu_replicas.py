@@ -124,3 +124,29 @@ def test_window_block_combine_variants_bitwise(variant, monkeypatch):
         fits[v] = {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
     for k, want in fits[variant].items():
         np.testing.assert_array_equal(fits["2"][k], want, err_msg=k)
+
+
+@pytest.mark.parametrize("path", ["vector", "mfma"])
+def test_grouped_validation_bitwise_equals_batch_loop(path, monkeypatch):
+    """validate_training with the validation batches on the replica axis (runs of <= 7 equal
+    batches per launch chain, parameter strides 0; FitEngine._run_values_grouped) against one
+    launch chain per batch: identical accumulators and confusion counts, bit for bit, with a
+    ragged last batch, after training has moved the parameters off their initial values."""
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    m = make(3, 10.0, 0.1)
+    oA, oB = opts(m, 5e-4, 2e-4)
+    train = data(64 * 2, seed=11)
+    for epoch in (0, 1, 2):
+        for bi, (Xb, Yb) in enumerate(train):
+            m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+    val = data(64 * 9 + 40, seed=12)  # 9 full batches (groups of 7 + 2) and a ragged one
+    eng = m.engine()
+    ds = eng.cache_dataset(val)
+    d = eng.workspace(ds["Bmax"], ds["T"])
+    acc_g, conf_g = eng.run_values(ds["X"], ds["lab"], d, ds["rows"], ds["sizes"])
+    acc_s, conf_s = eng.run_values(ds["X"], ds["lab"], d, ds["rows"], ds["sizes"], grouped=False)
+    assert acc_s[7] == len(val)
+    np.testing.assert_array_equal(acc_g, acc_s)
+    np.testing.assert_array_equal(conf_g, conf_s)
+    v1 = m.validate_training(val, 1, m.num_series, [], [], [], [], [])
+    assert v1[9] == acc_s[6] / len(val)
