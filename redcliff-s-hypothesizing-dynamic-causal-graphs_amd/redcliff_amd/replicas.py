@@ -156,6 +156,18 @@ class ReplicaPack:
             a.n_replicas = len(act)
         return a, engs
 
+    def _index(self, idx):
+        """Device index tensor of replica indices, cached per index set: building it from a python
+        list is a pageable host-to-device copy, which blocks the host until the stream drains."""
+        key = tuple(int(i) for i in idx)
+        cache = self.__dict__.setdefault("_idx_cache", {})
+        t = cache.get(key)
+        if t is None:
+            if len(cache) > 64:
+                cache.clear()
+            t = cache[key] = torch.as_tensor(np.asarray(key, dtype=np.int64)).to(self.device)
+        return t
+
     def _ensure_bound(self):
         if not self._bound_this_epoch:
             for e in self.engines:
@@ -248,7 +260,7 @@ class ReplicaPack:
         K = self.engines[0].K
         o, tot = self.ws_off["w"], self.ws_off["total"]
         ws = self.ws[:self.R * tot].view(self.R, tot)
-        return ws[idx, o:o + B * K].view(len(idx), B, K).clone()
+        return ws[:, o:o + B * K].index_select(0, self._index(idx)).view(len(idx), B, K)
 
     def gc_norms(self):
         """(G [R][K][p][p][L], G0 [R][K][p][p]) of every replica's factor weights (one launch)."""
@@ -347,7 +359,7 @@ class ReplicaPack:
                     w = torch.sigmoid(emb0.sigmoid_eccentricity_coeff * w_raw) if emb0.use_sigmoid_restriction else w_raw
                     G, G0 = self.gc_norms()
                     A = self.emb[:, :p * p].view(R, p, p)
-                    ai = torch.as_tensor(active, device=self.device)
+                    ai = self._index(active)
                     est_t, nolag_t = conditional_gc_estimates(w, G[ai], G0[ai], A[ai], nsup, ls, m0.primary_gc_est_mode)
                     Ra, S = est_t.shape[0], est_t.shape[1]
                     vals_d = None
@@ -435,13 +447,14 @@ class _PackBest:
     def copy_marked(self):
         if not self.marked:
             return
-        idx = torch.as_tensor(sorted(set(self.marked)), device=self.pack.device)
+        keys = sorted(set(self.marked))
+        idx = self.pack._index(keys)
         with torch.no_grad():
             self.emb.index_copy_(0, idx, self.pack.emb.index_select(0, idx))
             self.fac.index_copy_(0, idx, self.pack.fac.index_select(0, idx))
             self.bn.index_copy_(1, idx, self.pack.bn.index_select(1, idx))
             nbt = torch.stack([self.pack.models[int(r)].factor_score_embedder.dgcnn.dgcnn.BN1.num_batches_tracked
-                               for r in idx.tolist()])
+                               for r in keys])
             self.nbt.index_copy_(0, idx, nbt.to(self.nbt.dtype))
         self.marked = []
 
