@@ -400,13 +400,13 @@ class FitEngine:
         self.supports_fresh = True
         self._a_version = self.dgcnn.A._version
 
-    def _after(self, flags, nbn, nsteps):
+    def _after(self, flags, nbn, nsteps, bn=True):
         self._mark_fresh()
         if flags & nat.STEP_A:
             self.opt["A"]["t"] += nsteps
         if flags & nat.STEP_B:
             self.opt["B"]["t"] += nsteps
-        if nbn:
+        if nbn and bn:  # (a ReplicaPack advances its replicas' counters in one add)
             self.dgcnn.BN1.num_batches_tracked.add_(nbn * nsteps)
         self._sync_steps()
 

@@ -268,19 +268,24 @@ def _per_graph_appends(hists, run, n, G):
     return [run[i] / n for i in range(L)], L == G
 
 
-def train_confusion_many(trackers, cms):
-    """FitTracker.train_confusion of several fits (cms [Ra][nsup][nsup] integer counts): the
-    confusion rates of all of them in one vectorised pass (exact: integer-valued sums)."""
-    if not trackers or trackers[0].nsup <= 0:
-        return
+def confusion_rates_many(cms):
+    """_confusion_rates of a stack of confusion matrices [Ra][n][n] (integer counts, so every sum
+    is exact in any order): (TPR, TNR, FPR, FNR, ACC), each [Ra][n]."""
     cm = np.asarray(cms, dtype=np.float64)
     TP = np.diagonal(cm, axis1=1, axis2=2)
     FP = cm.sum(axis=1) - TP
     FN = cm.sum(axis=2) - TP
     TN = cm.sum(axis=(1, 2))[:, None] - (FP + FN + TP)
     with np.errstate(divide="ignore", invalid="ignore"):
-        rates = (TP / (TP + FN), TN / (TN + FP), FP / (FP + TN), FN / (TP + FN), (TP + TN) / (TP + FP + FN + TN))
-    TPR, TNR, FPR, FNR, ACC = rates
+        return TP / (TP + FN), TN / (TN + FP), FP / (FP + TN), FN / (TP + FN), (TP + TN) / (TP + FP + FN + TN)
+
+
+def train_confusion_many(trackers, cms):
+    """FitTracker.train_confusion of several fits (cms [Ra][nsup][nsup] integer counts): the
+    confusion rates of all of them in one vectorised pass (exact: integer-valued sums)."""
+    if not trackers or trackers[0].nsup <= 0:
+        return
+    TPR, TNR, FPR, FNR, ACC = confusion_rates_many(cms)
     for i, t in enumerate(trackers):
         for key, v in zip(CM_KEYS, (ACC, TPR, TNR, FPR, FNR)):
             t.cm_train[key].append(v[i].copy())

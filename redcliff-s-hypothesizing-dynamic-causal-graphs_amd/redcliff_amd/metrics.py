@@ -390,6 +390,34 @@ def track_values_finish(l1, dots):
     return l1, np.sqrt(np.diagonal(dots, axis1=-2, axis2=-1)), dots
 
 
+class _PendingFetch:
+    """fetch_async's handle: the packed values are on their way into pinned host memory."""
+
+    def __init__(self, tensors):
+        flat = torch.cat([t.reshape(-1).to(torch.float64) for t in tensors])
+        self.host = torch.empty(flat.shape, dtype=torch.float64, pin_memory=True)
+        self.host.copy_(flat, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        self.meta = [(tuple(t.shape), t.dtype, t.numel()) for t in tensors]
+
+    def wait(self):
+        self.ev.synchronize()
+        flat = self.host.numpy()
+        out, o = [], 0
+        for shape, dt, n in self.meta:
+            a = flat[o:o + n].reshape(shape)
+            out.append(a.copy() if dt == torch.float64 else a.astype(np.int64))
+            o += n
+        return out
+
+
+def fetch_async(tensors):
+    """fetch() without waiting: the copy is enqueued on the current stream (later launches may
+    follow it); .wait() blocks until the copy itself has landed and returns the arrays."""
+    return _PendingFetch(tensors)
+
+
 def fetch(tensors):
     """ONE device -> host copy of several small tensors (float64 / integer counts, exact as
     float64): numpy arrays of their shapes (integers come back as int64)."""

@@ -462,7 +462,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             hists = [None] * 5
         return self._validation_tuple(acc, float(ds["len"]), conf, *hists)
 
-    def _validation_tuple(self, acc, nb, conf, acc_h, tpr_h, tnr_h, fpr_h, fnr_h):
+    def _validation_tuple(self, acc, nb, conf, acc_h, tpr_h, tnr_h, fpr_h, fnr_h, rates=None):
         vals = [acc[nat_i] / nb for nat_i in range(7)]
         forecast, factor, cos, fwl1, smooth, adj, combo = vals
         out = [forecast, factor, cos, fwl1]
@@ -470,7 +470,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             out.append(smooth)
         out += [adj, 0.0, 0.0, 0.0, combo]
         if self.num_supervised_factors > 0:
-            TPR, TNR, FPR, FNR, ACC = _confusion_rates(conf)
+            TPR, TNR, FPR, FNR, ACC = _confusion_rates(conf) if rates is None else rates
             acc_h.append(ACC)
             tpr_h.append(TPR)
             tnr_h.append(TNR)

@@ -33,8 +33,8 @@ import torch
 from . import _native as nat
 from . import metrics as M
 from .engine import _stream, flags_for, phase_of_epoch
-from .fit_loop import (FitTracker, ParamSnapshot, conditional_gc_estimates, gc_progress_many, restore_parameters,
-                       standalone_copy, train_confusion_many)
+from .fit_loop import (FitTracker, ParamSnapshot, conditional_gc_estimates, confusion_rates_many, gc_progress_many,
+                       restore_parameters, standalone_copy, train_confusion_many)
 
 
 class ReplicaPack:
@@ -76,11 +76,19 @@ class ReplicaPack:
         self.ws = None
         self.ws_B = 0
         self._plans = {}
-        self._bound_this_epoch = False  # fit(): parameter bindings checked once per epoch
+        self._bound_this_epoch = False  # fit(): parameter bindings checked once per fit
         for r, (e, (oA, oB)) in enumerate(zip(self.engines, self.optimizers)):
             e.attach_pack(self, r)
             e.bind_optimizer("A", oA)
             e.bind_optimizer("B", oB)
+        # BatchNorm num_batches_tracked of every replica as a 0-d view of one [R] tensor, so a
+        # packed launch chain advances all of them with one add instead of R small launches
+        self.nbt = torch.zeros(R, device=dev, dtype=torch.long)
+        for r, e in enumerate(self.engines):
+            bn = e.dgcnn.BN1
+            with torch.no_grad():
+                self.nbt[r].copy_(bn.num_batches_tracked.reshape(()))
+            bn.num_batches_tracked = self.nbt[r]
 
     @staticmethod
     def _shape(e):
@@ -168,6 +176,47 @@ class ReplicaPack:
             t = cache[key] = torch.as_tensor(np.asarray(key, dtype=np.int64)).to(self.device)
         return t
 
+    def _mask(self, active):
+        """[R] long device tensor: 1 for the active replicas (all when None), cached per set."""
+        key = ("mask",) + (tuple(range(self.R)) if active is None else tuple(sorted(int(i) for i in active)))
+        cache = self.__dict__.setdefault("_idx_cache", {})
+        t = cache.get(key)
+        if t is None:
+            m = np.zeros(self.R, dtype=np.int64)
+            m[list(key[1:])] = 1
+            t = cache[key] = torch.as_tensor(m).to(self.device)
+        return t
+
+    def _state_tensors(self):
+        """(name, tensor, replica dim) of everything a training epoch advances per replica."""
+        return [("emb", self.emb, 0), ("fac", self.fac, 0), ("mA", self.m["A"], 0), ("vA", self.v["A"], 0),
+                ("mB", self.m["B"], 0), ("vB", self.v["B"], 0), ("bn", self.bn, 1), ("nbt", self.nbt, 0)]
+
+    def _save_state(self):
+        if getattr(self, "_prev", None) is None:
+            self._prev = dict((n, torch.empty_like(t)) for n, t, _ in self._state_tensors())
+        with torch.no_grad():
+            for n, t, _ in self._state_tensors():
+                self._prev[n].copy_(t)
+
+    def _step_counts(self, r):
+        e = self.engines[r]
+        return tuple(None if e.opt[g] is None else e.opt[g]["t"] for g in ("A", "B"))
+
+    def _roll_back(self, reps, steps_before):
+        """Replicas `reps` back to the state saved by _save_state (a speculative epoch undone)."""
+        idx = self._index(sorted(reps))
+        with torch.no_grad():
+            for n, t, dim in self._state_tensors():
+                t.index_copy_(dim, idx, self._prev[n].index_select(dim, idx))
+        for r in reps:
+            e = self.engines[r]
+            for g, t in zip(("A", "B"), steps_before[r]):
+                if t is not None:
+                    e.opt[g]["t"] = t
+            e._sync_steps()
+            e.supports_fresh = False
+
     def _ensure_bound(self):
         if not self._bound_this_epoch:
             for e in self.engines:
@@ -196,7 +245,10 @@ class ReplicaPack:
                                                      sizes_a.ctypes.data_as(ctypes.c_void_p), 2 * self.engines[0].F,
                                                      _stream()), "packed train_steps")
             for e in engs:
-                e._after(flags, nbn, len(rows_a))
+                e._after(flags, nbn, len(rows_a), bn=False)
+            if nbn:
+                with torch.no_grad():
+                    self.nbt.add_(self._mask(active), alpha=nbn * len(rows_a))
             for e in self.engines:
                 e.supports_fresh = False  # the single-fit workspace's supports are stale now
 
@@ -337,17 +389,29 @@ class ReplicaPack:
         # The module train/eval flags -- which no fused launch reads -- are set once, to the state
         # the reference leaves after every epoch (eval: GC tracking and validation call .eval()),
         # before checkpoints and at the end, instead of walking R module trees twice per epoch.
+        # nothing inside the loop re-points a parameter (snapshots and checkpoints copy), so the
+        # bindings of all R engines are checked once per fit, not per launch
+        self._bound_this_epoch = False
+        self._ensure_bound()
+        self._bound_this_epoch = True
+        # Overlap: while the host digests epoch `it` (trackers, stopping rule, snapshots), the GPU
+        # already trains epoch it + 1 for the replicas still active (speculatively).  The state
+        # every training epoch advances is copied aside first (`_save_state`); best-model
+        # snapshots of epoch `it` are taken from that copy, and a replica that stops at `it` is
+        # rolled back to it (parameters, Adam moments and step counts, BatchNorm statistics), so
+        # every replica ends exactly where its own fit() would.  No speculation across a
+        # checkpoint epoch (the files hold epoch `it`'s state) or past max_iter.
+        def launch_train(ep):
+            self.conf.zero_()
+            self.run_epoch(ep, train, active, set_modes=False)
+
         try:
-            for it in range(max_iter):
-                if not active:
-                    break
+            it = 0
+            if max_iter > 0:
+                launch_train(0)
+            while it < max_iter and active:
                 if verbose:
                     print("ReplicaPack.fit: epoch %d, %d of %d replicas active" % (it, len(active), R), flush=True)
-                self._bound_this_epoch = False
-                self._ensure_bound()
-                self._bound_this_epoch = True
-                self.conf.zero_()
-                self.run_epoch(it, train, active, set_modes=False)
                 tr_act = [trackers[r] for r in active]
                 # ---- the per-epoch evaluation of every active replica on the device, ONE copy
                 # back: train confusion, GC progress on the first validation batch (:1366-1414),
@@ -368,7 +432,14 @@ class ReplicaPack:
                                                       in_degree_coeff, out_degree_coeff, host=False)
                     l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
                     acc_d, confv_d = self._values(val, active, host=False)
-                    got = M.fetch([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
+                    pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] +
+                                            ([vals_d] if vals_d is not None else []))
+                spec = it + 1 < max_iter and not (dirs is not None and it % check_every == 0)
+                if spec:
+                    self._save_state()
+                    steps_before = [self._step_counts(r) for r in range(R)]
+                    launch_train(it + 1)
+                got = pending.wait()
                 cms, l1, dots, acc, conf = got[:5]
                 vals = got[5].reshape(Ra, S, *got[5].shape[1:]) if vals_d is not None else None
                 if nsup > 0:
@@ -377,23 +448,30 @@ class ReplicaPack:
                 ns = max(nsup, 1)
                 conf = conf.reshape(R, ns, ns)
                 nb = float(val["len"])
-                for r in active:
+                rates = confusion_rates_many(conf[active]) if nsup > 0 else None
+                for i, r in enumerate(active):
                     hist = [[] for _ in range(5)] if nsup > 0 else [None] * 5
-                    trackers[r].validation(models[r]._validation_tuple(acc[r], nb, conf[r], *hist))
+                    rt = tuple(x[i].copy() for x in rates) if nsup > 0 else None
+                    trackers[r].validation(models[r]._validation_tuple(acc[r], nb, conf[r], *hist, rates=rt))
                 # ---- early stopping, per replica (:1482-1559); snapshots copied in one batch
                 stopped = []
                 for r in active:
                     if trackers[r].step(it, lambda r=r: best.mark(r)):
                         stopped.append(r)
-                best.copy_marked()
+                best.copy_marked(self._prev if spec else None)
                 for r in stopped:
                     if verbose:
                         print("ReplicaPack.fit: replica %d stops early at epoch %d" % (r, it), flush=True)
+                if spec and stopped:
+                    self._roll_back(stopped, steps_before)
                 active = [r for r in active if r not in stopped]
                 if dirs is not None and it % check_every == 0:
                     _eval_modes(models)
                     for r in active:
                         trackers[r].checkpoint(dirs[r], it, optimizers=self.optimizers[r], save_plots=save_plots)
+                it += 1
+                if not spec and it < max_iter and active:
+                    launch_train(it)
         finally:
             self._bound_this_epoch = False
         _eval_modes(models)
@@ -444,18 +522,20 @@ class _PackBest:
         return ParamSnapshot(self.pack.models[r], emb=self.emb[r], fac=self.fac[r],
                              bn=(self.bn[0][r], self.bn[1][r], self.nbt[r]))
 
-    def copy_marked(self):
+    def copy_marked(self, src=None):
+        """src: a dict of [R][...] buffers holding the epoch's state (ReplicaPack._prev while the
+        next epoch already runs), else the live pack buffers."""
         if not self.marked:
             return
         keys = sorted(set(self.marked))
         idx = self.pack._index(keys)
+        pk = self.pack
+        s = src if src is not None else {"emb": pk.emb, "fac": pk.fac, "bn": pk.bn, "nbt": pk.nbt}
         with torch.no_grad():
-            self.emb.index_copy_(0, idx, self.pack.emb.index_select(0, idx))
-            self.fac.index_copy_(0, idx, self.pack.fac.index_select(0, idx))
-            self.bn.index_copy_(1, idx, self.pack.bn.index_select(1, idx))
-            nbt = torch.stack([self.pack.models[int(r)].factor_score_embedder.dgcnn.dgcnn.BN1.num_batches_tracked
-                               for r in keys])
-            self.nbt.index_copy_(0, idx, nbt.to(self.nbt.dtype))
+            self.emb.index_copy_(0, idx, s["emb"].index_select(0, idx))
+            self.fac.index_copy_(0, idx, s["fac"].index_select(0, idx))
+            self.bn.index_copy_(1, idx, s["bn"].index_select(1, idx))
+            self.nbt.index_copy_(0, idx, s["nbt"].index_select(0, idx))
         self.marked = []
 
 

@@ -44,8 +44,11 @@ def true_graphs(K, p, L, seed=11):
     return [(rng.rand(p, p, L) < 0.3).astype(np.float64) for _ in range(K)]
 
 
-@pytest.mark.parametrize("path", ["vector", "mfma"])
-def test_pack_fit_bitwise_equals_independent_fits(path, monkeypatch, tmp_path):
+@pytest.mark.parametrize("path,save", [("vector", True), ("mfma", True), ("vector", False), ("mfma", False)])
+def test_pack_fit_bitwise_equals_independent_fits(path, save, monkeypatch, tmp_path):
+    """save=False: no checkpoint files, so every epoch but the last trains the next one
+    speculatively while the host digests the current one, and replicas that stop are rolled
+    back (ReplicaPack._roll_back); their Adam moments and step counts are compared too."""
     from redcliff_amd import ReplicaPack
     monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     train = data(64 * 2 + 24, seed=3)
@@ -53,17 +56,19 @@ def test_pack_fit_bitwise_equals_independent_fits(path, monkeypatch, tmp_path):
     gc = true_graphs(4, 10, 4)
     kw = dict(lookback=1, check_every=1, GC=gc, deltaConEps=0.1)
     max_iter = 9
-    solo = []
+    solo, solo_opts = [], []
     for s, fc, adj, lrB, lrA, scf, scfa in GRID:
         m = make(s, fc, adj)
         oA, oB = opts(m, lrB, lrA)
+        solo_opts.append((oA, oB))
         m.fit(None, train, oA, oB, 4, 1, 1, max_iter, val, verbose=0, stopping_criteria_forecast_coeff=scf,
               stopping_criteria_factor_coeff=scfa, stopping_criteria_cosSim_coeff=1., **kw)
         torch.cuda.synchronize()
         solo.append(m)
     packed = [make(s, fc, adj) for s, fc, adj, _, _, _, _ in GRID]
-    pack = ReplicaPack(packed, [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA, _, _) in zip(packed, GRID)])
-    finals = pack.fit(str(tmp_path), train, val, max_iter, verbose=0,
+    pack_opts = [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA, _, _) in zip(packed, GRID)]
+    pack = ReplicaPack(packed, pack_opts)
+    finals = pack.fit(str(tmp_path) if save else None, train, val, max_iter, verbose=0,
                       stopping_criteria_forecast_coeff=[g[5] for g in GRID],
                       stopping_criteria_factor_coeff=[g[6] for g in GRID], stopping_criteria_cosSim_coeff=1., **kw)
     torch.cuda.synchronize()
@@ -80,10 +85,17 @@ def test_pack_fit_bitwise_equals_independent_fits(path, monkeypatch, tmp_path):
         sa, sb = a.state_dict(), b.state_dict()
         for k in sa:
             np.testing.assert_array_equal(sb[k].cpu().numpy(), sa[k].cpu().numpy(), err_msg="replica %d %s" % (r, k))
-        # the final model file holds this replica's own parameters only
-        f = os.path.join(str(tmp_path), "replica_%d" % r, "final_best_model.bin")
-        nparam = sum(t.numel() for t in b.parameters())
-        assert os.path.getsize(f) < 4 * nparam * 1.5 + 2 ** 20
+        for oa, ob in zip(solo_opts[r], pack_opts[r]):
+            stA, stB = oa.state_dict()["state"], ob.state_dict()["state"]
+            assert stA.keys() == stB.keys()
+            for i in stA:
+                for k in ("exp_avg", "exp_avg_sq", "step"):
+                    np.testing.assert_array_equal(stB[i][k].cpu().numpy(), stA[i][k].cpu().numpy(),
+                                                  err_msg="replica %d optimizer state %s %s" % (r, i, k))
+        if save:  # the final model file holds this replica's own parameters only
+            f = os.path.join(str(tmp_path), "replica_%d" % r, "final_best_model.bin")
+            nparam = sum(t.numel() for t in b.parameters())
+            assert os.path.getsize(f) < 4 * nparam * 1.5 + 2 ** 20
     assert len(finals) == len(GRID)
     print("stop epochs:", stops)
     assert any(s is not None for s in stops), "no replica stopped early: the active-list path went untested"
