@@ -394,6 +394,186 @@ def _eval_modes(model):
         f.eval()
 
 
+def _train_epoch(model, eng, train, d_train, plans, oA, oB, ep):
+    """Enqueue the training steps of epoch `ep` (one prepared launch chain per update kind)."""
+    kinds = phase_of_epoch(model, ep)
+    eng.conf.zero_()
+    if len(kinds) == 1:
+        key = kinds[0]
+        if key not in plans:
+            plans[key] = eng.plan_steps(key, train["X"], train["lab"], train["stats"], d_train, train["rows"],
+                                        train["sizes"], oA, oB)
+        plans[key].run()
+    else:  # several updates per batch: batch-major order as in batch_update
+        for bi, (r, s) in enumerate(zip(train["rows"], train["sizes"])):
+            for kind in kinds:
+                eng.run_steps([kind], train["X"], train["lab"], train["stats"][bi:bi + 1], d_train, [r], [s], oA, oB)
+
+
+class _SavedState:
+    """Everything a training epoch advances in a fused single fit (parameters, Adam moments and
+    step counts, BatchNorm statistics), copied on the device before a speculative epoch."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.t = {}
+        self.bufs = None
+
+    def _live(self):
+        e = self.eng
+        bn = e.dgcnn.BN1
+        out = [e.emb, e.fac, e.bn, bn.num_batches_tracked]
+        for g in ("A", "B"):
+            if e.opt[g] is not None:
+                out += [e.opt[g]["m"], e.opt[g]["v"]]
+        return out
+
+    def save(self):
+        live = self._live()
+        if self.bufs is None or len(self.bufs) != len(live):
+            self.bufs = [torch.empty_like(t) for t in live]
+        with torch.no_grad():
+            for d, t in zip(self.bufs, live):
+                d.copy_(t)
+        self.t = dict((g, None if self.eng.opt[g] is None else self.eng.opt[g]["t"]) for g in ("A", "B"))
+
+    def snapshot(self, model):
+        """ParamSnapshot (best_model) of the saved state."""
+        b = self.bufs
+        with torch.no_grad():
+            return ParamSnapshot(model, emb=b[0].clone(), fac=b[1].clone(),
+                                 bn=(b[2][0].clone(), b[2][1].clone(), b[3].clone()))
+
+    def restore(self):
+        e = self.eng
+        live = self._live()
+        assert len(live) == len(self.bufs), "an optimizer group was bound during the speculative epoch"
+        with torch.no_grad():
+            for d, t in zip(self.bufs, live):
+                t.copy_(d)
+        for g, t in self.t.items():
+            if t is not None:
+                e.opt[g]["t"] = t
+        e._sync_steps()
+        e.supports_fresh = False
+
+
+def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
+                   verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots):
+    """fit()'s epochs on the fused engine with the per-epoch evaluation on the device.
+
+    Per epoch the training steps are one prepared launch chain; the evaluation (train confusion
+    matrix, GC progress on the first validation batch (:1366-1414: one embedder launch, the group
+    norms, one broadcast, the metrics and tracker-statistics launches) and validation (:1416-1480,
+    batches on the replica axis)) is enqueued behind it and copied back ONCE.  While the host
+    digests epoch `it`, the GPU already trains epoch it + 1 (speculatively, state saved first):
+    the best-model snapshot of `it` comes from the saved state, and if the fit stops at `it` the
+    speculative epoch is undone (_SavedState.restore), so the fit ends exactly where the
+    reference's does.  No speculation past max_iter or across a checkpoint epoch.  The launches
+    take their BatchNorm mode from flags, so the module flags are set once (_eval_modes)."""
+    nsup, p = model.num_supervised_factors, model.num_chans
+    Lm, ls = model.Lmax, min(model.gen_lag, model.embed_lag)
+    saved = _SavedState(eng)
+    it = iter_start
+    if it < max_iter:
+        _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+    while it < max_iter:
+        if verbose:
+            print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
+        with torch.no_grad():
+            conf_d = eng.conf.clone()
+            nfirst = int(val["sizes"][0])
+            Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
+            w, _ = model._labels_from_w(eng.embed_raw(Xv))
+            G, G0 = eng.gc_norms()
+            est_t, nolag_t = conditional_gc_estimates(w, G, G0, eng.dgcnn.A.detach(), nsup, ls,
+                                                      model.primary_gc_est_mode)
+            vals_d = None
+            if GC is not None and nsup > 0 and est_t.shape[0] > 0:
+                vals_d = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff, host=False)
+            l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
+            acc_d, confv_d = eng.run_values(val["X"], val["lab"], d_train, val["rows"], val["sizes"], host=False)
+            pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
+        spec = it + 1 < max_iter and not (save_dir is not None and it % check_every == 0)
+        if spec:
+            saved.save()
+            _train_epoch(model, eng, train, d_train, plans, oA, oB, it + 1)
+        got = pending.wait()
+        cm, l1, dots, accs, confs = got[:5]
+        vals = got[5] if vals_d is not None else None
+        tr.train_confusion(cm.reshape(nsup, nsup) if nsup > 0 else None)
+        l1, nrm, dots = M.track_values_finish(l1, dots)
+        gc_progress_many([tr], None if vals is None else vals[None], l1[None], nrm[None], dots[None])
+        acc, confv = eng.values_from_rows(accs, confs)
+        hists = [[] for _ in range(5)] if nsup > 0 else [None] * 5
+        tr.validation(model._validation_tuple(acc, float(val["len"]), confv, *hists))
+        # ---- early stopping (:1482-1559)
+        if tr.step(it, (lambda: saved.snapshot(model)) if spec else (lambda: _best_model(model, True))):
+            if spec:
+                saved.restore()
+            if verbose:
+                print("Stopping early")
+            break
+        if it % check_every == 0 and save_dir is not None:
+            _eval_modes(model)
+            tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
+        it += 1
+        if not spec and it < max_iter:
+            _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+
+
+def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_val, oA, oB, output_length, iter_start,
+                 max_iter, save_dir, check_every, verbose, save_plots):
+    """fit()'s epochs when the GC-progress metrics run on the host (the generic path, or GC
+    modes / sizes outside the device metrics): the reference's loop (...withStateSmoothing.py:
+    1316-1559) with the fused training steps where available."""
+    nsup = model.num_supervised_factors
+    Lm = model.Lmax
+    for it in range(iter_start, max_iter):
+        if verbose:
+            print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
+        kinds = phase_of_epoch(model, it)
+        if not fused:  # generic path: the reference's batch loop (...withStateSmoothing.py:1331-1364)
+            cm = np.zeros((max(nsup, 1), max(nsup, 1)))
+            for bi, (Xb, Yb) in enumerate(X_train):
+                model.batch_update(it, bi, Xb, Yb, oA, oB, output_length,
+                                   running_factor_score_confusion_matrix=cm if nsup > 0 else None)
+            model._set_module_modes(kinds[-1] if kinds else None)  # the generic modules read their flags
+        else:
+            _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+            if nsup > 0:
+                cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
+        tr.train_confusion(cm if nsup > 0 else None)
+        # ---- GC progress on the first validation batch (:1366-1414)
+        _eval_modes(model)
+        with torch.no_grad():
+            if fused:
+                Xv = val["X"][:min(int(val["sizes"][0]), model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
+            else:
+                Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(),
+                                                                                          torch.float32)
+            est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
+            est_np = [[g.detach().cpu().numpy() for g in row] for row in est]
+            nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
+                             combine_wavelet_representations=True)
+            nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
+        tr.gc_progress(est_np, nolag_np, None)
+        # ---- validation (:1416-1480)
+        if fused:
+            tr.validation(model._validate_fused(X_val, nsup > 0))
+        elif nsup > 0:
+            tr.validation(model.validate_training(X_val, output_length, model.num_series, [], [], [], [], []))
+        else:
+            tr.validation(model.validate_training(X_val, output_length, model.num_series))
+        # ---- early stopping (:1482-1559)
+        if tr.step(it, lambda: _best_model(model, fused)):
+            if verbose:
+                print("Stopping early")
+            break
+        if it % check_every == 0 and save_dir is not None:
+            tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
+
+
 def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
              deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path, sc_forecast, sc_factor, sc_cos,
              save_plots):
@@ -422,101 +602,16 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
         val = eng.cache_dataset(X_val)
         d_train = eng.workspace(max(train["Bmax"], val["Bmax"]), train["T"])
         plans = {}
-    Lm = model.Lmax
-    ls = min(model.gen_lag, model.embed_lag)
 
     dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
         "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
-    for it in range(iter_start, max_iter):
-        if verbose:
-            print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
-        kinds = phase_of_epoch(model, it)
-        if not fused:  # generic path: the reference's batch loop (...withStateSmoothing.py:1331-1364)
-            cm = np.zeros((max(nsup, 1), max(nsup, 1)))
-            for bi, (Xb, Yb) in enumerate(X_train):
-                model.batch_update(it, bi, Xb, Yb, oA, oB, output_length,
-                                   running_factor_score_confusion_matrix=cm if nsup > 0 else None)
-        else:
-            eng.conf.zero_()
-            if len(kinds) == 1:
-                key = kinds[0]
-                if key not in plans:
-                    plans[key] = eng.plan_steps(key, train["X"], train["lab"], train["stats"], d_train,
-                                                train["rows"], train["sizes"], oA, oB)
-                plans[key].run()
-            else:  # several updates per batch: batch-major order as in batch_update
-                for bi, (r, s) in enumerate(zip(train["rows"], train["sizes"])):
-                    for kind in kinds:
-                        eng.run_steps([kind], train["X"], train["lab"], train["stats"][bi:bi + 1], d_train, [r], [s],
-                                      oA, oB)
-            if nsup > 0 and not dev_metrics:
-                cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
-        if not fused:  # the generic path's torch modules read their train/eval flags
-            model._set_module_modes(kinds[-1] if kinds else None)
-
-        if dev_metrics:
-            # The whole per-epoch evaluation on the device, ONE copy back: the train confusion
-            # matrix, GC progress on the first validation batch (:1366-1414: one embedder launch,
-            # the group norms, one broadcast, the metrics and tracker-statistics launches) and
-            # validation (:1416-1480, batches on the replica axis).  The launches take their
-            # BatchNorm mode from flags, so the module flags are set once (_eval_modes) instead
-            # of three tree walks per epoch.
-            with torch.no_grad():
-                conf_d = eng.conf.clone()
-                nfirst = int(val["sizes"][0])
-                Xv = val["X"][:min(nfirst, model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
-                w, _ = model._labels_from_w(eng.embed_raw(Xv))
-                G, G0 = eng.gc_norms()
-                est_t, nolag_t = conditional_gc_estimates(w, G, G0, eng.dgcnn.A.detach(), nsup, ls,
-                                                          model.primary_gc_est_mode)
-                vals_d = None
-                if GC is not None and nsup > 0 and est_t.shape[0] > 0:
-                    vals_d = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff, host=False)
-                l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
-                acc_d, confv_d = eng.run_values(val["X"], val["lab"], d_train, val["rows"], val["sizes"], host=False)
-                got = M.fetch([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
-            cm, l1, dots, accs, confs = got[:5]
-            vals = got[5] if vals_d is not None else None
-            tr.train_confusion(cm.reshape(nsup, nsup) if nsup > 0 else None)
-            l1, nrm, dots = M.track_values_finish(l1, dots)
-            gc_progress_many([tr], None if vals is None else vals[None], l1[None], nrm[None], dots[None])
-            acc, confv = eng.values_from_rows(accs, confs)
-            hists = [[] for _ in range(5)] if nsup > 0 else [None] * 5
-            tr.validation(model._validation_tuple(acc, float(val["len"]), confv, *hists))
-        else:
-            tr.train_confusion(cm if nsup > 0 else None)
-            # ---- GC progress on the first validation batch (:1366-1414)
-            _eval_modes(model)
-            with torch.no_grad():
-                if fused:
-                    Xv = val["X"][:min(int(val["sizes"][0]), model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING), :Lm, :]
-                else:
-                    Xv = X_val[0][0][:model.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING, :Lm, :].to(model._device(),
-                                                                                              torch.float32)
-                est = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=False)[:nsup]
-                est_np = [[g.detach().cpu().numpy() for g in row] for row in est]
-                nolag = model.GC(model.primary_gc_est_mode, X=Xv, threshold=False, ignore_lag=True,
-                                 combine_wavelet_representations=True)
-                nolag_np = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in nolag])
-            tr.gc_progress(est_np, nolag_np, None)
-            # ---- validation (:1416-1480)
-            if fused:
-                tr.validation(model._validate_fused(X_val, nsup > 0))
-            elif nsup > 0:
-                tr.validation(model.validate_training(X_val, output_length, model.num_series, [], [], [], [], []))
-            else:
-                tr.validation(model.validate_training(X_val, output_length, model.num_series))
-
-        # ---- early stopping (:1482-1559)
-        if tr.step(it, lambda: _best_model(model, fused)):
-            if verbose:
-                print("Stopping early")
-            break
-
-        if it % check_every == 0 and save_dir is not None:
-            if fused:
-                _eval_modes(model)
-            tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
+    if dev_metrics:
+        _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
+                       verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots)
+    else:
+        _host_epochs(model, eng, tr, fused, train if fused else None, val if fused else None,
+                     d_train if fused else None, plans if fused else None, X_train, X_val, oA, oB, output_length,
+                     iter_start, max_iter, save_dir, check_every, verbose, save_plots)
 
     if fused:
         _eval_modes(model)
