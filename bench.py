@@ -173,6 +173,45 @@ def cpu_baseline(c, seconds):
                       "(os.cpu_count() = %s on this host)" % (n, c["B"], dt, threads, os.cpu_count())}
 
 
+def cpu_fit_step_seconds(c, seconds):
+    """One combined-phase batch_update of the oracle on ONE thread (the reference's CPU grid
+    search runs one fit per core with torch.set_num_threads(1))."""
+    from oracle.redcliff_oracle import OracleREDCLIFF
+    prev = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        m = build_model(OracleREDCLIFF, c, seed=0)
+        oA, oB = adam_pair(m, c)
+        X, Y = synth(c, c["B"], seed=1)
+        m.batch_update(2, 0, X, Y, oA, oB, 1)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            m.batch_update(2, n, X, Y, oA, oB, 1)
+            n += 1
+        return (time.perf_counter() - t0) / n
+    finally:
+        torch.set_num_threads(prev)
+
+
+def hbm_roofline(c, eng, ms_per_step, ktimes_roof):
+    """HBM side of the roofline: algorithmic bytes of one step -- the windows,
+    4 (Lmax p + p + K) B each, plus 36 B per parameter (read W in forward and backward, write
+    the gradient, read and write both Adam moments, write W) -- over the step time; and the
+    dominant kernel's measured HBM bytes (PMC) over its launch time."""
+    P = int(eng.emb.numel() + eng.fac.numel())
+    Lmax = c["T"] - 1
+    step_bytes = c["B"] * 4 * (Lmax * c["p"] + c["p"] + c["K"]) + 36 * P
+    ach = step_bytes / (ms_per_step * 1e-3) / 1e9
+    out = {"bound": "hbm", "scope": "whole step", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 6), "algorithmic_bytes_per_step": step_bytes, "params": P}
+    if ktimes_roof and ktimes_roof.get("traffic"):
+        t = ktimes_roof["traffic"]
+        out["dominant_kernel"] = {"kernel": ktimes_roof["kernel"], "measured_bytes": round(t),
+                                  "achieved": round(t / (ktimes_roof["avg_launch_us"] * 1e-6) / 1e9, 2),
+                                  "frac": round(t / (ktimes_roof["avg_launch_us"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 6)}
+    return out
+
+
 def pmc_traffic(kernel_name, cfg):
     """HBM bytes per launch of ``kernel_name`` from committed rocprofv3 PMC summaries:
     FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE.  cfg "<config>"
@@ -374,11 +413,23 @@ def mode_fit(args, dev, rank, world, dist):
         return None
     if ktimes:
         out["roofline"] = roofline_of(ktimes, flops_per_window(c), B, args.config)
+    out["roofline_hbm"] = hbm_roofline(c, eng, 1e3 * elapsed / args.steps, out.get("roofline"))
     out["grid_search"] = grid
     out["fits_per_hour"] = fph
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds)
         out["gpu_over_cpu"] = round(value / world / out["cpu_baseline"]["value"], 1)
+        if fph is not None:
+            t1 = cpu_fit_step_seconds(c, args.cpu_seconds / 3.0)
+            cores = cpu_threads()
+            cpu_fit_s = fph["epochs_per_fit"] * (fph["train_windows"] // B) * t1
+            fph["cpu_baseline"] = {
+                "value": round(cores * 3600.0 / cpu_fit_s, 2), "unit": "fits/hour", "cores": cores,
+                "host_cpu_count": os.cpu_count(), "kind": "port",
+                "sample": "one-thread oracle combined-phase batch_update (%.3f s each) x %d training steps per fit, "
+                          "one fit per core; validation and GC tracking NOT counted, so this over-states the CPU "
+                          "rate" % (t1, fph["epochs_per_fit"] * (fph["train_windows"] // B))}
+            fph["gpu_over_cpu"] = round(fph["value"] / world / fph["cpu_baseline"]["value"], 1)
         if ns is not None:
             ns["cpu_baseline"] = cpu_baseline(CONFIGS["c1k4"], args.cpu_seconds * 2.0 / 3.0)
             ns["gpu_over_cpu"] = round(ns["windows_per_s"] / ns["cpu_baseline"]["value"], 1)

@@ -725,8 +725,20 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int
     kj = bx;
   } else {
     const int f = e - nemb, per = nUl * nQ - 1;
-    kj = f / per;
-    const int rem = f - kj * per + 1;
+    int rem;
+    if ((KP & 7) == 0) {
+      // XCD-aware order: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md, workgroup
+      // dispatch; a speed hint only), and lead kj is block kj.  Deal the non-lead workgroups so
+      // every workgroup of network kj lands in kj's block class: the per-network operands every
+      // one of them stages (predictions, embedder outputs, targets, group-norm partials, A
+      // column) are then fetched into one XCD's L2 instead of up to seven.
+      const int x = (KP + nemb + f) & 7, t = f >> 3;  // f's block class; each round of 8 covers all 8
+      kj = x + 8 * (t / per);
+      rem = t % per + 1;
+    } else {
+      kj = f / per;
+      rem = f - kj * per + 1;
+    }
     uc = rem / nQ;
     qc = rem - uc * nQ;
   }
