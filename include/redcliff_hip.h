@@ -230,7 +230,7 @@ int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt
                          double* out, void* stream);
 
 /* Per-epoch tracker statistics of fit() (replaces the host reductions of
- * general_utils/model_utils.py:163-186 track_l1_stats and :189-209 track_cosine_stats, which the
+ * general_utils/model_utils.py:163-188 (L1 tracker) and :191-209 (cosine tracker), which the
  * reference runs on float64 copies of every estimate):
  *   est      float32 [n_l1_rows][l1_len]     lagged estimates, one (sample, factor) per row
  *   l1_out   float64 [n_l1_rows]             sum |e / max(e)|
