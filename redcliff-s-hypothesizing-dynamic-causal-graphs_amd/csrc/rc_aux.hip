@@ -14,15 +14,24 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_norms(RedcliffDims d, const flo
   const float* W = fac + r * fs + fo.W0 + (int64_t)kj * h * Q;
   float* Gr = G + ((int64_t)r * d.K * p + kj) * Q;
   float* G0r = G0 + ((int64_t)r * d.K * p + kj) * p;
+  // G (Q outputs) and G0 (p outputs) on disjoint threads when they fit one pass, so the two
+  // sequential sums run side by side; each output keeps its ascending (u[, t]) fmaf order, the
+  // unrolled loops only issue the independent loads ahead.
+  const int g0_base = (Q + p <= RC_BLOCK) ? Q : 0;
   for (int e = threadIdx.x; e < Q; e += RC_BLOCK) {
     float s = 0.f;
+#pragma unroll 8
     for (int u = 0; u < h; ++u) s += W[(int64_t)u * Q + e] * W[(int64_t)u * Q + e];
     Gr[e] = sqrtf(s);
   }
-  for (int cc = threadIdx.x; cc < p; cc += RC_BLOCK) {
+  for (int cc = (int)threadIdx.x - g0_base; cc < p; cc += RC_BLOCK) {
+    if (cc < 0) break;
     float s = 0.f;
-    for (int u = 0; u < h; ++u)
-      for (int t = 0; t < L; ++t) s += W[(int64_t)u * Q + cc * L + t] * W[(int64_t)u * Q + cc * L + t];
+    for (int u = 0; u < h; ++u) {
+      const float* wr = W + (int64_t)u * Q + cc * L;
+#pragma unroll 4
+      for (int t = 0; t < L; ++t) s += wr[t] * wr[t];
+    }
     G0r[cc] = sqrtf(s);
   }
 }

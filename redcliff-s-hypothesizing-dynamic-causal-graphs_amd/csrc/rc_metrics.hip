@@ -18,9 +18,10 @@
 
 namespace {
 
-#define GP_NT 1024  // threads per workgroup: 16 waves keep the LDS / FP64 latencies of one (sample,
-                    // graph) hidden (one workgroup per CU: 36 p^2 bytes of LDS at p = 64)
-#define GP_NR 4     // matrix elements per thread: p * p <= GP_NR * GP_NT
+// Threads per workgroup NT: 1024 for p > 32 (16 waves keep the LDS / FP64 latencies of one
+// (sample, graph) hidden; one workgroup per CU at 36 p^2 bytes of LDS, p = 64), 256 for p <= 32
+// (a D4IC-sized graph has 100 entries: fewer idle lanes per barrier, several workgroups per CU).
+#define GP_NR 4     // matrix elements per thread: p * p <= GP_NR * NT
 
 // numpy's float32 pairwise sum of a contiguous run (loops_utils.h.src, n <= 128)
 __device__ inline float np_pairwise_f32(const float* a, int n) {
@@ -75,6 +76,7 @@ __device__ inline float np_pairwise_f32s(const float* a, int stride, int n) {
   return res;
 }
 
+template <int NT>
 __device__ inline float gp_block_max(float v, float* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -83,7 +85,7 @@ __device__ inline float gp_block_max(float v, float* red) {
   if (lane == 0) red[wv] = v;
   __syncthreads();
   float m = red[0];
-  for (int i = 1; i < GP_NT / 64; ++i) m = fmaxf(m, red[i]);
+  for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red[i]);
   __syncthreads();
   return m;
 }
@@ -91,9 +93,10 @@ __device__ inline float gp_block_max(float v, float* red) {
 // inverse of the p x p float64 matrix in the left half of Aug[p][2p] (right half := I):
 // Gauss-Jordan with partial pivoting (first maximal |pivot|, as LAPACK's idamax), result in
 // the right half.  Singular columns leave inf / nan, as numpy's inv would raise.
+template <int NT>
 __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
   const int tid = threadIdx.x, P2 = 2 * p;
-  for (int e = tid; e < p * p; e += GP_NT) {
+  for (int e = tid; e < p * p; e += NT) {
     const int i = e / p, j = e - i * p;
     Aug[i * P2 + p + j] = (i == j) ? 1.0 : 0.0;
   }
@@ -114,7 +117,7 @@ __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
     __syncthreads();
     const int piv = redi[0];
     if (piv != c)
-      for (int j = tid; j < P2; j += GP_NT) {
+      for (int j = tid; j < P2; j += NT) {
         const double t = Aug[c * P2 + j];
         Aug[c * P2 + j] = Aug[piv * P2 + j];
         Aug[piv * P2 + j] = t;
@@ -122,12 +125,12 @@ __device__ void gp_inverse(double* Aug, int p, double* redd, int* redi) {
     __syncthreads();
     const double inv = 1.0 / Aug[c * P2 + c];
     __syncthreads();
-    for (int j = tid; j < P2; j += GP_NT) Aug[c * P2 + j] *= inv;
+    for (int j = tid; j < P2; j += NT) Aug[c * P2 + j] *= inv;
     __syncthreads();
     // eliminate column c from every other row; the multipliers are read before any write
     if (tid < p) redd[tid] = Aug[tid * P2 + c];
     __syncthreads();
-    for (int e = tid; e < p * P2; e += GP_NT) {
+    for (int e = tid; e < p * P2; e += NT) {
       const int i = e / P2, j = e - i * P2;
       if (i != c) Aug[e] -= redd[i] * Aug[c * P2 + j];
     }
@@ -143,13 +146,14 @@ struct GpRoc {
 // scores are first compacted into LDS (xp, xn: any order -- the counts are integers, exact in
 // double in any summation order), then every thread walks all negatives for its positives with
 // one broadcast LDS read per pair.
+template <int NT>
 __device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* redd, float* xp, float* xn, int* cnt) {
   const int tid = threadIdx.x;
   // F1 counts (get_f1_score): masks of x > 0, x == 0, t > 0, t == 0
   double tp = 0., ppos = 0., pz = 0., tn = 0., nan = 0.;
   if (tid < 2) cnt[tid] = 0;
   __syncthreads();
-  for (int e = tid; e < pp; e += GP_NT) {
+  for (int e = tid; e < pp; e += NT) {
     const float x = xs[e];
     const double tv = t[e];
     const bool pp_ = x > 0.f, pn_ = x == 0.f, lp = tv > 0.0, ln = tv == 0.0;
@@ -174,7 +178,7 @@ __device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* red
   o.f1 = (prec + rec == 0.f) ? 0.0 : (double)((2.f * (prec * rec)) / (prec + rec));
   const int npos = cnt[0], nneg = cnt[1];
   double cnt2 = 0.;
-  for (int a = tid; a < npos; a += GP_NT) {
+  for (int a = tid; a < npos; a += NT) {
     const float xi = xp[a];
     int c2 = 0;
     for (int b = 0; b < nneg; ++b) {
@@ -191,7 +195,8 @@ __device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* red
 }
 
 // grid (S * G); dynamic LDS 36 p^2 bytes (+ small statics)
-__global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int p, int Lt, const float* est,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_gc_progress(int S, int nE, int G, int p, int Lt, const float* est,
                                                           const double* truth, const double* eps_pow, double cin,
                                                           double cout, double* out) {
   const int s = blockIdx.x / G, g = blockIdx.x - s * G;
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
   float* Ek = Ex + pp;                               // [pp] E^k
   float* En = Ek + pp;                               // [pp] E^(k+1)
   __shared__ double redd[64];
-  __shared__ float redf[GP_NT / 64];
+  __shared__ float redf[NT / 64];
   __shared__ int cnt[2];
   __shared__ int redi[4];
   __shared__ double degT[64], degE[64];
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
   float es[GP_NR];
 #pragma unroll
   for (int u = 0; u < GP_NR; ++u) {
-    const int e = tid + u * GP_NT;
+    const int e = tid + u * NT;
     es[u] = e < pp ? np_pairwise_f32(ep + (int64_t)e * Lt, Lt) : 0.f;
   }
   double* o = out + ((int64_t)s * G + g) * NM;
@@ -224,17 +229,17 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
     float mx = -INFINITY;
 #pragma unroll
     for (int u = 0; u < GP_NR; ++u) {
-      const int e = tid + u * GP_NT;
+      const int e = tid + u * NT;
       if (e < pp) {
         const int i = e / p;
         const float x = (v == 1 && e == i * p + i) ? 0.f : es[u];
         mx = fmaxf(mx, x);
       }
     }
-    mx = gp_block_max(mx, redf);
+    mx = gp_block_max<NT>(mx, redf);
 #pragma unroll
     for (int u = 0; u < GP_NR; ++u) {
-      const int e = tid + u * GP_NT;
+      const int e = tid + u * NT;
       if (e < pp) {
         const int i = e / p;
         float x = (v == 1 && e == i * p + i) ? 0.f : es[u];
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
       }
     }
     __syncthreads();
-    const GpRoc rr = gp_roc_f1(Ex, t, pp, redd, Ek, En, cnt);
+    const GpRoc rr = gp_roc_f1<NT>(Ex, t, pp, redd, Ek, En, cnt);
     if (tid == 0) {
       o[2 * v] = rr.f1;
       o[2 * v + 1] = rr.auc;
@@ -254,15 +259,15 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
   // ---- deltacon0 / with directed degrees (model_utils.py:90-160, metrics.py:136-216)
   const double* t0 = truth + (int64_t)g * pp;
   double tm_all = -INFINITY;
-  for (int e = tid; e < pp; e += GP_NT) {
+  for (int e = tid; e < pp; e += NT) {
     T[e] = t0[e];
     tm_all = fmax(tm_all, t0[e]);
   }
   float emx = -INFINITY;
 #pragma unroll
   for (int u = 0; u < GP_NR; ++u)
-    if (tid + u * GP_NT < pp) emx = fmaxf(emx, es[u]);
-  emx = gp_block_max(emx, redf);
+    if (tid + u * NT < pp) emx = fmaxf(emx, es[u]);
+  emx = gp_block_max<NT>(emx, redf);
   {
 #pragma unroll
     for (int o2 = 32; o2 > 0; o2 >>= 1) tm_all = fmax(tm_all, __shfl_xor(tm_all, o2, 64));
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
     if (lane == 0) redd[8 + wv] = tm_all;
     __syncthreads();
     double m = redd[8];
-    for (int i = 1; i < GP_NT / 64; ++i) m = fmax(m, redd[8 + i]);
+    for (int i = 1; i < NT / 64; ++i) m = fmax(m, redd[8 + i]);
     tm_all = m;
     __syncthreads();
   }
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
   const bool tnorm = tm_all != 0.0;
 #pragma unroll
   for (int u = 0; u < GP_NR; ++u) {
-    const int e = tid + u * GP_NT;
+    const int e = tid + u * NT;
     if (e < pp) Ex[e] = tnorm ? es[u] / emx : es[u];
   }
   __syncthreads();
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
     __syncthreads();
     for (int side = 0; side < 2; ++side) {
       // I + (eps^2) D - eps A
-      for (int e = tid; e < pp; e += GP_NT) {
+      for (int e = tid; e < pp; e += NT) {
         const int i = e / p, j = e - i * p;
         double mval;
         if (side == 0) {
@@ -319,11 +324,11 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
         Aug[i * 2 * p + j] = mval;
       }
       __syncthreads();
-      gp_inverse(Aug, p, redd, redi);
+      gp_inverse<NT>(Aug, p, redd, redi);
       if (side == 0) {
 #pragma unroll
         for (int u = 0; u < GP_NR; ++u) {
-          const int e = tid + u * GP_NT;
+          const int e = tid + u * NT;
           if (e < pp) {
             const int i = e / p, j = e - i * p;
             sreg[u] = Aug[i * 2 * p + p + j];
@@ -334,7 +339,7 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
         double acc = 0.;
 #pragma unroll
         for (int u = 0; u < GP_NR; ++u) {
-          const int e = tid + u * GP_NT;
+          const int e = tid + u * NT;
           if (e < pp) {
             const int i = e / p, j = e - i * p;
             const double df = sqrt(sreg[u]) - sqrt(Aug[i * 2 * p + p + j]);
@@ -353,16 +358,16 @@ __global__ __launch_bounds__(GP_NT) void k_gc_progress(int S, int nE, int G, int
   __syncthreads();
 
   // ---- deltaffinity and path-length MSE over k = 1..p-1 (metrics.py:142-252)
-  // Thread layout of this section: column j = tid % p, rows r0, r0 + rpp, ... (rpp = GP_NT / p
+  // Thread layout of this section: column j = tid % p, rows r0, r0 + rpp, ... (rpp = NT / p
   // rows per pass, at most GP_NR passes), so a thread's outputs of A^k = A^(k-1) A share the
   // column operand A[m][j] and run GP_NR independent fma chains (each output still sums over m
   // in ascending order, as before).  Tk/Tn and Ek/En alternate instead of being copied back.
-  const int rpp = GP_NT / p, jc = tid % p, r0 = tid / p;
+  const int rpp = NT / p, jc = tid % p, r0 = tid / p;
   const bool act = r0 < rpp;
   double* Tk = Aug;
   double* Tn = Aug + pp;
   double sa1[GP_NR], sa2[GP_NR];
-  for (int e = tid; e < pp; e += GP_NT) {
+  for (int e = tid; e < pp; e += NT) {
     Tk[e] = T[e];
     Ek[e] = Ex[e];
   }
@@ -520,14 +525,19 @@ extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p,
   }
   if (S * G == 0) return 0;
   const size_t lds = (size_t)36 * p * p;
-  if (lds > 64 * 1024) {
-    const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k_gc_progress),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
-                           "k_gc_progress LDS");
-    if (e) return e;
+  if (p <= 32) {
+    hipLaunchKernelGGL(k_gc_progress<256>, dim3(S * G), dim3(256), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
+                       truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
+  } else {
+    if (lds > 64 * 1024) {
+      const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k_gc_progress<1024>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                             "k_gc_progress LDS");
+      if (e) return e;
+    }
+    hipLaunchKernelGGL(k_gc_progress<1024>, dim3(S * G), dim3(1024), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
+                       truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
   }
-  hipLaunchKernelGGL(k_gc_progress, dim3(S * G), dim3(GP_NT), lds, (hipStream_t)stream, S, nE, G, p, Lt, est, truth,
-                     eps_pow, in_degree_coeff, out_degree_coeff, out);
   return rc_check(hipGetLastError(), "k_gc_progress");
 }
 
