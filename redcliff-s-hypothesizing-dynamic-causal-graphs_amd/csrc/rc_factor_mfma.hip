@@ -20,6 +20,16 @@
 #include <cstring>
 
 #include "rc_common.h"
+// k_fac_bwd_mfma occupancy (measured on the R = 32 D4IC grid and C5): without the epilogue-operand
+// prefetch the kernel fits 3 waves per SIMD without spills, which hides more latency than the
+// prefetch did at 2 waves (grid step 0.54 -> 0.51 ms, fac_bwd 140 -> 114 us; C5 0.52 -> 0.50 ms);
+// 4 waves spill.  Same arithmetic either way.
+#ifndef RC_FB_WAVES
+#define RC_FB_WAVES 3
+#endif
+#ifndef RC_FB_PREFETCH
+#define RC_FB_PREFETCH 0
+#endif
 
 namespace {
 
@@ -379,7 +389,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
 // the contraction: chunks of 32 windows, dZ built on the fly from the forward's activations,
 // dL/dy and the W1 snapshot.
 template <int NBW>
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
+__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_WAVES, 8))) void k_fac_bwd_mfma(StepCtx c) {
   constexpr int QT = 256 / NBW, Q4 = QT / 4;
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.z);
@@ -442,8 +452,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
     }
   };
 
-  // The epilogue's operands (W0, Adam moments, adjacency-L1 terms) are loaded before the
-  // contraction, so their latency overlaps the matrix-core work.
+  // The epilogue's operands (W0, Adam moments, adjacency-L1 terms): RC_FB_PREFETCH=1 loads half
+  // 0's before the contraction (latency overlap at 2 waves per SIMD); the default loads them
+  // after it, which frees the registers for a third wave (see RC_FB_WAVES).
   const int net = NBW == 2 ? (wv & 1) : wv, qh = NBW == 2 ? 64 * (wv >> 1) : 0, kh = lane >> 5, l31 = lane & 31;
   const int cbw = cb0 + net, kin = cbw < NB;
   const int kj = kin ? cbw / nUB : 0, ub0 = kin ? (cbw - kj * nUB) * 32 : 0;
@@ -492,7 +503,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
       }
     }
   };
+#if RC_FB_PREFETCH
   epi_load(0);
+#endif
 
   f32x16 acc0, acc1;
 #pragma unroll
@@ -513,6 +526,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_mfma(StepCtx c) {
     }
   }
   // ---- epilogue: + adjacency term through the group norms, then Adam (or store the gradient)
+#if !RC_FB_PREFETCH
+  epi_load(0);
+#endif
   epi_store(0, acc0);
   epi_load(1);
   epi_store(1, acc1);
