@@ -28,7 +28,10 @@ def dump(path):
         oA, oB = bench.adam_pair(m, c)
         X, Y = bench.synth(c, 2 * c["B"] + 40, seed=3)
         bs = [(X[i:i + c["B"]], Y[i:i + c["B"]]) for i in range(0, X.shape[0], c["B"])]
-        for epoch in (0, 1, 2, 3):
+        epochs = [int(e) for e in os.environ.get("COMPARE_EPOCHS", "0,1,2,3").split(",")]
+        if os.environ.get("COMPARE_ONE_BATCH"):
+            bs = bs[:1]
+        for epoch in epochs:
             for bi, (Xb, Yb) in enumerate(bs):
                 m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
         torch.cuda.synchronize()
