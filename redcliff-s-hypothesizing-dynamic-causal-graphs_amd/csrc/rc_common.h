@@ -466,12 +466,15 @@ __device__ inline RcAdamScalars rc_adam_scalars(const RedcliffAdamHyper& h, int 
 // torch.optim.Adam (_single_tensor_adam, coupled L2 weight decay) for one element:
 //   g += wd*p; m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
 //   p.addcdiv_(m, sqrt(v)/sqrt(bc2) + eps, -lr/bc1)
+// Every multiply-add is an explicit fmaf: left to -ffp-contract=fast, the compiler fuses (or,
+// when it packs two updates into v_pk_mul / v_pk_add, does not fuse) per call site, and the same
+// parameter stepped by two different kernels would then differ in the last ulp.
 __device__ inline void rc_adam(float& p, float& m, float& v, float g, const RcAdamScalars& s) {
-  if (s.wd != 0.f) g = g + p * s.wd;
-  m = m + s.omb1 * (g - m);
-  v = v * s.b2 + (s.omb2 * g) * g;
+  if (s.wd != 0.f) g = __builtin_fmaf(p, s.wd, g);
+  m = __builtin_fmaf(s.omb1, g - m, m);
+  v = __builtin_fmaf(s.omb2 * g, g, v * s.b2);
   const float denom = sqrtf(v) / s.bc2s + s.eps;
-  p = p + s.neg_step * (m / denom);
+  p = __builtin_fmaf(s.neg_step, m / denom, p);
 }
 
 // Apply Adam to element idx of a group, or (data-parallel shard, RC_GRAD_ONLY) store its

@@ -30,6 +30,9 @@
 #ifndef RC_FB_PREFETCH
 #define RC_FB_PREFETCH 0
 #endif
+#ifndef RC_FB_WAVES4  // the short-contraction variant also holds the recompute operands
+#define RC_FB_WAVES4 2
+#endif
 
 namespace {
 
@@ -68,6 +71,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_xwin(StepCtx c) {
 // (+ b1 in block 0) -> ws.y slot ub, squared group norms gq[ub][kj][q] = sum_{u in ub} W0[u][q]^2
 // (first row block), W1 snapshot.
 __device__ inline int mf_nub(const RedcliffDims& d) { return (d.h + 31) / 32; }
+// Short contractions (p*L <= 64, the k_fac_bwd_mfma<4> launch): the backward recomputes the
+// hidden activations and forms the output-layer gradients, so neither the forward's activation
+// store nor the mixing kernel's activation reads happen.
+__host__ __device__ inline bool mf_recompute(const RedcliffDims& d) { return d.p * d.L <= 64; }
 
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
   const RedcliffDims& d = c.d;
@@ -160,7 +167,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
   for (int reg = 0; reg < 16; ++reg) {
     const int b = b0 + 32 * (wv & 1) + mf_row(reg, lane);
     const float a = uv ? fmaxf(acc[reg] + bu, 0.f) : 0.f;
+#ifdef RC_RECOMP_DEBUG
     if (uv && b < c.B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+#else
+    if (uv && b < c.B && !mf_recompute(d)) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+#endif
     float ys = w1 * a;
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);  // within the 32-lane half
@@ -351,7 +362,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   float db1 = 0.f;
   for (int b = tid; b < B; b += RC_BLOCK) db1 += dyl[b];
   db1 = rc_block_sum(db1, red);
-  for (int u0 = 0; u0 < h; u0 += 32) {
+  for (int u0 = 0; u0 < (mf_recompute(d) ? 0 : h); u0 += 32) {  // else: in k_fac_bwd_mfma<4>
     const int uu = tid & 31, part = tid >> 5, u = u0 + uu;
     float dW1u = 0.f, db0u = 0.f;
     if (u < h) {
@@ -386,11 +397,20 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
 // NBW = 2 (long contractions, QT = 128): wave w owns block 2*bx + (w&1) and columns
 // [q0 + 64*(w>>1), +64); NBW = 4 (p*L <= 64, QT = 64): wave w owns block 4*bx + w and all 64
 // columns -- two 32x32 accumulators either way (rows = the block's hidden units).  The batch is
-// the contraction: chunks of 32 windows, dZ built on the fly from the forward's activations,
-// dL/dy and the W1 snapshot.
+// the contraction: chunks of 32 windows, dZ built on the fly from dL/dy and the W1 snapshot.
+//
+// NBW = 4 (mf_recompute): the hidden activations are RECOMPUTED per chunk instead of read back
+// from the forward -- the same v_mfma_f32_32x32x2f32 sequence as k_fac_fwd_mfma (windows as rows,
+// the block's units as columns, q ascending in steps of 2 over rc_qpad(d), bias, ReLU), so the
+// same bits (checked element by element against the stored activations with -DRC_RECOMP_DEBUG)
+// -- and this workgroup also forms the output-layer / hidden-bias gradients dW1, db0
+// (k_fac_mix's order: per unit, 8 partial sums over windows b = part (mod 8) in ascending order,
+// combined in part order) and their Adam step.  The forward then stores no activations and the
+// mixing kernel reads none (R = 32 D4IC grid: 3 x 65 MB per step less traffic).
 template <int NBW>
-__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_WAVES, 8))) void k_fac_bwd_mfma(StepCtx c) {
+__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW == 4 ? RC_FB_WAVES4 : RC_FB_WAVES, 8))) void k_fac_bwd_mfma(StepCtx c) {
   constexpr int QT = 256 / NBW, Q4 = QT / 4;
+  constexpr bool RECOMP = NBW == 4;
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.z);
   const int cb0 = blockIdx.x * NBW, q0 = blockIdx.y * QT;
@@ -408,26 +428,35 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_
   __shared__ float Zs[NBW][MB_BC][33];  // dZ[blk][b][u]
   __shared__ float Xs[MB_BC][QT + 4];    // Xw[b][q0 + .]
   __shared__ float w1s[NBW * 32];
+  __shared__ float Dys[RECOMP ? NBW : 1][MB_BC];  // dL/dy of the chunk's windows (recompute path)
 
   if (tid < NBW * 32) {
     const int cb = cb0 + (tid >> 5), kj = cb / nUB, u = (cb - kj * nUB) * 32 + (tid & 31);
     w1s[tid] = (cb < NB && u < h) ? ws[c.wo.w1 + (int64_t)kj * h + u] : 0.f;
   }
-  // staging maps: dZ NBW x 32 x 32 (4 NBW per thread: blk, b, u); X 32 x QT (QT / 32 float4 per thread)
-  float zr[4 * NBW];
+  // staging maps: dZ NBW x 32 x 32 (4 NBW per thread: blk, b, u) or, recomputing, dL/dy NBW x 32;
+  // X 32 x QT (QT / 32 float4 per thread)
+  float zr[RECOMP ? 1 : 4 * NBW];
   float4 xr[QT / 32];
   auto load = [&](int bb0) {
-#pragma unroll
-    for (int i = 0; i < 4 * NBW; ++i) {
-      const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31;
-      const int cb = cb0 + net, kj = cb / nUB, u = (cb - kj * nUB) * 32 + (e & 31), b = bb0 + bb;
-      float v = 0.f;
-      if (cb < NB && u < h && b < B) {
-        const float av = ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u];
-        const float dy = ws[c.wo.dyl + (int64_t)kj * d.Bmax + b];
-        v = av > 0.f ? dy : 0.f;
+    if constexpr (RECOMP) {
+      if (tid < NBW * MB_BC) {
+        const int cb = cb0 + (tid >> 5), kj = cb / nUB, b = bb0 + (tid & 31);
+        zr[0] = (cb < NB && b < B) ? ws[c.wo.dyl + (int64_t)kj * d.Bmax + b] : 0.f;
       }
-      zr[i] = v;  // times w1[u] at store time
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4 * NBW; ++i) {
+        const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31;
+        const int cb = cb0 + net, kj = cb / nUB, u = (cb - kj * nUB) * 32 + (e & 31), b = bb0 + bb;
+        float v = 0.f;
+        if (cb < NB && u < h && b < B) {
+          const float av = ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u];
+          const float dy = ws[c.wo.dyl + (int64_t)kj * d.Bmax + b];
+          v = av > 0.f ? dy : 0.f;
+        }
+        zr[i] = v;  // times w1[u] at store time
+      }
     }
 #pragma unroll
     for (int i = 0; i < QT / 32; ++i) {
@@ -437,10 +466,14 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_
     }
   };
   auto store = [&]() {
+    if constexpr (RECOMP) {
+      if (tid < NBW * MB_BC) Dys[tid >> 5][tid & 31] = zr[0];
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4 * NBW; ++i) {
-      const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31, u = e & 31;
-      Zs[net][bb][u] = zr[i] * w1s[net * 32 + u];
+      for (int i = 0; i < 4 * NBW; ++i) {
+        const int e = tid + i * RC_BLOCK, net = e >> 10, bb = (e >> 5) & 31, u = e & 31;
+        Zs[net][bb][u] = zr[i] * w1s[net * 32 + u];
+      }
     }
 #pragma unroll
     for (int i = 0; i < QT / 32; ++i) {
@@ -507,6 +540,21 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_
   epi_load(0);
 #endif
 
+  // recompute path: the lane's layer-0 operand column W0[ub0 + l31][2 kk + kh] (the forward's B
+  // operand), its bias, and the partial output-layer gradients of windows b = part (mod 8),
+  // part = (reg & 3) + 4 kh (the rows mf_row puts in this lane)
+  const int uR = ub0 + l31;
+  const bool uvR = RECOMP && kin && uR < h;
+  float wB[RECOMP ? 32 : 1], buR = 0.f, w1R = 0.f, pa[4] = {0.f, 0.f, 0.f, 0.f}, pb[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RECOMP) {
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+      const int q = 2 * kk + kh;
+      wB[kk] = (uvR && q < Q) ? W0[(int64_t)uR * Q + q] : 0.f;
+    }
+    buR = uvR ? P[c.fo.b0 + (int64_t)kj * h + uR] : 0.f;
+  }
+
   f32x16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
@@ -516,6 +564,44 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_
     store();
     __syncthreads();
     if (bb0 + MB_BC < B) load(bb0 + MB_BC);
+    if constexpr (RECOMP) {
+      // Z[b][u] of this chunk, exactly as k_fac_fwd_mfma forms it
+      f32x16 zc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) zc[i] = 0.f;
+      const int nk = Qp >> 1;
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) {
+        if (kk < nk) zc = __builtin_amdgcn_mfma_f32_32x32x2f32(Xs[l31][2 * kk + kh], wB[kk], zc, 0, 0, 0);
+      }
+      w1R = w1s[net * 32 + l31];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int reg = 4 * g4 + m, bl = mf_row(reg, lane), b = bb0 + bl;
+          const float a = uvR ? fmaxf(zc[reg] + buR, 0.f) : 0.f;
+#ifdef RC_RECOMP_DEBUG
+          if (uvR && b < B) {
+            const float st = ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + uR];
+            if (st != a)
+              printf("RECOMP kj=%d b=%d u=%d stored=%.9g recomputed=%.9g z=%.9g bias=%.9g\n", kj, b, uR, st, a,
+                     zc[reg], buR);
+          }
+#endif
+          const float dy = Dys[net][bl];
+          Zs[net][bl][l31] = (a > 0.f ? dy : 0.f) * w1R;
+          if (uvR && b < B) {
+            // k_fac_mix's operations exactly: a rounded product added to each running sum (that
+            // loop compiles to v_mul + v_pk_add, no fma), db0's product only where a > 0
+#pragma clang fp contract(off)
+            pa[m] = pa[m] + dy * a;
+            pb[m] = pb[m] + (a > 0.f ? dy * w1R : 0.f);
+          }
+        }
+      }
+      __syncthreads();
+    }
 #pragma unroll
     for (int k0 = 0; k0 < MB_BC; k0 += 2) {
       const float a = Zs[net][k0 + kh][l31];  // A[i = u][k = b]
@@ -523,6 +609,30 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_FB_
       const float x1 = Xs[k0 + kh][qh + 32 + l31];
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, x0, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, x1, acc1, 0, 0, 0);
+    }
+  }
+  if constexpr (RECOMP) {
+    // dW1[u], db0[u]: parts 0..3 live in lane l31, parts 4..7 in lane l31 + 32; summed in part order
+    float hi_a[4], hi_b[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      hi_a[m] = __shfl(pa[m], l31 + 32, 64);
+      hi_b[m] = __shfl(pb[m], l31 + 32, 64);
+    }
+    if (kh == 0 && uvR) {
+      float g1 = 0.f, g0 = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        g1 += pa[m];
+        g0 += pb[m];
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        g1 += hi_a[m];
+        g0 += hi_b[m];
+      }
+      rc_update(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + uR, g0, as);
+      rc_update(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + uR, g1, as);
     }
   }
   // ---- epilogue: + adjacency term through the group norms, then Adam (or store the gradient)

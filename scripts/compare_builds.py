@@ -31,6 +31,8 @@ def dump(path):
         epochs = [int(e) for e in os.environ.get("COMPARE_EPOCHS", "0,1,2,3").split(",")]
         if os.environ.get("COMPARE_ONE_BATCH"):
             bs = bs[:1]
+        if os.environ.get("COMPARE_BATCHES"):
+            bs = bs[:int(os.environ["COMPARE_BATCHES"])]
         for epoch in epochs:
             for bi, (Xb, Yb) in enumerate(bs):
                 m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
@@ -38,6 +40,11 @@ def dump(path):
         for k, v in m.state_dict().items():
             if not k.startswith("gen_model."):
                 out["%s/%s" % (cfg, k)] = v.detach().cpu().numpy()
+        for g, o in (("A", oA), ("B", oB)):
+            for i, st in o.state_dict()["state"].items():
+                for kk in ("exp_avg", "exp_avg_sq"):
+                    if kk in st:
+                        out["%s/opt%s/%d/%s" % (cfg, g, i, kk)] = st[kk].detach().cpu().numpy()
     np.savez(path, **out)
     print("dumped %d tensors to %s" % (len(out), path))
 
