@@ -224,6 +224,9 @@ class FitTracker:
         if it >= m.num_pretrain_epochs + m.num_acclimation_epochs:
             with np.errstate(all="ignore"):
                 cos_mean = np.mean([self.cos_hist[key][-1] for key in self.cos_hist.keys()]) if self.cos_hist else np.nan
+            if "Freeze" in m.training_mode:  # :1486-1491; raises as the reference's does
+                m.determine_which_factors_need_updates(self.best_model, [True] * self.K)
+                raise AssertionError("unreachable: the reference's Freeze decision cannot complete")
             if self.nsup > 0:
                 crit = self.sc_factor * self._vfac + self.sc_forecast * self._vf + (
                     self.sc_cos * cos_mean if self.nsup > 1 else 0.)
@@ -459,7 +462,7 @@ class _SavedState:
 
 
 def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
-                   verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots):
+                   verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook):
     """fit()'s epochs on the fused engine with the per-epoch evaluation on the device.
 
     Per epoch the training steps are one prepared launch chain; the evaluation (train confusion
@@ -474,8 +477,10 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
     nsup, p = model.num_supervised_factors, model.num_chans
     Lm, ls = model.Lmax, min(model.gen_lag, model.embed_lag)
     saved = _SavedState(eng)
+    freeze = "Freeze" in model.training_mode  # the Freeze decision raises: no epoch runs ahead of it
     it = iter_start
     if it < max_iter:
+        hook(it)
         _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
     while it < max_iter:
         if verbose:
@@ -494,7 +499,8 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
             l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
             acc_d, confv_d = eng.run_values(val["X"], val["lab"], d_train, val["rows"], val["sizes"], host=False)
             pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
-        spec = it + 1 < max_iter and not (save_dir is not None and it % check_every == 0)
+        spec = (it + 1 < max_iter and not (save_dir is not None and it % check_every == 0) and not freeze
+                and hook.at != it + 1)
         if spec:
             saved.save()
             _train_epoch(model, eng, train, d_train, plans, oA, oB, it + 1)
@@ -519,11 +525,12 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
             tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
         it += 1
         if not spec and it < max_iter:
+            hook(it)
             _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
 
 
 def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_val, oA, oB, output_length, iter_start,
-                 max_iter, save_dir, check_every, verbose, save_plots):
+                 max_iter, save_dir, check_every, verbose, save_plots, hook):
     """fit()'s epochs when the GC-progress metrics run on the host (the generic path, or GC
     modes / sizes outside the device metrics): the reference's loop (...withStateSmoothing.py:
     1316-1559) with the fused training steps where available."""
@@ -532,6 +539,7 @@ def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_v
     for it in range(iter_start, max_iter):
         if verbose:
             print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
+        hook(it)
         kinds = phase_of_epoch(model, it)
         if not fused:  # generic path: the reference's batch loop (...withStateSmoothing.py:1331-1364)
             cm = np.zeros((max(nsup, 1), max(nsup, 1)))
@@ -574,12 +582,36 @@ def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_v
             tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
 
 
+def _prior_hook(model, X_train, prior):
+    """it -> None: the factor re-ordering fit() runs at the start of epoch num_pretrain_epochs
+    of the "pretrain_factor" modes (...withStateSmoothing.py:1318-1326)."""
+    path, cost, start, nb = prior
+    at = model.num_pretrain_epochs if "pretrain_factor" in model.training_mode else None
+
+    def hook(it):
+        if it == at:
+            model.initialize_factors_with_prior(prior_factors_path=path, X_train=X_train, cost_criteria=cost,
+                                                unsupervised_start_index=start, max_batches=nb)
+    hook.at = at
+    return hook
+
+
+def _freeze_by_batch(model, fused, X_train, oA, oB, output_length, it):
+    """The first batch_update of a FreezeByBatch fit (:1331-1342): best_model is the copy fit()
+    makes before its loop (:1230), every factor is in training; batch_update's Freeze decision
+    raises as the reference's does (determine_which_factors_need_updates)."""
+    nsup = model.num_supervised_factors
+    cm = np.zeros((nsup, nsup)) if nsup > 0 else None
+    for bi, (Xb, Yb) in enumerate(X_train):
+        model.batch_update(it, bi, Xb, Yb, oA, oB, output_length, best_model=_best_model(model, fused),
+                           training_status_of_each_factor=[True] * model.num_factors_nK,
+                           running_factor_score_confusion_matrix=cm)
+
+
 def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
-             deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path, sc_forecast, sc_factor, sc_cos,
+             deltaConEps, in_degree_coeff, out_degree_coeff, prior, sc_forecast, sc_factor, sc_cos,
              save_plots):
-    if "Freeze" in model.training_mode:
-        raise NotImplementedError("Freeze* training modes are not on the fused path")
-    if prior_factors_path is not None:
+    if prior[0] is not None:
         raise NotImplementedError("prior-initialised factors (prior_factors_path) are not on the fused path")
     if output_length != 1:
         raise NotImplementedError("output_length must be 1")
@@ -589,6 +621,12 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
     tr = FitTracker(model, GC, deltaConEps, in_degree_coeff, out_degree_coeff, sc_forecast, sc_factor, sc_cos,
                     lookback, check_every)
     iter_start = tr.resume(fused)
+    if "Freeze" in model.training_mode:
+        if tr.best_model is None:  # fit()'s try block deep-copies the model before the loop (:1230)
+            tr.best_model = _best_model(model, fused)
+        if "FreezeByBatch" in model.training_mode and iter_start < max_iter:
+            _freeze_by_batch(model, fused, X_train, oA, oB, output_length, iter_start)
+    hook = _prior_hook(model, X_train, prior)
     ost = getattr(model, "chkpt_optimizer_state", None)
     if ost is not None:  # this package's optimizer_state.pt next to the resumed checkpoint
         oA.load_state_dict(ost["A"])
@@ -607,11 +645,11 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
         "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
     if dev_metrics:
         _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
-                       verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots)
+                       verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook)
     else:
         _host_epochs(model, eng, tr, fused, train if fused else None, val if fused else None,
                      d_train if fused else None, plans if fused else None, X_train, X_val, oA, oB, output_length,
-                     iter_start, max_iter, save_dir, check_every, verbose, save_plots)
+                     iter_start, max_iter, save_dir, check_every, verbose, save_plots, hook)
 
     if fused:
         _eval_modes(model)

@@ -375,6 +375,114 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             terms.append(smooth * getattr(self, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF", 0.0))
         return combo, terms + [adj, None]
 
+    # ------------------------------------------------------------------ factor prior / re-ordering
+    def initialize_factors_with_prior(self, prior_factors_path=None, X_train=None, cost_criteria="CosineSimilarity",
+                                      unsupervised_start_index=0, max_batches=10):
+        """...withStateSmoothing.py:149-206.  fit() calls it at the end of factor pretraining
+        ("pretrain_factor" modes, :1318-1326) with X_train: the factors are re-ordered so that
+        factor i is the one whose (eval-mode) embedder weighting matches label column i best
+        (misc.py:83-91, linear sum assignment on the cosine cost), the unmatched ones after.
+
+        The reference re-orders the module objects, so each factor's Adam state moves with it;
+        here the factor slots of the packed parameter buffer and of optimizerB's moments are
+        permuted, which is the same state.  ``prior_factors_path`` (replace the factors by those
+        of a saved model -- the reference's assignment leaves optimizerB holding the replaced
+        parameters, i.e. the loaded factors are never stepped) is not on this path."""
+        if prior_factors_path is not None:
+            raise NotImplementedError("prior-initialised factors (prior_factors_path) are not on the fused path")
+        if X_train is None:
+            return
+        if unsupervised_start_index != 0:
+            # the reference keeps only factors[start:] (:200-205), which changes num_factors
+            raise NotImplementedError("unsupervised_start_index != 0 drops factors in the reference")
+        Lm = self.Lmax
+        preds, labels = [], []
+        with torch.no_grad():
+            for batch_num, (X, Y) in enumerate(X_train):
+                if batch_num >= max_batches:
+                    break
+                if Y is not None and Y.dim() > 2:
+                    Y = Y[:, :, Lm] if Y.size(2) > Lm else Y[:, :, 0]
+                self.factor_score_embedder.eval()
+                for f in self.factors:
+                    f.eval()
+                _, _, fw, _ = self.forward(X[:, :Lm, :].to(self._device(), torch.float32))
+                preds.append(fw[0].detach().cpu().numpy())
+                labels.append(Y.detach().cpu().numpy())
+        preds, labels = np.vstack(preds), np.vstack(labels)
+        assert preds.ndim == 2 and labels.ndim == 2
+        from .evaluation import sort_unsupervised_estimates
+        _, est_inds, gt_inds = sort_unsupervised_estimates(
+            [preds[:, i] for i in range(preds.shape[1])], [labels[:, i] for i in range(labels.shape[1])],
+            cost_criteria=cost_criteria, unsupervised_start_index=0, return_sorting_inds=True)
+        order = [None] * len(est_inds)
+        for e, g in zip(est_inds, gt_inds):
+            order[g] = int(e)
+        if any(o is None for o in order):
+            raise ValueError("factor matching left a label column without a factor")
+        order += [i for i in range(self.num_factors_nK) if i not in est_inds]
+        self._permute_factors(order)
+
+    def _permute_factors(self, order):
+        """Factor slot i takes the parameters (and optimizerB state) of factor order[i]."""
+        if list(order) == list(range(self.num_factors_nK)):
+            return
+        if not self.fused_supported():  # the reference's own move: a re-ordered ModuleList (:205)
+            self.factors = nn.ModuleList([self.factors[i] for i in order])
+            return
+        eng = self.engine()
+        eng.ensure_bound()
+        base = eng.fac
+        slots = [[((prm.data_ptr() - base.data_ptr()) // 4, prm.numel()) for prm in f.parameters()]
+                 for f in self.factors]
+        bufs = [eng.fac] + ([eng.opt["B"]["m"], eng.opt["B"]["v"]] if eng.opt["B"] is not None else [])
+        with torch.no_grad():
+            for buf in bufs:
+                old = buf.clone()
+                for i, src in enumerate(order):
+                    for (od, n), (os_, n2) in zip(slots[i], slots[src]):
+                        assert n == n2
+                        buf[od:od + n].copy_(old[os_:os_ + n])
+        eng.invalidate()
+
+    def determine_which_factors_need_updates(self, cached_model, training_status_of_each_factor):
+        """...withStateSmoothing.py:1132-1172, the Freeze* training modes' per-factor accept /
+        revert decision.  Restated as the reference computes it, including its failure: the
+        fixed_factor_exclusive lag-free estimates are (p, p, 1) arrays (:444-455), and
+        np.linalg.norm(x, ord=1) of a 3-d array raises ValueError ("Improper number of dimensions
+        to norm."), so every Freeze* fit of the reference stops with that error at its first
+        decision; this method raises the same error at the same point."""
+        from .fit_loop import _as_module
+        cached_model = _as_module(cached_model)
+        with torch.no_grad():
+            cached = [x.detach().cpu().numpy() for x in cached_model.GC(
+                "fixed_factor_exclusive", X=None, threshold=False, ignore_lag=True)[0]]
+            cur = [x.detach().cpu().numpy() for x in self.GC(
+                "fixed_factor_exclusive", X=None, threshold=False, ignore_lag=True)[0]]
+        K = self.num_factors_nK
+        need = [False] * K
+        for f in range(K):
+            if not training_status_of_each_factor[f]:
+                continue
+            c_est = cached[f] / np.max(cached[f])
+            n_est = cur[f] / np.max(cur[f])
+            if "withComboCosSimL1" in self.training_mode:
+                cs_c, cs_n = 0., 0.
+                for o in range(K):
+                    if o != f:
+                        cs_c += M.compute_cosine_similarity(c_est, cached[o] / np.max(cached[o]))
+                        cs_n += M.compute_cosine_similarity(n_est, cur[o] / np.max(cur[o]))
+                cs_c /= (K - 1.)
+                cs_n /= (K - 1.)
+                if cs_n * np.linalg.norm(n_est, ord=1) < cs_c * np.linalg.norm(c_est, ord=1):
+                    need[f] = True
+            elif "withL1" in self.training_mode:
+                if np.linalg.norm(n_est, ord=1) < np.linalg.norm(c_est, ord=1):
+                    need[f] = True
+            else:
+                raise NotImplementedError()
+        return need
+
     def resume_training_from_checkpoint(self, training_meta_data_path):
         """...withStateSmoothing.py:209-251: histories of a previous run; fit() resumes at best_it+1.
         The reference does not checkpoint the optimizers (redcliff_s_cmlp.py:245) and restarts
@@ -395,8 +503,18 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
     def batch_update(self, epoch_num, batch_num, X, Y, optimizerA, optimizerB, output_length, best_model=None,
                      training_status_of_each_factor=None, running_factor_score_confusion_matrix=None):
         """One REDCLIFF-S update on a host or device batch (...withStateSmoothing.py:734-933)."""
-        if "FreezeByBatch" in self.training_mode:
-            raise NotImplementedError("FreezeByBatch training modes are not on the fused path")
+        best_model, running_factor_score_confusion_matrix = self._batch_update(
+            epoch_num, X, Y, optimizerA, optimizerB, output_length, best_model, running_factor_score_confusion_matrix)
+        if "FreezeByBatch" in self.training_mode:  # :910-929
+            assert best_model is not None
+            assert training_status_of_each_factor is not None
+            self.determine_which_factors_need_updates(best_model, training_status_of_each_factor)
+            # determine_which_factors_need_updates raises on the reference's (p, p, 1) estimates
+            raise AssertionError("unreachable: the reference's Freeze decision cannot complete")
+        return best_model, running_factor_score_confusion_matrix
+
+    def _batch_update(self, epoch_num, X, Y, optimizerA, optimizerB, output_length, best_model,
+                      running_factor_score_confusion_matrix):
         if output_length != 1:
             raise NotImplementedError("output_length must be 1 (num_sims * output_length target steps)")
         kinds = phase_of_epoch(self, epoch_num)
@@ -488,7 +606,8 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         """Epoch loop of ...withStateSmoothing.py:1175-1647 with the batches resident on the GPU."""
         from .fit_loop import run_fit
         return run_fit(self, save_dir, X_train, optimizerA, optimizerB, output_length, max_iter, X_val, lookback,
-                       check_every, verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, prior_factors_path,
+                       check_every, verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff,
+                       (prior_factors_path, cost_criteria, unsupervised_start_index, max_factor_prior_batches),
                        stopping_criteria_forecast_coeff, stopping_criteria_factor_coeff,
                        stopping_criteria_cosSim_coeff, save_plots)
 

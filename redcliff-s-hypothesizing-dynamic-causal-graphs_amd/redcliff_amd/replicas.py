@@ -401,7 +401,14 @@ class ReplicaPack:
         # rolled back to it (parameters, Adam moments and step counts, BatchNorm statistics), so
         # every replica ends exactly where its own fit() would.  No speculation across a
         # checkpoint epoch (the files hold epoch `it`'s state) or past max_iter.
+        # "pretrain_factor" modes re-order each fit's factors before epoch num_pretrain_epochs
+        # (...withStateSmoothing.py:1318-1326, initialize_factors_with_prior with fit()'s defaults)
+        reorder_at = m0.num_pretrain_epochs if "pretrain_factor" in m0.training_mode else None
+
         def launch_train(ep):
+            if ep == reorder_at:
+                for r in active:
+                    models[r].initialize_factors_with_prior(X_train=X_train)
             self.conf.zero_()
             self.run_epoch(ep, train, active, set_modes=False)
 
@@ -434,7 +441,8 @@ class ReplicaPack:
                     acc_d, confv_d = self._values(val, active, host=False)
                     pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] +
                                             ([vals_d] if vals_d is not None else []))
-                spec = it + 1 < max_iter and not (dirs is not None and it % check_every == 0)
+                spec = (it + 1 < max_iter and not (dirs is not None and it % check_every == 0)
+                        and it + 1 != reorder_at)
                 if spec:
                     self._save_state()
                     steps_before = [self._step_counts(r) for r in range(R)]

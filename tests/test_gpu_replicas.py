@@ -20,7 +20,7 @@ GRID8 = GRID + [(3 + i, (1.0, 10.0)[i % 2], (0.1, 0.01)[i % 2], (5e-4, 1e-4)[i %
                 for i in range(5)]
 
 
-def make(seed, fc, adj, pre=1, acc=1):
+def make(seed, fc, adj, pre=1, acc=1, mode="pretrain_embedder_then_acclimate_factors_then_combined"):
     import redcliff_amd
     K, p = CFG["K"], CFG["p"]
     coeff = {"FORECAST_COEFF": fc, "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0 / sum(range(1, K)),
@@ -33,7 +33,7 @@ def make(seed, fc, adj, pre=1, acc=1):
     return redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(
         p, CFG["L"], [CFG["h"]], CFG["F"], [0], CFG["L"], 1, K, CFG["nsup"], coeff, False, "DGCNN", eargs,
         "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
-        training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=pre,
+        training_mode=mode, num_pretrain_epochs=pre,
         num_acclimation_epochs=acc).cuda()
 
 
