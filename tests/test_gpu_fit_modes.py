@@ -37,11 +37,14 @@ def expected_order(model, X_train, max_batches=10):
         for b, (X, Y) in enumerate(X_train):
             if b >= max_batches:
                 break
-            Y = Y[:, :, Lm] if Y.size(2) > Lm else Y[:, :, 0]
+            if Y.dim() > 2:
+                Y = Y[:, :, Lm] if Y.size(2) > Lm else Y[:, :, 0]
             model.factor_score_embedder.eval()
-            _, _, fw, _ = model.forward(X[:, :Lm, :].cuda())
+            for f in model.factors:
+                f.eval()
+            _, _, fw, _ = model.forward(X[:, :Lm, :].cuda().float())
             preds.append(fw[0].cpu().numpy())
-            labs.append(Y.numpy())
+            labs.append(Y.cpu().numpy())
     P, Yl = np.vstack(preds), np.vstack(labs)
     cost = np.zeros((P.shape[1], Yl.shape[1]))
     for i in range(P.shape[1]):
@@ -156,3 +159,18 @@ def test_freeze_modes_fail_like_the_reference(mode):
     sa, sb = m.state_dict(), ref.state_dict()
     for k in sa:
         np.testing.assert_array_equal(sa[k].cpu().numpy(), sb[k].cpu().numpy(), err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["cemb", "vanilla"])
+def test_reorder_on_the_generic_path(name):
+    """Configurations outside the fused chain re-order the factor modules themselves, as the
+    reference does (:200-205): module i of the new list is old module order[i]."""
+    from golden_io import batches, load
+    from test_gpu_generic import build
+    d, meta = load(name)
+    m = build(meta)
+    bs = batches(d, meta)
+    want = expected_order(m, bs)
+    old = list(m.factors)
+    m.initialize_factors_with_prior(X_train=bs)
+    assert [id(f) for f in m.factors] == [id(old[i]) for i in want]
