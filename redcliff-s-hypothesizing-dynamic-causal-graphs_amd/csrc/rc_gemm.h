@@ -6,8 +6,9 @@
 // row-major, op(X) = X or X^T; z = blockIdx.z (batch / split-K slice); the contraction index
 // k in [0, K) is split as k = kb * Kblk + kr, which lets one launch sum products over many
 // small matrices (e.g. over the windows of a batch) without materialising per-window partials.
-// 64x64 output tile per 256-thread workgroup, 4x4 outputs per thread, K staged through LDS in
-// steps of 16; each output is an in-order fmaf chain over k (deterministic).
+// K staged through LDS in steps of 16.  Two cores: k_rc_gemm_mfma (fp32 matrix cores, the
+// default) and k_rc_gemm (vector-ALU fmaf chains, REDCLIFF_GEMM_CORE=valu); each is
+// deterministic and independent of the tile size it is launched with.
 #pragma once
 #include <cstdlib>
 
@@ -133,23 +134,122 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   }
 }
 
+// Matrix-core variant: the same tiles, staging and workgroup shape as k_rc_gemm, the
+// products on the fp32 matrix cores.  TT = 64: each of the 4 waves owns a 32x32 quarter
+// (v_mfma_f32_32x32x2f32); TT = 32: a 16x16 quarter (v_mfma_f32_16x16x4f32).  The fp32 MFMA
+// forms are exact fmaf chains over k in order (MI355X_MICROARCH.md, "F32 (f32 in)"), so an
+// output has the same bits as k_rc_gemm's in-order fmaf chain, whatever the tile or core
+// (tests/test_gpu_generic.py::test_gemm_cores_bitwise).
+template <int TT>
+__global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
+  constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
+  constexpr int QT = TT / 2;                      // quarter tile per wave
+  rc_critical_priority();
+  const int bz = blockIdx.z;
+  const float* A = g.A + bz * g.sA;
+  const float* B = g.B + bz * g.sB;
+  float* C = g.C + bz * g.sC;
+  const int n0 = blockIdx.x * TT, m0 = blockIdx.y * TT;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = QT * (wv >> 1), wn = QT * (wv & 1);
+  const RcDiv dkb(g.Kblk);
+  __shared__ float As[RC_GEMM_K][TT + 4];  // As[k][m]
+  __shared__ float Bs[RC_GEMM_K][TT + 4];  // Bs[k][n]
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x16 acc32;
+  f32x4 acc16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc32[i] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc16[i] = 0.f;
+  float av[NL], bv[NL];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < NL; ++r) {
+      const int e = tid + r * RC_BLOCK;  // 16 x TT elements of each tile
+      int kk, mm;
+      if (g.ta) { kk = e / TT; mm = e % TT; } else { mm = e >> 4; kk = e & 15; }
+      const int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < g.M && gk < g.K) {
+        const int kb = dkb.div(gk), kr = gk - kb * g.Kblk;
+        const float* Ab = A + kb * g.rA;
+        v = g.ta ? Ab[(int64_t)kr * g.lda + gm] : Ab[(int64_t)gm * g.lda + kr];
+      }
+      av[r] = v;
+      int kb2, nb;
+      if (g.tb) { nb = e >> 4; kb2 = e & 15; } else { kb2 = e / TT; nb = e % TT; }
+      const int gn = n0 + nb, gk2 = k0 + kb2;
+      float w = 0.f;
+      if (gn < g.N && gk2 < g.K) {
+        const int kb = dkb.div(gk2), kr = gk2 - kb * g.Kblk;
+        const float* Bb = B + kb * g.rB;
+        w = g.tb ? Bb[(int64_t)gn * g.ldb + kr] : Bb[(int64_t)kr * g.ldb + gn];
+      }
+      bv[r] = w;
+    }
+  };
+  if (g.K > 0) load(0);
+  for (int k0 = 0; k0 < g.K; k0 += RC_GEMM_K) {
+#pragma unroll
+    for (int r = 0; r < NL; ++r) {
+      const int e = tid + r * RC_BLOCK;
+      if (g.ta) As[e / TT][e % TT] = av[r]; else As[e & 15][e >> 4] = av[r];
+      if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e / TT][e % TT] = bv[r];
+    }
+    __syncthreads();
+    if (k0 + RC_GEMM_K < g.K) load(k0 + RC_GEMM_K);
+    if constexpr (TT == 64) {
+      const int l31 = lane & 31, kh = lane >> 5;
+#pragma unroll
+      for (int kk = 0; kk < RC_GEMM_K; kk += 2)
+        acc32 = __builtin_amdgcn_mfma_f32_32x32x2f32(As[kk + kh][wm + l31], Bs[kk + kh][wn + l31], acc32, 0, 0, 0);
+    } else {
+      const int l15 = lane & 15, kq = lane >> 4;
+#pragma unroll
+      for (int kk = 0; kk < RC_GEMM_K; kk += 4)
+        acc16 = __builtin_amdgcn_mfma_f32_16x16x4f32(As[kk + kq][wm + l15], Bs[kk + kq][wn + l15], acc16, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  constexpr int NR = TT == 64 ? 16 : 4;
+  const int gn = n0 + wn + (TT == 64 ? (lane & 31) : (lane & 15));
+  if (gn >= g.N) return;
+#pragma unroll
+  for (int reg = 0; reg < NR; ++reg) {
+    const int gm = m0 + wm + (TT == 64 ? mf_row(reg, lane) : 4 * (lane >> 4) + reg);
+    if (gm >= g.M) continue;
+    float* cp = C + (int64_t)gm * g.ldc + gn;
+    const float a = TT == 64 ? acc32[reg] : acc16[reg];
+    float v = g.beta == 0.f ? g.alpha * a : g.alpha * a + g.beta * *cp;
+    if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
+    else if (g.epi == RC_EPI_MASK) v = g.aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
+    *cp = v;
+  }
+}
+
 inline int rc_gemm_launch(const RcGemm& g, int batch, hipStream_t s, const char* what) {
   if (g.M <= 0 || g.N <= 0 || batch <= 0) return 0;
   if (batch > 65535) { rc_set_error("%s: batch %d > 65535", what, batch); return REDCLIFF_ELIMIT; }
   // fewer than two 64x64 tiles per CU: 32x32 tiles (more workgroups in flight to hide the
-  // operand latency of these short products).  REDCLIFF_GEMM_TILE=64|32 overrides (tuning).
+  // operand latency of these short products).  REDCLIFF_GEMM_TILE=64|32 overrides (tuning);
+  // REDCLIFF_GEMM_CORE=valu selects the vector-ALU fmaf kernel (measurements).
   static const int tile_env = [] {
     const char* v = getenv("REDCLIFF_GEMM_TILE");
     return v ? atoi(v) : 0;
   }();
+  const char* core = getenv("REDCLIFF_GEMM_CORE");  // read per launch: the tests switch it
+  const bool valu = core != nullptr && core[0] == 'v';
   const int64_t t64 = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * batch;
   const bool small = tile_env == 32 || (tile_env != 64 && t64 < 512);
   if (small) {
     dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, batch);
-    hipLaunchKernelGGL(k_rc_gemm<32>, grid, dim3(RC_BLOCK), 0, s, g);
+    if (valu) hipLaunchKernelGGL(k_rc_gemm<32>, grid, dim3(RC_BLOCK), 0, s, g);
+    else hipLaunchKernelGGL(k_rc_gemm_mfma<32>, grid, dim3(RC_BLOCK), 0, s, g);
   } else {
     dim3 grid((g.N + RC_GEMM_T - 1) / RC_GEMM_T, (g.M + RC_GEMM_T - 1) / RC_GEMM_T, batch);
-    hipLaunchKernelGGL(k_rc_gemm<RC_GEMM_T>, grid, dim3(RC_BLOCK), 0, s, g);
+    if (valu) hipLaunchKernelGGL(k_rc_gemm<RC_GEMM_T>, grid, dim3(RC_BLOCK), 0, s, g);
+    else hipLaunchKernelGGL(k_rc_gemm_mfma<RC_GEMM_T>, grid, dim3(RC_BLOCK), 0, s, g);
   }
   return rc_check(hipGetLastError(), what);
 }

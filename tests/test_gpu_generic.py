@@ -133,3 +133,24 @@ def test_hip_gemm_against_fp64():
     (torch.matmul(a2, b2) ** 2).sum().backward()
     np.testing.assert_allclose(a.grad.cpu().numpy(), a2.grad.numpy(), rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(b.grad.cpu().numpy(), b2.grad.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_gemm_cores_bitwise(monkeypatch):
+    """The matrix-core GEMM (k_rc_gemm_mfma: 32x32x2 / 16x16x4 fp32 MFMA) and the vector-ALU
+    one (k_rc_gemm, REDCLIFF_GEMM_CORE=valu) give the same bits: both are in-order fmaf chains
+    over k.  Shapes cover both tile sizes (64x64 tiles when the launch has >= 512 of them),
+    ragged edges and all transpose combinations."""
+    from redcliff_amd.generic import _raw_bmm
+    g = torch.Generator().manual_seed(1)
+    shapes = ((1, 1, 1, 3), (7, 65, 33, 3), (64, 64, 16, 3), (130, 3, 257, 3), (200, 300, 70, 2),
+              (256, 256, 40, 32), (100, 260, 129, 40))
+    for (M, N, K, nb) in shapes:
+        for ta in (0, 1):
+            for tb in (0, 1):
+                a = torch.randn((nb,) + ((K, M) if ta else (M, K)), generator=g).cuda()
+                b = torch.randn((nb,) + ((N, K) if tb else (K, N)), generator=g).cuda()
+                monkeypatch.delenv("REDCLIFF_GEMM_CORE", raising=False)
+                got = _raw_bmm(a, b, ta, tb).cpu().numpy()
+                monkeypatch.setenv("REDCLIFF_GEMM_CORE", "valu")
+                want = _raw_bmm(a, b, ta, tb).cpu().numpy()
+                np.testing.assert_array_equal(got, want, err_msg="M=%d N=%d K=%d ta=%d tb=%d" % (M, N, K, ta, tb))
