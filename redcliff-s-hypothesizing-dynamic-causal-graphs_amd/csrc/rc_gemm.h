@@ -15,7 +15,10 @@
 #include "rc_common.h"
 
 #define RC_GEMM_T 64
-#define RC_GEMM_K 16
+#ifndef RC_GEMM_K
+#define RC_GEMM_K 16  // K step staged through LDS (a power of two)
+#endif
+static_assert((RC_GEMM_K & (RC_GEMM_K - 1)) == 0 && RC_GEMM_K >= 16, "RC_GEMM_K: power of two >= 16");
 
 enum { RC_EPI_NONE = 0, RC_EPI_RELU = 1, RC_EPI_MASK = 2 };  // MASK: times (aux > 0)
 
@@ -70,9 +73,9 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   auto load = [&](int k0) {
 #pragma unroll
     for (int r = 0; r < NL; ++r) {
-      const int e = tid + r * RC_BLOCK;  // 16 x TT elements of each tile
+      const int e = tid + r * RC_BLOCK;  // RC_GEMM_K x TT elements of each tile
       int kk, mm;
-      if (g.ta) { kk = e / TT; mm = e % TT; } else { mm = e >> 4; kk = e & 15; }
+      if (g.ta) { kk = e / TT; mm = e % TT; } else { mm = e / RC_GEMM_K; kk = e % RC_GEMM_K; }
       const int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
       if (gm < g.M && gk < g.K) {
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
       }
       av[r] = v;
       int kb2, nb;
-      if (g.tb) { nb = e >> 4; kb2 = e & 15; } else { kb2 = e / TT; nb = e % TT; }
+      if (g.tb) { nb = e / RC_GEMM_K; kb2 = e % RC_GEMM_K; } else { kb2 = e / TT; nb = e % TT; }
       const int gn = n0 + nb, gk2 = k0 + kb2;
       float w = 0.f;
       if (gn < g.N && gk2 < g.K) {
@@ -98,8 +101,8 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
 #pragma unroll
     for (int r = 0; r < NL; ++r) {
       const int e = tid + r * RC_BLOCK;
-      if (g.ta) As[e / TT][e % TT] = av[r]; else As[e & 15][e >> 4] = av[r];
-      if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e / TT][e % TT] = bv[r];
+      if (g.ta) As[e / TT][e % TT] = av[r]; else As[e % RC_GEMM_K][e / RC_GEMM_K] = av[r];
+      if (g.tb) Bs[e % RC_GEMM_K][e / RC_GEMM_K] = bv[r]; else Bs[e / TT][e % TT] = bv[r];
     }
     __syncthreads();
     if (k0 + RC_GEMM_K < g.K) load(k0 + RC_GEMM_K);
@@ -166,9 +169,9 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
   auto load = [&](int k0) {
 #pragma unroll
     for (int r = 0; r < NL; ++r) {
-      const int e = tid + r * RC_BLOCK;  // 16 x TT elements of each tile
+      const int e = tid + r * RC_BLOCK;  // RC_GEMM_K x TT elements of each tile
       int kk, mm;
-      if (g.ta) { kk = e / TT; mm = e % TT; } else { mm = e >> 4; kk = e & 15; }
+      if (g.ta) { kk = e / TT; mm = e % TT; } else { mm = e / RC_GEMM_K; kk = e % RC_GEMM_K; }
       const int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
       if (gm < g.M && gk < g.K) {
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
       }
       av[r] = v;
       int kb2, nb;
-      if (g.tb) { nb = e >> 4; kb2 = e & 15; } else { kb2 = e / TT; nb = e % TT; }
+      if (g.tb) { nb = e / RC_GEMM_K; kb2 = e % RC_GEMM_K; } else { kb2 = e / TT; nb = e % TT; }
       const int gn = n0 + nb, gk2 = k0 + kb2;
       float w = 0.f;
       if (gn < g.N && gk2 < g.K) {
@@ -194,8 +197,8 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
 #pragma unroll
     for (int r = 0; r < NL; ++r) {
       const int e = tid + r * RC_BLOCK;
-      if (g.ta) As[e / TT][e % TT] = av[r]; else As[e & 15][e >> 4] = av[r];
-      if (g.tb) Bs[e & 15][e >> 4] = bv[r]; else Bs[e / TT][e % TT] = bv[r];
+      if (g.ta) As[e / TT][e % TT] = av[r]; else As[e % RC_GEMM_K][e / RC_GEMM_K] = av[r];
+      if (g.tb) Bs[e % RC_GEMM_K][e / RC_GEMM_K] = bv[r]; else Bs[e / TT][e % TT] = bv[r];
     }
     __syncthreads();
     if (k0 + RC_GEMM_K < g.K) load(k0 + RC_GEMM_K);
