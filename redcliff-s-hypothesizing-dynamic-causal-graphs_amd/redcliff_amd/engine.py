@@ -43,6 +43,18 @@ def phase_of_epoch(model, epoch_num):
     raise NotImplementedError()
 
 
+def step_flags(model, kind, nsup):
+    """flags_for, less optimizerB when the model's factors were replaced by a prior model's
+    (initialize_factors_with_prior: the reference's optimizerB keeps the replaced parameters, so
+    the loaded factors are never stepped).  flags 0: nothing of the update changes any state."""
+    flags, nbn = flags_for(kind, nsup)
+    if model.__dict__.get("_factors_detached", False):
+        flags &= ~nat.STEP_B
+        if not flags & nat.STEP_A:
+            return 0, 0
+    return flags, nbn
+
+
 def flags_for(kind, nsup):
     """Loss terms / optimizer steps of one update kind (compute_loss flags, :718-729)."""
     conf = nat.CONFUSION if nsup > 0 else 0
@@ -414,7 +426,9 @@ class FitEngine:
         """Run the update kinds of one phase over consecutive batches (rows/sizes)."""
         self.ensure_bound()
         for kind in kinds:
-            flags, nbn = flags_for(kind, self.nsup)
+            flags, nbn = step_flags(self.model, kind, self.nsup)
+            if flags == 0:
+                continue
             if flags & nat.STEP_A:
                 self.bind_optimizer("A", oA)
             if flags & nat.STEP_B:
@@ -582,7 +596,7 @@ class StepPlan:
     def __init__(self, eng, kind, X, lab, stats, d, rows, sizes, oA, oB):
         eng.ensure_bound()
         self.eng = eng
-        self.flags, self.nbn = flags_for(kind, eng.nsup)
+        self.flags, self.nbn = step_flags(eng.model, kind, eng.nsup)
         if self.flags & nat.STEP_A:
             eng.bind_optimizer("A", oA)
         if self.flags & nat.STEP_B:
@@ -600,6 +614,8 @@ class StepPlan:
 
     def run(self, stream=None):
         eng, a = self.eng, self.a
+        if self.flags == 0:
+            return
         eng._fresh_state()
         stA, stB = eng.opt["A"], eng.opt["B"]
         a.tA = (stA["t"] + 1) if stA else 1

@@ -500,7 +500,7 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
             acc_d, confv_d = eng.run_values(val["X"], val["lab"], d_train, val["rows"], val["sizes"], host=False)
             pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
         spec = (it + 1 < max_iter and not (save_dir is not None and it % check_every == 0) and not freeze
-                and hook.at != it + 1)
+                and it + 1 not in hook.at)
         if spec:
             saved.save()
             _train_epoch(model, eng, train, d_train, plans, oA, oB, it + 1)
@@ -586,10 +586,14 @@ def _prior_hook(model, X_train, prior):
     """it -> None: the factor re-ordering fit() runs at the start of epoch num_pretrain_epochs
     of the "pretrain_factor" modes (...withStateSmoothing.py:1318-1326)."""
     path, cost, start, nb = prior
-    at = model.num_pretrain_epochs if "pretrain_factor" in model.training_mode else None
+    at = set()
+    if "pretrain_factor" in model.training_mode:
+        at.add(model.num_pretrain_epochs)
+    if path is not None:
+        at.add(0)
 
     def hook(it):
-        if it == at:
+        if it in at:
             model.initialize_factors_with_prior(prior_factors_path=path, X_train=X_train, cost_criteria=cost,
                                                 unsupervised_start_index=start, max_batches=nb)
     hook.at = at
@@ -611,8 +615,6 @@ def _freeze_by_batch(model, fused, X_train, oA, oB, output_length, it):
 def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
              deltaConEps, in_degree_coeff, out_degree_coeff, prior, sc_forecast, sc_factor, sc_cos,
              save_plots):
-    if prior[0] is not None:
-        raise NotImplementedError("prior-initialised factors (prior_factors_path) are not on the fused path")
     if output_length != 1:
         raise NotImplementedError("output_length must be 1")
     fused = model.fused_supported()

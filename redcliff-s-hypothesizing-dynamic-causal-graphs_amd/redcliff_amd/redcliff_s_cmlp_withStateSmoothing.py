@@ -385,11 +385,30 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
 
         The reference re-orders the module objects, so each factor's Adam state moves with it;
         here the factor slots of the packed parameter buffer and of optimizerB's moments are
-        permuted, which is the same state.  ``prior_factors_path`` (replace the factors by those
-        of a saved model -- the reference's assignment leaves optimizerB holding the replaced
-        parameters, i.e. the loaded factors are never stepped) is not on this path."""
+        permuted, which is the same state.
+
+        ``prior_factors_path``: the factors are replaced by those of a model saved by fit() /
+        save_checkpoint (:151-153, loaded the way the reference loads it: a pickled module, so
+        only files this package or the reference wrote).  The reference's ``self.factors =
+        prior.factors`` leaves optimizerB (built on gen_model[1]) holding the replaced
+        parameters, so the loaded factors are never stepped again; on the fused path their
+        values are copied into the factor buffer and optimizerB's updates are dropped from
+        every later step (engine.step_flags).  gen_model[1] keeps pointing at the live factors
+        here, where the reference's still holds the replaced ones."""
         if prior_factors_path is not None:
-            raise NotImplementedError("prior-initialised factors (prior_factors_path) are not on the fused path")
+            prior = torch.load(prior_factors_path, map_location=self._device(), weights_only=False)
+            if not self.fused_supported():
+                self.factors = prior.factors  # the reference's move (:152)
+            else:
+                eng = self.engine()
+                eng.ensure_bound()
+                with torch.no_grad():
+                    for f_dst, f_src in zip(self.factors, prior.factors):
+                        for p_dst, p_src in zip(f_dst.parameters(), f_src.parameters()):
+                            p_dst.copy_(p_src.detach().to(p_dst.device, p_dst.dtype))
+                eng.invalidate()
+                self.__dict__["_factors_detached"] = True
+            del prior
         if X_train is None:
             return
         if unsupervised_start_index != 0:
@@ -435,7 +454,9 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         base = eng.fac
         slots = [[((prm.data_ptr() - base.data_ptr()) // 4, prm.numel()) for prm in f.parameters()]
                  for f in self.factors]
-        bufs = [eng.fac] + ([eng.opt["B"]["m"], eng.opt["B"]["v"]] if eng.opt["B"] is not None else [])
+        # detached factors (a prior model's): optimizerB's state belongs to the replaced ones
+        moments = eng.opt["B"] is not None and not self.__dict__.get("_factors_detached", False)
+        bufs = [eng.fac] + ([eng.opt["B"]["m"], eng.opt["B"]["v"]] if moments else [])
         with torch.no_grad():
             for buf in bufs:
                 old = buf.clone()

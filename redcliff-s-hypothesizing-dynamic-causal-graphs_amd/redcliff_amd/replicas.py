@@ -355,7 +355,7 @@ class ReplicaPack:
             raise NotImplementedError("output_length must be 1")
         R, models = self.R, self.models
         for m in models:
-            if not m.fused_supported() or "Freeze" in m.training_mode:
+            if not m.fused_supported() or "Freeze" in m.training_mode or m.__dict__.get("_factors_detached"):
                 raise NotImplementedError("packed fits cover the fused (published) configuration")
         sched = set((m.num_pretrain_epochs, m.num_acclimation_epochs, m.training_mode) for m in models)
         if len(sched) != 1:

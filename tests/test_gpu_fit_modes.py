@@ -174,3 +174,42 @@ def test_reorder_on_the_generic_path(name):
     old = list(m.factors)
     m.initialize_factors_with_prior(X_train=bs)
     assert [id(f) for f in m.factors] == [id(old[i]) for i in want]
+
+
+def test_prior_factors_path(tmp_path, monkeypatch):
+    """fit(prior_factors_path=...) (:1318-1326 at epoch 0 -> :149-206).  The reference replaces
+    the factors by the saved model's and re-orders them; its optimizerB still holds the replaced
+    parameters, so the loaded factors never change again, while the embedder keeps training
+    against them.  Twin: the same model given the permuted prior factors by hand and trained
+    with optimizerB at lr 0 (the fused Adam then leaves the factors bit-identical), so the
+    embedder's updates through the optimizerB-less steps must match it bit for bit."""
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "mfma")
+    train, val = data(64 * 2, seed=12), data(64, seed=13)
+    s, fc, adj, lrB, lrA = GRID[0]
+    mode = "pretrain_embedder_then_acclimate_factors_then_combined"
+    prior = mk(9, fc, adj, mode, pre=1, acc=1)
+    path = str(tmp_path / "prior.bin")
+    torch.save(prior, path)
+    pf = [[p.detach().cpu().numpy().copy() for p in f.parameters()] for f in prior.factors]
+
+    m = mk(s, fc, adj, mode, pre=1, acc=1)
+    order = expected_order(m, train)
+    oA, oB = opts(m, lrB, lrA)
+    m.fit(None, train, oA, oB, 4, 1, 1, 4, val, lookback=1, check_every=1, verbose=0, prior_factors_path=path)
+    torch.cuda.synchronize()
+    for i, f in enumerate(m.factors):
+        for got, want in zip(f.parameters(), pf[order[i]]):
+            np.testing.assert_array_equal(got.detach().cpu().numpy(), want)
+
+    twin = mk(s, fc, adj, mode, pre=1, acc=1)
+    with torch.no_grad():
+        for i, f in enumerate(twin.factors):
+            for p, want in zip(f.parameters(), pf[order[i]]):
+                p.copy_(torch.from_numpy(want))
+    tA, tB = opts(twin, 0.0, lrA)
+    twin.fit(None, train, tA, tB, 4, 1, 1, 4, val, lookback=1, check_every=1, verbose=0)
+    torch.cuda.synchronize()
+    sa, sb = m.state_dict(), twin.state_dict()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k].cpu().numpy(), sb[k].cpu().numpy(), err_msg=k)
+    assert m.fit_history["avg_combo_loss"] == twin.fit_history["avg_combo_loss"]
