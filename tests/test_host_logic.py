@@ -63,3 +63,31 @@ def test_compute_without_gpu_fails_loudly():
     X = torch.from_numpy(d["X"][:4])
     with pytest.raises(RuntimeError, match="GPU"):
         m(X[:, :5])
+
+
+def test_step_flags_after_prior_factors():
+    """A model whose factors came from prior_factors_path keeps training its embedder but never
+    steps optimizerB again (the reference's optimizerB keeps the replaced parameters); updates
+    that would only move the factors change nothing and are skipped."""
+    from redcliff_amd import _native as nat
+    from redcliff_amd.engine import flags_for, step_flags
+    d, meta = load("dgcnn_c1")
+    m = build(meta)
+    for kind in ("pretrain_embedder", "pretrain_factor", "acclimate", "post_train", "combined"):
+        assert step_flags(m, kind, 2) == flags_for(kind, 2)
+    m.__dict__["_factors_detached"] = True
+    for kind in ("pretrain_factor", "acclimate", "post_train"):
+        assert step_flags(m, kind, 2) == (0, 0)
+    for kind in ("pretrain_embedder", "combined"):
+        f, nbn = step_flags(m, kind, 2)
+        f0, nbn0 = flags_for(kind, 2)
+        assert f == f0 & ~nat.STEP_B and f & nat.STEP_A and nbn == nbn0
+
+
+def test_freeze_decision_raises_like_the_reference():
+    """determine_which_factors_need_updates on the (p, p, 1) lag-free estimates: numpy's
+    norm(ord=1) of a 3-d array raises, exactly as in the reference (...withStateSmoothing.py:
+    1159-1166)."""
+    x = np.random.RandomState(0).rand(5, 5, 1).astype(np.float32)
+    with pytest.raises(ValueError, match="Improper number of dimensions to norm"):
+        np.linalg.norm(x / np.max(x), ord=1)
