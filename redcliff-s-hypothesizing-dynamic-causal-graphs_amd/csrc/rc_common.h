@@ -104,6 +104,19 @@ __host__ __device__ inline int rc_emb_node_floats(const RedcliffDims& d, int BC)
   return 4 * BC * d.K + d.K * d.M1 + d.M1 * EMB_HC + nF * (EMB_HC + 1) + d.n * d.p + 8 + 4 * d.F + RC_BLOCK +
          BC * (2 * d.M1 + 2 * EMB_HC + 2 * nF + d.p * d.F);
 }
+// RC_EMB_LATE_X (experiment): the raw window tile of an embedder-backward sub-block is staged
+// after the dW_i phase into the LDS of the tiles that are dead by then (f1, df1, R, dZ, T), when
+// it fits there; the allocation shrinks by BC*p*F floats.  BC is still chosen on the full size,
+// so the arithmetic (and the bits) do not change.
+#ifndef RC_EMB_LATE_X
+#define RC_EMB_LATE_X 0
+#endif
+__host__ __device__ inline bool rc_emb_late_x(const RedcliffDims& d) {
+  return RC_EMB_LATE_X && d.p * d.F <= 2 * d.M1 + 2 * EMB_HC + d.n * d.F;
+}
+__host__ __device__ inline int rc_emb_node_alloc_floats(const RedcliffDims& d, int BC) {
+  return rc_emb_node_floats(d, BC) - (rc_emb_late_x(d) ? BC * d.p * d.F : 0);
+}
 // Windows per LDS sub-block: as many as fit the 64 KiB budget; with fewer than 4 (large p*F)
 // the budget grows to the CU's 160 KiB.
 __host__ __device__ inline int rc_emb_bc(const RedcliffDims& d) {

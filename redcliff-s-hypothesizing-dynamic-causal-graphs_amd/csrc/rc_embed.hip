@@ -272,7 +272,8 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   float* dZc = Rc + BC * HC;             // [BC][HC]
   float* Tc = dZc + BC * HC;             // [BC][n][F]   T_i row `node`
   float* dTc = Tc + BC * nF;             // [BC][n][F]
-  float* xc = dTc + BC * nF;             // [BC][p][F]   raw window
+  const bool late_x = rc_emb_late_x(d);
+  float* xc = late_x ? f1r : dTc + BC * nF;  // [BC][p][F] raw window (late: over f1r .. Tc)
 
   const RcDiv dF(F), dp(p), dpF(pF), dnF(nF), dK(K), dM1(M1);
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 33);
@@ -313,13 +314,15 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       const int s = dnF.div(e), rem = e - s * nF, i = dF.div(rem), f = rem - i * F;
       return Tg[(int64_t)(bw0 + s) * n * pF + i * pF + node * F + f];
     }, [&](int e, float v) { Tc[e] = v; });
-    auto sX = rc_seg<16>(nbc * pF, [&](int e) {
+    auto x_ld = [&](int e) {
       const int s = dpF.div(e), rem = e - s * pF;  // rem = f * p + cc (contiguous in the window row)
       return X[(c.row0 + bw0 + s) * d.T * p + (int64_t)(c.Lmax - F) * p + rem];
-    }, [&](int e, float v) {
+    };
+    auto x_st = [&](int e, float v) {
       const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), cc = rem - f * p;
       xc[s * pF + cc * F + f] = v;
-    });
+    };
+    auto sX = rc_seg<16>(late_x ? 0 : nbc * pF, x_ld, x_st);
     auto sF1 = rc_seg<4>(nbc * M1, [&](int e) { return f1[(int64_t)bw0 * M1 + e]; }, [&](int e, float v) { f1r[e] = v; });
     auto sW = rc_seg<1>(nbc * K, [&](int e) { return wraw[(int64_t)bw0 * K + e]; }, [&](int e, float v) { wrl[e] = v; });
     auto sL = rc_seg<1>(nbc * K, [&](int e) { return lab_on ? c.lab[r * c.labr + (c.row0 + bw0) * K + e] : 0.f; },
@@ -472,6 +475,10 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       dTc[e] = t0 + t1;
     }
     __syncthreads();
+    if (late_x) {  // f1 / df1 / R / dZ / T are dead: the window tile goes there
+      rc_stage_all(rc_seg<16>(nbc * pF, x_ld, x_st));
+      __syncthreads();
+    }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 37);
     // dS_i[node][c'] (i >= 1) and BatchNorm affine partials, windows split over thread slices
     if (slS < nslS) {
@@ -668,8 +675,12 @@ __device__ __forceinline__ void emb_bwd_dadj(const StepCtx& c, int r, int blk, b
 // grid (p * nchunk * nbw [+ 1] [+ nred], R): workgroups [0, p*nchunk*nbw) are (node, column
 // chunk, window block) blocks; then the optional head (loss values / confusion), then the
 // adjacency-L1 reduce workgroups.
+#ifndef RC_EMB_WAVES
+#define RC_EMB_WAVES 0  // experiment: amdgpu_waves_per_eu floor for k_emb_bwd (0: compiler's choice)
+#endif
 template <bool MULTI>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
+__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_EMB_WAVES > 0 ? RC_EMB_WAVES : 1)))
+void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   extern __shared__ float sm[];
   const int r = rc_rep(c, blockIdx.y);
   const int nch = rc_nchunk(c.d);
@@ -1167,7 +1178,7 @@ static int rc_lds_optin(Kern k, size_t bytes, const char* what) {
 
 size_t rc_emb_bwd_lds(const RedcliffDims& d) {
   const size_t head = 32 + (size_t)d.nsup * d.nsup;
-  const size_t node = rc_emb_node_floats(d, rc_emb_bc(d));
+  const size_t node = rc_emb_node_alloc_floats(d, rc_emb_bc(d));
   return (head > node ? head : node) * sizeof(float);
 }
 
