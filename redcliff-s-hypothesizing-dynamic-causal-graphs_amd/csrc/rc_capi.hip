@@ -87,7 +87,7 @@ int rc_check(hipError_t e, const char* what) {
   return (int)e;
 }
 
-size_t rc_emb_bwd_lds(const RedcliffDims& d);
+size_t rc_emb_bwd_lds(const RedcliffDims& d, bool late);
 
 // Shape limits of the kernels (LDS tiles, register-blocked accumulators).
 static int check_dims(const RedcliffDims* d) {
@@ -109,7 +109,7 @@ static int check_dims(const RedcliffDims* d) {
     rc_set_error("fused path needs embed_lag >= gen_lag (forward and GC embedder windows coincide)");
     return REDCLIFF_ELIMIT;
   }
-  if (rc_emb_bwd_lds(*d) > RC_LDS_MAX_FLOATS * sizeof(float)) {
+  if (rc_emb_bwd_lds(*d, false) > RC_LDS_MAX_FLOATS * sizeof(float)) {
     rc_set_error("embedder backward LDS budget exceeded for Bmax*K=%d", d->Bmax * d->K);
     return REDCLIFF_ELIMIT;
   }

@@ -234,7 +234,7 @@ __device__ __forceinline__ void emb_bwd_head(const StepCtx& c, int r, float* sm)
 // place (2), or by the block that arrives last (0: agent-scope release / ticket / acquire,
 // cdna_hip_programming.md §6 Guideline 16).  The first sub-block's inputs and the
 // fixed operands are staged by one multi-segment pass (one memory latency for everything).
-template <bool MULTI>
+template <bool MULTI, bool LATE = false>
 __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, int ch, int wb, int BC, int WPB, float* sm,
                              const unsigned* wait_cnt = nullptr, unsigned wait_target = 0) {
   const RedcliffDims& d = c.d;
@@ -272,7 +272,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   float* dZc = Rc + BC * HC;             // [BC][HC]
   float* Tc = dZc + BC * HC;             // [BC][n][F]   T_i row `node`
   float* dTc = Tc + BC * nF;             // [BC][n][F]
-  const bool late_x = rc_emb_late_x(d);
+  const bool late_x = LATE && rc_emb_late_x(d);
   float* xc = late_x ? f1r : dTc + BC * nF;  // [BC][p][F] raw window (late: over f1r .. Tc)
 
   const RcDiv dF(F), dp(p), dpF(pF), dnF(nF), dK(K), dM1(M1);
@@ -675,11 +675,14 @@ __device__ __forceinline__ void emb_bwd_dadj(const StepCtx& c, int r, int blk, b
 // grid (p * nchunk * nbw [+ 1] [+ nred], R): workgroups [0, p*nchunk*nbw) are (node, column
 // chunk, window block) blocks; then the optional head (loss values / confusion), then the
 // adjacency-L1 reduce workgroups.
+// The single-sub-block variant stages the window tile late (rc_emb_late_x) and runs with a floor
+// of RC_EMB_WAVES waves per SIMD (0: the compiler's choice); the multi-sub-block one (256 VGPRs)
+// keeps its layout and registers.
 #ifndef RC_EMB_WAVES
-#define RC_EMB_WAVES 0  // experiment: amdgpu_waves_per_eu floor for k_emb_bwd (0: compiler's choice)
+#define RC_EMB_WAVES 0
 #endif
 template <bool MULTI>
-__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_EMB_WAVES > 0 ? RC_EMB_WAVES : 1)))
+__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(MULTI || RC_EMB_WAVES == 0 ? 1 : RC_EMB_WAVES)))
 void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   extern __shared__ float sm[];
   const int r = rc_rep(c, blockIdx.y);
@@ -694,7 +697,7 @@ void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
   } else {
     const int grp = blockIdx.x / nbw, wb = blockIdx.x - grp * nbw;
-    emb_bwd_node<MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
+    emb_bwd_node<MULTI, !MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
   }
 }
 
@@ -1176,17 +1179,18 @@ static int rc_lds_optin(Kern k, size_t bytes, const char* what) {
                                       (int)bytes), what);
 }
 
-size_t rc_emb_bwd_lds(const RedcliffDims& d) {
+size_t rc_emb_bwd_lds(const RedcliffDims& d, bool late) {
   const size_t head = 32 + (size_t)d.nsup * d.nsup;
-  const size_t node = rc_emb_node_alloc_floats(d, rc_emb_bc(d));
+  const int BC = rc_emb_bc(d);
+  const size_t node = late ? rc_emb_node_alloc_floats(d, BC) : rc_emb_node_floats(d, BC);
   return (head > node ? head : node) * sizeof(float);
 }
 
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   const RedcliffDims& d = c.d;
-  const size_t lds = rc_emb_bwd_lds(d);
-  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   const int BC = rc_emb_bc(d), WPB = rc_emb_wpb(d);
+  const size_t lds = rc_emb_bwd_lds(d, WPB <= BC);  // the single-sub-block variant stages late
+  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   const int nnode = node_wgs ? d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB) : 0;
   const int head = (c.flags & (RC_VALUES | RC_CONFUSION)) ? 1 : 0;
   const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
@@ -1235,7 +1239,7 @@ int rc_bwd_merged_grid(const StepCtx& c) {
 int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (c.defer != 1 || (c.flags & RC_VALUES)) { rc_set_error("merged backward: needs defer == 1 and no values"); return REDCLIFF_EINVAL; }
-  const size_t le = rc_emb_bwd_lds(d), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
+  const size_t le = rc_emb_bwd_lds(d, false), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
   const size_t lds = le > lf ? le : lf;
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("merged backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   const int Q = d.p * d.L;
