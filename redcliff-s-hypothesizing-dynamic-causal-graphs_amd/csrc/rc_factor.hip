@@ -29,6 +29,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
 
 }  // namespace
 
+// The vector factor backward stages per-window terms of the whole batch in LDS; past the
+// 64 KiB budget (large K * Bmax) the matrix-core path, which tiles the windows, takes over.
+bool rc_fac_vector_fits(const RedcliffDims& d) {
+  return (size_t)fac_bwd_lds_floats(d) <= (size_t)RC_LDS_LIMIT_FLOATS;
+}
+
 int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int Q = d.p * d.L;

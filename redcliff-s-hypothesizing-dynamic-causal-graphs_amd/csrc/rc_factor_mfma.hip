@@ -656,13 +656,15 @@ size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
 // search: D4IC R = 32 runs 4.2 M -> 5.5 M windows/s, while a single D4IC fit is faster on the
 // latency-shaped vector kernels, 1.31 M vs 0.92 M).  REDCLIFF_FAC_PATH=mfma|vector overrides
 // (tests, tuning).
+bool rc_fac_vector_fits(const RedcliffDims& d);  // rc_factor.hip
+
 bool rc_fac_use_mfma(const RedcliffDims& d) {
   const char* v = getenv("REDCLIFF_FAC_PATH");  // read per call: tests switch paths in-process
   const int env = !v ? 0 : (!strcmp(v, "mfma") ? 1 : (!strcmp(v, "vector") ? 2 : 0));
   if (d.h > 128) return false;
   if (env == 1) return true;
   if (env == 2) return false;
-  return (d.p * d.L >= 256 && d.h <= 32) || d.R >= 8;
+  return (d.p * d.L >= 256 && d.h <= 32) || d.R >= 8 || !rc_fac_vector_fits(d);
 }
 
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {

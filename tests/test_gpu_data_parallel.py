@@ -114,3 +114,27 @@ def test_two_rank_data_parallel_matches_full_batch(tmp_path):
         bad = np.abs(got - w) > tol
         assert not bad.any(), "%s: %d/%d off, max err %.3e" % (k, int(bad.sum()), w.size, np.abs(got - w).max())
     np.testing.assert_array_equal(r0["conf"].numpy(), conf)
+
+
+def test_large_shard_takes_the_matrix_core_factor_path(monkeypatch):
+    """512 windows per step at the TST shape exceed the vector factor backward's 64 KiB LDS
+    budget (it stages per-window terms of the whole batch); the step then runs the matrix-core
+    factor path instead of failing -- the same bits as forcing that path."""
+    c = CFG
+    rng = np.random.RandomState(3)
+    X = torch.from_numpy(rng.randn(512, c["T"], c["p"]).astype(np.float32))
+    Y = torch.zeros(512, c["K"], c["T"])
+    Y[torch.arange(512), torch.from_numpy(rng.randint(0, c["K"], 512))] = 1.0
+    out = []
+    for path in (None, "mfma"):
+        if path is None:
+            monkeypatch.delenv("REDCLIFF_FAC_PATH", raising=False)
+        else:
+            monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+        m, oA, oB = _model()
+        for ep in (0, 1, 2):  # pretrain, acclimate, combined
+            m.batch_update(ep, 0, X, Y, oA, oB, 1)
+        torch.cuda.synchronize()
+        out.append(dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items()))
+    for k in out[0]:
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
