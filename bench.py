@@ -146,14 +146,39 @@ def adam_pair(m, c):
     return oA, oB
 
 
-def cpu_threads():
-    return int(os.environ.get("REDCLIFF_CPU_THREADS", min(16, os.cpu_count() or 1)))
+def host_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup CPU quota
+    when one is set (cgroup v2 cpu.max / v1 cfs_quota) -- os.cpu_count() reports the whole
+    machine even where a job gets a share of it."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = float(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(np.ceil(quota))))
+    return int(os.environ.get("REDCLIFF_CPU_THREADS", n))
 
 
-def cpu_baseline(c, seconds):
-    """The oracle (CPU restatement keeping the reference's op structure) on the host cores."""
+def _oracle_rate(c, threads, seconds):
+    """Combined-phase batch_updates of the oracle on `threads` threads for ~`seconds`:
+    (steps, elapsed seconds)."""
     from oracle.redcliff_oracle import OracleREDCLIFF
-    threads = cpu_threads()
     torch.set_num_threads(threads)
     m = build_model(OracleREDCLIFF, c, seed=0)
     oA, oB = adam_pair(m, c)
@@ -165,32 +190,63 @@ def cpu_baseline(c, seconds):
         Xb, Yb = bs[n % len(bs)]
         m.batch_update(2, n, Xb, Yb, oA, oB, 1)
         n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * c["B"] / dt, 2), "unit": "windows/s", "cores": threads,
-            "host_cpu_count": os.cpu_count(), "kind": "port",
-            "sample": "%d combined-phase batch_updates of B=%d (%.1f s) with oracle/redcliff_oracle.py "
-                      "(reference op structure: per-sample loops, autograd, torch.optim.Adam) on %d threads "
-                      "(os.cpu_count() = %s on this host)" % (n, c["B"], dt, threads, os.cpu_count())}
+    return n, time.perf_counter() - t0
 
 
-def cpu_fit_step_seconds(c, seconds):
-    """One combined-phase batch_update of the oracle on ONE thread (the reference's CPU grid
-    search runs one fit per core with torch.set_num_threads(1))."""
-    from oracle.redcliff_oracle import OracleREDCLIFF
+def cpu_baseline(c, seconds):
+    """The oracle (CPU restatement keeping the reference's op structure) on the host cores, at
+    1 / 8 / 16 / all threads (the best rate is the baseline; all rates are reported)."""
+    cores = host_cores()
+    counts = sorted(set(t for t in (1, 8, 16, cores) if t <= cores))
     prev = torch.get_num_threads()
-    torch.set_num_threads(1)
+    rates = {}
     try:
-        m = build_model(OracleREDCLIFF, c, seed=0)
-        oA, oB = adam_pair(m, c)
-        X, Y = synth(c, c["B"], seed=1)
-        m.batch_update(2, 0, X, Y, oA, oB, 1)
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < seconds:
-            m.batch_update(2, n, X, Y, oA, oB, 1)
-            n += 1
-        return (time.perf_counter() - t0) / n
+        for t in counts:
+            n, dt = _oracle_rate(c, t, seconds / len(counts))
+            rates[t] = (n * c["B"] / dt, n, dt)
     finally:
         torch.set_num_threads(prev)
+    best = max(rates, key=lambda t: rates[t][0])
+    v, n, dt = rates[best]
+    return {"value": round(v, 2), "unit": "windows/s", "cores": best, "host_cpu_count": os.cpu_count(),
+            "host_cores_available": cores, "kind": "port",
+            "by_threads": dict((str(t), round(r[0], 2)) for t, r in rates.items()),
+            "sample": "%d combined-phase batch_updates of B=%d (%.1f s) with oracle/redcliff_oracle.py (reference op "
+                      "structure: per-sample loops, autograd, torch.optim.Adam); best of %s threads = %d "
+                      "(%d CPUs available to this job; os.cpu_count() = %s)"
+                      % (n, c["B"], dt, "/".join(str(t) for t in counts), best, cores, os.cpu_count())}
+
+
+def _cpu_fit_worker(c, seconds, q):
+    torch.set_num_threads(1)
+    n, dt = _oracle_rate(c, 1, seconds)
+    q.put((n, dt))
+
+
+def cpu_fits_per_hour(c, seconds, steps_per_fit):
+    """The reference's CPU grid search: one fit per core, each single-threaded
+    (torch.set_num_threads(1)).  P concurrent one-thread oracle processes (P =
+    the CPUs available to this job) run combined-phase batch_updates for ~`seconds`; the
+    aggregate step rate over all of them gives fits/hour (training steps only)."""
+    import multiprocessing as mp
+    P = host_cores()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_cpu_fit_worker, args=(c, seconds, q)) for _ in range(P)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+    steps = sum(n for n, _ in res)
+    wall = max(dt for _, dt in res)
+    rate = steps / wall  # aggregate steps per second over the P processes
+    return {"value": round(rate * 3600.0 / steps_per_fit, 2), "unit": "fits/hour", "cores": P,
+            "host_cpu_count": os.cpu_count(), "kind": "port",
+            "sample": "%d concurrent single-thread oracle processes (one fit per core, the reference's grid), "
+                      "%d combined-phase batch_updates of B=%d in %.1f s in all (%.3f s per step per process) x %d "
+                      "training steps per fit; validation and GC tracking NOT counted, so this over-states the CPU "
+                      "rate" % (P, steps, c["B"], wall, P * wall / max(steps, 1), steps_per_fit)}
 
 
 def hbm_roofline(c, eng, ms_per_step, ktimes_roof):
@@ -399,6 +455,19 @@ def mode_fit(args, dev, rank, world, dist):
     if args.fit_replicas > 0:
         fph = fits_per_hour(c, args, dev, rank, dist, world)
 
+    dpl = None
+    if args.dp_leg_batch > 0 and dist is not None:
+        # configs[3] beside the replica numbers: ONE TST-shaped fit data-parallel over all ranks
+        # (global batch --dp-leg-batch, RCCL all-reduce of the flat gradient per update), so the
+        # driver's 1 -> 8 GPU runs record both scaling regimes
+        dsteps = max(20, min(args.steps, 200))
+        del_, dpo = dp_throughput(args.dp_leg_batch, dsteps, 5, dev, dist)
+        dpl = {"global_batch": args.dp_leg_batch, "windows_per_shard": args.dp_leg_batch // world, "ranks": world,
+               "updates": dsteps, "windows_per_s": round(dsteps * args.dp_leg_batch / del_, 1),
+               "ms_per_update": round(1e3 * del_ / dsteps, 4), "scaling": "strong",
+               "allreduce_floats_per_update": int(dpo.PA + dpo.PB),
+               "workload": CONFIGS["c4"]["workload"].replace("B=128", "global B=%d" % args.dp_leg_batch)}
+
     ns = None
     if world == 1 and not args.no_north_star and args.config != "c1k4":
         cn = CONFIGS["c1k4"]
@@ -416,19 +485,13 @@ def mode_fit(args, dev, rank, world, dist):
     out["roofline_hbm"] = hbm_roofline(c, eng, 1e3 * elapsed / args.steps, out.get("roofline"))
     out["grid_search"] = grid
     out["fits_per_hour"] = fph
+    out["data_parallel"] = dpl
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds)
         out["gpu_over_cpu"] = round(value / world / out["cpu_baseline"]["value"], 1)
         if fph is not None:
-            t1 = cpu_fit_step_seconds(c, args.cpu_seconds / 3.0)
-            cores = cpu_threads()
-            cpu_fit_s = fph["epochs_per_fit"] * (fph["train_windows"] // B) * t1
-            fph["cpu_baseline"] = {
-                "value": round(cores * 3600.0 / cpu_fit_s, 2), "unit": "fits/hour", "cores": cores,
-                "host_cpu_count": os.cpu_count(), "kind": "port",
-                "sample": "one-thread oracle combined-phase batch_update (%.3f s each) x %d training steps per fit, "
-                          "one fit per core; validation and GC tracking NOT counted, so this over-states the CPU "
-                          "rate" % (t1, fph["epochs_per_fit"] * (fph["train_windows"] // B))}
+            fph["cpu_baseline"] = cpu_fits_per_hour(c, args.cpu_seconds / 2.0,
+                                                    fph["epochs_per_fit"] * (fph["train_windows"] // B))
             fph["gpu_over_cpu"] = round(fph["value"] / world / fph["cpu_baseline"]["value"], 1)
         if ns is not None:
             ns["cpu_baseline"] = cpu_baseline(CONFIGS["c1k4"], args.cpu_seconds * 2.0 / 3.0)
@@ -437,26 +500,31 @@ def mode_fit(args, dev, rank, world, dist):
     return out
 
 
-def mode_dp(args, dev, rank, world, dist):
-    """BASELINE configs[3]: one TST-shaped fit sharded over the ranks (DataParallelFit)."""
+def dp_throughput(B, steps, warmup, dev, dist):
+    """BASELINE configs[3]: one TST-shaped fit sharded over the ranks (DataParallelFit), global
+    batch B per update: (elapsed seconds for `steps` combined-phase updates, the DataParallelFit)."""
     import redcliff_amd
     from redcliff_amd.data_parallel import DataParallelFit
-    c = dict(CONFIGS["c4"], B=args.dp_batch)
-    B = c["B"]
+    c = dict(CONFIGS["c4"], B=B)
     model = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).to(dev)
     oA, oB = adam_pair(model, c)
     nbatch = 16
     X, Y = synth(c, nbatch * B, seed=100)  # every rank holds the whole (identical) data set
     dp = DataParallelFit(model, oA, oB)
     ds = dp.cache_dataset([(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)])
-    epoch = model.num_pretrain_epochs + model.num_acclimation_epochs  # combined phase
 
     def run(n, start):
-        return lambda: [dp._step("combined", ds, (start + i) % nbatch) for i in range(n)]
+        return lambda: dp.run_steps("combined", ds, [(start + i) % nbatch for i in range(n)])
 
-    run(args.warmup, 0)()
-    elapsed = timed(run(args.steps, args.warmup), dist, dev)
-    del epoch
+    run(warmup, 0)()
+    return timed(run(steps, warmup), dist, dev), dp
+
+
+def mode_dp(args, dev, rank, world, dist):
+    """BASELINE configs[3]: one TST-shaped fit sharded over the ranks (DataParallelFit)."""
+    c = dict(CONFIGS["c4"], B=args.dp_batch)
+    B = c["B"]
+    elapsed, dp = dp_throughput(B, args.steps, args.warmup, dev, dist)
     if rank != 0:
         return None
     value = args.steps * B / elapsed
@@ -486,6 +554,23 @@ def mode_plumbing(args, rank, world, dist):
             "data": "none: no GPU visible, rank plumbing check only (backend %s)" % ("gloo" if dist else "none"),
             "config": {"workload": CONFIGS["c4" if args.mode == "dp" else args.config]["workload"], "ranks": world,
                        "parallelism": ("dp%d" if args.mode == "dp" else "replicas%d") % world}}
+
+
+def rank_devices(dist, rank, local, world, dev):
+    """[{rank, local_rank, device, name, pci}] of every rank (all-gathered), so the record shows
+    which GPU each rank ran on."""
+    if dev is None:  # the CPU plumbing check: no device, the process identifies the rank
+        me = {"rank": rank, "local_rank": local, "device": "cpu", "pid": os.getpid()}
+    else:
+        props = torch.cuda.get_device_properties(dev)
+        me = {"rank": rank, "local_rank": local, "device": dev.index, "name": props.name,
+              "pci": "%s:%s:%s" % (getattr(props, "pci_domain_id", "?"), getattr(props, "pci_bus_id", "?"),
+                                   getattr(props, "pci_device_id", "?"))}
+    if dist is None or world == 1:
+        return [me]
+    allr = [None] * world
+    dist.all_gather_object(allr, me)
+    return allr
 
 
 # --------------------------------------------------------------------------- launch
@@ -527,16 +612,20 @@ def main():
     ap.add_argument("--fit-epochs", type=int, default=40)
     ap.add_argument("--fit-train-batches", type=int, default=8)
     ap.add_argument("--dp-batch", type=int, default=128, help="global batch of --mode dp")
+    ap.add_argument("--dp-leg-batch", type=int, default=1024,
+                    help="global batch of the data-parallel leg of --mode fit (0: skip)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import __graft_entry__
+        __graft_entry__.build()  # once, in the parent (compiling touches no GPU); the ranks find it current
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
     dist = None
-    if world > 1 or args.mode == "dp":
+    if world > 1 or args.mode == "dp" or args.dp_leg_batch > 0:
         import torch.distributed as dist
         backend = "nccl" if cuda else "gloo"  # nccl is RCCL on ROCm; gloo only for the CPU plumbing check
         if cuda:
@@ -552,8 +641,11 @@ def main():
             raise SystemExit("%s world size %d != --gpus %d / WORLD_SIZE %d" % (backend, seen, args.gpus, world))
         world = seen
     if not cuda:
+        devices = rank_devices(dist, rank, local, world, None)
         out = mode_plumbing(args, rank, world, dist)
         if out is not None:
+            out["config"]["rank_devices"] = devices
+            out["config"]["world_size"] = world
             print(json.dumps(out), flush=True)
         if dist:
             dist.destroy_process_group()
@@ -561,11 +653,18 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    if world == 1:
+    # the library is built in-tree (a no-op when current); under an external launcher only the
+    # first local rank builds while the others wait, so no two ranks write the .so at once
+    if local == 0:
         import __graft_entry__
-        __graft_entry__.build()  # no-op when the in-tree library is up to date
+        __graft_entry__.build()
+    if dist is not None:
+        dist.barrier()
+    devices = rank_devices(dist, rank, local, world, dev)
     out = (mode_dp if args.mode == "dp" else mode_fit)(args, dev, rank, world, dist)
     if out is not None:
+        out["config"]["rank_devices"] = devices
+        out["config"]["world_size"] = world
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

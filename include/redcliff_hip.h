@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 5
+#define REDCLIFF_ABI_VERSION 6
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -172,6 +172,14 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
  * y[nU][Bmax][K][p] over 16-unit hidden chunks), xsim (mixed forecast), G / G0 (group norms)
  * back from a step run with RC_STORE_OUTPUTS. */
 int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out);
+
+/* Device status of the R replica slices of a workspace (no reference counterpart: the
+ * reference has no device code).  out[r] (host array of R u32) receives replica r's count of
+ * merged-backward hand-off waits that ran out of polls since the last call (the consumer then
+ * proceeded without its producers' records, so that step's results are invalid); the words are
+ * cleared.  Synchronises `stream`.  Returns the number of replicas with a non-zero count (0 =
+ * healthy) or a negative error code.  Callers check it where they already synchronise. */
+int redcliff_device_status(const RedcliffDims* d, void* ws, uint32_t* out, void* stream);
 
 /* Verification mode (tests only; no reference counterpart): with floats > 0 every workspace
  * region laid out afterwards is followed by a guard band of that many floats, the last band

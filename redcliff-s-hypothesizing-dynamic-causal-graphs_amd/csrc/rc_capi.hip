@@ -136,10 +136,26 @@ int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out
   if (check_dims(d) != 0) return REDCLIFF_EINVAL;
   const WsOff o = rc_ws_off(*d);
   const int64_t v[] = {o.T, o.R, o.f1, o.w, o.a, o.y, o.G, o.G0, o.w1, o.gq, o.ebp, o.ecnt, o.gfc1, o.dwp, o.dAadj, o.dWi, o.dS, o.dgb, o.S, o.dZ,
-                       o.amat, o.lossp, o.xsim, o.gfc, o.xw, o.dyl, o.dgs, o.total};
+                       o.amat, o.lossp, o.xsim, o.gfc, o.xw, o.dyl, o.dgs, o.errw, o.total};
   const int nv = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n_out && i < nv; ++i) out[i] = v[i];
   return nv;
+}
+
+int redcliff_device_status(const RedcliffDims* d, void* ws, uint32_t* out, void* stream) {
+  if (check_dims(d) != 0 || !ws || !out) { rc_set_error("device_status: bad arguments"); return REDCLIFF_EINVAL; }
+  const WsOff o = rc_ws_off(*d);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t pitch = sizeof(float) * (size_t)o.total;
+  char* base = (char*)ws + sizeof(float) * (size_t)o.errw;
+  int e = rc_check(hipMemcpy2DAsync(out, sizeof(uint32_t), base, pitch, sizeof(uint32_t), (size_t)d->R,
+                                    hipMemcpyDeviceToHost, s), "device_status copy");
+  if (!e) e = rc_check(hipMemset2DAsync(base, pitch, 0, sizeof(uint32_t), (size_t)d->R, s), "device_status clear");
+  if (!e) e = rc_check(hipStreamSynchronize(s), "device_status sync");
+  if (e) return e;
+  int bad = 0;
+  for (int r = 0; r < d->R; ++r) bad += out[r] != 0;
+  return bad;
 }
 
 // Verification mode: guard bands of `floats` floats after every workspace region (0 = off,
@@ -274,6 +290,11 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   int e = make_ctx(a, c);
   if (e) return e;
   if (c.nrep == 0) return 0;  // every replica of the pack has stopped
+  static const bool wait_dbg = [] {
+    const char* v = getenv("REDCLIFF_DEBUG_WAIT_TIMEOUT");
+    return v && strcmp(v, "0") != 0;
+  }();
+  c.wait_dbg = wait_dbg;
   hipStream_t s = (hipStream_t)stream;
   const int fl = a->flags;
   const bool emb_grad = fl & RC_STEP_A;

@@ -55,6 +55,9 @@ struct WsOff {
   int64_t eAf;    // [p][p*n]          [S_0^T | ... | S_{n-1}^T] interleaved (GEMM embedder)
   int64_t edr;    // [Bmax][K]         dL/d(raw embedder output) (GEMM embedder)
   int64_t cosb;   // [Bmax] doubles    per-window cosine-similarity penalty values
+  int64_t errw;   // [16] u32          device status words, never reset by a kernel: [0] counts the
+                  //                   merged backward's hand-off waits that timed out (rc_wait_count);
+                  //                   read and cleared by redcliff_device_status
   int64_t total;
 };
 
@@ -202,6 +205,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.eAf, p * p * d.n);
   put(o.edr, B * K);
   put(o.cosb, 2 * B);
+  put(o.errw, 16);
 #ifdef RC_TRACE
   x += RC_TRACE_FLOATS;  // phase-timing slots at the end of the workspace (trace builds only)
 #endif
@@ -256,6 +260,9 @@ struct StepCtx {
   // rident: all R in order; else the active list of a packed fit whose stopped replicas
   // (early stopping, ...withStateSmoothing.py:1483-1559) drop out of every grid.
   int nrep, rident;
+  // debug (REDCLIFF_DEBUG_WAIT_TIMEOUT=1): the merged backward's consumers wait for one more
+  // producer than exists, with a short poll bound -- forces the timeout path (tests)
+  int wait_dbg;
   uint8_t rmap[RC_MAX_ACTIVE];
 };
 
@@ -272,6 +279,7 @@ inline int rc_rep_host(const StepCtx& c, int i) { return rc_rep(c, i); }
 #define RC_KID_EMB_BWD 3
 #define RC_KID_EMB_FINAL 4
 #define RC_KID_FAC_MIX 5
+#define RC_KID_EMB_WAIT 7  // merged backward: a node workgroup's hand-off wait returned (start slot only)
 #ifdef RC_TRACE
 #define RC_WG_MARK(wsbase, total, kid, end)                                                        \
   do {                                                                                            \
@@ -306,7 +314,10 @@ inline int rc_rep_host(const StepCtx& c, int i) { return rc_rep(c, i); }
 // an sc1 load (agent-scope relaxed atomic load), so no acquire fence / L1 invalidate is needed --
 // only a compiler barrier keeps the loads below the poll.  Producers have lower workgroup ids than
 // their consumers and never wait, so they are dispatched first and finish (no co-residency
-// assumption); the bounded poll means a missing producer cannot hang the GPU.
+// assumption); the bounded poll means a missing producer cannot hang the GPU.  A poll that runs
+// out is NOT silent: it counts itself into the replica's status word (WsOff.errw, a vector
+// atomic), the host reads the words back (redcliff_device_status) and the Python side raises
+// instead of using the step's results.
 __device__ inline void rc_store_sc1(float* p, float v) {
   __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -328,12 +339,19 @@ __device__ inline void rc_publish(unsigned* cnt) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ inline void rc_wait_count(const unsigned* cnt, unsigned target) {
+#define RC_WAIT_POLLS (1u << 24)      // ~1 s of s_sleep(2) polls
+#define RC_WAIT_POLLS_DBG (1u << 12)  // the forced-timeout debug mode
+
+__device__ inline void rc_wait_count(const unsigned* cnt, unsigned target, unsigned* status, unsigned polls) {
   if (threadIdx.x == 0) {
     unsigned spins = 0;
-    while (__hip_atomic_load(const_cast<unsigned*>(cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-           ++spins < (1u << 24))
+    while (__hip_atomic_load(const_cast<unsigned*>(cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins >= polls) {
+        __hip_atomic_fetch_add(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
       __builtin_amdgcn_s_sleep(2);
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler barrier only: payload loads are sc1
   __syncthreads();
@@ -342,6 +360,11 @@ __device__ inline void rc_wait_count(const unsigned* cnt, unsigned target) {
 // the merged backward's factor-lead counter of replica slice `ws`
 __device__ inline unsigned* rc_fac_lead_cnt(const StepCtx& c, float* ws) {
   return reinterpret_cast<unsigned*>(ws + c.wo.ecnt) + c.d.p * ((c.d.H + EMB_HC - 1) / EMB_HC);
+}
+// a consumer of the merged backward waits for `target` published factor leads of replica slice ws
+__device__ inline void rc_wait_leads(const StepCtx& c, float* ws, const unsigned* cnt, unsigned target) {
+  rc_wait_count(cnt, target + (c.wait_dbg ? 1u : 0u), reinterpret_cast<unsigned*>(ws + c.wo.errw),
+                c.wait_dbg ? RC_WAIT_POLLS_DBG : RC_WAIT_POLLS);
 }
 
 __device__ inline float rc_wave_sum(float v) {

@@ -276,7 +276,10 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   float* xc = late_x ? f1r : dTc + BC * nF;  // [BC][p][F] raw window (late: over f1r .. Tc)
 
   const RcDiv dF(F), dp(p), dpF(pF), dnF(nF), dK(K), dM1(M1);
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 33);
+  // trace builds: the node workgroup's own index (inside the merged launch the factor leads come first)
+  const int pbx = wait_cnt ? (int)blockIdx.x - d.K * d.p : (int)blockIdx.x;
+  (void)pbx;
+  RC_PHASE(c.ws, c.wo.total, pbx, 33);
   bn_affine(c, r, E, alpha, beta, mean, inv);
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
@@ -371,7 +374,8 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
           }, [&](int e, float v) { Srow[e] = v; }),
           sR, sT, sX, sF1, sW, sL);
       if (wait_now) {
-        rc_wait_count(wait_cnt, wait_target);
+        rc_wait_leads(c, c.ws + r * c.wss, wait_cnt, wait_target);
+        RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_WAIT, 0);
         dw_load(0);
       }
       dw_store(0);
@@ -394,7 +398,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       }
       __syncthreads();
     }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 34);
+  RC_PHASE(c.ws, c.wo.total, pbx, 34);
     for (int e = tid; e < nbc * K; e += RC_BLOCK) dr[e] = draw_value(c, r, dK.mod(e), wrl[e], dwl[e], labl[e]);
     __syncthreads();
     // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
@@ -406,7 +410,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       df1c[e] = g;
     }
     __syncthreads();
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 35);
+  RC_PHASE(c.ws, c.wo.total, pbx, 35);
     // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
     for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
       const int s = e / HC, hh = e - s * HC;
@@ -452,7 +456,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       }
     }
     __syncthreads();
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 36);
+  RC_PHASE(c.ws, c.wo.total, pbx, 36);
     // dW_i chunk partial: awi[i][f][hh] += sum_s T_i[s][f] dZ[s][hh]
     for (int s = 0; s < nbc; ++s) {
 #pragma unroll
@@ -479,7 +483,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       rc_stage_all(rc_seg<16>(nbc * pF, x_ld, x_st));
       __syncthreads();
     }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 37);
+  RC_PHASE(c.ws, c.wo.total, pbx, 37);
     // dS_i[node][c'] (i >= 1) and BatchNorm affine partials, windows split over thread slices
     if (slS < nslS) {
       const int i = 1 + oS / p, cp = oS - (i - 1) * p;
@@ -509,7 +513,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       }
     }
   }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 38);
+  RC_PHASE(c.ws, c.wo.total, pbx, 38);
   // ---- publish this block's partials:
   //      [grp][wb][ afc M1*HC | awi nF*HC | dS nS | dgamma F | dbeta F | (group 0) dfc2W dfc2b dfc1b ]
   const int pst = rc_emb_pstride(d);
@@ -555,7 +559,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
     part[ofs_g + F + tid] = t;
   }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 39);
+  RC_PHASE(c.ws, c.wo.total, pbx, 39);
   if (c.defer) {  // k_emb_combine sums the window blocks after this kernel (no ticket / fences)
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
     return;
@@ -574,7 +578,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
     return;
   }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 40);
+  RC_PHASE(c.ws, c.wo.total, pbx, 40);
   // ---- last arriver: acquire, then combine the nbw partials in window-block order
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -612,7 +616,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       ws[c.wo.gfc + (e - ofs_h)] = t;                    // dfc2W | dfc2b | dfc1b
     }
   });
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 41);
+  RC_PHASE(c.ws, c.wo.total, pbx, 41);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
 }
 
@@ -721,8 +725,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int
   const int nemb = nnode + head + nred;
   const int e = bx - KP;
   if (e >= 0 && e < nemb) {
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
     if (e >= nnode + head) {
-      rc_wait_count(cnt, KP);
+      rc_wait_leads(c, c.ws + r * c.wss, cnt, KP);
       emb_bwd_dadj(c, r, e - nnode - head, true);
     } else if (e == nnode) {
       emb_bwd_head(c, r, sm);
@@ -1210,9 +1215,28 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
 
 // Workgroups of the merged launch, or 0 when it should not be used: the embedder side must be
 // the single-sub-block variant (the multi-sub-block one needs 256 VGPRs), and the whole grid
-// must fit the chip at once at the merged kernel's occupancy (174 VGPRs: 2 workgroups of 256
-// lanes per CU) -- otherwise the factor body's register budget throttles the embedder
-// workgroups and the two launches are faster (C1(K=4): 81 us merged vs 29 + 41 us).
+// must be resident at once at the merged kernel's occupancy, as the runtime computes it from
+// the kernel's VGPRs and this launch's LDS (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs;
+// 174 VGPRs -> 2 workgroups of 256 lanes per CU at D4IC).  Residency is the performance
+// condition (otherwise the factor body's register budget throttles the embedder workgroups and
+// the two launches are faster: C1(K=4) 81 us merged vs 29 + 41 us) and the safety margin of
+// the hand-off: with every workgroup resident no waiting consumer can hold a slot a producer
+// needs, even if dispatch order were not monotone.  (Producers precede consumers in workgroup
+// order and never wait, so in-order dispatch alone already guarantees progress; a poll that
+// still runs out is reported through the status word, rc_wait_count.)
+static int rc_bwd_merged_occupancy(size_t lds) {
+  static thread_local size_t cached_lds = (size_t)-1;
+  static thread_local int cached = 0;
+  if (lds == cached_lds) return cached;
+  int nb = 0;
+  if (rc_lds_optin(k_bwd_merged<false>, lds, "k_bwd_merged LDS") != 0 ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_bwd_merged<false>, RC_BLOCK, lds) != hipSuccess)
+    nb = 0;
+  cached_lds = lds;
+  cached = nb;
+  return nb;
+}
+
 int rc_bwd_merged_grid(const StepCtx& c) {
   const RedcliffDims& d = c.d;
   if (rc_emb_wpb(d) > rc_emb_bc(d)) return 0;
@@ -1231,7 +1255,9 @@ int rc_bwd_merged_grid(const StepCtx& c) {
   const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
   const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
   const int grid = d.K * d.p * nUl * nQ + nnode + head + nred;
-  return (int64_t)grid * c.nrep <= 2 * (int64_t)cus ? grid : 0;
+  const size_t le = rc_emb_bwd_lds(d, false), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
+  const int occ = rc_bwd_merged_occupancy(le > lf ? le : lf);
+  return (int64_t)grid * c.nrep <= (int64_t)occ * cus ? grid : 0;
 }
 
 // The merged backward (k_bwd_merged); requires the deferred combine (c.defer == 1) and no

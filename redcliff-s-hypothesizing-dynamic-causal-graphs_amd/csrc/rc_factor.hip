@@ -40,7 +40,16 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
   const int Q = d.p * d.L;
   const int nQ = (c.flags & RC_STEP_B) ? (Q + FB_QT - 1) / FB_QT : 1;
   const size_t lds = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
-  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
+    // only reached when the matrix-core path cannot take over (h > 128) or is overridden
+    // (REDCLIFF_FAC_PATH=vector): name the batch limit instead of a bare launch failure
+    RedcliffDims e = d;
+    while (e.Bmax > 1 && (size_t)fac_bwd_lds_floats(e) > (size_t)RC_LDS_LIMIT_FLOATS) --e.Bmax;
+    const char* why = d.h > 128 ? "the matrix-core factor path supports h <= 128" : "REDCLIFF_FAC_PATH=vector is set";
+    rc_set_error("vector factor backward: batches of %d windows with K=%d, h=%d need %zu KiB of LDS (64 KiB budget): "
+                 "use batches of at most %d windows (%s)", d.Bmax, d.K, d.h, lds / 1024, e.Bmax, why);
+    return REDCLIFF_ELIMIT;
+  }
   // without a factor update only the lead workgroup of each network has work
   const int nUl = (c.flags & RC_STEP_B) ? rc_nuchunk(d) : 1;
   hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ);

@@ -7,9 +7,11 @@ or does not export the expected ABI, so a broken build fails loudly.
 import ctypes
 import os
 
+import torch
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
@@ -26,14 +28,14 @@ REFRESH_SUPPORTS = 1 << 10
 GRAD_ONLY = 1 << 11
 
 WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt", "gfc1", "dwp", "dAadj", "dWi", "dS", "dgb", "S", "dZ", "amat",
-              "lossp", "xsim", "gfc", "xw", "dyl", "dgs", "total")
+              "lossp", "xsim", "gfc", "xw", "dyl", "dgs", "errw", "total")
 
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
             "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm",
             "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions",
-            "redcliff_gc_track_stats")
+            "redcliff_gc_track_stats", "redcliff_device_status")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine")
 
 
@@ -120,6 +122,7 @@ def lib():
     L.redcliff_gc_track_stats.argtypes = [ctypes.c_int32, _i64, _vp, _vp, ctypes.c_int32, ctypes.c_int32, _i64, _vp,
                                           _vp, _vp]
     L.redcliff_debug_guard_bands.argtypes = [ctypes.c_int32]
+    L.redcliff_device_status.argtypes = [ctypes.POINTER(Dims), _vp, ctypes.POINTER(ctypes.c_uint32), _vp]
     L.redcliff_workspace_regions.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(_i64), ctypes.c_int32]
     for name in EXPORTED[2:]:
         if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count"):
@@ -142,6 +145,36 @@ def workspace_layout(dims):
     if n < 0:
         check(n, "workspace_layout")
     return dict(zip(WS_REGIONS, [int(v) for v in out]))
+
+
+def status_view(ws, ws_off, R):
+    """int32 device view [R] of the replica status words of a workspace (WsOff.errw)."""
+    return ws.as_strided((R,), (ws_off["total"],), ws_off["errw"]).view(torch.int32)
+
+
+def raise_on_status(words, view=None, where="step"):
+    """words: host copy of status_view (or redcliff_device_status's output).  Non-zero = a merged
+    backward consumer stopped waiting for its producers (rc_wait_count ran out of polls), so the
+    steps since the last check computed gradients from unwritten records: clear and raise."""
+    import numpy as np
+    w = np.asarray(words).reshape(-1)
+    bad = np.nonzero(w)[0]
+    if bad.size:
+        if view is not None:
+            view.zero_()
+        raise RuntimeError("redcliff device status (%s): %d merged-backward hand-off wait(s) timed out in replica(s) %s "
+                           "-- the affected training steps used unwritten gradient records; results are invalid "
+                           "(set REDCLIFF_MERGE=0 to run the two-launch backward)" % (where, int(w[bad].sum()),
+                                                                                     bad.tolist()))
+
+
+def device_status(dims, ws, stream):
+    """redcliff_device_status: read and clear the R status words (synchronises `stream`)."""
+    out = (ctypes.c_uint32 * int(dims.R))()
+    rc = lib().redcliff_device_status(ctypes.byref(dims), ws, out, stream)
+    if rc < 0:
+        check(rc, "device_status")
+    return [int(v) for v in out]
 
 
 def workspace_regions(dims):

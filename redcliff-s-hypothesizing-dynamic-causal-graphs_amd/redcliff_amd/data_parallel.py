@@ -101,7 +101,14 @@ class DataParallelFit:
         eng._after(flags, nbn, 1)
         eng.supports_fresh = False  # A moved after the step's own support refresh
 
-    def run_epoch(self, epoch, ds):
+    def run_steps(self, kind, ds, batches):
+        """Updates of one kind over the global batches `batches` (indices into ds), back to back:
+        everything is enqueued on the stream (the RCCL all-reduce included), the host never
+        waits."""
+        for bi in batches:
+            self._step(kind, ds, bi)
+
+    def run_epoch(self, epoch, ds, set_modes=True):
         """The batch_update phase of `epoch` (...withStateSmoothing.py:741-759) over every global
         batch of `ds`, sharded over the ranks."""
         kinds = phase_of_epoch(self.model, epoch)
@@ -109,7 +116,45 @@ class DataParallelFit:
         for bi in range(int(ds["len"])):
             for kind in kinds:
                 self._step(kind, ds, bi)
-        self.model._set_module_modes(kinds[-1] if kinds else None)
+        if set_modes:
+            self.model._set_module_modes(kinds[-1] if kinds else None)
+
+    def fit(self, save_dir, X_train, output_length, max_iter, X_val, lookback=5, check_every=50, verbose=1, GC=None,
+            deltaConEps=0.1, in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=1.,
+            stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., save_plots=False):
+        """The reference's whole ``fit`` (models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647)
+        with every training epoch sharded over the ranks:
+
+          * training: run_epoch (one RCCL all-reduce of the flat gradient per update), then the
+            epoch's factor-score confusion matrix summed over the ranks (:786-803, :1344-1364);
+          * everything after the training steps of an epoch -- GC tracking on the first
+            validation batch (:1366-1414), validate_training (:1416-1480), the stopping rule
+            (:1482-1559), best-model snapshots, restore_parameters (:1621) and the final
+            validation -- is the single fit's device-side epoch (fit_loop._device_epochs) run
+            on EVERY rank: every rank holds the same parameters (bit-identical after each
+            replicated Adam step) and the same validation windows, so every rank computes the
+            same values with the same fixed-order kernels and takes the same decisions without
+            a collective (tests/test_gpu_data_parallel.py checks the ranks end bit-identical);
+          * checkpoints and the final model file are written by rank 0 only.
+        The next epoch trains speculatively while the host digests the current one, exactly as in
+        the single fit (undone on every rank when the fit stops).  Returns what fit returns;
+        model.fit_history holds the histories."""
+        from .fit_loop import run_fit
+        m = self.model
+        if "Freeze" in m.training_mode or "pretrain_factor" in m.training_mode:
+            raise NotImplementedError("the data-parallel fit runs the published schedule (pretrain embedder, "
+                                      "acclimate, combined); got training_mode=%s" % m.training_mode)
+        ds = self.cache_dataset(X_train)
+
+        def runner(epoch):
+            self.run_epoch(epoch, ds, set_modes=False)
+            if self.eng.nsup > 0:
+                dist.all_reduce(self.eng.conf, op=dist.ReduceOp.SUM, group=self.group)
+
+        return run_fit(m, save_dir, X_train, self.oA, self.oB, output_length, max_iter, X_val, lookback, check_every,
+                       verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, (None, "CosineSimilarity", 0, 10),
+                       stopping_criteria_forecast_coeff, stopping_criteria_factor_coeff,
+                       stopping_criteria_cosSim_coeff, save_plots, runner=runner, writer=self.rank == 0)
 
     def train_confusion(self):
         """Factor-score confusion matrix of the last epoch summed over ranks (:786-803)."""

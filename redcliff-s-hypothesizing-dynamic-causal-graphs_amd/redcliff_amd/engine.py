@@ -305,11 +305,28 @@ class FitEngine:
         return nat.Dims(R=1, Bmax=int(Bmax), T=int(T), p=self.p, L=self.L, K=self.K, h=self.h, F=self.F, n=self.n,
                         H=self.H, M1=M1, nsup=self.nsup, use_sigmoid=int(self.sig), sigmoid_ecc=self.ecc)
 
+    def status_view(self):
+        """int32 device view of this engine's workspace status word (WsOff.errw; see
+        _native.raise_on_status)."""
+        return nat.status_view(self.ws, self.ws_off, 1)
+
+    def raise_on_status(self, words, where):
+        nat.raise_on_status(words, self.status_view(), where)
+
+    def check_device_status(self, where="check"):
+        """Read the status word (synchronises) and raise if a merged-backward hand-off timed out
+        since the last check.  fit() checks once per epoch inside its single copy back,
+        validate_training after its copy back; callers driving batch_update themselves can
+        call model.check_device_status()."""
+        if self.ws is not None:
+            self.raise_on_status(self.status_view().cpu().numpy(), where)
+
     def workspace(self, Bmax, T):
         Bmax = max(int(Bmax), 1)
         if self.ws_dims is not None and self.ws_dims[0] >= Bmax:
             d = self.dims(self.ws_dims[0], T)
         else:
+            self.check_device_status("workspace growth")  # the old workspace's word would be lost
             d = self.dims(Bmax, T)
             nbytes = nat.lib().redcliff_workspace_bytes(ctypes.byref(d))
             if nbytes == 0:

@@ -30,6 +30,10 @@ HIST_KEYS = ["avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_pena
              "avg_fw_smoothing_penalty", "avg_adj_penalty", "avg_dagness_reg_loss", "avg_dagness_lag_loss",
              "avg_dagness_node_loss", "avg_combo_loss"]
 CM_KEYS = ("acc", "tpr", "tnr", "fpr", "fnr")
+# The reference's epoch loop re-binds these two history lists to [] before every validation
+# (...withStateSmoothing.py:1427-1428, redcliff_s_cmlp.py:1415-1416), so they only ever hold the
+# last epoch's value -- in fit_history and in every checkpoint (tests/golden/fit_*.npz).
+RESET_EACH_EPOCH = ("avg_dagness_lag_loss", "avg_dagness_node_loss")
 
 
 def standalone_copy(model):
@@ -214,6 +218,8 @@ class FitTracker:
         if not self.model._WITH_SMOOTHING:
             vals = vals[:4] + [0.0] + vals[4:]
         for k, v in zip(HIST_KEYS, vals):
+            if k in RESET_EACH_EPOCH:
+                self.h[k] = []
             self.h[k].append(v)
         self._vf, self._vfac = vals[0], vals[1]
 
@@ -376,14 +382,14 @@ def conditional_gc_estimates(w, G, G0, A, nsup, ls, mode):
     return est, nolag
 
 
-def run_fit(*args):
+def run_fit(*args, **kw):
     """fit() on the fused engine (see _run_fit).  The host side of an epoch is python; the cyclic
     garbage collector is paused for the fit (restored afterwards): its full passes over the model's
     module tree land inside epochs."""
     gc_was = gc.isenabled()
     gc.disable()
     try:
-        return _run_fit(*args)
+        return _run_fit(*args, **kw)
     finally:
         if gc_was:
             gc.enable()
@@ -462,7 +468,8 @@ class _SavedState:
 
 
 def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
-                   verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook):
+                   verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook, runner=None,
+                   writer=True):
     """fit()'s epochs on the fused engine with the per-epoch evaluation on the device.
 
     Per epoch the training steps are one prepared launch chain; the evaluation (train confusion
@@ -477,11 +484,16 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
     nsup, p = model.num_supervised_factors, model.num_chans
     Lm, ls = model.Lmax, min(model.gen_lag, model.embed_lag)
     saved = _SavedState(eng)
+    if runner is None:
+        def train_epoch(ep):
+            _train_epoch(model, eng, train, d_train, plans, oA, oB, ep)
+    else:
+        train_epoch = runner
     freeze = "Freeze" in model.training_mode  # the Freeze decision raises: no epoch runs ahead of it
     it = iter_start
     if it < max_iter:
         hook(it)
-        _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+        train_epoch(it)
     while it < max_iter:
         if verbose:
             print("REDCLIFF_S_CMLP_withStateSmoothing.fit: now on epoch it == ", it, flush=True)
@@ -498,15 +510,17 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
                 vals_d = M.gc_progress_values(GC, est_t, deltaConEps, in_degree_coeff, out_degree_coeff, host=False)
             l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
             acc_d, confv_d = eng.run_values(val["X"], val["lab"], d_train, val["rows"], val["sizes"], host=False)
-            pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] + ([vals_d] if vals_d is not None else []))
+            pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d, eng.status_view()] +
+                                    ([vals_d] if vals_d is not None else []))
         spec = (it + 1 < max_iter and not (save_dir is not None and it % check_every == 0) and not freeze
                 and it + 1 not in hook.at)
         if spec:
             saved.save()
-            _train_epoch(model, eng, train, d_train, plans, oA, oB, it + 1)
+            train_epoch(it + 1)
         got = pending.wait()
         cm, l1, dots, accs, confs = got[:5]
-        vals = got[5] if vals_d is not None else None
+        vals = got[6] if vals_d is not None else None
+        eng.raise_on_status(got[5], "fit epoch %d" % it)
         tr.train_confusion(cm.reshape(nsup, nsup) if nsup > 0 else None)
         l1, nrm, dots = M.track_values_finish(l1, dots)
         gc_progress_many([tr], None if vals is None else vals[None], l1[None], nrm[None], dots[None])
@@ -520,17 +534,17 @@ def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_star
             if verbose:
                 print("Stopping early")
             break
-        if it % check_every == 0 and save_dir is not None:
+        if it % check_every == 0 and save_dir is not None and writer:
             _eval_modes(model)
             tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
         it += 1
         if not spec and it < max_iter:
             hook(it)
-            _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+            train_epoch(it)
 
 
 def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_val, oA, oB, output_length, iter_start,
-                 max_iter, save_dir, check_every, verbose, save_plots, hook):
+                 max_iter, save_dir, check_every, verbose, save_plots, hook, runner=None, writer=True):
     """fit()'s epochs when the GC-progress metrics run on the host (the generic path, or GC
     modes / sizes outside the device metrics): the reference's loop (...withStateSmoothing.py:
     1316-1559) with the fused training steps where available."""
@@ -548,7 +562,11 @@ def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_v
                                    running_factor_score_confusion_matrix=cm if nsup > 0 else None)
             model._set_module_modes(kinds[-1] if kinds else None)  # the generic modules read their flags
         else:
-            _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+            if runner is not None:
+                runner(it)
+            else:
+                _train_epoch(model, eng, train, d_train, plans, oA, oB, it)
+            eng.check_device_status("fit epoch %d" % it)
             if nsup > 0:
                 cm = eng.conf.cpu().numpy().reshape(nsup, nsup)
         tr.train_confusion(cm if nsup > 0 else None)
@@ -578,7 +596,7 @@ def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_v
             if verbose:
                 print("Stopping early")
             break
-        if it % check_every == 0 and save_dir is not None:
+        if it % check_every == 0 and save_dir is not None and writer:
             tr.checkpoint(save_dir, it, optimizers=(oA, oB), save_plots=save_plots)
 
 
@@ -614,7 +632,9 @@ def _freeze_by_batch(model, fused, X_train, oA, oB, output_length, it):
 
 def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
              deltaConEps, in_degree_coeff, out_degree_coeff, prior, sc_forecast, sc_factor, sc_cos,
-             save_plots):
+             save_plots, runner=None, writer=True):
+    """runner(it), when given, trains epoch `it` in place of the fused single-fit epoch (the
+    data-parallel fit: redcliff_amd.data_parallel); writer=False: no files (ranks > 0)."""
     if output_length != 1:
         raise NotImplementedError("output_length must be 1")
     fused = model.fused_supported()
@@ -630,7 +650,7 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
             _freeze_by_batch(model, fused, X_train, oA, oB, output_length, iter_start)
     hook = _prior_hook(model, X_train, prior)
     ost = getattr(model, "chkpt_optimizer_state", None)
-    if ost is not None:  # this package's optimizer_state.pt next to the resumed checkpoint
+    if ost is not None:  # resume_training_from_checkpoint(..., load_optimizer_state=True)
         oA.load_state_dict(ost["A"])
         oB.load_state_dict(ost["B"])
         if fused:
@@ -647,16 +667,18 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
         "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
     if dev_metrics:
         _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
-                       verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook)
+                       verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook, runner=runner,
+                       writer=writer)
     else:
         _host_epochs(model, eng, tr, fused, train if fused else None, val if fused else None,
                      d_train if fused else None, plans if fused else None, X_train, X_val, oA, oB, output_length,
-                     iter_start, max_iter, save_dir, check_every, verbose, save_plots, hook)
+                     iter_start, max_iter, save_dir, check_every, verbose, save_plots, hook, runner=runner,
+                     writer=writer)
 
     if fused:
         _eval_modes(model)
     restore_parameters(model, tr.best_model)
-    if save_dir is not None:
+    if save_dir is not None and writer:
         torch.save(standalone_copy(model), os.path.join(save_dir, "final_best_model.bin"))
     if nsup > 0:
         final = model.validate_training(X_val, output_length, model.num_series, [], [], [], [], [])
@@ -684,8 +706,9 @@ def save_checkpoint(model, save_dir, it, best_model, avg_forecasting_loss, avg_f
     The model is saved as a standalone copy (its own parameter storage, not the pack's).
     With `optimizers` (fit passes its two Adams) a third file, optimizer_state.pt, holds their
     state: the reference does not checkpoint it (redcliff_s_cmlp.py:245), so a resumed
-    reference fit restarts Adam; resume_training_from_checkpoint here picks the file up when
-    present, which makes a resumed fit continue exactly (tests/test_gpu_checkpoint.py)."""
+    reference fit restarts Adam, and so does resume_training_from_checkpoint here by default;
+    with load_optimizer_state=True it loads the file, which makes a resumed fit continue
+    exactly (tests/test_gpu_checkpoint.py)."""
     os.makedirs(save_dir, exist_ok=True)
     torch.save(standalone_copy(best_model), os.path.join(save_dir, "final_best_model.bin"))
     if optimizers is not None:

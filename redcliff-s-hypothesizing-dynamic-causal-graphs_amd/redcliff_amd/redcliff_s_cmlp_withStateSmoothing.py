@@ -156,6 +156,12 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                 and self.embed_lag >= self.gen_lag
                 and self.primary_gc_est_mode == "conditional_factor_fixed_embedder")
 
+    def check_device_status(self):
+        """Raise if a merged-backward hand-off wait on the device timed out since the last check
+        (synchronises; fit() and validate_training check on their own, see engine.FitEngine)."""
+        if self._engine is not None:
+            self._engine.check_device_status("model.check_device_status")
+
     def engine(self):
         if not self.fused_supported():
             raise NotImplementedError(
@@ -504,11 +510,15 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                 raise NotImplementedError()
         return need
 
-    def resume_training_from_checkpoint(self, training_meta_data_path):
+    def resume_training_from_checkpoint(self, training_meta_data_path, load_optimizer_state=False):
         """...withStateSmoothing.py:209-251: histories of a previous run; fit() resumes at best_it+1.
-        The reference does not checkpoint the optimizers (redcliff_s_cmlp.py:245) and restarts
-        Adam; when this package's save_checkpoint left optimizer_state.pt next to the metadata,
-        fit() loads it into its optimizers, so the resumed fit continues exactly."""
+
+        Default = the reference's behaviour: the optimizers are NOT restored, the resumed fit
+        starts from the caller's fresh Adam objects (redcliff_s_cmlp.py:245 warns about exactly
+        this), so it reproduces the reference's resumed fit on the same files.
+        ``load_optimizer_state=True`` (an extension): the Adam state this package's
+        save_checkpoint wrote next to the metadata (optimizer_state.pt) is loaded into fit()'s
+        optimizers, which makes an interrupted fit continue bit for bit; a missing file raises."""
         import os
         import pickle
         with open(training_meta_data_path, "rb") as f:
@@ -516,8 +526,12 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         self.chkpt_epoch = meta["epoch"]
         for k, v in meta.items():
             setattr(self, "chkpt_" + k, v)
-        opt_path = os.path.join(os.path.dirname(os.path.abspath(training_meta_data_path)), "optimizer_state.pt")
-        if os.path.exists(opt_path):
+        if hasattr(self, "chkpt_optimizer_state"):
+            del self.chkpt_optimizer_state
+        if load_optimizer_state:
+            opt_path = os.path.join(os.path.dirname(os.path.abspath(training_meta_data_path)), "optimizer_state.pt")
+            if not os.path.exists(opt_path):
+                raise FileNotFoundError("load_optimizer_state=True but %s does not exist" % opt_path)
             self.chkpt_optimizer_state = torch.load(opt_path, map_location=self._device(), weights_only=True)
 
     # ------------------------------------------------------------------ training step
@@ -595,6 +609,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         ds = eng.cache_dataset(X_val)
         d = eng.workspace(ds["Bmax"], ds["T"])
         acc, conf = eng.run_values(ds["X"], ds["lab"], d, ds["rows"], ds["sizes"])
+        eng.check_device_status("validate_training")
         if fresh_histories:
             hists = [[] for _ in range(5)]
         elif not hists:

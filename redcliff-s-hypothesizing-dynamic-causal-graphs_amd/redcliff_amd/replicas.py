@@ -103,8 +103,16 @@ class ReplicaPack:
         d.R = self.R
         return d
 
+    def check_device_status(self, where="check"):
+        """Raise if a merged-backward hand-off wait of any replica timed out since the last check
+        (synchronises; the packed fit checks once per epoch inside its single copy back)."""
+        if self.ws is not None:
+            v = nat.status_view(self.ws, self.ws_off, self.R)
+            nat.raise_on_status(v.cpu().numpy(), v, where)
+
     def _workspace(self, Bmax, T):
         if self.ws is None or self.ws_B < Bmax:
+            self.check_device_status("workspace growth")
             d = self._dims(Bmax, T)
             nbytes = nat.lib().redcliff_workspace_bytes(ctypes.byref(d))
             if nbytes == 0:
@@ -439,7 +447,8 @@ class ReplicaPack:
                                                       in_degree_coeff, out_degree_coeff, host=False)
                     l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
                     acc_d, confv_d = self._values(val, active, host=False)
-                    pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d] +
+                    pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d,
+                                             nat.status_view(self.ws, self.ws_off, R)] +
                                             ([vals_d] if vals_d is not None else []))
                 spec = (it + 1 < max_iter and not (dirs is not None and it % check_every == 0)
                         and it + 1 != reorder_at)
@@ -449,7 +458,8 @@ class ReplicaPack:
                     launch_train(it + 1)
                 got = pending.wait()
                 cms, l1, dots, acc, conf = got[:5]
-                vals = got[5].reshape(Ra, S, *got[5].shape[1:]) if vals_d is not None else None
+                nat.raise_on_status(got[5], nat.status_view(self.ws, self.ws_off, R), "packed fit epoch %d" % it)
+                vals = got[6].reshape(Ra, S, *got[6].shape[1:]) if vals_d is not None else None
                 if nsup > 0:
                     train_confusion_many(tr_act, cms.reshape(R, nsup, nsup)[active])
                 gc_progress_many(tr_act, vals, *M.track_values_finish(l1, dots))

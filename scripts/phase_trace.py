@@ -45,6 +45,9 @@ def main():
     tot = eng.ws_off["total"]
     tr = eng.ws[tot - 32768:tot].cpu().numpy().view(np.uint64).astype(np.int64).reshape(8, 2048)
     names = ["emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix"]
+    # merged backward: node workgroups' wait-return times (kid 7, start slots only)
+    wt = tr[7][0::2]
+    wt = wt[wt > 0]
     t_first = min(int(tr[k][0::2][tr[k][0::2] > 0].min()) for k in range(len(names)) if (tr[k][0::2] > 0).any())
     ph = tr[6]
     for lo, hi, label in ((0, 16, "emb_fwd WG0 phases"), (16, 32, "fac_bwd WG0 phases"), (32, 48, "emb_bwd WG0 phases"),
@@ -63,6 +66,11 @@ def main():
         print("%-9s WGs %4d  start %7.2f us  span %7.2f us  start spread %6.2f  WG dur min/med/max %6.2f %6.2f %6.2f"
               % (name, ok.sum(), (st.min() - t_first) / 100.0, (en.max() - st.min()) / 100.0,
                  (st.max() - st.min()) / 100.0, dur.min(), np.median(dur), dur.max()))
+
+
+    if wt.size:
+        print("emb wait returned (merged backward node WGs): %d WGs, first %.2f us  median %.2f  last %.2f"
+              % (wt.size, (wt.min() - t_first) / 100.0, (np.median(wt) - t_first) / 100.0, (wt.max() - t_first) / 100.0))
 
 
 if __name__ == "__main__":

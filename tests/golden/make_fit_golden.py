@@ -1,0 +1,316 @@
+"""Generate multi-epoch fit() fixtures from the REFERENCE itself (build container only).
+
+    python tests/golden/make_fit_golden.py [fit_c1] [fit_d4ic]
+
+Each scenario runs the reference's own ``REDCLIFF_S_CMLP_withStateSmoothing.fit``
+(models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647) at a published model shape on
+seeded sVAR data, with early stopping engaged, and records:
+
+* the validation histories (``avg_*``), ``best_it``, ``best_loss``, the last epoch, the
+  per-epoch GC-progress histories (F1 / ROC-AUC, on / off diagonal; deltacon0 family; L1;
+  cosine) and the train / validation confusion rates;
+* the final ``state_dict`` (after ``restore_parameters``, :1621), the value ``fit`` returns;
+* the final GC estimate on the first validation batch (lagged, unthresholded), its
+  thresholded graphs ``(GC > 0)`` and ``general_utils/metrics.py:396-430`` ``get_f1_score``
+  of every (sample, factor) graph against the true graphs;
+* the keys and value types of the metadata dictionary ``save_checkpoint`` pickles
+  (:936-990), captured from the live call (``pkl.dump`` is wrapped, nothing is unpickled);
+* a reference-style RESUME: the model ``save_checkpoint`` stored at a mid-fit checkpoint
+  (``best_model``) and its metadata go through the reference's own
+  ``resume_training_from_checkpoint`` (:209-251) and ``fit`` again with FRESH optimizers
+  (the reference does not checkpoint them, redcliff_s_cmlp.py:245); histories, best_it and
+  final state of that resumed fit.
+
+The reference is imported with the stubs of oracle/ref_import.py.  Only arrays and JSON
+leave this script (``.npz``).  The data come from redcliff_amd.data.generate_synthetic_data,
+which is bit-identical to the reference generator (tests/test_data.py).
+
+Note on the reference's resume path: its ``fit`` reads ``self.chkpt_roc_au_OffDiagc_histories``
+(a typo, :1253) inside the try block, so with supervised factors the history restore stops
+there; the loss histories, best_loss, best_it and the starting epoch are set before it, so the
+recorded ``resume/hist/avg_*``, ``best_it`` and final state are unaffected.  The GC-progress
+histories of the resumed fit are not recorded (they depend on that typo, SURVEY 8(a) hazard 14).
+"""
+import copy
+import json
+import os
+import pickle
+import sys
+import tempfile
+import time
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "redcliff-s-hypothesizing-dynamic-causal-graphs_amd"))
+
+from oracle.ref_import import import_reference  # noqa: E402
+from oracle.redcliff_oracle import reference_coeffs  # noqa: E402
+from redcliff_amd.data import generate_synthetic_data  # noqa: E402
+
+REF = import_reference()
+
+HIST_KEYS = ["avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
+             "avg_fw_smoothing_penalty", "avg_adj_penalty", "avg_dagness_reg_loss", "avg_dagness_lag_loss",
+             "avg_dagness_node_loss", "avg_combo_loss"]
+
+SCENARIOS = {
+    # configs[0] C1: sVAR, p=10, L=gen_lag=5, K=2, h=25, DGCNN F=16 / 3 layers / 100 hidden, B=128,
+    # the published synthetic lrs / coefficients; 2 training batches, 1 validation batch
+    "fit_c1": dict(seed=0, p=10, L=5, K=2, nsup=2, h=25, F=16, n=3, H=100, B=128, N=256, Nv=128, T=24,
+                   label="onehot", pre=2, acc=2, max_iter=40, lookback=1, check_every=3, lrA=5e-4, lrB=5e-4,
+                   data_seed=9999, resume_at=None),
+    # configs[1] D4IC shape: p=10, L=4, K=4, h=100, DGCNN F=20 / 2 layers / 30 hidden, labels (N, K, 1),
+    # T_rec=21, embed lr 2e-4; one full + one ragged training batch
+    # (lrs raised to 1e-3 so that the validation criterion turns within ~20 epochs: at the published
+    # 2e-4 / 5e-4 it still improves every epoch at epoch 40 on this small set)
+    "fit_d4ic": dict(seed=1, p=10, L=4, K=4, nsup=4, h=100, F=20, n=2, H=30, B=128, N=200, Nv=96, T=21,
+                     label="d4ic", pre=2, acc=1, max_iter=40, lookback=1, check_every=2, lrA=1e-3, lrB=1e-3,
+                     data_seed=4242, resume_at=None),
+}
+
+
+def _np(t):
+    return t.detach().cpu().numpy().copy()
+
+
+def system(rng, S, D, density=0.3):
+    """S lagged adjacency graphs (S, D, D, 2): self-loops plus a sparse random off-diagonal
+    pattern per state, 0.3 strength (the published generator's off-diagonal strength)."""
+    A = np.zeros((S, D, D, 2))
+    for k in range(S):
+        mask = (rng.rand(D, D) < density) & ~np.eye(D, dtype=bool)
+        A[k, :, :, 0] = mask * 0.3
+        A[k, :, :, 1] = mask * 0.3 * (rng.rand(D, D) < 0.5)
+        A[k, np.arange(D), np.arange(D), 0] = 0.6
+    return A
+
+
+def make_data(cfg):
+    rng = np.random.RandomState(cfg["data_seed"])
+    p, K = cfg["p"], cfg["K"]
+    A = system(rng, K, p)
+    N = cfg["N"] + cfg["Nv"]
+    freqs = rng.uniform(0.05, 0.2, (p, 1))
+    X, Y = generate_synthetic_data(N, cfg["T"], "OneHot", 10, p, K, K, 2, A, freqs, np.zeros((p, 1)),
+                                   np.ones((p, 1)), np.ones((p, 1)), 0.1, noise_type="gaussian", rng=rng)
+    X = (X - X.mean(axis=(0, 1), keepdims=True)) / X.std(axis=(0, 1), keepdims=True)
+    if cfg["label"] == "d4ic":
+        # D4IC labels are (N, K, 1): the dominant state of the recording, coefficient 10
+        # (data/dream4_insilicoCombo.py:113-125), background 0.1
+        dom = Y.mean(axis=2).argmax(axis=1)
+        Y = np.full((N, K, 1), 0.1)
+        Y[np.arange(N), dom, 0] = 10.0
+    X, Y = X.astype(np.float32), Y.astype(np.float32)
+    true_gc = [A[k].copy() for k in range(K)]
+    return X[:cfg["N"]], Y[:cfg["N"]], X[cfg["N"]:], Y[cfg["N"]:], true_gc
+
+
+def build(cfg):
+    torch.manual_seed(cfg["seed"])
+    eargs = [("num_features_per_node", cfg["F"]), ("num_graph_conv_layers", cfg["n"]),
+             ("num_hidden_nodes", cfg["H"]), ("sigmoid_eccentricity_coeff", 10.0)]
+    coeff = reference_coeffs(cfg["K"], cfg["p"])
+    m = REF.redcliff_smooth.REDCLIFF_S_CMLP_withStateSmoothing(
+        cfg["p"], cfg["L"], [cfg["h"]], cfg["F"], [0], cfg["L"], 1, cfg["K"], cfg["nsup"], coeff, False, "DGCNN", eargs,
+        "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
+        wavelet_level=None, save_path=None, training_mode="pretrain_embedder_then_acclimate_factors_then_combined",
+        num_pretrain_epochs=cfg["pre"], num_acclimation_epochs=cfg["acc"], STATE_SCORE_SMOOTHING_EPSILON=0.0001).float()
+    return m, coeff
+
+
+def _sd(prefix, model, out):
+    for k, v in model.state_dict().items():
+        if not k.startswith("gen_model."):
+            out["%s/%s" % (prefix, k)] = _np(v)
+
+
+def _type_tree(v):
+    """JSON-able description of a metadata value: container kinds, key sets, leaf types."""
+    if isinstance(v, dict):
+        return {"dict": dict((str(k), _type_tree(x)) for k, x in v.items())}
+    if isinstance(v, (list, tuple)):
+        return {"list": len(v), "first": _type_tree(v[0]) if len(v) else None}
+    if isinstance(v, np.ndarray):
+        return "ndarray%s" % (list(v.shape),)
+    if v is None:
+        return None
+    return type(v).__name__
+
+
+class _Capture:
+    """Wraps the reference module's ``pkl`` (save_checkpoint's pickle.dump) and ``torch.save``
+    of the best model: keeps every checkpoint's metadata dict and a deep copy of the best model
+    in memory; files still go to a temporary directory as the reference writes them."""
+
+    def __init__(self):
+        self.metas = []
+        self.models = []
+
+    def __enter__(self):
+        mod = REF.redcliff_smooth
+        self.saved = (mod.pkl, mod.torch.save, mod.plot_curve)
+        cap = self
+
+        def dump(obj, f, *a, **k):
+            cap.metas.append(copy.deepcopy(obj))
+            return pickle.dump(obj, f, *a, **k)
+
+        def tsave(obj, path, *a, **k):
+            if os.path.basename(path) == "final_best_model.bin" and isinstance(obj, torch.nn.Module):
+                cap.models.append(copy.deepcopy(obj))
+            return self.saved[1](obj, path, *a, **k)
+
+        mod.pkl = types.SimpleNamespace(dump=dump, load=pickle.load)
+        mod.torch.save = tsave
+        mod.plot_curve = lambda *a, **k: None   # plots are out of scope and slow
+        return self
+
+    def __exit__(self, *exc):
+        mod = REF.redcliff_smooth
+        mod.pkl, mod.torch.save, mod.plot_curve = self.saved
+
+
+class _FitLocals:
+    """Captures the local variables of the reference's ``fit`` frame at its end (every history
+    list, best_it, best_loss, the last epoch ``it``): ``restore_parameters`` (:1621), which fit
+    calls once after its epoch loop, is wrapped to read its caller's frame.  The last checkpoint
+    is written before the stopping epoch, so its metadata lacks that epoch."""
+
+    def __init__(self):
+        self.locals = None
+
+    def __enter__(self):
+        mod = REF.redcliff_smooth
+        self.orig = mod.restore_parameters
+        cap = self
+
+        def wrapped(model, best_model):
+            cap.locals = dict(sys._getframe(1).f_locals)
+            return cap.orig(model, best_model)
+        mod.restore_parameters = wrapped
+        return self
+
+    def __exit__(self, *exc):
+        REF.redcliff_smooth.restore_parameters = self.orig
+
+
+def _record_hist(prefix, meta, out, nsup):
+    for k in HIST_KEYS:
+        out["%s/%s" % (prefix, k)] = np.asarray(meta[k], dtype=np.float64)
+    out[prefix + "/best_it"] = np.asarray(meta["best_it"])
+    out[prefix + "/best_loss"] = np.asarray(float(meta["best_loss"]))
+    out[prefix + "/epoch"] = np.asarray(meta["epoch"])
+
+
+def _record_tracking(prefix, meta, out, nsup, p):
+    for name in ("f1score_histories", "f1score_OffDiag_histories", "roc_auc_histories", "roc_auc_OffDiag_histories"):
+        out["%s/%s" % (prefix, name)] = np.asarray([meta[name][0.0][sf] for sf in range(nsup)], dtype=np.float64)
+    for name in ("gc_factor_l1_loss_histories", "deltacon0_histories", "deltacon0_with_directed_degrees_histories",
+                 "deltaffinity_histories"):
+        out["%s/%s" % (prefix, name)] = np.asarray([[float(x) for x in meta[name][sf]] for sf in range(nsup)],
+                                                   dtype=np.float64)
+    out[prefix + "/path_length_mse_histories"] = np.asarray(
+        [[meta["path_length_mse_histories"][pl][sf] for sf in range(nsup)] for pl in range(1, p)], dtype=np.float64)
+    keys = sorted(meta["gc_factor_cosine_sim_histories"])
+    out[prefix + "/gc_factor_cosine_sim_keys"] = np.asarray(json.dumps(keys))
+    out[prefix + "/gc_factor_cosine_sim_histories"] = np.asarray(
+        [[float(x) for x in meta["gc_factor_cosine_sim_histories"][k]] for k in keys], dtype=np.float64)
+    for name in ("factor_score_train_acc_history", "factor_score_train_tpr_history"):
+        out["%s/%s" % (prefix, name)] = np.asarray(meta[name], dtype=np.float64)
+
+
+def run(name, cfg):
+    t0 = time.time()
+    X, Y, Xv, Yv, true_gc = make_data(cfg)
+    m, coeff = build(cfg)
+    out = {"X": X, "Y": Y, "Xv": Xv, "Yv": Yv}
+    for k, g in enumerate(true_gc):
+        out["true_gc%d" % k] = g
+    _sd("init", m, out)
+    B = cfg["B"]
+    train = [(torch.from_numpy(X[i:i + B]), torch.from_numpy(Y[i:i + B])) for i in range(0, len(X), B)]
+    val = [(torch.from_numpy(Xv[i:i + B]), torch.from_numpy(Yv[i:i + B])) for i in range(0, len(Xv), B)]
+
+    def opts(model):
+        return (torch.optim.Adam(model.gen_model[0].parameters(), lr=cfg["lrA"], betas=(0.9, 0.999), eps=1e-4,
+                                 weight_decay=1e-4),
+                torch.optim.Adam(model.gen_model[1].parameters(), lr=cfg["lrB"], betas=(0.9, 0.999), eps=1e-4,
+                                 weight_decay=1e-4))
+
+    fit_kw = dict(lookback=cfg["lookback"], check_every=cfg["check_every"], verbose=0, GC=true_gc, deltaConEps=0.1,
+                  in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=10.,
+                  stopping_criteria_factor_coeff=100., stopping_criteria_cosSim_coeff=1.)
+    oA, oB = opts(m)
+    with tempfile.TemporaryDirectory() as d, _Capture() as cap, _FitLocals() as fl:
+        ret = m.fit(d, train, oA, oB, cfg["L"], 1, 1, cfg["max_iter"], val, **fit_kw)
+    loc = fl.locals
+    meta = dict((k, loc[k]) for k in cap.metas[-1] if k in loc)
+    meta["epoch"] = loc["it"]
+    for k in ("factor_score_train_acc_history", "factor_score_train_tpr_history"):
+        meta[k] = loc[k]
+    last = loc["it"]
+    print("%s: fit stopped at epoch %d (max_iter %d), best_it %d, %d checkpoints, %.1f s"
+          % (name, last, cfg["max_iter"], loc["best_it"], len(cap.metas), time.time() - t0))
+    assert last < cfg["max_iter"] - 1, "early stopping never engaged"
+    _record_hist("hist", meta, out, cfg["nsup"])
+    out["hist/n_epochs"] = np.asarray(len(meta["avg_combo_loss"]))
+    _record_tracking("hist", meta, out, cfg["nsup"], cfg["p"])
+    _record_hist("ckpt_last", cap.metas[-1], out, cfg["nsup"])
+    out["fit_return"] = np.asarray(float(ret))
+    _sd("final", m, out)
+    out["checkpoint_meta_types"] = np.asarray(json.dumps(dict((k, _type_tree(v)) for k, v in cap.metas[-1].items())))
+    out["checkpoint_epochs"] = np.asarray([mm["epoch"] for mm in cap.metas])
+    m.eval()
+    Lm = max(cfg["L"], cfg["F"])
+    with torch.no_grad():
+        gcs = m.GC("conditional_factor_fixed_embedder", X=val[0][0][:40, :Lm, :], threshold=False, ignore_lag=False,
+                   combine_wavelet_representations=True)
+    arr = np.stack([np.stack([_np(g) for g in row]) for row in gcs])
+    out["final_gc"] = arr
+    out["final_graphs"] = (arr > 0).astype(np.int8)
+    out["f1"] = np.asarray([[REF.metrics.get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), true_gc[k].sum(axis=2))
+                             for k, g in enumerate(row)] for row in arr], dtype=np.float64)
+
+    # ---- reference-style resume from a mid-fit checkpoint (fresh optimizers)
+    ck = [i for i, mm in enumerate(cap.metas) if mm["epoch"] >= cfg["pre"] + cfg["acc"]]
+    ci = ck[0] if ck else len(cap.metas) // 2
+    cmeta, cmodel = cap.metas[ci], cap.models[ci]
+    out["resume/ckpt_epoch"] = np.asarray(cmeta["epoch"])
+    _record_hist("resume/ckpt", cmeta, out, cfg["nsup"])
+    _sd("resume/ckpt_model", cmodel, out)
+    rm = copy.deepcopy(cmodel)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "training_meta_data_and_hyper_parameters.pkl")
+        with open(path, "wb") as f:
+            pickle.dump(cmeta, f)
+        rm.resume_training_from_checkpoint(path)
+        rA, rB = opts(rm)
+        with _Capture(), _FitLocals() as fl2:
+            rret = rm.fit(d, train, rA, rB, cfg["L"], 1, 1, cfg["max_iter"], val, **fit_kw)
+    rloc = fl2.locals
+    rmeta = dict((k, rloc[k]) for k in HIST_KEYS + ["best_it", "best_loss"])
+    rmeta["epoch"] = rloc["it"]
+    _record_hist("resume/hist", rmeta, out, cfg["nsup"])
+    out["resume/fit_return"] = np.asarray(float(rret))
+    _sd("resume/final", rm, out)
+    print("%s: resumed at epoch %d, stopped at %d, best_it %d" % (name, cmeta["best_it"] + 1, rmeta["epoch"],
+                                                                  rmeta["best_it"]))
+
+    mcfg = dict(cfg)
+    mcfg["coeff"] = coeff
+    out["meta"] = np.asarray(json.dumps(mcfg))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print("wrote", name, len(out), "arrays, %.1f s" % (time.time() - t0))
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    only = sys.argv[1:]
+    for n_, c in SCENARIOS.items():
+        if not only or n_ in only:
+            run(n_, c)

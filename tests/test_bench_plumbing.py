@@ -28,6 +28,9 @@ def test_bench_spawns_ranks_itself(mode):
                         "--warmup", "1"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
-    assert line["n_gpus"] == 2 and line["config"]["ranks"] == 2
+    assert line["n_gpus"] == 2 and line["config"]["ranks"] == 2 and line["config"]["world_size"] == 2
+    devs = line["config"]["rank_devices"]  # every rank's record, all-gathered: distinct processes
+    assert [d["rank"] for d in devs] == [0, 1] and [d["local_rank"] for d in devs] == [0, 1]
+    assert all(d["device"] == "cpu" for d in devs) and len(set(d["pid"] for d in devs)) == 2
     assert line["scaling"] == ("strong" if mode == "dp" else "weak")
     assert sum(1 for l in r.stdout.splitlines() if l.startswith("{")) == 1  # rank 0 only

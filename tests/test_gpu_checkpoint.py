@@ -82,7 +82,8 @@ def test_resume_from_checkpoint_continues_exactly(tmp_path):
     part, (pA, pB) = fresh()
     part.fit(str(tmp_path), train, pA, pB, 4, 1, 1, 3, val, **kw)  # epochs 0..2, checkpoint at 2
     res = torch.load(os.path.join(str(tmp_path), "final_best_model.bin"), weights_only=False).cuda()
-    res.resume_training_from_checkpoint(os.path.join(str(tmp_path), "training_meta_data_and_hyper_parameters.pkl"))
+    res.resume_training_from_checkpoint(os.path.join(str(tmp_path), "training_meta_data_and_hyper_parameters.pkl"),
+                                        load_optimizer_state=True)
     assert res.chkpt_best_it == 2
     rA, rB = opts(res, 5e-4, 2e-4)
     res.train()

@@ -138,3 +138,91 @@ def test_large_shard_takes_the_matrix_core_factor_path(monkeypatch):
         out.append(dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items()))
     for k in out[0]:
         np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+
+
+FIT_KW = dict(lookback=1, check_every=1, verbose=0, stopping_criteria_forecast_coeff=10.,
+              stopping_criteria_factor_coeff=100., stopping_criteria_cosSim_coeff=1.)
+FIT_EPOCHS = 7
+
+
+def _val_loader():
+    c = CFG
+    rng = np.random.RandomState(8)
+    X = rng.randn(40, c["T"], c["p"]).astype(np.float32)
+    Y = np.zeros((40, c["K"], c["T"]), np.float32)
+    Y[np.arange(40), rng.randint(0, c["K"], 40), :] = 1.0
+    X, Y = torch.from_numpy(X), torch.from_numpy(Y)
+    return [(X[i:i + 24], Y[i:i + 24]) for i in range(0, 40, 24)]
+
+
+def _true_gc():
+    rng = np.random.RandomState(9)
+    return [(rng.rand(CFG["p"], CFG["p"], CFG["L"]) < 0.25).astype(np.float64) for _ in range(CFG["nsup"])]
+
+
+def _fit_worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from redcliff_amd import DataParallelFit
+    m, oA, oB = _model()
+    dp = DataParallelFit(m, oA, oB)
+    save = os.path.join(outdir, "ckpt%d" % rank)
+    ret = dp.fit(save, _loader(), 1, FIT_EPOCHS, _val_loader(), GC=_true_gc(), **FIT_KW)
+    torch.cuda.synchronize()
+    h = m.fit_history
+    sd = dict((k, v.detach().cpu()) for k, v in m.state_dict().items())
+    hist = dict((k, torch.tensor(np.asarray(h[k], np.float64))) for k in
+                ("avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
+                 "avg_adj_penalty", "avg_combo_loss"))
+    f1 = torch.tensor(np.asarray([h["f1score_histories"][0.0][sf] for sf in range(CFG["nsup"])], np.float64))
+    torch.save({"state": sd, "hist": hist, "f1": f1, "best_it": int(h["best_it"]),
+                "stopped_at": -1 if h["stopped_at"] is None else int(h["stopped_at"]), "ret": float(ret),
+                "files": sorted(os.listdir(save)) if os.path.isdir(save) else []},
+               os.path.join(outdir, "fit%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_data_parallel_fit_matches_single_device_fit(tmp_path):
+    """DataParallelFit.fit (configs[3]: a whole fit, not just epochs): two ranks (gloo, one GPU)
+    vs the single-device fit() of the same model on the same batches -- loss histories within
+    1e-4 relative (the sharded gradient sum re-associates fp32 additions), the same best epoch,
+    stopping epoch and F1 history, final parameters within the step test's tolerance; both ranks
+    bit-identical; checkpoints written by rank 0 only."""
+    world = 2
+    mp.start_processes(_fit_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn",
+                       join=True)
+    r0 = torch.load(str(tmp_path / "fit0.pt"), weights_only=True)
+    r1 = torch.load(str(tmp_path / "fit1.pt"), weights_only=True)
+    for k in r0["state"]:
+        np.testing.assert_array_equal(r0["state"][k].numpy(), r1["state"][k].numpy(), err_msg="ranks differ: " + k)
+    for k in r0["hist"]:
+        np.testing.assert_array_equal(r0["hist"][k].numpy(), r1["hist"][k].numpy(), err_msg=k)
+    assert r0["best_it"] == r1["best_it"] and r0["stopped_at"] == r1["stopped_at"]
+    assert "training_meta_data_and_hyper_parameters.pkl" in r0["files"] and r1["files"] == []
+    m, oA, oB = _model()
+    ret = m.fit(None, _loader(), oA, oB, CFG["L"], 1, 1, FIT_EPOCHS, _val_loader(), GC=_true_gc(), **FIT_KW)
+    h = m.fit_history
+    for k, v in r0["hist"].items():
+        w = np.asarray(h[k], np.float64)
+        assert v.numpy().shape == w.shape, k
+        np.testing.assert_allclose(v.numpy(), w, rtol=1e-4, atol=1e-6, err_msg=k)
+    assert r0["best_it"] == h["best_it"]
+    assert r0["stopped_at"] == (-1 if h["stopped_at"] is None else h["stopped_at"])
+    f1 = np.asarray([h["f1score_histories"][0.0][sf] for sf in range(CFG["nsup"])], np.float64)
+    np.testing.assert_allclose(r0["f1"].numpy(), f1, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(r0["ret"], ret, rtol=1e-4)
+    for k, v in m.state_dict().items():
+        got = r0["state"][k].numpy().astype(np.float64)
+        w = v.detach().cpu().numpy().astype(np.float64)
+        if k.endswith("num_batches_tracked"):
+            assert int(got) == int(w), k
+            continue
+        tol = 5e-6 * max(1.0, np.abs(w).max()) + 2e-4 * np.abs(w)
+        bad = np.abs(got - w) > tol
+        assert not bad.any(), "%s: %d/%d off, max err %.3e" % (k, int(bad.sum()), w.size, np.abs(got - w).max())

@@ -1,0 +1,169 @@
+"""Fit-level parity at published model shapes, pinned to the REFERENCE's own multi-epoch fit.
+
+Fixtures: tests/golden/fit_c1.npz (configs[0] C1: p=10, L=5, K=2, h=25, DGCNN 16/3/100) and
+tests/golden/fit_d4ic.npz (configs[1] D4IC shape: p=10, L=4, K=4, h=100, DGCNN 20/2/30), written
+by tests/golden/make_fit_golden.py, which runs the reference's ``fit``
+(models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647) with early stopping engaged, and then a
+reference-style resume (fresh optimizers, :209-251, redcliff_s_cmlp.py:245) from a mid-fit
+checkpoint.
+
+The HIP fit runs on the same seeded model and the same windows and must give (north_star):
+  * the same stopping epoch and best_it, and the same number of history entries;
+  * validation-loss histories within 1e-4 relative (the fit's fp32 rounding order differs from
+    torch's CPU one: reductions over windows / contractions run in a fixed GPU order);
+  * GC-progress histories (F1 at threshold 0 / ROC-AUC / L1 / cosine / deltacon0 family)
+    within 1e-4 (F1 and ROC-AUC are rank statistics: identical unless a graph entry sits within
+    fp32 rounding of a tie, which the 1e-4 bound would expose);
+  * final parameters / buffers within rtol 2e-4 (the published-config schedule tolerance of
+    tests/test_gpu_parity.py), the final GC estimate within 1e-4 relative, thresholded graphs
+    (GC > 0) and get_f1_score identical.
+"""
+import json
+import os
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_close, load, state
+
+pytestmark = pytest.mark.gpu
+
+HKEYS = ["avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
+         "avg_fw_smoothing_penalty", "avg_adj_penalty", "avg_dagness_reg_loss", "avg_dagness_lag_loss",
+         "avg_dagness_node_loss", "avg_combo_loss"]
+
+
+def build(meta):
+    import redcliff_amd
+    eargs = [("num_features_per_node", meta["F"]), ("num_graph_conv_layers", meta["n"]),
+             ("num_hidden_nodes", meta["H"]), ("sigmoid_eccentricity_coeff", 10.0)]
+    torch.manual_seed(meta["seed"])
+    return redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(
+        meta["p"], meta["L"], [meta["h"]], meta["F"], [0], meta["L"], 1, meta["K"], meta["nsup"], meta["coeff"], False,
+        "DGCNN", eargs, "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
+        wavelet_level=None, save_path=None, training_mode="pretrain_embedder_then_acclimate_factors_then_combined",
+        num_pretrain_epochs=meta["pre"], num_acclimation_epochs=meta["acc"],
+        STATE_SCORE_SMOOTHING_EPSILON=0.0001).float().cuda()
+
+
+def opts(m, meta):
+    return (torch.optim.Adam(m.gen_model[0].parameters(), lr=meta["lrA"], betas=(0.9, 0.999), eps=1e-4,
+                             weight_decay=1e-4),
+            torch.optim.Adam(m.gen_model[1].parameters(), lr=meta["lrB"], betas=(0.9, 0.999), eps=1e-4,
+                             weight_decay=1e-4))
+
+
+def data(d, meta):
+    B = meta["B"]
+    X, Y, Xv, Yv = [torch.from_numpy(d[k]) for k in ("X", "Y", "Xv", "Yv")]
+    train = [(X[i:i + B], Y[i:i + B]) for i in range(0, len(X), B)]
+    val = [(Xv[i:i + B], Yv[i:i + B]) for i in range(0, len(Xv), B)]
+    return train, val
+
+
+def fit_kw(meta, d):
+    return dict(lookback=meta["lookback"], check_every=meta["check_every"], verbose=0,
+                GC=[d["true_gc%d" % k] for k in range(meta["K"])], deltaConEps=0.1, in_degree_coeff=1.,
+                out_degree_coeff=1., stopping_criteria_forecast_coeff=10., stopping_criteria_factor_coeff=100.,
+                stopping_criteria_cosSim_coeff=1.)
+
+
+def compare_state(tag, model, want, rtol=2e-4, atol=5e-6):
+    got = dict((k, v.detach().cpu().numpy()) for k, v in model.state_dict().items() if not k.startswith("gen_model."))
+    assert set(got) == set(want), tag
+    for k in want:
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(want[k]), tag + k
+            continue
+        scale = max(1.0, float(np.abs(want[k]).max()))
+        assert_close("%s/%s" % (tag, k), got[k], want[k], rtol, atol * scale)
+
+
+def compare_hist(tag, h, d, prefix):
+    for k in HKEYS:
+        assert_close("%s/%s" % (tag, k), np.asarray(h[k], np.float64), d["%s/%s" % (prefix, k)], 1e-4, 1e-6)
+    assert h["best_it"] == int(d[prefix + "/best_it"]), (tag, h["best_it"], int(d[prefix + "/best_it"]))
+    assert_close(tag + "/best_loss", h["best_loss"], d[prefix + "/best_loss"], 1e-4, 1e-6)
+
+
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic"])
+def test_fit_matches_reference_fit(name):
+    d, meta = load(name)
+    m = build(meta)
+    compare_state("init", m, state(d, "init"), rtol=0, atol=0)  # seeded construction: bit-identical
+    train, val = data(d, meta)
+    oA, oB = opts(m, meta)
+    ret = m.fit(None, train, oA, oB, meta["L"], 1, 1, meta["max_iter"], val, **fit_kw(meta, d))
+    h = m.fit_history
+    n = int(d["hist/n_epochs"])
+    assert len(h["avg_combo_loss"]) == n, (len(h["avg_combo_loss"]), n)
+    assert h["stopped_at"] == int(d["hist/epoch"]), (h["stopped_at"], int(d["hist/epoch"]))
+    compare_hist(name, h, d, "hist")
+    nsup = meta["nsup"]
+    for key in ("f1score_histories", "f1score_OffDiag_histories", "roc_auc_histories", "roc_auc_OffDiag_histories"):
+        got = np.asarray([h[key][0.0][sf] for sf in range(nsup)], np.float64)
+        assert_close(key, got, d["hist/" + key], 1e-4, 1e-6)
+    for key, hk in (("gc_factor_l1_loss_histories", "gc_factor_l1_loss_histories"),
+                    ("deltacon0_histories", "deltacon0_histories"),
+                    ("deltacon0_with_directed_degrees_histories", "deltacon0_with_directed_degrees_histories"),
+                    ("deltaffinity_histories", "deltaffinity_histories")):
+        got = np.asarray([[float(x) for x in h[hk][sf]] for sf in range(nsup)], np.float64)
+        assert_close(key, got, d["hist/" + key], 1e-4, 1e-6)
+    plm = np.asarray([[h["path_length_mse_histories"][pl][sf] for sf in range(nsup)] for pl in range(1, meta["p"])],
+                     np.float64)
+    assert_close("path_length_mse", plm, d["hist/path_length_mse_histories"], 1e-4, 1e-6)
+    keys = json.loads(str(d["hist/gc_factor_cosine_sim_keys"]))
+    got = np.asarray([h["gc_factor_cosine_sim_histories"][k] for k in keys], np.float64)
+    assert_close("cosine", got, d["hist/gc_factor_cosine_sim_histories"], 1e-4, 1e-6)
+    for key, ck in (("factor_score_train_acc_history", "acc"), ("factor_score_train_tpr_history", "tpr")):
+        got = np.asarray(h["factor_score_train_history"][ck], np.float64)
+        np.testing.assert_array_equal(np.nan_to_num(got, nan=-1.0), np.nan_to_num(d["hist/" + key], nan=-1.0),
+                                      err_msg=key)
+    compare_state("final", m, state(d, "final"))
+    assert_close("fit return", ret, d["fit_return"], 1e-4, 1e-6)
+    m.eval()
+    Lm = max(meta["L"], meta["F"])
+    with torch.no_grad():
+        gcs = m.GC("conditional_factor_fixed_embedder", X=val[0][0][:40, :Lm].cuda(), threshold=False,
+                   ignore_lag=False, combine_wavelet_representations=True)
+    arr = np.stack([np.stack([g.cpu().numpy() for g in row]) for row in gcs])
+    assert_close("final_gc", arr, d["final_gc"], 1e-4, 1e-5)
+    np.testing.assert_array_equal((arr > 0).astype(np.int8), d["final_graphs"])
+    from redcliff_amd.metrics import get_f1_score
+    true_gc = [d["true_gc%d" % k] for k in range(meta["K"])]
+    f1 = np.asarray([[get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), true_gc[k].sum(axis=2))
+                      for k, g in enumerate(row)] for row in arr])
+    np.testing.assert_array_equal(f1, d["f1"])
+
+
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic"])
+def test_resume_matches_reference_resume(name, tmp_path):
+    """The reference's resume: the model saved at a mid-fit checkpoint (best_model) plus its
+    metadata, resume_training_from_checkpoint, fit with FRESH Adam objects (the default here,
+    as in the reference) -- histories, best_it and final state as the reference's resumed fit."""
+    d, meta = load(name)
+    m = build(meta)
+    with torch.no_grad():
+        sd = state(d, "resume/ckpt_model")
+        m.load_state_dict(dict((k, torch.from_numpy(v)) for k, v in sd.items()), strict=False)
+    compare_state("ckpt", m, sd, rtol=0, atol=0)
+    ck = dict((k, list(d["resume/ckpt/" + k])) for k in HKEYS)
+    ck.update(epoch=int(d["resume/ckpt/epoch"]), best_it=int(d["resume/ckpt/best_it"]),
+              best_loss=float(d["resume/ckpt/best_loss"]))
+    path = os.path.join(str(tmp_path), "training_meta_data_and_hyper_parameters.pkl")
+    with open(path, "wb") as f:
+        pickle.dump(ck, f)
+    m.resume_training_from_checkpoint(path)
+    assert not hasattr(m, "chkpt_optimizer_state")
+    assert m.chkpt_best_it == int(d["resume/ckpt/best_it"])
+    train, val = data(d, meta)
+    oA, oB = opts(m, meta)
+    m.train()
+    ret = m.fit(None, train, oA, oB, meta["L"], 1, 1, meta["max_iter"], val, **fit_kw(meta, d))
+    h = m.fit_history
+    assert h["stopped_at"] == int(d["resume/hist/epoch"])
+    compare_hist(name + "/resume", h, d, "resume/hist")
+    compare_state("resume/final", m, state(d, "resume/final"))
+    assert_close("resume fit return", ret, d["resume/fit_return"], 1e-4, 1e-6)

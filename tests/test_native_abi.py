@@ -67,7 +67,7 @@ def test_guard_band_layout():
     from redcliff_amd import _native as nat
     d = c1_dims()
     plain = nat.workspace_regions(d)
-    assert len(plain) == 34 and nat.workspace_layout(d)["total"] >= plain[-1][0] + plain[-1][1]
+    assert len(plain) == 35 and nat.workspace_layout(d)["total"] >= plain[-1][0] + plain[-1][1]
     prev = nat.guard_bands(64)
     try:
         regs = nat.workspace_regions(d)
