@@ -612,7 +612,8 @@ def main():
     ap.add_argument("--fit-epochs", type=int, default=40)
     ap.add_argument("--fit-train-batches", type=int, default=8)
     ap.add_argument("--dp-batch", type=int, default=128, help="global batch of --mode dp")
-    ap.add_argument("--dp-leg-batch", type=int, default=1024,
+    # 512 = the most windows one launch takes (Bmax), so one rank can run the same global batch
+    ap.add_argument("--dp-leg-batch", type=int, default=512,
                     help="global batch of the data-parallel leg of --mode fit (0: skip)")
     args = ap.parse_args()
 

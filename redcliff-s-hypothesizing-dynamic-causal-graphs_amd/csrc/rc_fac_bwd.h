@@ -105,36 +105,65 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   // being written by the forward and read back (2 MB each way per D4IC step)
   const bool recompute = rc_fac_recompute(d);
 
-  // ---- one staging pass for everything the workgroup reads
+  // ---- staging: one pass for everything the workgroup reads, except for the lead workgroup of
+  // a merged launch, which stages only what its published records need (predictions, embedder
+  // outputs, targets, group-norm partials, A column), publishes, and then stages the operands of
+  // its own dW0 / Adam work (the embedder workgroups of the launch wait for the K*p leads)
   const int tq = tid & 15, tu = tid >> 4;
   const int64_t kjW0 = c.fo.W0 + (int64_t)kj * h * Q;
   float pw[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f}, pv[4] = {0.f, 0.f, 0.f, 0.f};
   float sb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, s1[3] = {0.f, 0.f, 0.f};
   const bool gonly = c.flags & RC_GRAD_ONLY;
-  if (stepB && !gonly) {  // Adam state of the parameters this thread updates
-    if (u0 + tu < h)
+  const bool split = lead && publish != nullptr;
+  auto adam_loads = [&]() {
+    if (stepB && !gonly) {  // Adam state of the parameters this thread updates
+      if (u0 + tu < h)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int q = q0 + tq + 16 * jj;
-        if (q < Q) {
-          const int64_t idx = kjW0 + (int64_t)(u0 + tu) * Q + q;
-          pw[jj] = P[idx]; pm[jj] = PM[idx]; pv[jj] = PV[idx];
+        for (int jj = 0; jj < 4; ++jj) {
+          const int q = q0 + tq + 16 * jj;
+          if (q < Q) {
+            const int64_t idx = kjW0 + (int64_t)(u0 + tu) * Q + q;
+            pw[jj] = P[idx]; pm[jj] = PM[idx]; pv[jj] = PV[idx];
+          }
         }
+      if (qc == 0 && tid < FAC_UC && u0 + tid < h) {
+        const int64_t ib = c.fo.b0 + (int64_t)kj * h + u0 + tid, iw = c.fo.W1 + (int64_t)kj * h + u0 + tid;
+        sb[0] = P[ib]; sb[1] = PM[ib]; sb[2] = PV[ib];
+        sb[3] = P[iw]; sb[4] = PM[iw]; sb[5] = PV[iw];
       }
-    if (qc == 0 && tid < FAC_UC && u0 + tid < h) {
-      const int64_t ib = c.fo.b0 + (int64_t)kj * h + u0 + tid, iw = c.fo.W1 + (int64_t)kj * h + u0 + tid;
-      sb[0] = P[ib]; sb[1] = PM[ib]; sb[2] = PV[ib];
-      sb[3] = P[iw]; sb[4] = PM[iw]; sb[5] = PV[iw];
+      if (qc == 0 && uc == 0 && tid == 0) {
+        const int64_t i1 = c.fo.b1 + kj;
+        s1[0] = P[i1]; s1[1] = PM[i1]; s1[2] = PV[i1];
+      }
     }
-    if (qc == 0 && uc == 0 && tid == 0) {
-      const int64_t i1 = c.fo.b1 + kj;
-      s1[0] = P[i1]; s1[1] = PM[i1]; s1[2] = PV[i1];
-    }
-  }
+  };
+  if (!split) adam_loads();
   const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
   const float* W1snap = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by the forward
   const int64_t ys_ = (int64_t)d.Bmax * K * p;
   const int nb0 = min(B, FB_BT);
+  // the dW0 / Adam operands (late: staged after the lead's publish)
+  auto stage_update = [&](bool on) {
+    rc_stage_all(
+        rc_seg<1>(on && stepB ? FAC_UC : 0, [&](int e) { return u0 + e < h ? W1snap[u0 + e] : 0.f; },
+                  [&](int e, float v) { w1s[e] = v; }),
+        rc_seg<8>(on && stepB && !recompute ? nb0 * FAC_UC : 0, [&](int e) {
+          const int bb = e >> 4, uu = e & 15;
+          return u0 + uu < h ? aw[(int64_t)bb * h + u0 + uu] : 0.f;
+        }, [&](int e, float v) { awl[(e >> 4) * (FAC_UC + 1) + (e & 15)] = v; }),
+        rc_seg<4>(on && stepB && recompute ? FAC_UC * Q : 0, [&](int e) {
+          const int uu = e / Q, q = e - uu * Q;
+          return u0 + uu < h ? P[kjW0 + (int64_t)(u0 + uu) * Q + q] : 0.f;
+        }, [&](int e, float v) { Wc[(e / Q) * (FB_QT + 1) + e % Q] = v; }),
+        rc_seg<1>(on && stepB && recompute ? FAC_UC : 0, [&](int e) {
+          return u0 + e < h ? P[c.fo.b0 + (int64_t)kj * h + u0 + e] : 0.f;
+        }, [&](int e, float v) { bc0[e] = v; }),
+        rc_seg<32>(on && stepB ? nb0 * FB_QT : 0, [&](int e) {
+          const int bb = e >> 6, qq = e & 63;
+          return q0 + qq < Q ? xwin(c, dL, X, bb, q0 + qq) : 0.f;
+        }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
+  };
+  if (!split) stage_update(true);
   rc_stage_all(
       rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order)
         const int b = dK.div(e), kk = e - b * K;
@@ -156,23 +185,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
         for (int q = 0; q < nU; ++q) sq += ws[c.wo.gq + ((int64_t)q * K * p + kj) * Q + e];
         return sq;
       }, [&](int e, float v) { sqs[e] = v; }),
-      rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }),
-      rc_seg<1>(stepB ? FAC_UC : 0, [&](int e) { return u0 + e < h ? W1snap[u0 + e] : 0.f; },
-                [&](int e, float v) { w1s[e] = v; }),
-      rc_seg<8>(stepB && !recompute ? nb0 * FAC_UC : 0, [&](int e) {
-        const int bb = e >> 4, uu = e & 15;
-        return u0 + uu < h ? aw[(int64_t)bb * h + u0 + uu] : 0.f;
-      }, [&](int e, float v) { awl[(e >> 4) * (FAC_UC + 1) + (e & 15)] = v; }),
-      rc_seg<4>(stepB && recompute ? FAC_UC * Q : 0, [&](int e) {
-        const int uu = e / Q, q = e - uu * Q;
-        return u0 + uu < h ? P[kjW0 + (int64_t)(u0 + uu) * Q + q] : 0.f;
-      }, [&](int e, float v) { Wc[(e / Q) * (FB_QT + 1) + e % Q] = v; }),
-      rc_seg<1>(stepB && recompute ? FAC_UC : 0, [&](int e) { return u0 + e < h ? P[c.fo.b0 + (int64_t)kj * h + u0 + e] : 0.f; },
-                [&](int e, float v) { bc0[e] = v; }),
-      rc_seg<32>(stepB ? nb0 * FB_QT : 0, [&](int e) {
-        const int bb = e >> 6, qq = e & 63;
-        return q0 + qq < Q ? xwin(c, dL, X, bb, q0 + qq) : 0.f;
-      }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
+      rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }));
   for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
@@ -306,6 +319,10 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 18);
   if (publish && lead) rc_publish(publish);
   if (!stepB) return;
+  if (split) {  // the lead's own update operands, after its records are out
+    adam_loads();
+    stage_update(true);
+  }
   __syncthreads();
 
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);

@@ -61,14 +61,16 @@ class _CMLPForward(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, cmlps, *params):
         ctx.cmlps = cmlps
-        ctx.save_for_backward(X)
+        # the parameters are saved too: an in-place change before backward (an optimizer step
+        # between two backwards of a retained graph) trips autograd's version check, as stock
+        # modules do, instead of silently differentiating the new values
+        ctx.save_for_backward(X, *params)
         return torch.stack(kernels.cmlp_forward(list(cmlps), X.detach()), 0)  # (F, B, S, p)
 
     @staticmethod
     def backward(ctx, gout):
-        X, = ctx.saved_tensors
+        X, *params = ctx.saved_tensors
         cmlps = ctx.cmlps
-        params = _factor_params(cmlps)
         with torch.enable_grad():
             Xr = _leaf(X, ctx.needs_input_grad[0])
             lp = [_leaf(p, p.requires_grad) for p in params]
@@ -156,9 +158,10 @@ def dgcnn_params(dg):
                                                            dg.fc1.linear.bias, dg.fc2.linear.weight, dg.fc2.linear.bias]
 
 
-def _dgcnn_recompute(dg, params, x, train_bn):
+def _dgcnn_recompute(dg, params, x, train_bn, bn_stats=None):
     """torcheeg DGCNN forward on node features x (B, p, F) with explicit parameter tensors;
-    BatchNorm with batch statistics (train) / running statistics (eval), never advancing them."""
+    BatchNorm with batch statistics (train) / running statistics (eval: `bn_stats`, the
+    (running_mean, running_var) snapshot taken at forward time), never advancing them."""
     A, gcw = params[0], params[1:1 + dg.num_layers]
     bnw, bnb, f1w, f1b, f2w, f2b = params[1 + dg.num_layers:]
     bn = dg.BN1
@@ -166,7 +169,8 @@ def _dgcnn_recompute(dg, params, x, train_bn):
     if train_bn:
         xt = torch.nn.functional.batch_norm(xt, None, None, bnw, bnb, True, 0.0, bn.eps)
     else:
-        xt = torch.nn.functional.batch_norm(xt, bn.running_mean, bn.running_var, bnw, bnb, False, 0.0, bn.eps)
+        rm, rv = bn_stats if bn_stats is not None else (bn.running_mean, bn.running_var)
+        xt = torch.nn.functional.batch_norm(xt, rm, rv, bnw, bnb, False, 0.0, bn.eps)
     xb = xt.transpose(1, 2)
     B = xb.shape[0]
     Ar = torch.relu(A)
@@ -193,20 +197,21 @@ class _FusedForward(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, model, train_bn, *params):
         eng = model.engine()
+        bn = _bn_snapshot(model, train_bn)  # eval mode: the running statistics this forward used
         w_raw, y, xs = eng.forward_outputs(X.detach(), train_bn=train_bn, bn_updates=1)
         ctx.model, ctx.train_bn = model, train_bn
-        ctx.save_for_backward(X)
+        ctx.save_for_backward(X, *params, *bn)
         return xs, y.contiguous(), w_raw
 
     @staticmethod
     def backward(ctx, gxs, gy, gw):
-        X, = ctx.saved_tensors
+        X, *rest = ctx.saved_tensors
         m = ctx.model
-        params = fused_params(m)
+        params, bn = (rest, None) if ctx.train_bn else (rest[:-2], tuple(rest[-2:]))
         with torch.enable_grad():
             Xr = _leaf(X, ctx.needs_input_grad[0])
             lp = [_leaf(p, p.requires_grad) for p in params]
-            xs, y, w = _fused_recompute(m, Xr, lp, ctx.train_bn)
+            xs, y, w = _fused_recompute(m, Xr, lp, ctx.train_bn, bn)
             g = _grads([xs, y, w], [gxs, gy, gw], [Xr] + lp)
         return (g[0], None, None) + tuple(g[1:])
 
@@ -216,11 +221,21 @@ def fused_params(model):
     return dgcnn_params(dg) + _factor_params(model.factors)
 
 
-def _fused_recompute(m, X, lp, train_bn):
+def _bn_snapshot(model, train_bn):
+    """() in train mode (batch statistics); else copies of the BatchNorm running statistics as
+    the forward sees them, so a later train-mode forward advancing them cannot change an earlier
+    eval-mode graph's backward."""
+    if train_bn:
+        return ()
+    bn = model.factor_score_embedder.dgcnn.dgcnn.BN1
+    return (bn.running_mean.detach().clone(), bn.running_var.detach().clone())
+
+
+def _fused_recompute(m, X, lp, train_bn, bn_stats=None):
     dg = m.factor_score_embedder.dgcnn.dgcnn
     ne = 1 + dg.num_layers + 6
     F, L, K, p = m.embed_lag, m.gen_lag, m.num_factors_nK, m.num_series
-    w = _dgcnn_recompute(dg, lp[:ne], X[:, X.shape[1] - F:, :].transpose(1, 2), train_bn)
+    w = _dgcnn_recompute(dg, lp[:ne], X[:, X.shape[1] - F:, :].transpose(1, 2), train_bn, bn_stats)
     fp = lp[ne:]
     nets = [fp[4 * i:4 * i + 4] for i in range(K * p)]
     y = _mlp_group_params(nets, X[:, X.shape[1] - L:, :]).view(X.shape[0], K, p)
@@ -248,22 +263,23 @@ class _EmbedderForward(torch.autograd.Function):
     @staticmethod
     def forward(ctx, Xw, model, train_bn, *params):
         eng = model.engine()
+        bn = _bn_snapshot(model, train_bn)
         w_raw, _, _ = eng.forward_outputs(Xw.detach(), train_bn=train_bn, bn_updates=1)
         ctx.model, ctx.train_bn = model, train_bn
-        ctx.save_for_backward(Xw)
+        ctx.save_for_backward(Xw, *params, *bn)
         return w_raw
 
     @staticmethod
     def backward(ctx, gw):
-        Xw, = ctx.saved_tensors
+        Xw, *rest = ctx.saved_tensors
         m = ctx.model
         dg = m.factor_score_embedder.dgcnn.dgcnn
-        params = dgcnn_params(dg)
+        params, bn = (rest, None) if ctx.train_bn else (rest[:-2], tuple(rest[-2:]))
         with torch.enable_grad():
             Xr = _leaf(Xw, ctx.needs_input_grad[0])
             lp = [_leaf(p, p.requires_grad) for p in params]
             F = m.embed_lag
-            w = _dgcnn_recompute(dg, lp, Xr[:, Xr.shape[1] - F:, :].transpose(1, 2), ctx.train_bn)
+            w = _dgcnn_recompute(dg, lp, Xr[:, Xr.shape[1] - F:, :].transpose(1, 2), ctx.train_bn, bn)
             g = _grads([w], [gw], [Xr] + lp)
         return (g[0], None, None) + tuple(g[1:])
 

@@ -77,7 +77,7 @@ class DataParallelFit:
         if Bl < 1:
             raise ValueError("batch %d has %d windows for %d ranks: every rank needs at least one window"
                              % (bi, B, self.world))
-        d = eng.workspace(ds["Bmax"], ds["T"])
+        d = eng.workspace(-(-int(ds["Bmax"]) // self.world), ds["T"])  # the largest shard
         stats = ds["stats"][bi:bi + 1] if flags & nat.BN_TRAIN else None
         a = eng._args(d, flags | nat.GRAD_ONLY, nbn, ds["X"], ds["lab"], stats)
         a.row0 = int(ds["rows"][bi]) + off
@@ -90,7 +90,7 @@ class DataParallelFit:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
         self.comm_bytes += buf.numel() * 4
         hyp = eng._hyper()
-        d1 = eng.dims(ds["Bmax"], ds["T"])
+        d1 = eng.dims(1, ds["T"])  # Adam over the flat groups: only R and the layouts matter
         for g, on, P, buf_g, n in (("A", stepA, eng.emb, self.gE, self.PA), ("B", stepB, eng.fac, self.gF, self.PB)):
             if not on:
                 continue

@@ -22,6 +22,8 @@ from . import _native as nat
 from .dgcnn import M1
 from .kernels import factor_views, ptr
 
+BMAX_LIMIT = 512  # windows per launch (include/redcliff_hip.h: Bmax <= 512)
+
 
 # ----------------------------------------------------------------------------- phases
 def phase_of_epoch(model, epoch_num):
@@ -370,7 +372,10 @@ class FitEngine:
         Xall = torch.cat(xs, 0).to(self.device).contiguous()
         lab = torch.cat(ys, 0).to(self.device, torch.float32).contiguous()
         rows = np.cumsum([0] + sizes[:-1]).astype(np.int64)
-        d = self.workspace(max(sizes), Xall.shape[1])
+        # the BatchNorm statistics kernel takes any batch size; the step workspace is sized for
+        # the batches (a data-parallel fit's global batches may exceed one launch's Bmax: it
+        # sizes the workspace for its shards itself)
+        d = self.workspace(max(sizes), Xall.shape[1]) if max(sizes) <= BMAX_LIMIT else self.dims(1, Xall.shape[1])
         if all(s == sizes[0] for s in sizes[:-1]) and sizes[-1] <= sizes[0]:
             # consecutive equal batches (a ragged last one allowed): one launch for all of them
             stats = self.bn_stats(d, Xall, int(Xall.shape[0]), sizes[0])

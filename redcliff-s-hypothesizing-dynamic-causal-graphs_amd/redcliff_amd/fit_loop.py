@@ -603,7 +603,8 @@ def _host_epochs(model, eng, tr, fused, train, val, d_train, plans, X_train, X_v
 def _prior_hook(model, X_train, prior):
     """it -> None: the factor re-ordering fit() runs at the start of epoch num_pretrain_epochs
     of the "pretrain_factor" modes (...withStateSmoothing.py:1318-1326)."""
-    path, cost, start, nb = prior
+    path, cost, start, nb = prior[:4]
+    allow_pickle = prior[4] if len(prior) > 4 else False
     at = set()
     if "pretrain_factor" in model.training_mode:
         at.add(model.num_pretrain_epochs)
@@ -613,7 +614,8 @@ def _prior_hook(model, X_train, prior):
     def hook(it):
         if it in at:
             model.initialize_factors_with_prior(prior_factors_path=path, X_train=X_train, cost_criteria=cost,
-                                                unsupervised_start_index=start, max_batches=nb)
+                                                unsupervised_start_index=start, max_batches=nb,
+                                                allow_pickle=allow_pickle)
     hook.at = at
     return hook
 
@@ -660,7 +662,8 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
     if fused:
         train = eng.cache_dataset(X_train)
         val = eng.cache_dataset(X_val)
-        d_train = eng.workspace(max(train["Bmax"], val["Bmax"]), train["T"])
+        # (a data-parallel runner sizes the workspace for its shards; validation is unsharded)
+        d_train = eng.workspace(max(train["Bmax"] if runner is None else 1, val["Bmax"]), train["T"])
         plans = {}
 
     dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (

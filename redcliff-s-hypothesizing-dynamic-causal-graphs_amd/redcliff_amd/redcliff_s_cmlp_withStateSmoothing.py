@@ -382,8 +382,39 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         return combo, terms + [adj, None]
 
     # ------------------------------------------------------------------ factor prior / re-ordering
+    def _load_prior_factors(self, path, allow_pickle):
+        """Factor parameter tensors [K][params in module order] of a prior model file.  Default:
+        weights-only loading (torch.load(weights_only=True)), which takes a state_dict of the
+        model (or of its factors: keys factors.{k}.networks.{j}.layers.{0,1}.{weight,bias}) and
+        executes nothing from the file.  A whole pickled module -- what the reference's fit
+        writes and loads (:151) -- is unpickled only with allow_pickle=True (trusted files)."""
+        import pickle
+        dev = self._device()
+        try:
+            obj = torch.load(path, map_location=dev, weights_only=True)
+        except (pickle.UnpicklingError, RuntimeError, AttributeError) as e:
+            if not allow_pickle:
+                raise RuntimeError(
+                    "prior_factors_path %s is not a weights-only file (a pickled module?): pass "
+                    "prior_factors_allow_pickle=True for a trusted file, or save the prior model's state_dict()"
+                    % path) from e
+            obj = torch.load(path, map_location=dev, weights_only=False)
+        if isinstance(obj, dict):
+            sd = obj.get("state_dict", obj)
+            out = []
+            for k, f in enumerate(self.factors):
+                ts = []
+                for name, _ in f.named_parameters():
+                    key = "factors.%d.%s" % (k, name)
+                    if key not in sd:
+                        raise KeyError("prior state_dict has no %s" % key)
+                    ts.append(sd[key])
+                out.append(ts)
+            return out, None
+        return [list(f.parameters()) for f in obj.factors], obj
+
     def initialize_factors_with_prior(self, prior_factors_path=None, X_train=None, cost_criteria="CosineSimilarity",
-                                      unsupervised_start_index=0, max_batches=10):
+                                      unsupervised_start_index=0, max_batches=10, allow_pickle=False):
         """...withStateSmoothing.py:149-206.  fit() calls it at the end of factor pretraining
         ("pretrain_factor" modes, :1318-1326) with X_train: the factors are re-ordered so that
         factor i is the one whose (eval-mode) embedder weighting matches label column i best
@@ -402,19 +433,25 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         every later step (engine.step_flags).  gen_model[1] keeps pointing at the live factors
         here, where the reference's still holds the replaced ones."""
         if prior_factors_path is not None:
-            prior = torch.load(prior_factors_path, map_location=self._device(), weights_only=False)
+            tensors, prior = self._load_prior_factors(prior_factors_path, allow_pickle)
             if not self.fused_supported():
-                self.factors = prior.factors  # the reference's move (:152)
+                if prior is not None:
+                    self.factors = prior.factors  # the reference's move (:152)
+                else:
+                    with torch.no_grad():
+                        for f_dst, ts in zip(self.factors, tensors):
+                            for p_dst, p_src in zip(f_dst.parameters(), ts):
+                                p_dst.copy_(p_src.detach().to(p_dst.device, p_dst.dtype))
             else:
                 eng = self.engine()
                 eng.ensure_bound()
                 with torch.no_grad():
-                    for f_dst, f_src in zip(self.factors, prior.factors):
-                        for p_dst, p_src in zip(f_dst.parameters(), f_src.parameters()):
+                    for f_dst, ts in zip(self.factors, tensors):
+                        for p_dst, p_src in zip(f_dst.parameters(), ts):
                             p_dst.copy_(p_src.detach().to(p_dst.device, p_dst.dtype))
                 eng.invalidate()
                 self.__dict__["_factors_detached"] = True
-            del prior
+            del prior, tensors
         if X_train is None:
             return
         if unsupervised_start_index != 0:
@@ -638,12 +675,15 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             X_val, lookback=5, check_every=50, verbose=1, GC=None, deltaConEps=0.1, in_degree_coeff=1.,
             out_degree_coeff=1., prior_factors_path=None, cost_criteria="CosineSimilarity",
             unsupervised_start_index=0, max_factor_prior_batches=10, stopping_criteria_forecast_coeff=1.,
-            stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., save_plots=False):
-        """Epoch loop of ...withStateSmoothing.py:1175-1647 with the batches resident on the GPU."""
+            stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., save_plots=False,
+            prior_factors_allow_pickle=False):
+        """Epoch loop of ...withStateSmoothing.py:1175-1647 with the batches resident on the GPU.
+        prior_factors_allow_pickle (extension): see initialize_factors_with_prior."""
         from .fit_loop import run_fit
         return run_fit(self, save_dir, X_train, optimizerA, optimizerB, output_length, max_iter, X_val, lookback,
                        check_every, verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff,
-                       (prior_factors_path, cost_criteria, unsupervised_start_index, max_factor_prior_batches),
+                       (prior_factors_path, cost_criteria, unsupervised_start_index, max_factor_prior_batches,
+                        prior_factors_allow_pickle),
                        stopping_criteria_forecast_coeff, stopping_criteria_factor_coeff,
                        stopping_criteria_cosSim_coeff, save_plots)
 

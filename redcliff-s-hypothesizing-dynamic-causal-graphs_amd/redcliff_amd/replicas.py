@@ -349,7 +349,8 @@ class ReplicaPack:
 
     def _fit(self, save_dir, X_train, X_val, max_iter, lookback=5, check_every=50, verbose=0, GC=None,
              deltaConEps=0.1, in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=1.,
-             stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., output_length=1, save_plots=False):
+             stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., output_length=1, save_plots=False,
+             cost_criteria="CosineSimilarity", unsupervised_start_index=0, max_factor_prior_batches=10):
         """R fits of ``fit()`` (...withStateSmoothing.py:1175-1647) in one packed launch chain.
 
         Every replica follows exactly the rules (and the host code, FitTracker) of a single fit:
@@ -410,13 +411,16 @@ class ReplicaPack:
         # every replica ends exactly where its own fit() would.  No speculation across a
         # checkpoint epoch (the files hold epoch `it`'s state) or past max_iter.
         # "pretrain_factor" modes re-order each fit's factors before epoch num_pretrain_epochs
-        # (...withStateSmoothing.py:1318-1326, initialize_factors_with_prior with fit()'s defaults)
+        # (...withStateSmoothing.py:1318-1326, initialize_factors_with_prior with fit()'s cost_criteria,
+        # unsupervised_start_index and max_factor_prior_batches)
         reorder_at = m0.num_pretrain_epochs if "pretrain_factor" in m0.training_mode else None
 
         def launch_train(ep):
             if ep == reorder_at:
-                for r in active:
-                    models[r].initialize_factors_with_prior(X_train=X_train)
+                for r in active:  # with the caller's settings, as each single fit's _prior_hook passes them
+                    models[r].initialize_factors_with_prior(X_train=X_train, cost_criteria=cost_criteria,
+                                                            unsupervised_start_index=unsupervised_start_index,
+                                                            max_batches=max_factor_prior_batches)
             self.conf.zero_()
             self.run_epoch(ep, train, active, set_modes=False)
 

@@ -76,6 +76,76 @@ class FlipNearTies:
         torch.relu, F_.relu, torch.norm = self.saved
 
 
+class PermutedContraction:
+    """The oracle's factor layer-0 contraction (Conv1d over p channels x L lags, OMLP.forward)
+    with its input channels taken in a permuted order: the same mathematics, another fp32
+    summation order of the pre-activations z.  Window permutations (perm<s>) only reorder the
+    batch reductions; this realisation varies what the HIP path varies too (the matrix-core
+    k-order of the p*L-term contraction), so near-tie hidden-unit gates can fall either way."""
+
+    def __init__(self, p, seed):
+        self.perm = torch.from_numpy(np.random.RandomState(seed).permutation(p))
+
+    def __enter__(self):
+        from oracle import redcliff_oracle as R
+        self.saved = R.OMLP.forward
+        perm = self.perm
+
+        def forward(mod, X):
+            z = X.transpose(2, 1)
+            for i, layer in enumerate(mod.layers):
+                if i == 0:
+                    z = torch.nn.functional.conv1d(z[:, perm, :], layer.weight[:, perm, :], layer.bias)
+                else:
+                    z = layer(torch.relu(z))
+            return z.transpose(2, 1)
+        R.OMLP.forward = forward
+        return self
+
+    def __exit__(self, *exc):
+        from oracle import redcliff_oracle as R
+        R.OMLP.forward = self.saved
+
+
+class GateMargins:
+    """Records, for every factor hidden unit (k, j, u), the smallest relative distance of its
+    pre-activation from the ReLU threshold over every window of every training step:
+    min |z_bu| / max |z| of its network.  A unit whose margin is within fp32 resolution of the
+    trajectory is a near-tie gate: another fp32 implementation may take the other branch."""
+
+    def __init__(self, model):
+        self.ids = {}
+        for k, f in enumerate(model.factors):
+            for j, net in enumerate(f.networks):
+                self.ids[id(net)] = (k, j)
+        K, p = len(model.factors), len(model.factors[0].networks)
+        h = model.factors[0].networks[0].layers[0].weight.shape[0]
+        self.margin = np.full((K, p, h), np.inf)
+        self.on = False
+
+    def __enter__(self):
+        from oracle import redcliff_oracle as R
+        self.saved = R.OMLP.forward
+        rec = self
+
+        def forward(mod, X):
+            z = mod.layers[0](X.transpose(2, 1))
+            if rec.on and id(mod) in rec.ids:
+                zz = z.detach().abs()
+                m = (zz / zz.max().clamp_min(1e-300)).amin(dim=(0, 2)).double().numpy()
+                k, j = rec.ids[id(mod)]
+                rec.margin[k, j] = np.minimum(rec.margin[k, j], m)
+            for layer in mod.layers[1:]:
+                z = layer(torch.relu(z))
+            return z.transpose(2, 1)
+        R.OMLP.forward = forward
+        return self
+
+    def __exit__(self, *exc):
+        from oracle import redcliff_oracle as R
+        R.OMLP.forward = self.saved
+
+
 def build_oracle(cfg, seed=0):
     from oracle.redcliff_oracle import OracleREDCLIFF, reference_coeffs
     coeff = reference_coeffs(cfg["K"], cfg["p"])
@@ -97,7 +167,8 @@ def gc_of(mod, Xin):
 def trajectory(kind, cfg, X, Y, Xv, Yv, nb, threads=3):
     """One oracle realisation of the schedule (pretrain, acclimate, combined; nb batches of
     cfg["B"] windows each): kind "fp32", "perm<s>" (rows of every batch permuted with seed s),
-    "fp64" or "fp64flip".  Returns its state (numpy), validation values, lag-free GC on the
+    "chperm<s>" (the factor contraction's channel order permuted, PermutedContraction), "fp64"
+    or "fp64flip".  Returns its state (numpy), validation values, lag-free GC on the
     first 8 validation windows and the flipped-decision counts."""
     from oracle.redcliff_oracle import make_optimizers
     torch.set_num_threads(threads)
@@ -112,8 +183,12 @@ def trajectory(kind, cfg, X, Y, Xv, Yv, nb, threads=3):
         perm = torch.from_numpy(np.random.RandomState(100 + int(kind[4:])).permutation(B))
     flip = FlipNearTies() if kind == "fp64flip" else None
     ctx = Float64Default() if dbl else _Null()
-    with ctx:
+    cperm = PermutedContraction(cfg["p"], 200 + int(kind[6:])) if kind.startswith("chperm") else _Null()
+    gates = GateMargins(o) if kind == "fp64" else None
+    with ctx, cperm, (gates if gates is not None else _Null()):
         oA, oB = make_optimizers(o, LR, 1e-4, 1e-4, LR, 1e-4, 1e-4)
+        if gates is not None:
+            gates.on = True
         with (flip if flip is not None else _Null()):
             for epoch in (0, 1, 2):
                 for bi in range(nb):
@@ -123,6 +198,8 @@ def trajectory(kind, cfg, X, Y, Xv, Yv, nb, threads=3):
                     if dbl:
                         Xb, Yb = Xb.double(), Yb.double()
                     o.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+        if gates is not None:
+            gates.on = False
         val = o.validate([(Xv.double(), Yv.double()) if dbl else (Xv, Yv)])
         o.eval()
         Lm = max(cfg["L"], cfg["F"])
@@ -131,7 +208,8 @@ def trajectory(kind, cfg, X, Y, Xv, Yv, nb, threads=3):
             g = gc_of(o, Xg.double() if dbl else Xg)
     sd = dict((k, v.detach().numpy().copy()) for k, v in o.state_dict().items() if not k.startswith("gen_model."))
     return dict(state=sd, val=dict((k, float(v)) for k, v in val.items()), gc=g,
-                flipped=None if flip is None else dict(flip.flipped))
+                flipped=None if flip is None else dict(flip.flipped),
+                gate_margin=None if gates is None else gates.margin)
 
 
 class _Null:

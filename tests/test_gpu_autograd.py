@@ -200,3 +200,41 @@ def test_embedder_forward_on_loaded_model():
     with torch.no_grad():
         w_copy, _ = m3.factor_score_embedder(x)
     np.testing.assert_array_equal(w_copy.cpu().numpy(), w_live.cpu().numpy())
+
+
+def test_inplace_parameter_change_before_backward_is_caught():
+    """The fused forward saves its parameters for backward: an in-place change between forward
+    and backward trips autograd's version check (as stock modules do) instead of differentiating
+    the new values."""
+    d, meta, m, _ = pair("dgcnn_c1")
+    m.train()
+    Xb, _ = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    x_sim, _, _, _ = m(Xb[:, :Lm, :].cuda())
+    with torch.no_grad():
+        m.factors[0].networks[0].layers[0].weight.add_(1e-3)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        x_sim.sum().backward()
+
+
+def test_eval_graph_uses_forward_time_batchnorm_statistics():
+    """An eval-mode forward's backward uses the running statistics of that forward, even when a
+    train-mode forward advanced them before the backward runs."""
+    d, meta, m, _ = pair("dgcnn_c1")
+    Xb, _ = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    X = Xb[:, :Lm, :].cuda()
+    params = [p for p in m.parameters() if p.requires_grad]
+    m.eval()
+    want = torch.autograd.grad(m(X)[0].sum(), params, allow_unused=True)
+    out = m(X)[0]
+    m.train()
+    with torch.no_grad():
+        m(X)  # advances the BatchNorm running statistics
+    m.eval()
+    got = torch.autograd.grad(out.sum(), params, allow_unused=True)
+    for i, (a, b) in enumerate(zip(got, want)):
+        if a is None or b is None:
+            assert a is None and b is None
+            continue
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg="param %d" % i)

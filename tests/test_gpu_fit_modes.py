@@ -176,26 +176,35 @@ def test_reorder_on_the_generic_path(name):
     assert [id(f) for f in m.factors] == [id(old[i]) for i in want]
 
 
-def test_prior_factors_path(tmp_path, monkeypatch):
+@pytest.mark.parametrize("form", ["state_dict", "module"])
+def test_prior_factors_path(form, tmp_path, monkeypatch):
     """fit(prior_factors_path=...) (:1318-1326 at epoch 0 -> :149-206).  The reference replaces
     the factors by the saved model's and re-orders them; its optimizerB still holds the replaced
     parameters, so the loaded factors never change again, while the embedder keeps training
     against them.  Twin: the same model given the permuted prior factors by hand and trained
     with optimizerB at lr 0 (the fused Adam then leaves the factors bit-identical), so the
-    embedder's updates through the optimizerB-less steps must match it bit for bit."""
+    embedder's updates through the optimizerB-less steps must match it bit for bit.
+    form "state_dict": the prior's state_dict, loaded weights-only (the default); "module": the
+    pickled module the reference writes, loaded only with prior_factors_allow_pickle=True."""
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "mfma")
     train, val = data(64 * 2, seed=12), data(64, seed=13)
     s, fc, adj, lrB, lrA = GRID[0]
     mode = "pretrain_embedder_then_acclimate_factors_then_combined"
     prior = mk(9, fc, adj, mode, pre=1, acc=1)
     path = str(tmp_path / "prior.bin")
-    torch.save(prior, path)
+    torch.save(prior.state_dict() if form == "state_dict" else prior, path)
     pf = [[p.detach().cpu().numpy().copy() for p in f.parameters()] for f in prior.factors]
 
     m = mk(s, fc, adj, mode, pre=1, acc=1)
     order = expected_order(m, train)
     oA, oB = opts(m, lrB, lrA)
-    m.fit(None, train, oA, oB, 4, 1, 1, 4, val, lookback=1, check_every=1, verbose=0, prior_factors_path=path)
+    if form == "module":  # a pickled module needs the explicit opt-in
+        m0 = mk(s, fc, adj, mode, pre=1, acc=1)
+        a0, b0 = opts(m0, lrB, lrA)
+        with pytest.raises(RuntimeError, match="prior_factors_allow_pickle"):
+            m0.fit(None, train, a0, b0, 4, 1, 1, 4, val, lookback=1, check_every=1, verbose=0, prior_factors_path=path)
+    m.fit(None, train, oA, oB, 4, 1, 1, 4, val, lookback=1, check_every=1, verbose=0, prior_factors_path=path,
+          prior_factors_allow_pickle=(form == "module"))
     torch.cuda.synchronize()
     for i, f in enumerate(m.factors):
         for got, want in zip(f.parameters(), pf[order[i]]):

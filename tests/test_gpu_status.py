@@ -70,12 +70,12 @@ def test_status_clean_after_normal_steps():
 def test_vector_factor_path_names_its_batch_limit(monkeypatch):
     """REDCLIFF_FAC_PATH=vector on a batch whose per-window LDS tiles exceed 64 KiB: a clear
     ELIMIT naming the largest batch that fits (the default path switches to the matrix cores)."""
+    from test_gpu_data_parallel import CFG as TST, _model
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
-    m = make(0, 10.0, 0.1)
-    oA, oB = opts(m, 5e-4, 2e-4)
+    m, oA, oB = _model()  # TST shape: K = 9 factors, 512 windows (the configs[3] large-shard case)
     rng = np.random.RandomState(0)
-    X = torch.from_numpy(rng.randn(1024, 21, 10).astype(np.float32))
-    Y = torch.zeros(1024, 4, 1)
-    Y[:, 0] = 10.0
+    X = torch.from_numpy(rng.randn(512, TST["T"], TST["p"]).astype(np.float32))
+    Y = torch.zeros(512, TST["K"], TST["T"])
+    Y[:, 0] = 1.0
     with pytest.raises(RuntimeError, match="use batches of at most"):
         m.batch_update(2, 0, X, Y, oA, oB, 1)
