@@ -227,14 +227,27 @@ def cpu_fits_per_hour(c, seconds, steps_per_fit):
     """The reference's CPU grid search: one fit per core, each single-threaded
     (torch.set_num_threads(1)).  P concurrent one-thread oracle processes (P =
     the CPUs available to this job) run combined-phase batch_updates for ~`seconds`; the
-    aggregate step rate over all of them gives fits/hour (training steps only)."""
+    aggregate step rate over all of them gives fits/hour (training steps only).  At most 15
+    workers: the GPU box admits 16 processes with the card open, this one included, and a
+    spawned interpreter that imports torch counts even with the devices hidden from it."""
     import multiprocessing as mp
-    P = host_cores()
+    P = min(host_cores(), int(os.environ.get("REDCLIFF_CPU_FIT_PROCS", 15)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_cpu_fit_worker, args=(c, seconds, q)) for _ in range(P)]
-    for pr in procs:
-        pr.start()
+    hide = ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")
+    saved = dict((k, os.environ.get(k)) for k in hide)
+    try:
+        for k in hide[:2]:
+            os.environ[k] = ""  # the workers are CPU-only: inherited at spawn
+        for pr in procs:
+            pr.start()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     res = [q.get(timeout=600) for _ in procs]
     for pr in procs:
         pr.join(timeout=60)
@@ -243,6 +256,7 @@ def cpu_fits_per_hour(c, seconds, steps_per_fit):
     rate = steps / wall  # aggregate steps per second over the P processes
     return {"value": round(rate * 3600.0 / steps_per_fit, 2), "unit": "fits/hour", "cores": P,
             "host_cpu_count": os.cpu_count(), "kind": "port",
+            "host_cores_available": host_cores(),
             "sample": "%d concurrent single-thread oracle processes (one fit per core, the reference's grid), "
                       "%d combined-phase batch_updates of B=%d in %.1f s in all (%.3f s per step per process) x %d "
                       "training steps per fit; validation and GC tracking NOT counted, so this over-states the CPU "

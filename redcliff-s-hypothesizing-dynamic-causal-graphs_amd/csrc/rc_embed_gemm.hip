@@ -310,11 +310,17 @@ int ds_splits(int B) {
 
 }  // namespace
 
+// GEMM-shaped embedder: large p (C5), or a packed grid search of >= RC_EMB_GEMM_R replicas, whose
+// products batched over the replicas keep the matrix cores busy where the fused node-chunk
+// kernels' per-workgroup latency chains set the time.  REDCLIFF_EMB_PATH=gemm|fused overrides.
+#ifndef RC_EMB_GEMM_R
+#define RC_EMB_GEMM_R 16
+#endif
 bool rc_emb_use_gemm(const RedcliffDims& d) {
   const char* v = getenv("REDCLIFF_EMB_PATH");  // read per call: tests switch paths in-process
   if (v && !strcmp(v, "gemm")) return d.F <= 64;
   if (v && !strcmp(v, "fused")) return false;
-  return d.p >= 32 && d.F <= 64;
+  return (d.p >= 32 || d.R >= RC_EMB_GEMM_R) && d.F <= 64 && d.M1 <= 64;
 }
 
 void rc_emb_partial_layout(StepCtx& c, bool gemm) {
@@ -335,6 +341,11 @@ void rc_emb_partial_layout(StepCtx& c, bool gemm) {
   }
 }
 
+// Products of the GEMM-shaped embedder: one launch per product for ALL replicas of the step (the
+// replica axis of rc_gemm.h: operands of replica r at r * c.wss in the workspace and r * c.es in
+// the embedder parameters), so a packed grid search runs the same launch chain as one fit.  Each
+// output keeps the in-order fmaf chain of the one-replica launch, so packed and single fits agree
+// bit for bit.
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
@@ -343,23 +354,26 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
   hipLaunchKernelGGL(k_lemb_prep, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_lemb_prep");
   const int nsp = fc1_splits(d), Ks = p * H / nsp;
-  for (int i = 0; i < c.nrep && !e; ++i) {
-    const int r = rc_rep_host(c, i);
-    float* ws = c.ws + r * c.wss;
-    const float* E = c.emb + r * c.es;
-    float* T = ws + c.wo.T;
-    // T_i[b] = S_i x_bn[b]  (p x p x F per window)
-    for (int i = 1; i < n && !e; ++i)
-      e = rc_gemm_launch(rc_gemm_args(0, 0, p, F, p, ws + c.wo.S + (int64_t)i * p * p, p, 0, T, nF, pnF, T + i * F, nF,
-                                      pnF), B, s, "emb T_i");
-    if (e) break;
-    // R = relu(T gcW): (B*p) x (n*F) x H
+  float* ws = c.ws;  // replica 0's slice; the replica axis adds r * c.wss
+  const float* E = c.emb;
+  float* T = ws + c.wo.T;
+  // T_i[b] = S_i x_bn[b]  (p x p x F per window)
+  for (int i = 1; i < n && !e; ++i) {
+    RcGemm g = rc_gemm_args(0, 0, p, F, p, ws + c.wo.S + (int64_t)i * p * p, p, 0, T, nF, pnF, T + i * F, nF, pnF);
+    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
+    e = rc_gemm_launch(g, B, s, "emb T_i");
+  }
+  if (!e) {  // R = relu(T gcW): (B*p) x (n*F) x H
     RcGemm g = rc_gemm_args(0, 0, B * p, H, (int)nF, T, nF, 0, E + c.eo.gcW, H, 0, ws + c.wo.R, H, 0);
     g.epi = RC_EPI_RELU;
-    if ((e = rc_gemm_launch(g, 1, s, "emb graph conv"))) break;
-    // fc1 partials over nsp slices of the p*H contraction
-    e = rc_gemm_launch(rc_gemm_args(0, 1, B, M1, Ks, ws + c.wo.R, (int64_t)p * H, Ks, E + c.eo.fc1W, (int64_t)p * H, Ks,
-                                    ws + c.wo.f1p, M1, (int64_t)d.Bmax * M1), nsp, s, "emb fc1");
+    rc_gemm_reps(g, c, c.wss, c.es, c.wss);
+    e = rc_gemm_launch(g, 1, s, "emb graph conv");
+  }
+  if (!e) {  // fc1 partials over nsp slices of the p*H contraction
+    RcGemm g = rc_gemm_args(0, 1, B, M1, Ks, ws + c.wo.R, (int64_t)p * H, Ks, E + c.eo.fc1W, (int64_t)p * H, Ks,
+                            ws + c.wo.f1p, M1, (int64_t)d.Bmax * M1);
+    rc_gemm_reps(g, c, c.wss, c.es, c.wss);
+    e = rc_gemm_launch(g, nsp, s, "emb fc1");
   }
   if (e) return e;
   hipLaunchKernelGGL(k_lemb_head, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
@@ -378,43 +392,49 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
     e = rc_check(hipGetLastError(), "k_lemb_gfc");
   }
   const int nds = ds_splits(B), wps = B / nds;
-  for (int i = 0; i < c.nrep && !e; ++i) {
-    const int r = rc_rep_host(c, i);
-    float* ws = c.ws + r * c.wss;
-    const float* E = c.emb + r * c.es;
-    const float* T = ws + c.wo.T;
-    const float* df1 = ws + c.wo.edf1;
-    // dfc1W = df1^T R   (M1 x B x p*H), applied by the final kernel's Adam
-    if ((e = rc_gemm_launch(rc_gemm_args(1, 0, M1, (int)pH, B, df1, M1, 0, ws + c.wo.R, pH, 0, ws + c.wo.gfc1, pH, 0),
-                            1, s, "emb dfc1W")))
-      break;
-    // dZ = [R > 0] (df1 fc1W)   (B x M1 x p*H)
+  float* ws = c.ws;  // replica 0's slice; the replica axis adds r * c.wss
+  const float* E = c.emb;
+  const float* T = ws + c.wo.T;
+  const float* df1 = ws + c.wo.edf1;
+  if (!e) {  // dfc1W = df1^T R   (M1 x B x p*H), applied by the final kernel's Adam
+    RcGemm g = rc_gemm_args(1, 0, M1, (int)pH, B, df1, M1, 0, ws + c.wo.R, pH, 0, ws + c.wo.gfc1, pH, 0);
+    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
+    e = rc_gemm_launch(g, 1, s, "emb dfc1W");
+  }
+  if (!e) {  // dZ = [R > 0] (df1 fc1W)   (B x M1 x p*H)
     RcGemm g = rc_gemm_args(0, 0, B, (int)pH, M1, df1, M1, 0, E + c.eo.fc1W, pH, 0, ws + c.wo.dZ, pH, 0);
     g.epi = RC_EPI_MASK;
     g.aux = ws + c.wo.R;
     g.ldaux = pH;
-    if ((e = rc_gemm_launch(g, 1, s, "emb dZ"))) break;
-    // dW slices: dWi[s] = T[rows s]^T dZ[rows s], p slices of B rows of the (b, c) axis
-    if ((e = rc_gemm_launch(rc_gemm_args(1, 0, (int)nF, H, B, T, nF, (int64_t)B * nF, ws + c.wo.dZ, H, (int64_t)B * H,
-                                         ws + c.wo.dWi, H, nF * H), p, s, "emb dW")))
-      break;
-    // dT = dZ gcW^T   ((B*p) x H x n*F)
-    if ((e = rc_gemm_launch(rc_gemm_args(0, 1, B * p, (int)nF, H, ws + c.wo.dZ, H, 0, E + c.eo.gcW, H, 0, ws + c.wo.edT,
-                                         nF, 0), 1, s, "emb dT")))
-      break;
-    // dx_bn[b] = Af dT[b]   (p x p*n x F per window)
-    if ((e = rc_gemm_launch(rc_gemm_args(0, 0, p, F, p * n, ws + c.wo.eAf, (int64_t)p * n, 0, ws + c.wo.edT, F, pnF,
-                                         ws + c.wo.edX, F, (int64_t)p * F), B, s, "emb dx_bn")))
-      break;
-    // dS_i slices: sum over the windows of group z of dT_i[b] x_bn[b]^T   (p x wps*F x p)
-    for (int i = 1; i < n && !e; ++i) {
-      RcGemm q = rc_gemm_args(0, 1, p, p, wps * F, ws + c.wo.edT + i * F, nF, (int64_t)wps * pnF, T, nF, (int64_t)wps * pnF,
-                              ws + c.wo.dS + (int64_t)i * p * p, p, c.dsS);
-      q.Kblk = F;
-      q.rA = pnF;
-      q.rB = pnF;
-      e = rc_gemm_launch(q, nds, s, "emb dS");
-    }
+    rc_gemm_reps(g, c, c.wss, c.es, c.wss, c.wss);
+    e = rc_gemm_launch(g, 1, s, "emb dZ");
+  }
+  if (!e) {  // dW slices: dWi[s] = T[rows s]^T dZ[rows s], p slices of B rows of the (b, c) axis
+    RcGemm g = rc_gemm_args(1, 0, (int)nF, H, B, T, nF, (int64_t)B * nF, ws + c.wo.dZ, H, (int64_t)B * H, ws + c.wo.dWi,
+                            H, nF * H);
+    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
+    e = rc_gemm_launch(g, p, s, "emb dW");
+  }
+  if (!e) {  // dT = dZ gcW^T   ((B*p) x H x n*F)
+    RcGemm g = rc_gemm_args(0, 1, B * p, (int)nF, H, ws + c.wo.dZ, H, 0, E + c.eo.gcW, H, 0, ws + c.wo.edT, nF, 0);
+    rc_gemm_reps(g, c, c.wss, c.es, c.wss);
+    e = rc_gemm_launch(g, 1, s, "emb dT");
+  }
+  if (!e) {  // dx_bn[b] = Af dT[b]   (p x p*n x F per window)
+    RcGemm g = rc_gemm_args(0, 0, p, F, p * n, ws + c.wo.eAf, (int64_t)p * n, 0, ws + c.wo.edT, F, pnF, ws + c.wo.edX,
+                            F, (int64_t)p * F);
+    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
+    e = rc_gemm_launch(g, B, s, "emb dx_bn");
+  }
+  // dS_i slices: sum over the windows of group z of dT_i[b] x_bn[b]^T   (p x wps*F x p)
+  for (int i = 1; i < n && !e; ++i) {
+    RcGemm q = rc_gemm_args(0, 1, p, p, wps * F, ws + c.wo.edT + i * F, nF, (int64_t)wps * pnF, T, nF, (int64_t)wps * pnF,
+                            ws + c.wo.dS + (int64_t)i * p * p, p, c.dsS);
+    q.Kblk = F;
+    q.rA = pnF;
+    q.rB = pnF;
+    rc_gemm_reps(q, c, c.wss, c.wss, c.wss);
+    e = rc_gemm_launch(q, nds, s, "emb dS");
   }
   if (e) return e;
   const int ndr = (int)(((int64_t)(n - 1) * p * p + RC_BLOCK - 1) / RC_BLOCK);

@@ -145,11 +145,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
         ws[c.wo.gq + ((int64_t)ub * KP + kj) * Q + q] = sq;
       }
     }
+    // k-steps only up to Q (rounded to the step of 2): the zero padding to Qp adds exact zeros
+    // (k_fac_bwd_mfma's recompute runs the same (Q + 1) / 2 steps, so both give the same bits)
+    const int kmax = Q - q0;
 #pragma unroll
     for (int k0 = 0; k0 < MF_QC; k0 += 2) {
-      const float a = Xs[arow][k0 + kh];
-      const float bv = Ws[bcol][k0 + kh];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+      if (k0 < kmax) {
+        const float a = Xs[arow][k0 + kh];
+        const float bv = Ws[bcol][k0 + kh];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc, 0, 0, 0);
+      }
     }
   }
   // ---- epilogue
@@ -569,7 +574,7 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW ==
       f32x16 zc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) zc[i] = 0.f;
-      const int nk = Qp >> 1;
+      const int nk = (Q + 1) >> 1;  // the forward's k-steps (up to Q, not the padding to Qp)
 #pragma unroll
       for (int kk = 0; kk < 32; ++kk) {
         if (kk < nk) zc = __builtin_amdgcn_mfma_f32_32x32x2f32(Xs[l31][2 * kk + kh], wB[kk], zc, 0, 0, 0);

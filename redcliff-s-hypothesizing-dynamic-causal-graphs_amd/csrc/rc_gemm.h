@@ -31,6 +31,12 @@ struct RcGemm {
   int Kblk; int64_t rA, rB;
   int epi;
   const float* aux; int64_t ldaux, sAux;
+  // replica axis (packed grid-search fits): grid z = nrep x batch, z = i * batch + zb; operand
+  // bases advance by replica r = rmap[i] (or i when rident) times the r-strides.  nrep = 1,
+  // strides 0: a plain batched product.
+  int batch, nrep, rident;
+  int64_t qA, qB, qC, qAux;
+  uint8_t rmap[RC_MAX_ACTIVE];
 };
 
 inline RcGemm rc_gemm_args(int ta, int tb, int M, int N, int K, const float* A, int64_t lda, int64_t sA,
@@ -43,7 +49,28 @@ inline RcGemm rc_gemm_args(int ta, int tb, int M, int N, int K, const float* A, 
   g.alpha = 1.f; g.beta = 0.f;
   g.Kblk = K > 0 ? K : 1; g.rA = 0; g.rB = 0;
   g.epi = RC_EPI_NONE; g.aux = nullptr; g.ldaux = 0; g.sAux = 0;
+  g.batch = 1; g.nrep = 1; g.rident = 1; g.qA = g.qB = g.qC = g.qAux = 0;
   return g;
+}
+
+// Replica axis of a step's products: c.nrep replicas (c's active list), operand r-strides.
+inline void rc_gemm_reps(RcGemm& g, const StepCtx& c, int64_t qA, int64_t qB, int64_t qC, int64_t qAux = 0) {
+  g.nrep = c.nrep;
+  g.rident = c.rident;
+  for (int i = 0; i < c.nrep && i < RC_MAX_ACTIVE; ++i) g.rmap[i] = c.rmap[i];
+  g.qA = qA; g.qB = qB; g.qC = qC; g.qAux = qAux;
+}
+
+// The replica of grid slice z and the slice inside it: (replica, zb).
+struct RcGemmZ {
+  int64_t r;
+  int zb;
+};
+__device__ inline RcGemmZ rc_gemm_z(const RcGemm& g) {
+  const int z = blockIdx.z;
+  if (g.nrep == 1) return RcGemmZ{0, z};
+  const int i = z / g.batch, zb = z - i * g.batch;
+  return RcGemmZ{g.rident ? i : (int)g.rmap[i], zb};
 }
 
 // TT x TT output tile per 256-thread workgroup (TT = 64: 4x4 outputs per thread; TT = 32:
@@ -54,10 +81,12 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   constexpr int TP = TT / 16;           // outputs per thread along each tile dimension
   constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
   rc_critical_priority();
-  const int bz = blockIdx.z;
-  const float* A = g.A + bz * g.sA;
-  const float* B = g.B + bz * g.sB;
-  float* C = g.C + bz * g.sC;
+  const RcGemmZ zz = rc_gemm_z(g);
+  const int bz = zz.zb;
+  const float* A = g.A + bz * g.sA + zz.r * g.qA;
+  const float* B = g.B + bz * g.sB + zz.r * g.qB;
+  float* C = g.C + bz * g.sC + zz.r * g.qC;
+  const float* aux = g.aux ? g.aux + zz.r * g.qAux : nullptr;
   const int n0 = blockIdx.x * TT, m0 = blockIdx.y * TT;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const RcDiv dkb(g.Kblk);
@@ -131,7 +160,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
       float* cp = C + (int64_t)gm * g.ldc + gn;
       float v = g.beta == 0.f ? g.alpha * acc[i][j] : g.alpha * acc[i][j] + g.beta * *cp;
       if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
-      else if (g.epi == RC_EPI_MASK) v = g.aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
+      else if (g.epi == RC_EPI_MASK) v = aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
       *cp = v;
     }
   }
@@ -148,10 +177,12 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
   constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
   constexpr int QT = TT / 2;                      // quarter tile per wave
   rc_critical_priority();
-  const int bz = blockIdx.z;
-  const float* A = g.A + bz * g.sA;
-  const float* B = g.B + bz * g.sB;
-  float* C = g.C + bz * g.sC;
+  const RcGemmZ zz = rc_gemm_z(g);
+  const int bz = zz.zb;
+  const float* A = g.A + bz * g.sA + zz.r * g.qA;
+  const float* B = g.B + bz * g.sB + zz.r * g.qB;
+  float* C = g.C + bz * g.sC + zz.r * g.qC;
+  const float* aux = g.aux ? g.aux + zz.r * g.qAux : nullptr;
   const int n0 = blockIdx.x * TT, m0 = blockIdx.y * TT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = QT * (wv >> 1), wn = QT * (wv & 1);
@@ -226,14 +257,29 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
     const float a = TT == 64 ? acc32[reg] : acc16[reg];
     float v = g.beta == 0.f ? g.alpha * a : g.alpha * a + g.beta * *cp;
     if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
-    else if (g.epi == RC_EPI_MASK) v = g.aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
+    else if (g.epi == RC_EPI_MASK) v = aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
     *cp = v;
   }
 }
 
-inline int rc_gemm_launch(const RcGemm& g, int batch, hipStream_t s, const char* what) {
-  if (g.M <= 0 || g.N <= 0 || batch <= 0) return 0;
+inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char* what) {
+  if (g0.M <= 0 || g0.N <= 0 || batch <= 0 || g0.nrep <= 0) return 0;
   if (batch > 65535) { rc_set_error("%s: batch %d > 65535", what, batch); return REDCLIFF_ELIMIT; }
+  RcGemm g = g0;
+  g.batch = batch;
+  if ((int64_t)batch * g.nrep > 65535) {  // grid z limit: the replicas in groups
+    const int per = 65535 / batch;
+    for (int i0 = 0; i0 < g0.nrep; i0 += per) {
+      RcGemm h = g;
+      h.nrep = g0.nrep - i0 < per ? g0.nrep - i0 : per;
+      h.rident = 0;
+      for (int i = 0; i < h.nrep; ++i) h.rmap[i] = (uint8_t)(g0.rident ? i0 + i : g0.rmap[i0 + i]);
+      const int e = rc_gemm_launch(h, batch, s, what);
+      if (e) return e;
+    }
+    return 0;
+  }
+  batch *= g.nrep;  // grid z: replicas x slices
   // fewer than two 64x64 tiles per CU: 32x32 tiles (more workgroups in flight to hide the
   // operand latency of these short products).  REDCLIFF_GEMM_TILE=64|32 overrides (tuning);
   // REDCLIFF_GEMM_CORE=valu selects the vector-ALU fmaf kernel (measurements).

@@ -271,15 +271,16 @@ def test_stress_config_error_budget_vs_fp64():
 
     Outliers are counted per DECISION: the entries of one factor hidden unit (its W0 row, b0 and
     W1 entries) move together when that unit's ReLU gate falls the other way for some window, so
-    a unit with any outlier counts once.  Required:
-      * every outlier unit of the HIP path is a NEAR-TIE gate of the float64 trajectory: for some
-        window of some training step its pre-activation came within 1e-4 of zero relative to its
-        network's largest (c5_oracle_runs.GateMargins) -- the HIP path's p*L = 1280-term
-        contraction is one fmaf chain on the matrix cores, the CPU's is vectorised, so its fp32
-        error is its own and such gates can fall either way; at most 1e-3 of the 12,800 units;
-        inside them no entry further than 2 lr (two Adam steps) from float64;
-      * outside its outlier units, at most max(reference runs' outlier entries + 2, one per
-        million) outlier entries, none exceeding 2x the reference runs' worst excess or 1e-2 lr;
+    a unit with any outlier counts once.  A GATE-FLIP unit is an outlier unit whose float64 gate
+    is a near-tie: for some window of some training step its pre-activation came within 1e-6 (the
+    fp32 resolution of the p*L = 1280-term contraction, FlipNearTies' band) of zero relative to its
+    network's largest (c5_oracle_runs.GateMargins) -- the HIP path's contraction is one fmaf chain
+    on the matrix cores, the CPU's is vectorised, so its fp32 error is its own and such gates can
+    fall either way.  Required:
+      * at most 1e-3 of the 12,800 units are gate-flip units, and inside them no entry is further
+        than 2 lr (two Adam steps) from float64;
+      * every other outlier entry is fp32 tail: at most max(reference runs' tail entries + 2, one
+        per million) of them, none exceeding 2x the reference runs' worst excess or 1e-2 lr;
       * losses within |oracle_fp32 - fp64| + 1e-4 |fp64|;
       * GC extraction on the HIP model's own final parameters within 1e-4 relative of the float64
         oracle's on the same parameters, with identical thresholded graphs.
@@ -304,6 +305,7 @@ def test_stress_config_error_budget_vs_fp64():
     cfg = dict(C5, B=128)
     NB = 2
     lr = C5R.LR
+    TIE = 1e-6  # fp32 tie band of a hidden pre-activation (c5_oracle_runs.FlipNearTies tau_factor)
     X, Y = synth(cfg, NB * cfg["B"], seed=5)
     Xv, Yv = synth(cfg, 40, seed=9)
     kinds = ["fp32", "perm1", "chperm1", "fp64", "fp64flip"]
@@ -353,21 +355,27 @@ def test_stress_config_error_budget_vs_fp64():
             continue
         envelope(k, [got[k]] + [r_["state"][k] for r_ in runs], r64["state"][k].astype(np.float64),
                  r64f["state"][k].astype(np.float64))
-    rest = [[o for o in outl[z] if o[3] not in units[z]] for z in range(nreal)]
-    worst_rest = [max([o[2] for o in rest[z]], default=0.0) for z in range(nreal)]
-    in_units = [o for o in outl[0] if o[3] in units[0]]
-    print("outlier units (hidden-unit gate decisions): HIP %s, oracle runs %s"
-          % (sorted(units[0]), [len(u_) for u_ in units[1:]]))
-    print("outlier entries outside those units: HIP %d (worst excess %.3e), oracle runs %s (worst %s)"
-          % (len(rest[0]), worst_rest[0], [len(r_) for r_ in rest[1:]], ["%.3e" % w for w in worst_rest[1:]]))
-    if in_units:
-        print("HIP outlier units: %d entries, largest |HIP - fp64| %.3e (= %.2f lr)"
-              % (len(in_units), max(o[6] for o in in_units), max(o[6] for o in in_units) / lr))
     margin = r64["gate_margin"]  # (K, p, h): min over steps / windows of |z| / max|z| in float64
-    print("float64 gate margins of the HIP outlier units: %s" % ["%s %.2e" % (u_, margin[u_]) for u_ in sorted(units[0])])
-    print("units with a float64 gate margin below 1e-4: %d of %d" % (int((margin <= 1e-4).sum()), margin.size))
-    assert all(margin[u_] <= 1e-4 for u_ in units[0]), "a HIP outlier unit whose float64 gate is not a near-tie"
-    assert len(units[0]) <= 1e-3 * margin.size, "too many gate-flip units: %d" % len(units[0])
+    print("float64 gate margins of the outlier units: HIP %s" % ["%s %.2e" % (u_, margin[u_]) for u_ in sorted(units[0])])
+    print("units with a float64 gate margin below 1e-6 / 1e-4: %d / %d of %d"
+          % (int((margin <= TIE).sum()), int((margin <= 1e-4).sum()), margin.size))
+    # a gate-flip unit: an outlier unit whose float64 gate came within the fp32 tie band; every
+    # other outlier entry (single entries of units whose gate never came that close, embedder
+    # tensors) is fp32 tail and is held to the tail rule below
+    gate = [set(u_ for u_ in units[z] if margin[u_] <= TIE) for z in range(nreal)]
+    rest = [[o for o in outl[z] if o[3] not in gate[z]] for z in range(nreal)]
+    worst_rest = [max([o[2] for o in rest[z]], default=0.0) for z in range(nreal)]
+    in_units = [o for o in outl[0] if o[3] in gate[0]]
+    print("gate-flip units: HIP %s, oracle runs %s" % (sorted(gate[0]), [len(g_) for g_ in gate[1:]]))
+    print("outlier entries outside them: HIP %d (worst excess %.3e), oracle runs %s (worst %s)"
+          % (len(rest[0]), worst_rest[0], [len(r_) for r_ in rest[1:]], ["%.3e" % w for w in worst_rest[1:]]))
+    for o in sorted(rest[0], key=lambda o: -o[2])[:12]:
+        print("  HIP tail entry %s[%d]: excess %.3e, |HIP - fp64| %.3e (%.3f lr), fp64 %.6e, unit %s"
+              % (o[0], o[1], o[2], o[6], o[6] / lr, o[4], o[3]))
+    if in_units:
+        print("HIP gate-flip units: %d entries, largest |HIP - fp64| %.3e (= %.2f lr)"
+              % (len(in_units), max(o[6] for o in in_units), max(o[6] for o in in_units) / lr))
+    assert len(gate[0]) <= 1e-3 * margin.size, "too many gate-flip units: %d" % len(gate[0])
     assert all(o[6] <= 2.0 * lr for o in in_units), "a gate-flip unit moved further than two Adam steps"
     assert len(rest[0]) <= max(max(len(r_) for r_ in rest[1:]) + 2, 1e-6 * n_entries[0]), \
         "HIP path's fp32 tail beyond the reference's"

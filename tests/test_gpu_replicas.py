@@ -52,11 +52,16 @@ def data(N, seed):
     return [(X[i:i + 64], Y[i:i + 64]) for i in range(0, N, 64)]
 
 
-@pytest.mark.parametrize("path,grid", [("vector", GRID), ("mfma", GRID), ("mfma", GRID8)])
-def test_packed_replicas_match_independent_fits(path, grid, monkeypatch):
+@pytest.mark.parametrize("path,grid,emb", [("vector", GRID, None), ("mfma", GRID, None), ("mfma", GRID8, None),
+                                          ("mfma", GRID, "gemm")])
+def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
     """Both factor paths (the default picks the matrix cores for packs of >= 8 replicas, so the
-    path is pinned here to compare like with like); R = 3 and the packed-only paths at R = 8."""
+    path is pinned here to compare like with like); R = 3 and the packed-only paths at R = 8.
+    emb "gemm": the GEMM-shaped embedder (the default for packs of >= 16 replicas) with its
+    products batched over the replicas, against single fits on the same embedder path."""
     monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    if emb:
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", emb)
     GRID = grid
     from redcliff_amd import ReplicaPack
     train = data(64 * 2 + 24, seed=3)  # two full batches + a ragged one
