@@ -188,7 +188,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.dAadj, K * p * p);
   put(o.dWi, p * d.n * d.F * d.H);
   put(o.dS, (rc_nchunk(d) > 64 ? rc_nchunk(d) : 64) * d.n * p * p);
-  put(o.dgb, p * rc_nchunk(d) * 2 * d.F);
+  put(o.dgb, (p * rc_nchunk(d) > 64 ? p * rc_nchunk(d) : 64) * 2 * d.F);
   put(o.S, d.n * p * p);
   put(o.dZ, p * B * d.H);
   put(o.amat, 8 * p * p);

@@ -921,7 +921,20 @@ template <int NR>
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.y);
+  // the adjacency workgroups (the longest) are dispatched first for ALL replicas: linear
+  // workgroup i < nrep is replica i's adjacency workgroup, the rest run the parameter updates
+  // (R = 128 D4IC grid: the last replicas' adjacency workgroups no longer start behind ~10K
+  // parameter workgroups)
+  const int lin = blockIdx.x + blockIdx.y * gridDim.x;
+  int wx, wy;
+  if (lin < c.nrep) {
+    wx = 0;
+    wy = lin;
+  } else {
+    wy = (lin - c.nrep) / nw;
+    wx = 1 + (lin - c.nrep) - wy * nw;
+  }
+  const int r = rc_rep(c, wy);
   const int p = d.p, n = d.n, F = d.F, H = d.H, K = d.K, M1 = d.M1;
   float* E = c.emb + r * c.es;
   float* Mm = c.embM + r * c.es;
@@ -938,9 +951,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 0);
   // workgroup 0 is the adjacency workgroup (the longest; dispatched first), 1..nw the parameters
-  if (blockIdx.x > 0) {
+  if (wx > 0) {
     if (!stepA) return;
-    const int e = (blockIdx.x - 1) * RC_BLOCK + threadIdx.x;
+    const int e = (wx - 1) * RC_BLOCK + threadIdx.x;
     if (e >= total) return;
     float g = 0.f;
     int64_t idx;
@@ -1017,7 +1030,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   float* dd = dinv + 64;           // [64]
   // dense index e of a stack of p x p matrices -> padded LDS index
   auto at = [&](int e) { const int i = dpv.div(e); return i * P + (e - i * p); };
-  RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 48);
+  RC_PHASE(c.ws, c.wo.total, wx, 48);
   if (stepA) {
     float* A = E + c.eo.A;
     const float* S = ws + c.wo.S;
@@ -1032,7 +1045,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       mreg[u] = in ? Mm[c.eo.A + e] : 0.f;
       vreg[u] = in ? V[c.eo.A + e] : 0.f;
     }
-    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 49);
+    RC_PHASE(c.ws, c.wo.total, wx, 49);
 #ifdef RC_PROBE_DELAY
     // race probe (scripts/race_probe.py): waves >= 1 store their staged operands late, as they
     // do when their loads come back later than wave 0's (e.g. under a concurrent kernel chain)
@@ -1067,12 +1080,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
     // of round 1 ("Root cause of the round-1 A mismatch").
     __syncthreads();
 #endif
-    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 50);
+    RC_PHASE(c.ws, c.wo.total, wx, 50);
     for (int e = tid; e < pp2; e += RC_BLOCK) dL[at(e)] = 0.f;
     lds_rowsum(p, [&](int i, int j) { return Ar[i * P + j]; },
                [&](int i, float s) { dinv[i] = 1.f / sqrtf(s + 1e-10f); });
     __syncthreads();
-    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 51);
+    RC_PHASE(c.ws, c.wo.total, wx, 51);
     // back through S_l = S_{l-1} L, l = n-1 .. 2
     for (int l = n - 1; l >= 2; --l) {
       const float* dSl = dSw + (l - 1) * PP;
@@ -1090,7 +1103,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       }
       __syncthreads();
     }
-    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 52);
+    RC_PHASE(c.ws, c.wo.total, wx, 52);
     // normalize_A backward: L[i][j] = dinv_i relu(A)[i][j] dinv_j, dinv_i = (sum_j relu(A)[i][j] + 1e-10)^-1/2,
     // d(dinv)/d(sum) = -1/2 (sum + 1e-10)^-3/2
     lds_rowsum(p, [&](int i, int j) {
@@ -1115,12 +1128,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       }
     }
     __syncthreads();
-    RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 53);
+    RC_PHASE(c.ws, c.wo.total, wx, 53);
     // supports of the updated A for the next step (after a gradient-only shard step A changes
     // later, in redcliff_adam_apply, and the host refreshes them)
     if (adam) supports_lds(Al, Sl, ws + c.wo.S, dinv, p, n);
   }
-  RC_PHASE(c.ws, c.wo.total, (int)blockIdx.x, 54);
+  RC_PHASE(c.ws, c.wo.total, wx, 54);
   // BatchNorm running statistics (torch: double math, momentum*stat + (1-momentum)*running)
   if (c.nbn > 0 && tid < F) {
     const double* st = c.bns + r * c.bnsr;

@@ -16,7 +16,9 @@
 //           kernel)  ->  dT = dZ gcW^T  ->  dx_bn = sum_i S_i^T dT_i  ->  dS_i = sum_b dT_i x_bn^T
 //           (window-group slices)  ->  BatchNorm affine partials.  The final kernel (rc_embed.hip,
 //           k_emb_final) applies Adam, the Chebyshev / normalize_A backward and the BN running stats.
-// Every contraction is the shared GEMM core (rc_gemm.h); the replica axis is a host loop.
+// The window-sized products of small node counts (p < 32: T_i, dx_bn, dS_i, BN partials) run in
+// the windowed kernels k_lemb_prep_win / k_lemb_win_bwd instead; every other contraction is the
+// shared GEMM core (rc_gemm.h), one launch per product for all replicas.
 #include <cstdlib>
 #include <cstring>
 
@@ -74,42 +76,38 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
   }
 }
 
-// f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (B, R): one window per
-// workgroup, lanes (m, g): g sums every 4th partial (all loads in flight), fixed-order combine.
+// f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (ceil(B / 4), R): one window
+// per wave, lane m sums the partials in 4 interleaved chains (all loads in flight), combined in
+// fixed order; lane k forms w[k] from the wave's relu(f1) by shuffles (no LDS, no barrier).
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y), lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= c.B) return;
   const int M1 = d.M1, K = d.K;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
-  __shared__ float f1s[64];
-  const int tid = threadIdx.x, m = tid >> 2, g = tid & 3;
-  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + m;
-  float v = 0.f;
-  if (m < M1) {
+  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + lane;
+  float t4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (lane < M1) {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {  // nsplit <= 64
-      const int q = g + 4 * u;
-      if (q < nsplit) v += part[(int64_t)q * d.Bmax * M1];
-    }
+    for (int q = 0; q < 64; ++q)  // nsplit <= 64
+      if (q < nsplit) t4[q & 3] += part[(int64_t)q * d.Bmax * M1];
   }
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  if (m < M1 && g == 0) {
-    v += E[c.eo.fc1b + m];
-    f1s[m] = v;
-    ws[c.wo.f1 + (int64_t)b * M1 + m] = v;
+  float v = 0.f;
+  if (lane < M1) {
+    v = ((t4[0] + t4[1]) + (t4[2] + t4[3])) + E[c.eo.fc1b + lane];
+    ws[c.wo.f1 + (int64_t)b * M1 + lane] = v;
   }
-  __syncthreads();
-  // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]): lanes (k, g) over every 4th m
-  const int k = tid >> 2;
+  const float rv = fmaxf(v, 0.f);
+  // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]), m ascending
   float a = 0.f;
-  if (k < K)
-    for (int mm = g; mm < M1; mm += 4) a += E[c.eo.fc2W + k * M1 + mm] * fmaxf(f1s[mm], 0.f);
-  a += __shfl_xor(a, 1);
-  a += __shfl_xor(a, 2);
-  if (k < K && g == 0) ws[c.wo.w + (int64_t)b * K + k] = a + E[c.eo.fc2b + k];
+  const float* w2 = E + c.eo.fc2W + (lane < K ? lane : 0) * M1;
+  for (int mm = 0; mm < M1; ++mm) {
+    const float fm = __shfl(rv, mm, 64);
+    if (lane < K) a = fmaf(w2[mm], fm, a);
+  }
+  if (lane < K) ws[c.wo.w + (int64_t)b * K + lane] = a + E[c.eo.fc2b + lane];
 }
 
 // dL/d(raw embedder output) (the same rule as the node-chunk kernel, rc_embed.hip), dL/df1,
@@ -293,6 +291,190 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dsred(StepCtx c, int nds) {
   dS[0] = (t4[0] + t4[1]) + (t4[2] + t4[3]);
 }
 
+// ---- small-node windowed kernels (p < 32): the per-window products T_i = S_i x_bn (forward) and
+// dx_bn = sum_i S_i^T dT_i, dS_i = sum_b dT_i x_bn^T and the BatchNorm affine partials (backward)
+// are p x p x F per window -- 2000 multiply-adds at D4IC, a 5 % corner of one 64 x 64 matrix-core
+// tile.  As batched GEMMs they cost one latency-bound workgroup per (window, replica) (R = 128:
+// 16384 workgroups, 75 us per product); here one workgroup stages `wb` windows of one replica in
+// LDS with every load in flight and runs the products as fmaf chains in the GEMM's k-order.
+#define RC_LEMB_LDS 12288  // LDS floats for the staged windows of one workgroup (48 KiB)
+
+// dynamic LDS bytes of the two windowed kernels
+__host__ __device__ inline int lemb_win_lds_fwd(const RedcliffDims& d, int wb) {
+  return 4 * (128 + (d.n - 1) * d.p * d.p + wb * d.p * d.F);
+}
+__host__ __device__ inline int lemb_win_lds_bwd(const RedcliffDims& d, int wb) {
+  return 4 * (d.n * d.p * d.p + wb * d.p * d.F * (d.n + 2) + 2 * RC_BLOCK);
+}
+
+// windows per workgroup, 0 when the node count or batch needs the GEMM products (p >= 32, or
+// more than 64 window groups: the dS / BN partial regions hold 64 slots)
+__host__ __device__ inline int lemb_win(const RedcliffDims& d, int B) {
+  if (d.p >= 32 || B < 1) return 0;
+  int wb = RC_LEMB_LDS / (d.p * (d.n + 2) * d.F);
+  if (wb > 16) wb = 16;
+  if (wb < 1 || (B + wb - 1) / wb > 64) return 0;
+  if (lemb_win_lds_bwd(d, wb) > 65536) return 0;  // default dynamic LDS limit
+  return wb;
+}
+
+// x_bn and T_i (i >= 1) of windows [b0, b0 + wb) of replica r.  grid (ceil(B / wb), R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
+  rc_critical_priority();
+  const RedcliffDims& d = c.d;
+  const int r = rc_rep(c, blockIdx.y), b0 = blockIdx.x * wb;
+  const int p = d.p, F = d.F, n = d.n, pF = p * F, pp2 = p * p;
+  const int nw = min(wb, c.B - b0), tot = nw * pF;  // tot <= RC_LEMB_LDS / 3 = 16 * RC_BLOCK
+  const float* E = c.emb + r * c.es;
+  float* ws = c.ws + r * c.wss;
+  const float* X = c.X + r * c.xr + ((c.row0 + b0) * d.T + (c.Lmax - F)) * p;
+  extern __shared__ float sm[];
+  float* alpha = sm;             // [64]
+  float* beta = alpha + 64;      // [64]
+  float* S = beta + 64;          // S_1 .. S_{n-1}
+  float* xb = S + (n - 1) * pp2; // [w][c][f]
+  const int tid = threadIdx.x;
+  const RcDiv dpf(pF), dp(p);
+  float v[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {  // window w's F rows of X are contiguous ([t][c])
+    const int e = u * RC_BLOCK + tid;
+    v[u] = 0.f;
+    if (e < tot) {
+      const int w = dpf.div(e);
+      v[u] = X[(int64_t)w * d.T * p + (e - w * pF)];
+    }
+  }
+  for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) S[e] = ws[c.wo.S + pp2 + e];
+  if (tid < F) {
+    const bool train = c.flags & RC_BN_TRAIN;
+    float mean, inv;
+    if (train) {
+      mean = (float)c.bns[r * c.bnsr + tid];
+      inv = (float)(1.0 / sqrt(c.bns[r * c.bnsr + F + tid] + c.hyp[r].bn_eps));
+    } else {
+      mean = c.rm[r * F + tid];
+      inv = 1.0f / sqrtf(c.rv[r * F + tid] + (float)c.hyp[r].bn_eps);
+    }
+    const float a = inv * E[c.eo.bnw + tid];
+    alpha[tid] = a;
+    beta[tid] = E[c.eo.bnb + tid] - mean * a;
+  }
+  __syncthreads();
+  const int64_t pnF = (int64_t)pF * n, nF = (int64_t)n * F;
+  float* T = ws + c.wo.T + (int64_t)b0 * pnF;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = u * RC_BLOCK + tid;
+    if (e < tot) {
+      const int w = dpf.div(e), rem = e - w * pF, f = dp.div(rem), ch = rem - f * p;
+      const float x = v[u] * alpha[f] + beta[f];
+      xb[w * pF + ch * F + f] = x;
+      T[w * pnF + ch * nF + f] = x;
+    }
+  }
+  if (n == 1) return;
+  __syncthreads();
+  // T_i[w][ch][f] = sum_{c'} S_i[ch][c'] x_bn[w][c'][f]  (c' in order), items (i, w, ch, f)
+  const RcDiv dF(F);
+  for (int e = tid; e < (n - 1) * tot; e += RC_BLOCK) {
+    const int i1 = dpf.div(e) / nw, q = e - i1 * tot;  // q = (w, ch, f)
+    const int w = dpf.div(q), rem = q - w * pF, ch = dF.div(rem), f = rem - ch * F;
+    const float* Si = S + i1 * pp2 + ch * p;
+    const float* xw = xb + w * pF + f;
+    float t = 0.f;
+    for (int cp = 0; cp < p; ++cp) t = fmaf(Si[cp], xw[cp * F], t);
+    T[w * pnF + ch * nF + (i1 + 1) * F + f] = t;
+  }
+}
+
+// Backward of the per-window products for windows [g * wb, g * wb + wb) of replica r: dx_bn
+// (never stored), its BatchNorm affine partials into ws.dgb slot g and the dS_i partials into
+// ws.dS slot g (summed by k_emb_final's adjacency workgroup, c.dsN = c.dgN = ceil(B / wb)).
+// grid (ceil(B / wb), R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
+  rc_critical_priority();
+  const RedcliffDims& d = c.d;
+  const int r = rc_rep(c, blockIdx.y), g = blockIdx.x, b0 = g * wb;
+  const int p = d.p, F = d.F, n = d.n, pF = p * F, pp2 = p * p;
+  const int nw = min(wb, c.B - b0);
+  const int64_t pnF = (int64_t)pF * n, nF = (int64_t)n * F;
+  float* ws = c.ws + r * c.wss;
+  extern __shared__ float sm[];
+  float* S = sm;                    // S_0 .. S_{n-1}
+  float* dT = S + n * pp2;          // [w][c'][i][f]
+  float* x0 = dT + nw * pnF;        // x_bn [w][c][f]
+  float* xr = x0 + nw * pF;         // raw X [w][f][c]
+  float* red = xr + nw * pF;        // [2][RC_BLOCK]
+  const int tid = threadIdx.x;
+  const float* X = c.X + r * c.xr + ((c.row0 + b0) * d.T + (c.Lmax - F)) * p;
+  const float* dTg = ws + c.wo.edT + (int64_t)b0 * pnF;
+  const float* Tg = ws + c.wo.T + (int64_t)b0 * pnF;
+  const RcDiv dpf(pF), dF(F);
+  // stage (every segment's loads in flight together): dT (contiguous over the group's windows),
+  // x_bn = the T_0 rows, raw X, S
+  rc_stage_all(rc_seg<8>(nw * (int)pnF, [&](int e) { return dTg[e]; }, [&](int e, float v) { dT[e] = v; }),
+               rc_seg<4>(nw * pF, [&](int e) {
+                 const int w = dpf.div(e), rem = e - w * pF, ch = dF.div(rem);
+                 return Tg[w * pnF + ch * nF + (rem - ch * F)];
+               }, [&](int e, float v) { x0[e] = v; }),
+               rc_seg<4>(nw * pF, [&](int e) {
+                 const int w = dpf.div(e);
+                 return X[(int64_t)w * d.T * p + (e - w * pF)];
+               }, [&](int e, float v) { xr[e] = v; }),
+               rc_seg<2>(n * pp2, [&](int e) { return ws[c.wo.S + e]; }, [&](int e, float v) { S[e] = v; }));
+  const int f = tid % F, sl = tid / F, nsl = RC_BLOCK / F;
+  float mean = 0.f, inv = 0.f;
+  if (sl < nsl) {
+    if (c.flags & RC_BN_TRAIN) {
+      mean = (float)c.bns[r * c.bnsr + f];
+      inv = (float)(1.0 / sqrt(c.bns[r * c.bnsr + F + f] + c.hyp[r].bn_eps));
+    } else {
+      mean = c.rm[r * F + f];
+      inv = 1.0f / sqrtf(c.rv[r * F + f] + (float)c.hyp[r].bn_eps);
+    }
+  }
+  __syncthreads();
+  // dx_bn[w][ch][f] = sum_{c'} sum_i S_i[c'][ch] dT[w][c'][i][f]  (k = c' n + i, the GEMM's order);
+  // lanes (f, slot) over rows (w, ch): dgamma[f] += dx xhat, dbeta[f] += dx
+  float ag = 0.f, ab = 0.f;
+  if (sl < nsl)
+    for (int row = sl; row < nw * p; row += nsl) {
+      const int w = row / p, ch = row - w * p;
+      const float* dtw = dT + w * pnF + f;
+      float dx = 0.f;
+      for (int cp = 0; cp < p; ++cp)
+        for (int i = 0; i < n; ++i) dx = fmaf(S[i * pp2 + cp * p + ch], dtw[cp * nF + i * F], dx);
+      const float x = xr[w * pF + f * p + ch];
+      ag += dx * ((x - mean) * inv);
+      ab += dx;
+    }
+  red[tid] = ag;
+  red[RC_BLOCK + tid] = ab;
+  // dS_i[ch][c'] partial = sum_w sum_f dT[w][ch][i][f] x_bn[w][c'][f]   (w outer, f inner), i >= 1
+  float* dS = ws + c.wo.dS + (int64_t)g * c.dsS;
+  for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) {
+    const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, ch = rem / p, cp = rem - ch * p;
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) {
+      const float* a = dT + w * pnF + ch * nF + i * F;
+      const float* bq = x0 + w * pF + cp * F;
+      for (int ff = 0; ff < F; ++ff) t = fmaf(a[ff], bq[ff], t);
+    }
+    dS[i * pp2 + rem] = t;
+  }
+  __syncthreads();
+  if (tid < F) {
+    float ga = 0.f, gb = 0.f;
+    for (int q = 0; q < nsl; ++q) {
+      ga += red[q * F + tid];
+      gb += red[RC_BLOCK + q * F + tid];
+    }
+    ws[c.wo.dgb + ((int64_t)g * 2) * F + tid] = ga;
+    ws[c.wo.dgb + ((int64_t)g * 2 + 1) * F + tid] = gb;
+  }
+}
+
 // splits of the fc1 contraction (p*H): largest divisor of p*H that is <= 64 with >= 64 terms each
 int fc1_splits(const RedcliffDims& d) {
   const int pH = d.p * d.H;
@@ -323,10 +505,24 @@ bool rc_emb_use_gemm(const RedcliffDims& d) {
   return (d.p >= 32 || d.R >= RC_EMB_GEMM_R) && d.F <= 64 && d.M1 <= 64;
 }
 
+// windows per workgroup of the windowed kernels for this step (0: the GEMM products);
+// REDCLIFF_EMB_WIN=0 forces the GEMM products (tests, tuning)
+static int lemb_win_step(const StepCtx& c) {
+  const char* v = getenv("REDCLIFF_EMB_WIN");
+  if (v && !strcmp(v, "0")) return 0;
+  return lemb_win(c.d, c.B);
+}
+
 void rc_emb_partial_layout(StepCtx& c, bool gemm) {
   const RedcliffDims& d = c.d;
   const int nch = rc_nchunk(d), n = d.n, p = d.p;
-  if (gemm) {  // dS partials [s][i][cc][c'] over window groups, reduced into slot 0; BN partials over row slices
+  const int wb = gemm ? lemb_win_step(c) : 0;
+  if (wb) {  // k_lemb_win_bwd: one dS / BN record [s][i][cc][c'] / [s][2][F] per window group
+    c.dsN = c.dgN = (c.B + wb - 1) / wb;
+    c.dsCC = p;
+    c.dsS = (int64_t)n * p * p;
+    c.dsI = (int64_t)p * p;
+  } else if (gemm) {  // dS partials [s][i][cc][c'] over window groups, reduced into slot 0; BN partials over row slices
     c.dsN = 1;
     c.dsCC = p;
     c.dsS = (int64_t)n * p * p;
@@ -351,14 +547,22 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F;
   if (F > 64 || M1 > 64) { rc_set_error("GEMM embedder: F <= 64 and M1 <= 64 required"); return REDCLIFF_ELIMIT; }
-  hipLaunchKernelGGL(k_lemb_prep, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c);
-  int e = rc_check(hipGetLastError(), "k_lemb_prep");
+  const int wb = lemb_win_step(c);
+  int e;
+  if (wb) {
+    hipLaunchKernelGGL(k_lemb_prep_win, dim3((B + wb - 1) / wb, c.nrep), dim3(RC_BLOCK), lemb_win_lds_fwd(d, wb), s, c,
+                       wb);
+    e = rc_check(hipGetLastError(), "k_lemb_prep_win");
+  } else {
+    hipLaunchKernelGGL(k_lemb_prep, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c);
+    e = rc_check(hipGetLastError(), "k_lemb_prep");
+  }
   const int nsp = fc1_splits(d), Ks = p * H / nsp;
   float* ws = c.ws;  // replica 0's slice; the replica axis adds r * c.wss
   const float* E = c.emb;
   float* T = ws + c.wo.T;
   // T_i[b] = S_i x_bn[b]  (p x p x F per window)
-  for (int i = 1; i < n && !e; ++i) {
+  for (int i = 1; i < n && !e && !wb; ++i) {
     RcGemm g = rc_gemm_args(0, 0, p, F, p, ws + c.wo.S + (int64_t)i * p * p, p, 0, T, nF, pnF, T + i * F, nF, pnF);
     rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
     e = rc_gemm_launch(g, B, s, "emb T_i");
@@ -376,7 +580,7 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
     e = rc_gemm_launch(g, nsp, s, "emb fc1");
   }
   if (e) return e;
-  hipLaunchKernelGGL(k_lemb_head, dim3(B, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
+  hipLaunchKernelGGL(k_lemb_head, dim3((B + 3) / 4, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
   return rc_check(hipGetLastError(), "k_lemb_head");
 }
 
@@ -386,8 +590,13 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F, pH = (int64_t)p * H;
   hipLaunchKernelGGL(k_lemb_dhead, dim3((B + lemb_wpw(d) - 1) / lemb_wpw(d), c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_lemb_dhead");
+  const int wb = lemb_win_step(c);
+  if (wb && c.dsN != (B + wb - 1) / wb) {
+    rc_set_error("windowed embedder backward: partial layout of %d groups, %d expected", c.dsN, (B + wb - 1) / wb);
+    return REDCLIFF_EINVAL;
+  }
   if (!e) {
-    const int ngfc = (d.K * M1 + d.K + M1 + 63) / 64, naf = (p * p * n + RC_BLOCK - 1) / RC_BLOCK;
+    const int ngfc = (d.K * M1 + d.K + M1 + 63) / 64, naf = wb ? 0 : (p * p * n + RC_BLOCK - 1) / RC_BLOCK;
     hipLaunchKernelGGL(k_lemb_gfc, dim3(ngfc + naf, c.nrep), dim3(RC_BLOCK), 0, s, c, ngfc);
     e = rc_check(hipGetLastError(), "k_lemb_gfc");
   }
@@ -419,6 +628,11 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
     RcGemm g = rc_gemm_args(0, 1, B * p, (int)nF, H, ws + c.wo.dZ, H, 0, E + c.eo.gcW, H, 0, ws + c.wo.edT, nF, 0);
     rc_gemm_reps(g, c, c.wss, c.es, c.wss);
     e = rc_gemm_launch(g, 1, s, "emb dT");
+  }
+  if (wb) {  // dx_bn, its BatchNorm partials and the dS_i partials, wb windows per workgroup
+    if (e) return e;
+    hipLaunchKernelGGL(k_lemb_win_bwd, dim3(c.dsN, c.nrep), dim3(RC_BLOCK), lemb_win_lds_bwd(d, wb), s, c, wb);
+    return rc_check(hipGetLastError(), "k_lemb_win_bwd");
   }
   if (!e) {  // dx_bn[b] = Af dT[b]   (p x p*n x F per window)
     RcGemm g = rc_gemm_args(0, 0, p, F, p * n, ws + c.wo.eAf, (int64_t)p * n, 0, ws + c.wo.edT, F, pnF, ws + c.wo.edX,

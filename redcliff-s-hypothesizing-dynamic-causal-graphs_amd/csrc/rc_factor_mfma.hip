@@ -44,18 +44,30 @@ __device__ inline float4 ld4(const float* p) { return *reinterpret_cast<const fl
 
 // ------------------------------------------------------------------------------------------
 // Window transpose: Xw[b][c*L + t] = X[row0 + b][Lmax - L + t][c], zero-padded to Qp columns.
-// grid (B, R); reads one contiguous L*p window, writes one Xw row.
+// grid (ceil(B * Qp / (4 * 256)), R): 4 elements (window b, source offset e = t*p + c of its
+// contiguous L*p slice) per thread, every load issued before the stores.
+#define XW_PER 4
 __global__ __launch_bounds__(RC_BLOCK) void k_xwin(StepCtx c) {
-  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y);
   const RedcliffDims& d = c.d;
-  const int L = d.L, p = d.p, Q = p * L, Qp = rc_qpad(d);
-  const float* src = c.X + r * c.xr + ((c.row0 + b) * d.T + (c.Lmax - L)) * p;
-  float* dst = c.ws + r * c.wss + c.wo.xw + (int64_t)b * Qp;
-  const RcDiv dp(p);
-  for (int e = threadIdx.x; e < Qp; e += RC_BLOCK) {
-    if (e < Q) {
-      const int t = dp.div(e), ch = e - t * p;
-      dst[ch * L + t] = src[e];
+  const int L = d.L, p = d.p, Q = p * L, Qp = rc_qpad(d), n = c.B * Qp;
+  const float* src = c.X + r * c.xr + (c.row0 * d.T + (c.Lmax - L)) * p;
+  float* dst = c.ws + r * c.wss + c.wo.xw;
+  const RcDiv dq(Qp), dp(p);
+  const int e0 = blockIdx.x * XW_PER * RC_BLOCK + threadIdx.x;
+  float v[XW_PER];
+#pragma unroll
+  for (int u = 0; u < XW_PER; ++u) {
+    const int e = e0 + u * RC_BLOCK, b = dq.div(e), k = e - b * Qp;
+    v[u] = (e < n && k < Q) ? src[(int64_t)b * d.T * p + k] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < XW_PER; ++u) {
+    const int e = e0 + u * RC_BLOCK, b = dq.div(e), k = e - b * Qp;
+    if (e >= n) continue;
+    if (k < Q) {
+      const int t = dp.div(k), ch = k - t * p;
+      dst[(int64_t)b * Qp + ch * L + t] = v[u];
     } else {
       dst[e] = 0.f;
     }
@@ -185,6 +197,99 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
       // slot ub holds this block's partial; block 0 also clears the slots past nUB
       if (l == 0) ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = ys + b1;
       else if (ub == 0 && l >= nUB && l < nU) ws[c.wo.y + (((int64_t)l * d.Bmax + b) * K + k) * p + j] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Short contractions (p*L <= 64, mf_recompute): the same product with the operands loaded
+// straight from global memory into the matrix-core registers -- no LDS staging, no barrier.
+// Workgroup = 4 column blocks, wave w owns block cb = 4 bx + w (network kj, 32-unit block ub) and
+// keeps that block's W0 rows as the A operand (rows = hidden units, k = q) for the whole launch;
+// it runs every 32-window row tile of the batch (B operand = the Xw rows), the next tile's loads
+// in flight during the current tile's k-steps.  Each z[b][u] is the same k-step sequence as
+// k_fac_fwd_mfma and k_fac_bwd_mfma<4>'s recompute (q ascending in steps of 2 up to Q; the
+// operand roles are swapped, and a product is commutative), so the bits agree.  The accumulator
+// holds rows = units, column = window, so the output layer's partial sum over the block's units
+// is in-lane (16 registers) plus one cross-half shuffle.  The 40-workgroup-per-replica grid
+// (D4IC) replaces the tiled kernel's 160 latency-bound 64 x 64 tiles.
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_short(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = rc_rep(c, blockIdx.z);
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), nUB = mf_nub(d), NB = K * p * nUB;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, kh = lane >> 5, l31 = lane & 31;
+  const int cb = blockIdx.x * 4 + wv;
+  if (cb >= NB) return;  // no barrier below
+  const float* P = c.fac + r * c.fs;
+  float* ws = c.ws + r * c.wss;
+  const float* Xw = ws + c.wo.xw;
+  const int kj = cb / nUB, ub = cb - kj * nUB, k = kj / p, j = kj - k * p;
+  const int nk = (Q + 1) >> 1, B = c.B;
+  const int uA = ub * 32 + l31;
+  const float* W0 = P + c.fo.W0 + ((int64_t)kj * h + uA) * Q;
+  float wA[32];
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) {
+    const int q = 2 * kk + kh;
+    wA[kk] = (kk < nk && uA < h && q < Q) ? W0[q] : 0.f;
+  }
+  // epilogue operands of the accumulator rows u = ub*32 + mf_row(reg, lane)
+  float bu[16], w1[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int u = ub * 32 + mf_row(reg, lane);
+    bu[reg] = u < h ? P[c.fo.b0 + (int64_t)kj * h + u] : 0.f;
+    w1[reg] = u < h ? P[c.fo.W1 + (int64_t)kj * h + u] : 0.f;
+  }
+  const float b1 = ub == 0 ? P[c.fo.b1 + kj] : 0.f;
+  if (kh == 0 && uA < h) ws[c.wo.w1 + (int64_t)kj * h + uA] = P[c.fo.W1 + (int64_t)kj * h + uA];
+  // GC group norms of the block (pre-update weights): gq[ub][kj][q] = sum_u W0[u][q]^2
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) {
+    if (kk < nk) {
+      float s = wA[kk] * wA[kk];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);  // within the 32-lane half
+      const int q = 2 * kk + kh;
+      if (l31 == 0 && q < Q) ws[c.wo.gq + ((int64_t)ub * K * p + kj) * Q + q] = s;
+    }
+  }
+  const int nU = rc_nuchunk(d);
+  float xb[32];
+  auto load = [&](int t0) {
+    const int b = t0 + l31;
+    const float* xr = Xw + (int64_t)b * Qp + kh;
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) xb[kk] = (kk < nk && b < B) ? xr[2 * kk] : 0.f;
+  };
+  load(0);
+  for (int t0 = 0; t0 < B; t0 += 32) {
+    float xc[32];
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) xc[kk] = xb[kk];
+    if (t0 + 32 < B) load(t0 + 32);
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk)
+      if (kk < nk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wA[kk], xc[kk], acc, 0, 0, 0);
+    const int b = t0 + l31;
+    float ys = 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const float a = fmaxf(acc[reg] + bu[reg], 0.f);  // units u >= h: w1 = 0
+#ifdef RC_RECOMP_DEBUG
+      const int u = ub * 32 + mf_row(reg, lane);
+      if (u < h && b < B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
+#endif
+      ys += w1[reg] * a;
+    }
+    const float yo = __shfl_xor(ys, 32, 64);  // rows 4..7 (mod 8) of the other half
+    if (kh == 0 && b < B) {
+      ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = (ys + yo) + b1;
+      if (ub == 0)  // block 0 also clears the slots past nUB
+        for (int l = nUB; l < nU; ++l) ws[c.wo.y + (((int64_t)l * d.Bmax + b) * K + k) * p + j] = 0.f;
     }
   }
 }
@@ -649,6 +754,151 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW ==
   epi_store(1, acc1);
 }
 
+// ------------------------------------------------------------------------------------------
+// Short contractions (p*L <= 64): layer-0 backward on v_mfma_f32_16x16x4_f32 with 16-unit blocks
+// (h = 100 pads to 112 units instead of 128), operands straight from global memory into the
+// matrix-core registers -- no LDS, no barrier.  Wave = (network kj, 16-unit block ub): cb =
+// 4 bx + w.  Lane l: index l15 = l & 15 (rows of A / columns of B and D), group g = l >> 4 (k
+// index); D rows 4 g + reg.
+//   recompute  zT[b][u] = sum_q X[b][q] W0[u][q]   (A = X rows, B = the block's W0 rows; the
+//              forward's q-ascending fmaf chain, k-steps of 4 instead of 2: the same bits);
+//   dZ[b][u] = [relu(z + b0) > 0] dL/dy[b] * W1[u], in registers: lane (u = l15, g) holds the
+//              windows b = 4 g + reg of the tile;
+//   dW0[u][q] += sum_b dZ[b][u] X[b][q]: k-step `reg` of a tile takes windows 4 g + reg from
+//              lane group g (the A operand IS the dZ register), B = X[4 g + reg][16 qt + l15];
+//   output-layer gradients dW1[u] = sum_b dy a, db0[u] = sum_b [a > 0] dy W1[u]: per lane over
+//              its windows, then the four groups in order;
+//   epilogue: + the adjacency-L1 term through the group norms, Adam (or the gradient).
+// Windows are visited in 16-window tiles, ascending; inside a tile in the k-step order above.
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_short(StepCtx c) {
+  const RedcliffDims& d = c.d;
+  const int r = rc_rep(c, blockIdx.z);
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), B = c.B;
+  const int nU16 = (h + 15) >> 4, NB = K * p * nU16;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l15 = lane & 15, g = lane >> 4;
+  const int cb = blockIdx.x * 4 + wv;
+  if (cb >= NB) return;  // no barrier below
+  const int kj = cb / nU16, u0 = (cb - kj * nU16) * 16;
+  float* P = c.fac + r * c.fs;
+  float* PM = c.facM + r * c.fs;
+  float* PV = c.facV + r * c.fs;
+  float* GF = c.gF + r * c.fs;
+  const float* ws = c.ws + r * c.wss;
+  const float* Xw = ws + c.wo.xw;
+  const float* dyl = ws + c.wo.dyl + (int64_t)kj * d.Bmax;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
+  const bool adam = !(c.flags & RC_GRAD_ONLY);
+  const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
+  const int nk4 = (Q + 3) >> 2, nqt = (Q + 15) >> 4;  // <= 16, <= 4
+  // the lane's unit (B operand column / dZ column): W0 row, bias, output weight (pre-update snapshot)
+  const int uL = u0 + l15;
+  const bool uvL = uL < h;
+  float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
+  float wB[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int q = 4 * s + g;
+    wB[s] = (s < nk4 && uvL && q < Q) ? W0[(int64_t)uL * Q + q] : 0.f;
+  }
+  const float bu = uvL ? P[c.fo.b0 + (int64_t)kj * h + uL] : 0.f;
+  const float w1 = uvL ? ws[c.wo.w1 + (int64_t)kj * h + uL] : 0.f;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float pa = 0.f, pb = 0.f;
+  float xa[16], xb[16], dy[4];
+  auto load = [&](int t0) {
+    const int b = t0 + l15;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) xa[s] = (s < nk4 && b < B) ? Xw[(int64_t)b * Qp + 4 * s + g] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int bb = t0 + 4 * g + reg;
+      dy[reg] = bb < B ? dyl[bb] : 0.f;
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+        xb[reg * 4 + qt] = (qt < nqt && bb < B) ? Xw[(int64_t)bb * Qp + 16 * qt + l15] : 0.f;
+    }
+  };
+  load(0);
+  for (int t0 = 0; t0 < B; t0 += 16) {
+    float xac[16], xbc[16], dyc[4];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) { xac[s] = xa[s]; xbc[s] = xb[s]; }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) dyc[reg] = dy[reg];
+    if (t0 + 16 < B) load(t0 + 16);
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      if (s < nk4) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xac[s], wB[s], z, 0, 0, 0);
+    float dz[4];
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+#pragma clang fp contract(off)
+      const float a = fmaxf(z[reg] + bu, 0.f);
+      const float dv = dyc[reg];  // 0 past the batch
+      dz[reg] = (a > 0.f ? dv : 0.f) * w1;
+      pa = pa + dv * a;
+      pb = pb + (a > 0.f ? dv * w1 : 0.f);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt)
+        if (qt < nqt) acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[reg], xbc[reg * 4 + qt], acc[qt], 0, 0, 0);
+  }
+  // output layer / hidden bias of the lane's unit: the four groups' partial sums in group order
+  {
+    const float a1 = __shfl(pa, l15 + 16, 64), a2 = __shfl(pa, l15 + 32, 64), a3 = __shfl(pa, l15 + 48, 64);
+    const float b1 = __shfl(pb, l15 + 16, 64), b2 = __shfl(pb, l15 + 32, 64), b3 = __shfl(pb, l15 + 48, 64);
+    if (g == 0 && uvL) {
+      rc_update(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + uL, ((pb + b1) + b2) + b3, as);
+      rc_update(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + uL, ((pa + a1) + a2) + a3, as);
+    }
+  }
+  if (!(c.flags & RC_STEP_B)) return;
+  // ---- epilogue: dW0[u = u0 + 4 g + reg][q = 16 qt + l15]
+  float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
+  float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
+  float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    const int q = 16 * qt + l15;
+    if (qt >= nqt || q >= Q) continue;
+    const float dg = adj_grad ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
+    const float gn = adj_grad ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
+    float pw[4], pm[4], pv[4];
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int u = u0 + 4 * g + reg;
+      const int64_t idx = (int64_t)u * Q + q;
+      const bool in = u < h;
+      pw[reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
+      pm[reg] = (in && adam) ? M0[idx] : 0.f;
+      pv[reg] = (in && adam) ? V0[idx] : 0.f;
+    }
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int u = u0 + 4 * g + reg;
+      if (u >= h) continue;
+      const int64_t idx = (int64_t)u * Q + q;
+      float gr = acc[qt][reg];
+      if (adj_grad && gn > 0.f) gr += dg * (pw[reg] / gn);
+      if (!adam) {
+        G0w[idx] = gr;
+      } else {
+        rc_adam(pw[reg], pm[reg], pv[reg], gr, as);
+        W0[idx] = pw[reg];
+        M0[idx] = pm[reg];
+        V0[idx] = pv[reg];
+      }
+    }
+  }
+}
+
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
   const int Q = d.p * d.L;
   return sizeof(float) * (size_t)(2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + d.Bmax * d.K + 2 * RC_BLOCK + d.Bmax);
@@ -675,10 +925,16 @@ bool rc_fac_use_mfma(const RedcliffDims& d) {
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int KP = d.K * d.p;
-  hipLaunchKernelGGL(k_xwin, dim3(c.B, c.nrep), dim3(RC_BLOCK), 0, s, c);
+  const int nxw = (c.B * rc_qpad(d) + XW_PER * RC_BLOCK - 1) / (XW_PER * RC_BLOCK);
+  hipLaunchKernelGGL(k_xwin, dim3(nxw, c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_xwin");
   if (e) return e;
   const int NB = KP * ((d.h + 31) / 32);
+  const char* fv = getenv("REDCLIFF_FAC_FWD");  // "tile": the LDS-tiled kernel for short contractions too (tuning)
+  if (mf_recompute(d) && !(fv && !strcmp(fv, "tile"))) {
+    hipLaunchKernelGGL(k_fac_fwd_short, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
+    return rc_check(hipGetLastError(), "k_fac_fwd_short");
+  }
   hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_fwd_mfma");
 }
@@ -696,6 +952,12 @@ int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (!(c.flags & RC_STEP_B)) return 0;
   const int NB = d.K * d.p * ((d.h + 31) / 32), Q = d.p * d.L;
+  const char* fv = getenv("REDCLIFF_FAC_BWD");  // "tile": the LDS-tiled recompute kernel (tuning)
+  if (Q <= 64 && !(fv && !strcmp(fv, "tile"))) {
+    const int NB16 = d.K * d.p * ((d.h + 15) / 16);
+    hipLaunchKernelGGL(k_fac_bwd_short, dim3((NB16 + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
+    return rc_check(hipGetLastError(), "k_fac_bwd_short");
+  }
   if (Q <= 64)  // short contraction rows: four column blocks share one 64-column X tile
     hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
   else
