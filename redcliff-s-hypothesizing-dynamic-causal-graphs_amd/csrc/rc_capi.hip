@@ -281,6 +281,7 @@ static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
   c.fo = rc_fac_off(d);
   c.wo = wo;
   rc_emb_partial_layout(c, rc_emb_use_gemm(d));
+  c.fslots = rc_fac_slots(d);
   return 0;
 }
 

@@ -250,6 +250,8 @@ struct StepCtx {
   // dS_i[cc][c'] = sum_s ws.dS[cc*dsCC + s*dsS + i*dsI + c'], s < dsN;  BN affine: ws.dgb[s][2][F], s < dgN
   int dsN, dgN;
   int64_t dsCC, dsS, dsI;
+  // matrix-core factor path: y / group-norm partial slots the forward writes (rc_fac_slots)
+  int fslots;
   // 1: k_emb_bwd's node blocks leave their per-window-block partial records unreduced and
   // k_emb_combine sums them (no cross-workgroup ticket / fences inside the backward kernel)
   int defer;
@@ -544,6 +546,7 @@ int rc_launch_cos_values(const StepCtx& c, hipStream_t s);  // per-window cos-si
 int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);
+int rc_fac_slots(const RedcliffDims& d);  // rc_factor_mfma.hip
 void rc_emb_partial_layout(StepCtx& c, bool gemm);
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);

@@ -311,9 +311,12 @@ __host__ __device__ inline int lemb_win_lds_bwd(const RedcliffDims& d, int wb) {
 // more than 64 window groups: the dS / BN partial regions hold 64 slots)
 __host__ __device__ inline int lemb_win(const RedcliffDims& d, int B) {
   if (d.p >= 32 || B < 1) return 0;
-  int wb = RC_LEMB_LDS / (d.p * (d.n + 2) * d.F);
-  if (wb > 16) wb = 16;
-  if (wb < 1 || (B + wb - 1) / wb > 64) return 0;
+  const int fit = RC_LEMB_LDS / (d.p * (d.n + 2) * d.F);  // windows whose tiles fit the LDS budget
+  // few windows per workgroup (many workgroups: the per-window chains are latency-bound; R = 128
+  // D4IC: 16 windows per workgroup ran 71 us), but at most 64 groups (the partial slots)
+  int wb = (B + 63) / 64;
+  if (wb < 4) wb = B < 4 ? B : 4;
+  if (wb > fit) return 0;
   if (lemb_win_lds_bwd(d, wb) > 65536) return 0;  // default dynamic LDS limit
   return wb;
 }

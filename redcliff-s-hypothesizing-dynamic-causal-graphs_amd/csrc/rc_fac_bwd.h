@@ -317,7 +317,10 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       }
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 18);
-  if (publish && lead) rc_publish(publish);
+  if (publish && lead) {
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_WAIT, 1);  // trace builds: the lead's publish time (end slot)
+    rc_publish(publish);
+  }
   if (!stepB) return;
   if (split) {  // the lead's own update operands, after its records are out
     adam_loads();

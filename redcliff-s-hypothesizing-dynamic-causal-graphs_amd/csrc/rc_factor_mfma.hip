@@ -82,7 +82,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_xwin(StepCtx c) {
 // Epilogue: a = relu(z + b0) -> ws.a (backward), partial y_ub = sum_{u in ub} W1[u] a[u]
 // (+ b1 in block 0) -> ws.y slot ub, squared group norms gq[ub][kj][q] = sum_{u in ub} W0[u][q]^2
 // (first row block), W1 snapshot.
-__device__ inline int mf_nub(const RedcliffDims& d) { return (d.h + 31) / 32; }
+__host__ __device__ inline int mf_nub(const RedcliffDims& d) { return (d.h + 31) / 32; }
 // Short contractions (p*L <= 64, the k_fac_bwd_mfma<4> launch): the backward recomputes the
 // hidden activations and forms the output-layer gradients, so neither the forward's activation
 // store nor the mixing kernel's activation reads happen.
@@ -202,99 +202,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Short contractions (p*L <= 64, mf_recompute): the same product with the operands loaded
-// straight from global memory into the matrix-core registers -- no LDS staging, no barrier.
-// Workgroup = 4 column blocks, wave w owns block cb = 4 bx + w (network kj, 32-unit block ub) and
-// keeps that block's W0 rows as the A operand (rows = hidden units, k = q) for the whole launch;
-// it runs every 32-window row tile of the batch (B operand = the Xw rows), the next tile's loads
-// in flight during the current tile's k-steps.  Each z[b][u] is the same k-step sequence as
-// k_fac_fwd_mfma and k_fac_bwd_mfma<4>'s recompute (q ascending in steps of 2 up to Q; the
-// operand roles are swapped, and a product is commutative), so the bits agree.  The accumulator
-// holds rows = units, column = window, so the output layer's partial sum over the block's units
-// is in-lane (16 registers) plus one cross-half shuffle.  The 40-workgroup-per-replica grid
-// (D4IC) replaces the tiled kernel's 160 latency-bound 64 x 64 tiles.
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_short(StepCtx c) {
-  const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.z);
-  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), nUB = mf_nub(d), NB = K * p * nUB;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, kh = lane >> 5, l31 = lane & 31;
-  const int cb = blockIdx.x * 4 + wv;
-  if (cb >= NB) return;  // no barrier below
-  const float* P = c.fac + r * c.fs;
-  float* ws = c.ws + r * c.wss;
-  const float* Xw = ws + c.wo.xw;
-  const int kj = cb / nUB, ub = cb - kj * nUB, k = kj / p, j = kj - k * p;
-  const int nk = (Q + 1) >> 1, B = c.B;
-  const int uA = ub * 32 + l31;
-  const float* W0 = P + c.fo.W0 + ((int64_t)kj * h + uA) * Q;
-  float wA[32];
-#pragma unroll
-  for (int kk = 0; kk < 32; ++kk) {
-    const int q = 2 * kk + kh;
-    wA[kk] = (kk < nk && uA < h && q < Q) ? W0[q] : 0.f;
-  }
-  // epilogue operands of the accumulator rows u = ub*32 + mf_row(reg, lane)
-  float bu[16], w1[16];
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int u = ub * 32 + mf_row(reg, lane);
-    bu[reg] = u < h ? P[c.fo.b0 + (int64_t)kj * h + u] : 0.f;
-    w1[reg] = u < h ? P[c.fo.W1 + (int64_t)kj * h + u] : 0.f;
-  }
-  const float b1 = ub == 0 ? P[c.fo.b1 + kj] : 0.f;
-  if (kh == 0 && uA < h) ws[c.wo.w1 + (int64_t)kj * h + uA] = P[c.fo.W1 + (int64_t)kj * h + uA];
-  // GC group norms of the block (pre-update weights): gq[ub][kj][q] = sum_u W0[u][q]^2
-#pragma unroll
-  for (int kk = 0; kk < 32; ++kk) {
-    if (kk < nk) {
-      float s = wA[kk] * wA[kk];
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);  // within the 32-lane half
-      const int q = 2 * kk + kh;
-      if (l31 == 0 && q < Q) ws[c.wo.gq + ((int64_t)ub * K * p + kj) * Q + q] = s;
-    }
-  }
-  const int nU = rc_nuchunk(d);
-  float xb[32];
-  auto load = [&](int t0) {
-    const int b = t0 + l31;
-    const float* xr = Xw + (int64_t)b * Qp + kh;
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) xb[kk] = (kk < nk && b < B) ? xr[2 * kk] : 0.f;
-  };
-  load(0);
-  for (int t0 = 0; t0 < B; t0 += 32) {
-    float xc[32];
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) xc[kk] = xb[kk];
-    if (t0 + 32 < B) load(t0 + 32);
-    f32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk)
-      if (kk < nk) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wA[kk], xc[kk], acc, 0, 0, 0);
-    const int b = t0 + l31;
-    float ys = 0.f;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const float a = fmaxf(acc[reg] + bu[reg], 0.f);  // units u >= h: w1 = 0
-#ifdef RC_RECOMP_DEBUG
-      const int u = ub * 32 + mf_row(reg, lane);
-      if (u < h && b < B) ws[c.wo.a + ((int64_t)kj * d.Bmax + b) * h + u] = a;
-#endif
-      ys += w1[reg] * a;
-    }
-    const float yo = __shfl_xor(ys, 32, 64);  // rows 4..7 (mod 8) of the other half
-    if (kh == 0 && b < B) {
-      ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = (ys + yo) + b1;
-      if (ub == 0)  // block 0 also clears the slots past nUB
-        for (int l = nUB; l < nU; ++l) ws[c.wo.y + (((int64_t)l * d.Bmax + b) * K + k) * p + j] = 0.f;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // Per-network work between the GEMMs.  grid (K*p, R), one workgroup per network kj:
 //   x_sim = sum_k w_k y_k, forecast residual, dL/dy (-> ws.dyl), dL/dw (forecast + adjacency
 //   terms, -> ws.dwp), group norms G / G0, adjacency-L1 value and its gradients wrt the
@@ -338,7 +245,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
-  const int nUB = mf_nub(d);
+  const int nUB = c.fslots;  // y / group-norm slots of the forward (16- or 32-unit blocks)
   for (int e = tid; e < B * K; e += RC_BLOCK) {
     const int b = e / K, kk = e - b * K;
     float yv = ws[c.wo.y + ((int64_t)b * K + kk) * p + j];
@@ -755,145 +662,234 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW ==
 }
 
 // ------------------------------------------------------------------------------------------
-// Short contractions (p*L <= 64): layer-0 backward on v_mfma_f32_16x16x4_f32 with 16-unit blocks
-// (h = 100 pads to 112 units instead of 128), operands straight from global memory into the
-// matrix-core registers -- no LDS, no barrier.  Wave = (network kj, 16-unit block ub): cb =
-// 4 bx + w.  Lane l: index l15 = l & 15 (rows of A / columns of B and D), group g = l >> 4 (k
-// index); D rows 4 g + reg.
-//   recompute  zT[b][u] = sum_q X[b][q] W0[u][q]   (A = X rows, B = the block's W0 rows; the
-//              forward's q-ascending fmaf chain, k-steps of 4 instead of 2: the same bits);
-//   dZ[b][u] = [relu(z + b0) > 0] dL/dy[b] * W1[u], in registers: lane (u = l15, g) holds the
-//              windows b = 4 g + reg of the tile;
-//   dW0[u][q] += sum_b dZ[b][u] X[b][q]: k-step `reg` of a tile takes windows 4 g + reg from
-//              lane group g (the A operand IS the dZ register), B = X[4 g + reg][16 qt + l15];
-//   output-layer gradients dW1[u] = sum_b dy a, db0[u] = sum_b [a > 0] dy W1[u]: per lane over
-//              its windows, then the four groups in order;
-//   epilogue: + the adjacency-L1 term through the group norms, Adam (or the gradient).
-// Windows are visited in 16-window tiles, ascending; inside a tile in the k-step order above.
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_short(StepCtx c) {
+// Short contractions (p*L <= 64, mf_recompute; the D4IC grid): layer 0 forward and backward on
+// v_mfma_f32_16x16x4_f32 with 16-UNIT blocks (h = 100 pads to 112 units, not 128).  A workgroup
+// stages its replica's batch of windows ONCE in LDS, straight from X (Xs[b][c*L + t], row stride
+// S = Qp16 + 4 so the operand reads below are bank-conflict free; no k_xwin, no Xw round trip),
+// then each wave works through `bpw` 16-unit blocks cb = (bx * bpw + i) * 4 + w with no further
+// barrier.  Lane l: l15 = l & 15, group g = l >> 4; D rows 4 g + reg, column l15.
+//
+// The hidden pre-activations are q-ascending k-ordered fmaf chains in both kernels (the forward
+// as z[u][b] with W0 rows as the A operand, the backward's recompute as zT[b][u] with the X rows
+// as A: a product is commutative), so the backward's recompute reproduces the forward's bits.
+// y and the group norms are written per 16-unit block into slots ub < ceil(h/16) (= rc_nuchunk,
+// the vector path's hidden chunks; StepCtx.fslots tells k_fac_mix how many to sum).
+__host__ __device__ inline int ms_qp16(const RedcliffDims& d) { return ((d.p * d.L + 15) >> 4) << 4; }
+__host__ __device__ inline int ms_rows(int B) { return (B + 31) & ~31; }
+inline size_t ms_lds(const RedcliffDims& d, int B) { return sizeof(float) * (size_t)ms_rows(B) * (ms_qp16(d) + 4); }
+
+__device__ inline void ms_stage_x(const StepCtx& c, int r, float* Xs) {
+  const RedcliffDims& d = c.d;
+  const int p = d.p, L = d.L, Q = p * L, Qp16 = ms_qp16(d), S = Qp16 + 4, B = c.B, rows = ms_rows(B);
+  const float* src = c.X + r * c.xr + (c.row0 * d.T + (c.Lmax - L)) * p;
+  const RcDiv dQ(Q), dp(p);
+  rc_stage<8>(B * Q, [&](int e) {
+    const int b = dQ.div(e);
+    return src[(int64_t)b * d.T * p + (e - b * Q)];
+  }, [&](int e, float v) {
+    const int b = dQ.div(e), k = e - b * Q, t = dp.div(k), ch = k - t * p;
+    Xs[b * S + ch * L + t] = v;
+  });
+  const int pad = Qp16 - Q;  // zero columns [Q, Qp16) of the batch rows and all of rows [B, rows)
+  for (int e = threadIdx.x; e < B * pad; e += RC_BLOCK) {
+    const int b = e / pad;
+    Xs[b * S + Q + (e - b * pad)] = 0.f;
+  }
+  for (int e = B * S + threadIdx.x; e < rows * S; e += RC_BLOCK) Xs[e] = 0.f;
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Forward: z[u][b] = sum_q W0[u][q] X[b][q] (A = the block's W0 rows in registers, B = Xs rows),
+// two 16-window tiles at a time; epilogue a = relu(z + b0), y slot ub = sum_u W1[u] a (in-lane
+// over the 4 rows, then the 4 groups in order), + b1 in block 0; group norms of the block; W1
+// snapshot for the backward.
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.z);
-  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, Qp = rc_qpad(d), B = c.B;
-  const int nU16 = (h + 15) >> 4, NB = K * p * nU16;
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
+  const int nk4 = (Q + 3) >> 2, S = ms_qp16(d) + 4;
+  extern __shared__ float Xs[];
+  const float* P = c.fac + r * c.fs;
+  float* ws = c.ws + r * c.wss;
+  ms_stage_x(c, r, Xs);
+  __syncthreads();
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l15 = lane & 15, g = lane >> 4;
-  const int cb = blockIdx.x * 4 + wv;
-  if (cb >= NB) return;  // no barrier below
-  const int kj = cb / nU16, u0 = (cb - kj * nU16) * 16;
+  for (int i = 0; i < bpw; ++i) {
+    const int cb = ((int)blockIdx.x * bpw + i) * 4 + wv;
+    if (cb >= NB) break;
+    const int kj = cb / nU, ub = cb - kj * nU, u0 = ub * 16, k = kj / p, j = kj - k * p;
+    const int uA = u0 + l15;
+    const float* W0 = P + c.fo.W0 + ((int64_t)kj * h + uA) * Q;
+    float wA[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int q = 4 * s + g;
+      wA[s] = (s < nk4 && uA < h && q < Q) ? W0[q] : 0.f;
+    }
+    float bu[4], w1[4];
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int u = u0 + 4 * g + reg;
+      bu[reg] = u < h ? P[c.fo.b0 + (int64_t)kj * h + u] : 0.f;
+      w1[reg] = u < h ? P[c.fo.W1 + (int64_t)kj * h + u] : 0.f;
+    }
+    const float b1 = ub == 0 ? P[c.fo.b1 + kj] : 0.f;
+    if (g == 0 && uA < h) ws[c.wo.w1 + (int64_t)kj * h + uA] = P[c.fo.W1 + (int64_t)kj * h + uA];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {  // gq[ub][kj][q] = sum over the block's units of W0[u][q]^2
+      if (s < nk4) {
+        float sq = wA[s] * wA[s];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);  // within the 16-lane group
+        const int q = 4 * s + g;
+        if (l15 == 0 && q < Q) ws[c.wo.gq + ((int64_t)ub * K * p + kj) * Q + q] = sq;
+      }
+    }
+    for (int t0 = 0; t0 < B; t0 += 32) {
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      const float* x0 = Xs + (t0 + l15) * S + g;
+      const float* x1 = x0 + 16 * S;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        if (s < nk4) {
+          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x0[4 * s], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x1[4 * s], a1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const f32x4 z = tt ? a1 : a0;
+        float ys = 0.f;
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) ys += w1[reg] * fmaxf(z[reg] + bu[reg], 0.f);  // w1 = 0 past h
+        ys += __shfl_xor(ys, 16, 64);
+        ys += __shfl_xor(ys, 32, 64);
+        const int b = t0 + 16 * tt + l15;
+        if (g == 0 && b < B) ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = ys + b1;
+      }
+    }
+  }
+}
+
+// Backward (RC_STEP_B): per 16-unit block,
+//   recompute  zT[b][u] (A = Xs rows, B = the block's W0 rows in registers; the forward's bits);
+//   dZ[b][u] = [relu(z + b0) > 0] dL/dy[b] W1[u] in registers: lane (u = l15, g) holds the windows
+//              b = t0 + 4 g + reg of the tile;
+//   dW0[u][q] += sum_b dZ[b][u] X[b][q]: k-step `reg` of a tile takes windows t0 + 4 g + reg from
+//              lane group g -- the A operand IS the dZ register; B = Xs[t0 + 4 g + reg][16 qt + l15];
+//   dW1[u] = sum_b dy a, db0[u] = sum_b [a > 0] dy W1[u]: per lane over its windows, then the four
+//              groups in order, and their Adam step;
+//   epilogue: + the adjacency-L1 term through the group norms, Adam (or the gradient).
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
+  const RedcliffDims& d = c.d;
+  const int r = rc_rep(c, blockIdx.z);
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
+  const int nk4 = (Q + 3) >> 2, nqt = (Q + 15) >> 4, S = ms_qp16(d) + 4;
+  extern __shared__ float Xs[];
   float* P = c.fac + r * c.fs;
   float* PM = c.facM + r * c.fs;
   float* PV = c.facV + r * c.fs;
   float* GF = c.gF + r * c.fs;
   const float* ws = c.ws + r * c.wss;
-  const float* Xw = ws + c.wo.xw;
-  const float* dyl = ws + c.wo.dyl + (int64_t)kj * d.Bmax;
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
   const bool adam = !(c.flags & RC_GRAD_ONLY);
   const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
-  const int nk4 = (Q + 3) >> 2, nqt = (Q + 15) >> 4;  // <= 16, <= 4
-  // the lane's unit (B operand column / dZ column): W0 row, bias, output weight (pre-update snapshot)
-  const int uL = u0 + l15;
-  const bool uvL = uL < h;
-  float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
-  float wB[16];
+  ms_stage_x(c, r, Xs);
+  __syncthreads();
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l15 = lane & 15, g = lane >> 4;
+  for (int i = 0; i < bpw; ++i) {
+    const int cb = ((int)blockIdx.x * bpw + i) * 4 + wv;
+    if (cb >= NB) break;
+    const int kj = cb / nU, u0 = (cb - kj * nU) * 16;
+    const int uL = u0 + l15;
+    const bool uvL = uL < h;
+    float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
+    const float* dyl = ws + c.wo.dyl + (int64_t)kj * d.Bmax;
+    float wB[16];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int q = 4 * s + g;
-    wB[s] = (s < nk4 && uvL && q < Q) ? W0[(int64_t)uL * Q + q] : 0.f;
-  }
-  const float bu = uvL ? P[c.fo.b0 + (int64_t)kj * h + uL] : 0.f;
-  const float w1 = uvL ? ws[c.wo.w1 + (int64_t)kj * h + uL] : 0.f;
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  f32x4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float pa = 0.f, pb = 0.f;
-  float xa[16], xb[16], dy[4];
-  auto load = [&](int t0) {
-    const int b = t0 + l15;
-#pragma unroll
-    for (int s = 0; s < 16; ++s) xa[s] = (s < nk4 && b < B) ? Xw[(int64_t)b * Qp + 4 * s + g] : 0.f;
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int bb = t0 + 4 * g + reg;
-      dy[reg] = bb < B ? dyl[bb] : 0.f;
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt)
-        xb[reg * 4 + qt] = (qt < nqt && bb < B) ? Xw[(int64_t)bb * Qp + 16 * qt + l15] : 0.f;
+    for (int s = 0; s < 16; ++s) {
+      const int q = 4 * s + g;
+      wB[s] = (s < nk4 && uvL && q < Q) ? W0[(int64_t)uL * Q + q] : 0.f;
     }
-  };
-  load(0);
-  for (int t0 = 0; t0 < B; t0 += 16) {
-    float xac[16], xbc[16], dyc[4];
+    const float bu = uvL ? P[c.fo.b0 + (int64_t)kj * h + uL] : 0.f;
+    const float w1 = uvL ? ws[c.wo.w1 + (int64_t)kj * h + uL] : 0.f;  // pre-update snapshot
+    f32x4 acc[4];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) { xac[s] = xa[s]; xbc[s] = xb[s]; }
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float pa = 0.f, pb = 0.f;
+    for (int t0 = 0; t0 < B; t0 += 16) {
+      float dy[4];
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) dyc[reg] = dy[reg];
-    if (t0 + 16 < B) load(t0 + 16);
-    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      for (int reg = 0; reg < 4; ++reg) {
+        const int b = t0 + 4 * g + reg;
+        dy[reg] = b < B ? dyl[b] : 0.f;
+      }
+      f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const float* xr = Xs + (t0 + l15) * S + g;
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
-      if (s < nk4) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xac[s], wB[s], z, 0, 0, 0);
-    float dz[4];
+      for (int s = 0; s < 16; ++s)
+        if (s < nk4) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], wB[s], z, 0, 0, 0);
+      float dz[4];
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
+      for (int reg = 0; reg < 4; ++reg) {
 #pragma clang fp contract(off)
-      const float a = fmaxf(z[reg] + bu, 0.f);
-      const float dv = dyc[reg];  // 0 past the batch
-      dz[reg] = (a > 0.f ? dv : 0.f) * w1;
-      pa = pa + dv * a;
-      pb = pb + (a > 0.f ? dv * w1 : 0.f);
+        const float a = fmaxf(z[reg] + bu, 0.f);
+        dz[reg] = (a > 0.f ? dy[reg] : 0.f) * w1;
+        pa = pa + dy[reg] * a;
+        pb = pb + (a > 0.f ? dy[reg] * w1 : 0.f);
+      }
+      const float* xq = Xs + (t0 + 4 * g) * S + l15;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt)
+          if (qt < nqt) acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[reg], xq[reg * S + 16 * qt], acc[qt], 0, 0, 0);
     }
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg)
-#pragma unroll
-      for (int qt = 0; qt < 4; ++qt)
-        if (qt < nqt) acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[reg], xbc[reg * 4 + qt], acc[qt], 0, 0, 0);
-  }
-  // output layer / hidden bias of the lane's unit: the four groups' partial sums in group order
-  {
-    const float a1 = __shfl(pa, l15 + 16, 64), a2 = __shfl(pa, l15 + 32, 64), a3 = __shfl(pa, l15 + 48, 64);
-    const float b1 = __shfl(pb, l15 + 16, 64), b2 = __shfl(pb, l15 + 32, 64), b3 = __shfl(pb, l15 + 48, 64);
-    if (g == 0 && uvL) {
-      rc_update(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + uL, ((pb + b1) + b2) + b3, as);
-      rc_update(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + uL, ((pa + a1) + a2) + a3, as);
+    {  // output layer / hidden bias of the lane's unit: the four groups' partial sums in order
+      const float a1 = __shfl(pa, l15 + 16, 64), a2 = __shfl(pa, l15 + 32, 64), a3 = __shfl(pa, l15 + 48, 64);
+      const float b1 = __shfl(pb, l15 + 16, 64), b2 = __shfl(pb, l15 + 32, 64), b3 = __shfl(pb, l15 + 48, 64);
+      if (g == 0 && uvL) {
+        rc_update(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + uL, ((pb + b1) + b2) + b3, as);
+        rc_update(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + uL, ((pa + a1) + a2) + a3, as);
+      }
     }
-  }
-  if (!(c.flags & RC_STEP_B)) return;
-  // ---- epilogue: dW0[u = u0 + 4 g + reg][q = 16 qt + l15]
-  float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
-  float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
-  float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
+    // ---- epilogue: dW0[u = u0 + 4 g + reg][q = 16 qt + l15]
+    float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
+    float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
+    float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt) {
-    const int q = 16 * qt + l15;
-    if (qt >= nqt || q >= Q) continue;
-    const float dg = adj_grad ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
-    const float gn = adj_grad ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
-    float pw[4], pm[4], pv[4];
+    for (int qt = 0; qt < 4; ++qt) {
+      const int q = 16 * qt + l15;
+      if (qt >= nqt || q >= Q) continue;
+      const float dg = adj_grad ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
+      const float gn = adj_grad ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
+      float pw[4], pm[4], pv[4];
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int u = u0 + 4 * g + reg;
-      const int64_t idx = (int64_t)u * Q + q;
-      const bool in = u < h;
-      pw[reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
-      pm[reg] = (in && adam) ? M0[idx] : 0.f;
-      pv[reg] = (in && adam) ? V0[idx] : 0.f;
-    }
+      for (int reg = 0; reg < 4; ++reg) {
+        const int u = u0 + 4 * g + reg;
+        const int64_t idx = (int64_t)u * Q + q;
+        const bool in = u < h;
+        pw[reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
+        pm[reg] = (in && adam) ? M0[idx] : 0.f;
+        pv[reg] = (in && adam) ? V0[idx] : 0.f;
+      }
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      const int u = u0 + 4 * g + reg;
-      if (u >= h) continue;
-      const int64_t idx = (int64_t)u * Q + q;
-      float gr = acc[qt][reg];
-      if (adj_grad && gn > 0.f) gr += dg * (pw[reg] / gn);
-      if (!adam) {
-        G0w[idx] = gr;
-      } else {
-        rc_adam(pw[reg], pm[reg], pv[reg], gr, as);
-        W0[idx] = pw[reg];
-        M0[idx] = pm[reg];
-        V0[idx] = pv[reg];
+      for (int reg = 0; reg < 4; ++reg) {
+        const int u = u0 + 4 * g + reg;
+        if (u >= h) continue;
+        const int64_t idx = (int64_t)u * Q + q;
+        float gr = acc[qt][reg];
+        if (adj_grad && gn > 0.f) gr += dg * (pw[reg] / gn);
+        if (!adam) {
+          G0w[idx] = gr;
+        } else {
+          rc_adam(pw[reg], pm[reg], pv[reg], gr, as);
+          W0[idx] = pw[reg];
+          M0[idx] = pm[reg];
+          V0[idx] = pv[reg];
+        }
       }
     }
   }
@@ -922,19 +918,47 @@ bool rc_fac_use_mfma(const RedcliffDims& d) {
   return (d.p * d.L >= 256 && d.h <= 32) || d.R >= 8 || !rc_fac_vector_fits(d);
 }
 
+// Short-contraction kernels (k_fac_fwd_s16 / k_fac_bwd_s16) for p*L <= 64; REDCLIFF_FAC_SHORT=0
+// runs the 32-unit tiled kernels there instead (tuning, A/B).  Read per call like the path choice.
+bool rc_fac_short(const RedcliffDims& d) {
+  const char* v = getenv("REDCLIFF_FAC_SHORT");
+  return mf_recompute(d) && !(v && !strcmp(v, "0"));
+}
+// y / group-norm slots the forward writes (k_fac_mix sums them): 16- or 32-unit blocks
+int rc_fac_slots(const RedcliffDims& d) { return rc_fac_short(d) ? (d.h + 15) / 16 : mf_nub(d); }
+
+// blocks per wave of the short kernels: 4 when the replica axis fills the chip, else 1
+static int ms_bpw(const StepCtx& c) {
+  const RedcliffDims& d = c.d;
+  const int NB = d.K * d.p * ((d.h + 15) / 16);
+  return (int64_t)c.nrep * ((NB + 15) / 16) >= 1024 ? 4 : 1;
+}
+
+template <class Kern>
+static int ms_launch(Kern k, const StepCtx& c, hipStream_t s, const char* what) {
+  const RedcliffDims& d = c.d;
+  const size_t lds = ms_lds(d, c.B);
+  if (lds > 160 * 1024) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
+  if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
+    const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds), what);
+    if (e) return e;
+  }
+  const int NB = d.K * d.p * ((d.h + 15) / 16), bpw = ms_bpw(c);
+  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw);
+  return rc_check(hipGetLastError(), what);
+}
+
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
+  if (c.fslots != rc_fac_slots(d)) { rc_set_error("factor forward: slot layout changed within a step"); return REDCLIFF_EINVAL; }
+  if (rc_fac_short(d)) return ms_launch(k_fac_fwd_s16, c, s, "k_fac_fwd_s16");
   const int KP = d.K * d.p;
   const int nxw = (c.B * rc_qpad(d) + XW_PER * RC_BLOCK - 1) / (XW_PER * RC_BLOCK);
   hipLaunchKernelGGL(k_xwin, dim3(nxw, c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_xwin");
   if (e) return e;
   const int NB = KP * ((d.h + 31) / 32);
-  const char* fv = getenv("REDCLIFF_FAC_FWD");  // "tile": the LDS-tiled kernel for short contractions too (tuning)
-  if (mf_recompute(d) && !(fv && !strcmp(fv, "tile"))) {
-    hipLaunchKernelGGL(k_fac_fwd_short, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
-    return rc_check(hipGetLastError(), "k_fac_fwd_short");
-  }
   hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_fwd_mfma");
 }
@@ -952,12 +976,7 @@ int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (!(c.flags & RC_STEP_B)) return 0;
   const int NB = d.K * d.p * ((d.h + 31) / 32), Q = d.p * d.L;
-  const char* fv = getenv("REDCLIFF_FAC_BWD");  // "tile": the LDS-tiled recompute kernel (tuning)
-  if (Q <= 64 && !(fv && !strcmp(fv, "tile"))) {
-    const int NB16 = d.K * d.p * ((d.h + 15) / 16);
-    hipLaunchKernelGGL(k_fac_bwd_short, dim3((NB16 + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
-    return rc_check(hipGetLastError(), "k_fac_bwd_short");
-  }
+  if (rc_fac_short(d)) return ms_launch(k_fac_bwd_s16, c, s, "k_fac_bwd_s16");
   if (Q <= 64)  // short contraction rows: four column blocks share one 64-column X tile
     hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
   else

@@ -68,6 +68,15 @@ def main():
                  (st.max() - st.min()) / 100.0, dur.min(), np.median(dur), dur.max()))
 
 
+    pub = tr[7][1::2]
+    pub = pub[pub > 0]
+    if pub.size:
+        print("factor leads published (merged backward): %d leads, first %.2f us  median %.2f  last %.2f"
+              % (pub.size, (pub.min() - t_first) / 100.0, (np.median(pub) - t_first) / 100.0,
+                 (pub.max() - t_first) / 100.0))
+        order = np.argsort(tr[7][1::2])[::-1][:5]
+        print("  latest leads (workgroup: publish us): %s" % ", ".join(
+            "%d: %.2f" % (i, (tr[7][1::2][i] - t_first) / 100.0) for i in order if tr[7][1::2][i] > 0))
     if wt.size:
         print("emb wait returned (merged backward node WGs): %d WGs, first %.2f us  median %.2f  last %.2f"
               % (wt.size, (wt.min() - t_first) / 100.0, (np.median(wt) - t_first) / 100.0, (wt.max() - t_first) / 100.0))
