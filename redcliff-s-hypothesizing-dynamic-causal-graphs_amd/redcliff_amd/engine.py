@@ -160,12 +160,16 @@ class FitEngine:
     def _fac_pairs(self):
         return factor_views(self.fac, list(self.model.factors), self.p, self.h, self.L)
 
-    def bind(self):
-        """Copy current parameter values into the packed buffers and alias the parameters."""
+    def bind(self, copy=True):
+        """Copy current parameter values into the packed buffers and alias the parameters.
+        copy=False: the buffers already hold the values (attach_pack moved them in bulk)."""
         with torch.no_grad():
             self.pairs = self._emb_pairs() + self._fac_pairs()
+            if copy:  # one multi-tensor launch instead of a copy kernel per parameter
+                views = [view for _, view in self.pairs]
+                srcs = [prm.detach().to(view.device).reshape(view.shape) for prm, view in self.pairs]
+                torch._foreach_copy_(views, srcs)
             for prm, view in self.pairs:
-                view.copy_(prm.detach())
                 prm.data = view
             bnm = self.dgcnn.BN1
             self.bn[0].copy_(bnm.running_mean)
@@ -258,7 +262,7 @@ class FitEngine:
             self.emb.copy_(emb_old)
             self.fac.copy_(fac_old)
             self.bn.copy_(bn_old)
-        self.bind()
+        self.bind(copy=False)
         for g in ("A", "B"):
             st = self.opt[g]
             if st is None:
