@@ -180,9 +180,16 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       rc_seg<4>(B * K, [&](int e) { return ws[c.wo.w + e]; }, [&](int e, float v) { wrl[e] = v; }),
       rc_seg<1>(tgt ? B : 0, [&](int b) { return X[((c.row0 + b) * d.T + c.Lmax) * p + j]; },
                 [&](int b, float v) { xt[b] = v; }),
-      rc_seg<1>(Q, [&](int e) {
+      rc_seg<1>(Q, [&](int e) {  // the nU (<= 8) partials loaded together, summed in slot order
+        const float* gp = ws + c.wo.gq + (int64_t)kj * Q + e;
+        const int64_t gs_ = (int64_t)K * p * Q;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = q < nU ? gp[q * gs_] : 0.f;
         float sq = 0.f;
-        for (int q = 0; q < nU; ++q) sq += ws[c.wo.gq + ((int64_t)q * K * p + kj) * Q + e];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (q < nU) sq += v[q];
         return sq;
       }, [&](int e, float v) { sqs[e] = v; }),
       rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }));

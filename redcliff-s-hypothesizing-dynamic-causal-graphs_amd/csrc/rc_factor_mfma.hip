@@ -666,8 +666,19 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW ==
 // v_mfma_f32_16x16x4_f32 with 16-UNIT blocks (h = 100 pads to 112 units, not 128).  A workgroup
 // stages its replica's batch of windows ONCE in LDS, straight from X (Xs[b][c*L + t], row stride
 // S = Qp16 + 4 so the operand reads below are bank-conflict free; no k_xwin, no Xw round trip),
-// then each wave works through `bpw` 16-unit blocks cb = (bx * bpw + i) * 4 + w with no further
+// then each wave works through `bpw` 16-unit blocks cb = bx * 4 bpw + 4 i + w with no further
 // barrier.  Lane l: l15 = l & 15, group g = l >> 4; D rows 4 g + reg, column l15.
+//
+// The k-step count NK4 = ceil(p*L / 4) is a template parameter (1..16): operand arrays live in
+// registers, the row stride is a constant, the loops unroll.  A block's parameters are one
+// contiguous run of W0 (its 16 rows of p*L weights), read and written lane-linearly through
+// buffer descriptors whose range ends at the last real unit (loads past it return 0, stores past
+// it are dropped), so the loads take immediate offsets and no address arithmetic or branches; the
+// weights pass through a wave-private LDS tile to the MFMA operand layout, and the backward's
+// gradient tile comes back through the same LDS.  The windows' dL/dy of the networks a
+// workgroup covers is staged in LDS next to the window tile, so the tile loop touches no global
+// memory.  Everything except the address arithmetic is the previous kernels' arithmetic in the
+// same order.
 //
 // The hidden pre-activations are q-ascending k-ordered fmaf chains in both kernels (the forward
 // as z[u][b] with W0 rows as the A operand, the backward's recompute as zT[b][u] with the X rows
@@ -676,7 +687,18 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW ==
 // the vector path's hidden chunks; StepCtx.fslots tells k_fac_mix how many to sum).
 __host__ __device__ inline int ms_qp16(const RedcliffDims& d) { return ((d.p * d.L + 15) >> 4) << 4; }
 __host__ __device__ inline int ms_rows(int B) { return (B + 31) & ~31; }
+__host__ __device__ inline int ms_nk4(const RedcliffDims& d) { return (d.p * d.L + 3) >> 2; }
+// networks the 4*bpw consecutive blocks of one workgroup can touch
+__host__ __device__ inline int ms_nnet(int bpw, int nU) { return (4 * bpw - 1) / nU + 2; }
+// per-wave LDS of the backward: the weight / gradient tile (64 NK4 floats) + dL/dG and G rows
+__host__ __device__ inline int ms_wave_floats(int nk4) { return 64 * nk4 + 128; }
 inline size_t ms_lds(const RedcliffDims& d, int B) { return sizeof(float) * (size_t)ms_rows(B) * (ms_qp16(d) + 4); }
+inline size_t ms_lds_fwd(const RedcliffDims& d, int B) {
+  return ms_lds(d, B) + sizeof(float) * 4 * (size_t)64 * ms_nk4(d);
+}
+inline size_t ms_lds_bwd(const RedcliffDims& d, int B, int bpw) {
+  return ms_lds(d, B) + sizeof(float) * ((size_t)ms_rows(B) * ms_nnet(bpw, (d.h + 15) >> 4) + 4 * (size_t)ms_wave_floats(ms_nk4(d)));
+}
 
 __device__ inline void ms_stage_x(const StepCtx& c, int r, float* Xs) {
   const RedcliffDims& d = c.d;
@@ -700,62 +722,119 @@ __device__ inline void ms_stage_x(const StepCtx& c, int r, float* Xs) {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Buffer descriptor over n floats from p (built from wave-uniform values): loads at or past the
+// end return 0, stores there are dropped.  Offsets in bytes.
+#define MS_OOB 0x40000000  // a byte offset past every range
+__device__ inline __amdgpu_buffer_rsrc_t ms_rsrc(const float* p, int n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, n * 4, 0x00020000);
+}
+// (the b32 builtins move raw 32-bit words: bit casts, not conversions)
+__device__ inline float ms_ld(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ inline void ms_st(__amdgpu_buffer_rsrc_t r, int off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+
+// row_ror:N within each 16-lane row (DPP): lane l reads lane (l -/+ N) mod 16 of its row
+template <int N>
+__device__ inline float ms_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + N, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of a row, every lane getting the same bits: the xor-8/4/2/1 butterfly
+// (lane l adds lane l^o); after the step with offset o the values repeat with period o, so
+// rotating by o reads the same operand as xor o.
+__device__ inline float ms_row_sum(float v) {
+  v += ms_ror<8>(v);
+  v += ms_ror<4>(v);
+  v += ms_ror<2>(v);
+  v += ms_ror<1>(v);
+  return v;
+}
+
+// The block's W0 rows (16 x p*L, contiguous; rows past h read as 0) lane-linearly into
+// registers: element e = lane + 64 k.
+template <int NK4>
+__device__ inline void ms_load_tile(__amdgpu_buffer_rsrc_t r, int lane, float (&t)[NK4]) {
+#pragma unroll
+  for (int k = 0; k < NK4; ++k) t[k] = ms_ld(r, 4 * (lane + 64 * k));
+}
+// ... through the wave's LDS tile into the MFMA operand layout: w[s] = W0[u0 + l15][4 s + g]
+template <int NK4>
+__device__ inline void ms_tile_operands(float* Wt, const float (&t)[NK4], int lane, int l15, int g, int Q, float (&w)[NK4]) {
+#pragma unroll
+  for (int k = 0; k < NK4; ++k) Wt[lane + 64 * k] = t[k];
+  const float* row = Wt + l15 * Q + g;
+#pragma unroll
+  for (int s = 0; s < NK4; ++s) {
+    const float v = row[4 * s];
+    w[s] = (s + 1 < NK4 || 4 * s + g < Q) ? v : 0.f;  // only the last k-step can pass Q
+  }
+}
+
 // Forward: z[u][b] = sum_q W0[u][q] X[b][q] (A = the block's W0 rows in registers, B = Xs rows),
 // two 16-window tiles at a time; epilogue a = relu(z + b0), y slot ub = sum_u W1[u] a (in-lane
 // over the 4 rows, then the 4 groups in order), + b1 in block 0; group norms of the block; W1
 // snapshot for the backward.
+template <int NK4>
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
+  constexpr int S = ((NK4 + 3) / 4) * 16 + 4;  // == ms_qp16(d) + 4
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.z);
-  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
-  const int nk4 = (Q + 3) >> 2, S = ms_qp16(d) + 4;
+  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU, KP = K * p;
+  const int rows = ms_rows(B);
   extern __shared__ float Xs[];
   const float* P = c.fac + r * c.fs;
   float* ws = c.ws + r * c.wss;
   ms_stage_x(c, r, Xs);
   __syncthreads();
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l15 = lane & 15, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  float* Wt = Xs + rows * S + wv * 64 * NK4;
+  const int cbase = (int)blockIdx.x * 4 * bpw + wv;
+  // lane offsets of the stores: y of window column l15 (group 0), the W1 snapshot of unit l15
+  // (group 0), the group norms of k-step l15 (q = 4 l15 + g)
+  const int y_off = g == 0 ? 4 * l15 * KP : MS_OOB;
+  const int w1_off = g == 0 ? 4 * l15 : MS_OOB;
+  const int gq_off = l15 < NK4 ? 4 * (4 * l15 + g) : MS_OOB;
   for (int i = 0; i < bpw; ++i) {
-    const int cb = ((int)blockIdx.x * bpw + i) * 4 + wv;
+    const int cb = cbase + 4 * i;
     if (cb >= NB) break;
     const int kj = cb / nU, ub = cb - kj * nU, u0 = ub * 16, k = kj / p, j = kj - k * p;
-    const int uA = u0 + l15;
-    const float* W0 = P + c.fo.W0 + ((int64_t)kj * h + uA) * Q;
-    float wA[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int q = 4 * s + g;
-      wA[s] = (s < nk4 && uA < h && q < Q) ? W0[q] : 0.f;
-    }
-    float bu[4], w1[4];
+    const int nu = min(16, h - u0);
+    // ---- the block's operands, all requested together
+    const auto rW = ms_rsrc(P + c.fo.W0 + ((int64_t)kj * h + u0) * Q, nu * Q);
+    const auto rB0 = ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu);
+    const auto rW1 = ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu);
+    float wt[NK4], wA[NK4], bu[4], w1[4];
+    ms_load_tile<NK4>(rW, lane, wt);
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
-      const int u = u0 + 4 * g + reg;
-      bu[reg] = u < h ? P[c.fo.b0 + (int64_t)kj * h + u] : 0.f;
-      w1[reg] = u < h ? P[c.fo.W1 + (int64_t)kj * h + u] : 0.f;
+      bu[reg] = ms_ld(rB0, 4 * (4 * g + reg));  // 0 past h
+      w1[reg] = ms_ld(rW1, 4 * (4 * g + reg));
     }
-    const float b1 = ub == 0 ? P[c.fo.b1 + kj] : 0.f;
-    if (g == 0 && uA < h) ws[c.wo.w1 + (int64_t)kj * h + uA] = P[c.fo.W1 + (int64_t)kj * h + uA];
+    const float w1A = ms_ld(rW1, 4 * l15);
+    const float b1v = P[c.fo.b1 + kj];
+    const float b1 = ub == 0 ? b1v : 0.f;
+    ms_tile_operands<NK4>(Wt, wt, lane, l15, g, Q, wA);
+    // ---- gq[ub][kj][q] = sum over the block's units of W0[u][q]^2 (pre-update weights); lane
+    // (l15, g) stores the sum of k-step s = l15, q = 4 l15 + g
+    float gsel = 0.f;
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {  // gq[ub][kj][q] = sum over the block's units of W0[u][q]^2
-      if (s < nk4) {
-        float sq = wA[s] * wA[s];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 64);  // within the 16-lane group
-        const int q = 4 * s + g;
-        if (l15 == 0 && q < Q) ws[c.wo.gq + ((int64_t)ub * K * p + kj) * Q + q] = sq;
-      }
+    for (int s = 0; s < NK4; ++s) {
+      const float sq = ms_row_sum(wA[s] * wA[s]);
+      gsel = l15 == s ? sq : gsel;
     }
+    ms_st(ms_rsrc(ws + c.wo.gq + ((int64_t)ub * KP + kj) * Q, Q), gq_off, gsel);
+    const auto rY = ms_rsrc(ws + c.wo.y + (int64_t)ub * d.Bmax * KP + k * p + j, B * KP);
     for (int t0 = 0; t0 < B; t0 += 32) {
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
       const float* x0 = Xs + (t0 + l15) * S + g;
       const float* x1 = x0 + 16 * S;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        if (s < nk4) {
-          a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x0[4 * s], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x1[4 * s], a1, 0, 0, 0);
-        }
+      for (int s = 0; s < NK4; ++s) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x0[4 * s], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wA[s], x1[4 * s], a1, 0, 0, 0);
       }
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
@@ -765,10 +844,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
         for (int reg = 0; reg < 4; ++reg) ys += w1[reg] * fmaxf(z[reg] + bu[reg], 0.f);  // w1 = 0 past h
         ys += __shfl_xor(ys, 16, 64);
         ys += __shfl_xor(ys, 32, 64);
-        const int b = t0 + 16 * tt + l15;
-        if (g == 0 && b < B) ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = ys + b1;
+        ms_st(rY, y_off + 4 * (t0 + 16 * tt) * KP, ys + b1);  // window t0 + 16 tt + l15 (dropped at or past B)
       }
     }
+    ms_st(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), w1_off, w1A);
   }
 }
 
@@ -780,12 +859,17 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
 //              lane group g -- the A operand IS the dZ register; B = Xs[t0 + 4 g + reg][16 qt + l15];
 //   dW1[u] = sum_b dy a, db0[u] = sum_b [a > 0] dy W1[u]: per lane over its windows, then the four
 //              groups in order, and their Adam step;
-//   epilogue: + the adjacency-L1 term through the group norms, Adam (or the gradient).
+//   epilogue (lane-linear over the block's W0 run, the gradient tile through LDS): + the
+//              adjacency-L1 term through the group norms, Adam (or the gradient).
+// A block costs one memory round trip: its W0 run, Adam moments, adjacency rows and output-layer
+// state are requested together at its start; dL/dy comes from the workgroup's LDS copy.
+template <int NK4>
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
+  constexpr int S = ((NK4 + 3) / 4) * 16 + 4, NQT = (NK4 + 3) / 4;
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.z);
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
-  const int nk4 = (Q + 3) >> 2, nqt = (Q + 15) >> 4, S = ms_qp16(d) + 4;
+  const int rows = ms_rows(B);
   extern __shared__ float Xs[];
   float* P = c.fac + r * c.fs;
   float* PM = c.facM + r * c.fs;
@@ -796,101 +880,134 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
   const bool adam = !(c.flags & RC_GRAD_ONLY);
   const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
+  // the Adam moments are read only when they exist (RC_GRAD_ONLY steps may run without them)
+  float* PMr = adam ? PM : P;
+  float* PVr = adam ? PV : P;
+  const int cb_lo = (int)blockIdx.x * 4 * bpw, cb_hi = min(NB, cb_lo + 4 * bpw) - 1;
+  const int kjlo = cb_lo / nU, nnet = cb_hi / nU - kjlo + 1;
+  float* Dys = Xs + rows * S;
+  {  // dL/dy of the workgroup's networks (zero past B), then the window tile
+    const RcDiv drow(rows);
+    const float* dyg = ws + c.wo.dyl;
+    rc_stage<4>(nnet * rows, [&](int e) {
+      const int n_ = drow.div(e), b = e - n_ * rows;
+      return b < B ? dyg[(int64_t)(kjlo + n_) * d.Bmax + b] : 0.f;
+    }, [&](int e, float v) { Dys[e] = v; });
+  }
   ms_stage_x(c, r, Xs);
   __syncthreads();
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, l15 = lane & 15, g = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  float* Wt = Dys + ms_nnet(bpw, nU) * rows + wv * ms_wave_floats(NK4);  // weight, then gradient tile
+  float* Dg = Wt + 64 * NK4;  // dL/dG row of the network (adjacency L1), then its group norms G
+  float* Gn = Dg + 64;
+  const int u_off = g == 0 ? 4 * l15 : MS_OOB;  // output-layer updates: group 0, unit l15
+  // lane-linear epilogue elements e = lane + 64 k of the block's run: (row, column) = (e / Q, e % Q)
+  const int q0 = lane % Q, dq = 64 % Q;
   for (int i = 0; i < bpw; ++i) {
-    const int cb = ((int)blockIdx.x * bpw + i) * 4 + wv;
+    const int cb = cb_lo + 4 * i + wv;
     if (cb >= NB) break;
     const int kj = cb / nU, u0 = (cb - kj * nU) * 16;
-    const int uL = u0 + l15;
-    const bool uvL = uL < h;
-    float* W0 = P + c.fo.W0 + (int64_t)kj * h * Q;
-    const float* dyl = ws + c.wo.dyl + (int64_t)kj * d.Bmax;
-    float wB[16];
+    const int nu = min(16, h - u0), uL = u0 + l15;
+    const int64_t wofs = c.fo.W0 + ((int64_t)kj * h + u0) * Q;
+    const auto rW = ms_rsrc(P + wofs, nu * Q);
+    const auto rB0 = ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu);
+    const auto rW1 = ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu);
+    // ---- the block's operands, all requested together: recompute operands first
+    float wt[NK4], mt[NK4], vt[NK4], wB[NK4];
+    ms_load_tile<NK4>(rW, lane, wt);
+    const float tbu = ms_ld(rB0, 4 * l15);                                               // 0 past h
+    const float tw1 = ms_ld(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), 4 * l15);  // pre-update snapshot
+    // issue order = arrival order: the tile loop then waits only for the operands above
+    asm volatile("" ::: "memory");
+    ms_load_tile<NK4>(ms_rsrc(PMr + wofs, nu * Q), lane, mt);
+    ms_load_tile<NK4>(ms_rsrc(PVr + wofs, nu * Q), lane, vt);
+    const float dgv = ms_ld(ms_rsrc(ws + c.wo.dgs + (int64_t)kj * Q, Q), 4 * lane);
+    const float gnv = ms_ld(ms_rsrc(ws + c.wo.G + (int64_t)kj * Q, Q), 4 * lane);
+    const auto rMb = ms_rsrc(PMr + c.fo.b0 + (int64_t)kj * h + u0, nu), rVb = ms_rsrc(PVr + c.fo.b0 + (int64_t)kj * h + u0, nu);
+    const auto rMw = ms_rsrc(PMr + c.fo.W1 + (int64_t)kj * h + u0, nu), rVw = ms_rsrc(PVr + c.fo.W1 + (int64_t)kj * h + u0, nu);
+    float sb[6] = {tbu, ms_ld(rMb, 4 * l15), ms_ld(rVb, 4 * l15), ms_ld(rW1, 4 * l15), ms_ld(rMw, 4 * l15), ms_ld(rVw, 4 * l15)};
+    ms_tile_operands<NK4>(Wt, wt, lane, l15, g, Q, wB);
+    const float bu = tbu, w1 = tw1;  // 0 past h
+    f32x4 acc[NQT];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int q = 4 * s + g;
-      wB[s] = (s < nk4 && uvL && q < Q) ? W0[(int64_t)uL * Q + q] : 0.f;
-    }
-    const float bu = uvL ? P[c.fo.b0 + (int64_t)kj * h + uL] : 0.f;
-    const float w1 = uvL ? ws[c.wo.w1 + (int64_t)kj * h + uL] : 0.f;  // pre-update snapshot
-    f32x4 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NQT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float pa = 0.f, pb = 0.f;
+    const float* dyn = Dys + (kj - kjlo) * rows + 4 * g;
     for (int t0 = 0; t0 < B; t0 += 16) {
-      float dy[4];
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int b = t0 + 4 * g + reg;
-        dy[reg] = b < B ? dyl[b] : 0.f;
-      }
+      const f32x4 dy = *reinterpret_cast<const f32x4*>(dyn + t0);  // windows t0 + 4 g + reg
       f32x4 z = {0.f, 0.f, 0.f, 0.f};
       const float* xr = Xs + (t0 + l15) * S + g;
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
-        if (s < nk4) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], wB[s], z, 0, 0, 0);
+      for (int s = 0; s < NK4; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], wB[s], z, 0, 0, 0);
       float dz[4];
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
 #pragma clang fp contract(off)
         const float a = fmaxf(z[reg] + bu, 0.f);
-        dz[reg] = (a > 0.f ? dy[reg] : 0.f) * w1;
+        // dZ = [a > 0] dL/dy W1; the output-layer sums take the same rounded product (a zero
+        // dZ adds nothing whatever its sign)
+        dz[reg] = a > 0.f ? dy[reg] * w1 : 0.f;
         pa = pa + dy[reg] * a;
-        pb = pb + (a > 0.f ? dy[reg] * w1 : 0.f);
+        pb = pb + dz[reg];
       }
       const float* xq = Xs + (t0 + 4 * g) * S + l15;
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
 #pragma unroll
-        for (int qt = 0; qt < 4; ++qt)
-          if (qt < nqt) acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[reg], xq[reg * S + 16 * qt], acc[qt], 0, 0, 0);
+        for (int qt = 0; qt < NQT; ++qt)
+          acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[reg], xq[reg * S + 16 * qt], acc[qt], 0, 0, 0);
     }
     {  // output layer / hidden bias of the lane's unit: the four groups' partial sums in order
       const float a1 = __shfl(pa, l15 + 16, 64), a2 = __shfl(pa, l15 + 32, 64), a3 = __shfl(pa, l15 + 48, 64);
       const float b1 = __shfl(pb, l15 + 16, 64), b2 = __shfl(pb, l15 + 32, 64), b3 = __shfl(pb, l15 + 48, 64);
-      if (g == 0 && uvL) {
-        rc_update(c, P, PM, PV, GF, c.fo.b0 + (int64_t)kj * h + uL, ((pb + b1) + b2) + b3, as);
-        rc_update(c, P, PM, PV, GF, c.fo.W1 + (int64_t)kj * h + uL, ((pa + a1) + a2) + a3, as);
+      const float g0 = ((pb + b1) + b2) + b3, g1 = ((pa + a1) + a2) + a3;
+      if (!adam) {  // group 0 stores, rows past h dropped
+        ms_st(ms_rsrc(GF + c.fo.b0 + (int64_t)kj * h + u0, nu), u_off, g0);
+        ms_st(ms_rsrc(GF + c.fo.W1 + (int64_t)kj * h + u0, nu), u_off, g1);
+      } else {
+        rc_adam(sb[0], sb[1], sb[2], g0, as);
+        rc_adam(sb[3], sb[4], sb[5], g1, as);
+        ms_st(rB0, u_off, sb[0]);
+        ms_st(rMb, u_off, sb[1]);
+        ms_st(rVb, u_off, sb[2]);
+        ms_st(rW1, u_off, sb[3]);
+        ms_st(rMw, u_off, sb[4]);
+        ms_st(rVw, u_off, sb[5]);
       }
     }
-    // ---- epilogue: dW0[u = u0 + 4 g + reg][q = 16 qt + l15]
-    float* M0 = PM + c.fo.W0 + (int64_t)kj * h * Q;
-    float* V0 = PV + c.fo.W0 + (int64_t)kj * h * Q;
-    float* G0w = GF + c.fo.W0 + (int64_t)kj * h * Q;
+    // ---- gradient tile (row stride Q) into the wave's LDS tile: the weight operands were read
+    // from it before the tile loop; the pre-update weights stay in wt[]
+    Dg[lane] = dgv;
+    Gn[lane] = gnv;
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
+    for (int qt = 0; qt < NQT; ++qt) {
       const int q = 16 * qt + l15;
-      if (qt >= nqt || q >= Q) continue;
-      const float dg = adj_grad ? ws[c.wo.dgs + (int64_t)kj * Q + q] : 0.f;
-      const float gn = adj_grad ? ws[c.wo.G + (int64_t)kj * Q + q] : 0.f;
-      float pw[4], pm[4], pv[4];
+      if (qt + 1 < NQT || q < Q)
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int u = u0 + 4 * g + reg;
-        const int64_t idx = (int64_t)u * Q + q;
-        const bool in = u < h;
-        pw[reg] = (in && (adam || adj_grad)) ? W0[idx] : 0.f;
-        pm[reg] = (in && adam) ? M0[idx] : 0.f;
-        pv[reg] = (in && adam) ? V0[idx] : 0.f;
-      }
+        for (int reg = 0; reg < 4; ++reg) Wt[(4 * g + reg) * Q + q] = acc[qt][reg];
+    }
+    // ---- epilogue, lane-linear: + the adjacency term through the group norms, then Adam (or the
+    // gradient); elements past the block's run are computed on zeros and their stores dropped
+    const auto rM = ms_rsrc(PMr + wofs, nu * Q), rV = ms_rsrc(PVr + wofs, nu * Q), rG = ms_rsrc(GF + wofs, nu * Q);
+    int q = q0;
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int u = u0 + 4 * g + reg;
-        if (u >= h) continue;
-        const int64_t idx = (int64_t)u * Q + q;
-        float gr = acc[qt][reg];
-        if (adj_grad && gn > 0.f) gr += dg * (pw[reg] / gn);
-        if (!adam) {
-          G0w[idx] = gr;
-        } else {
-          rc_adam(pw[reg], pm[reg], pv[reg], gr, as);
-          W0[idx] = pw[reg];
-          M0[idx] = pm[reg];
-          V0[idx] = pv[reg];
-        }
+    for (int k = 0; k < NK4; ++k) {
+      const int e = lane + 64 * k;  // gradient tile element (row e / Q, column q = e % Q)
+      float gr = Wt[e];
+      const float dg = Dg[q], gn = Gn[q], pw = wt[k];
+      if (adj_grad && gn > 0.f) gr += dg * (pw / gn);
+      if (!adam) {
+        ms_st(rG, 4 * e, gr);
+      } else {
+        float pp = pw, mm = mt[k], vv = vt[k];
+        rc_adam(pp, mm, vv, gr, as);
+        ms_st(rW, 4 * e, pp);
+        ms_st(rM, 4 * e, mm);
+        ms_st(rV, 4 * e, vv);
       }
+      q += dq;
+      q = q >= Q ? q - Q : q;
     }
   }
 }
@@ -927,24 +1044,85 @@ bool rc_fac_short(const RedcliffDims& d) {
 // y / group-norm slots the forward writes (k_fac_mix sums them): 16- or 32-unit blocks
 int rc_fac_slots(const RedcliffDims& d) { return rc_fac_short(d) ? (d.h + 15) / 16 : mf_nub(d); }
 
-// blocks per wave of the short kernels: 4 when the replica axis fills the chip, else 1
-static int ms_bpw(const StepCtx& c) {
-  const RedcliffDims& d = c.d;
-  const int NB = d.K * d.p * ((d.h + 15) / 16);
-  return (int64_t)c.nrep * ((NB + 15) / 16) >= 1024 ? 4 : 1;
+// Launch of the short-contraction kernels: the k-step count picks the instantiation, and the
+// blocks per wave are chosen so the grid is about one round of resident workgroups (the
+// occupancy the runtime computes from the kernel's registers and this launch's LDS, times the
+// CUs): at the D4IC grid (R = 128, 280 blocks per replica) 12 forward / 8 backward workgroups
+// per replica instead of 1.5 rounds with a half-empty tail.  REDCLIFF_FAC_BPW=n overrides.
+typedef void (*MsKern)(StepCtx, int);
+template <int N>
+struct MsTab {
+  static void fill(MsKern* f, MsKern* b) {
+    f[N - 1] = k_fac_fwd_s16<N>;
+    b[N - 1] = k_fac_bwd_s16<N>;
+    MsTab<N - 1>::fill(f, b);
+  }
+};
+template <>
+struct MsTab<0> {
+  static void fill(MsKern*, MsKern*) {}
+};
+
+static int ms_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return v;
+  }();
+  return n;
 }
 
-template <class Kern>
-static int ms_launch(Kern k, const StepCtx& c, hipStream_t s, const char* what) {
+static int ms_occupancy(MsKern k, size_t lds) {
+  struct Ent { MsKern k; size_t lds; int occ; };
+  static thread_local Ent cache[32];
+  static thread_local int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (cache[i].k == k && cache[i].lds == lds) return cache[i].occ;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, RC_BLOCK, lds) != hipSuccess) nb = 0;
+  cache[n < 32 ? n++ : 31] = Ent{k, lds, nb};
+  return nb;
+}
+
+static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
+  static MsKern tf[16], tb[16];
+  static const bool init = (MsTab<16>::fill(tf, tb), true);
+  (void)init;
   const RedcliffDims& d = c.d;
-  const size_t lds = ms_lds(d, c.B);
-  if (lds > 160 * 1024) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
+  const char* what = bwd ? "k_fac_bwd_s16" : "k_fac_fwd_s16";
+  const int nk4 = ms_nk4(d);
+  if (nk4 < 1 || nk4 > 16) { rc_set_error("%s: p*L = %d outside the short-contraction kernels", what, d.p * d.L); return REDCLIFF_ELIMIT; }
+  MsKern k = bwd ? tb[nk4 - 1] : tf[nk4 - 1];
+  const int NB = d.K * d.p * ((d.h + 15) / 16);
+  const size_t cap = RC_LDS_MAX_FLOATS * sizeof(float);
+  size_t lds = bwd ? ms_lds_bwd(d, c.B, 1) : ms_lds_fwd(d, c.B);
+  if (lds > cap) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
+  int bpw = 1;
+  const char* env = getenv("REDCLIFF_FAC_BPW");
+  if (env && atoi(env) > 0) {
+    bpw = atoi(env);
+  } else {
+    static bool optin[2][16];
+    if (!optin[bwd][nk4 - 1]) {  // the occupancy query of a launch past 64 KiB needs the opt-in
+      const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap), what);
+      if (e) return e;
+      optin[bwd][nk4 - 1] = true;
+    }
+    const int64_t slots = (int64_t)ms_occupancy(k, lds) * ms_cus();
+    if (slots > 0) {
+      const int64_t blocks = (int64_t)NB * c.nrep, want = (blocks + 4 * slots - 1) / (4 * slots);
+      bpw = (int)(want < 1 ? 1 : (want > 16 ? 16 : want));
+    }
+  }
+  if (bwd)
+    while (bpw > 1 && ms_lds_bwd(d, c.B, bpw) > cap) --bpw;
+  if (bwd) lds = ms_lds_bwd(d, c.B, bpw);
+  if (lds > cap) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
-    const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)lds), what);
+    const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), what);
     if (e) return e;
   }
-  const int NB = d.K * d.p * ((d.h + 15) / 16), bpw = ms_bpw(c);
   hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw);
   return rc_check(hipGetLastError(), what);
 }
@@ -952,7 +1130,7 @@ static int ms_launch(Kern k, const StepCtx& c, hipStream_t s, const char* what) 
 int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (c.fslots != rc_fac_slots(d)) { rc_set_error("factor forward: slot layout changed within a step"); return REDCLIFF_EINVAL; }
-  if (rc_fac_short(d)) return ms_launch(k_fac_fwd_s16, c, s, "k_fac_fwd_s16");
+  if (rc_fac_short(d)) return ms_launch(false, c, s);
   const int KP = d.K * d.p;
   const int nxw = (c.B * rc_qpad(d) + XW_PER * RC_BLOCK - 1) / (XW_PER * RC_BLOCK);
   hipLaunchKernelGGL(k_xwin, dim3(nxw, c.nrep), dim3(RC_BLOCK), 0, s, c);
@@ -976,7 +1154,7 @@ int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (!(c.flags & RC_STEP_B)) return 0;
   const int NB = d.K * d.p * ((d.h + 31) / 32), Q = d.p * d.L;
-  if (rc_fac_short(d)) return ms_launch(k_fac_bwd_s16, c, s, "k_fac_bwd_s16");
+  if (rc_fac_short(d)) return ms_launch(true, c, s);
   if (Q <= 64)  // short contraction rows: four column blocks share one 64-column X tile
     hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
   else

@@ -53,8 +53,14 @@ def compare(a, b):
     A, B = np.load(a), np.load(b)
     assert set(A.files) == set(B.files)
     bad = [k for k in A.files if not np.array_equal(A[k], B[k])]
-    for k in bad[:20]:
-        print("DIFF %s: max |d| %.3e" % (k, float(np.abs(A[k].astype(np.float64) - B[k]).max())))
+    nshow = int(os.environ.get("COMPARE_SHOW", "20"))
+    for k in bad[:nshow]:
+        d = np.abs(A[k].astype(np.float64) - B[k])
+        i = np.unravel_index(int(np.argmax(d)), d.shape) if d.ndim else ()
+        rel = d / np.maximum(np.abs(A[k].astype(np.float64)), 1e-30)
+        print("DIFF %s %s: max |d| %.3e at %s (a=%.6g b=%.6g), %d/%d differ, %d with rel > 1e-4"
+              % (k, A[k].shape, float(d.max()), i, float(A[k][i]), float(B[k][i]), int((d > 0).sum()), d.size,
+                 int((rel > 1e-4).sum())))
     print("%d / %d tensors differ" % (len(bad), len(A.files)))
     sys.exit(1 if bad else 0)
 
