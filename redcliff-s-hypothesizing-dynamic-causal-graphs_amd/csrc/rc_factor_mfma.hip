@@ -246,12 +246,19 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
   const int nUB = c.fslots;  // y / group-norm slots of the forward (16- or 32-unit blocks)
-  for (int e = tid; e < B * K; e += RC_BLOCK) {
-    const int b = e / K, kk = e - b * K;
-    float yv = ws[c.wo.y + ((int64_t)b * K + kk) * p + j];
-    for (int ub = 1; ub < nUB; ++ub) yv += ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + kk) * p + j];
-    ybuf[e] = yv;
-  }
+  // the nUB (<= 8) slot partials of every prediction requested together, summed in slot order
+  rc_stage<2>(B * K, [&](int e) {
+    const float* yp = ws + c.wo.y + (int64_t)e * p + j;  // e = b * K + kk
+    const int64_t ys_ = (int64_t)d.Bmax * K * p;
+    float v[8];
+#pragma unroll
+    for (int ub = 0; ub < 8; ++ub) v[ub] = ub < nUB ? yp[ub * ys_] : 0.f;
+    float yv = v[0];
+#pragma unroll
+    for (int ub = 1; ub < 8; ++ub)
+      if (ub < nUB) yv += v[ub];
+    return yv;
+  }, [&](int e, float v) { ybuf[e] = v; });
   __syncthreads();
   float fsum = 0.f;
   for (int b = tid; b < B; b += RC_BLOCK) {
@@ -283,8 +290,15 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 17);
   // ---- group norms G[kj][c][t], G0[kj][c] (cmlp.py:147-167) from the forward's squared norms
   for (int e = tid; e < Q; e += RC_BLOCK) {
-    float sq = ws[c.wo.gq + (int64_t)kj * Q + e];
-    for (int ub = 1; ub < nUB; ++ub) sq += ws[c.wo.gq + ((int64_t)ub * K * p + kj) * Q + e];
+    const float* gp = ws + c.wo.gq + (int64_t)kj * Q + e;
+    const int64_t gs_ = (int64_t)K * p * Q;
+    float v[8];
+#pragma unroll
+    for (int ub = 0; ub < 8; ++ub) v[ub] = ub < nUB ? gp[ub * gs_] : 0.f;
+    float sq = v[0];
+#pragma unroll
+    for (int ub = 1; ub < 8; ++ub)
+      if (ub < nUB) sq += v[ub];
     sqs[e] = sq;
     Gs[e] = sqrtf(sq);
     ws[c.wo.G + (int64_t)kj * Q + e] = Gs[e];
@@ -797,26 +811,36 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
   const int y_off = g == 0 ? 4 * l15 * KP : MS_OOB;
   const int w1_off = g == 0 ? 4 * l15 : MS_OOB;
   const int gq_off = l15 < NK4 ? 4 * (4 * l15 + g) : MS_OOB;
+  // a block's operands: its W0 run (lane-linear), b0 / W1 of rows 4 g + reg, W1 of unit l15, b1;
+  // requested one block ahead, so their latency overlaps the previous block's matrix-core work
+  struct Ops {
+    float wt[NK4], bu[4], w1[4], w1A, b1;
+  };
+  auto issue = [&](int cb, Ops& o) {
+    if (cb >= NB) return;
+    const int kj = cb / nU, u0 = (cb - kj * nU) * 16, nu = min(16, h - u0);
+    ms_load_tile<NK4>(ms_rsrc(P + c.fo.W0 + ((int64_t)kj * h + u0) * Q, nu * Q), lane, o.wt);
+    const auto rB0 = ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu);
+    const auto rW1 = ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      o.bu[reg] = ms_ld(rB0, 4 * (4 * g + reg));  // 0 past h
+      o.w1[reg] = ms_ld(rW1, 4 * (4 * g + reg));
+    }
+    o.w1A = ms_ld(rW1, 4 * l15);
+    o.b1 = P[c.fo.b1 + kj];
+  };
+  Ops cur, nxt;
+  issue(cbase, cur);
   for (int i = 0; i < bpw; ++i) {
     const int cb = cbase + 4 * i;
     if (cb >= NB) break;
     const int kj = cb / nU, ub = cb - kj * nU, u0 = ub * 16, k = kj / p, j = kj - k * p;
     const int nu = min(16, h - u0);
-    // ---- the block's operands, all requested together
-    const auto rW = ms_rsrc(P + c.fo.W0 + ((int64_t)kj * h + u0) * Q, nu * Q);
-    const auto rB0 = ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu);
-    const auto rW1 = ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu);
-    float wt[NK4], wA[NK4], bu[4], w1[4];
-    ms_load_tile<NK4>(rW, lane, wt);
-#pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-      bu[reg] = ms_ld(rB0, 4 * (4 * g + reg));  // 0 past h
-      w1[reg] = ms_ld(rW1, 4 * (4 * g + reg));
-    }
-    const float w1A = ms_ld(rW1, 4 * l15);
-    const float b1v = P[c.fo.b1 + kj];
-    const float b1 = ub == 0 ? b1v : 0.f;
-    ms_tile_operands<NK4>(Wt, wt, lane, l15, g, Q, wA);
+    float wA[NK4];
+    ms_tile_operands<NK4>(Wt, cur.wt, lane, l15, g, Q, wA);
+    issue(cb + 4, nxt);
+    const float b1 = ub == 0 ? cur.b1 : 0.f;
     // ---- gq[ub][kj][q] = sum over the block's units of W0[u][q]^2 (pre-update weights); lane
     // (l15, g) stores the sum of k-step s = l15, q = 4 l15 + g
     float gsel = 0.f;
@@ -841,13 +865,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
         const f32x4 z = tt ? a1 : a0;
         float ys = 0.f;
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) ys += w1[reg] * fmaxf(z[reg] + bu[reg], 0.f);  // w1 = 0 past h
+        for (int reg = 0; reg < 4; ++reg) ys += cur.w1[reg] * fmaxf(z[reg] + cur.bu[reg], 0.f);  // w1 = 0 past h
         ys += __shfl_xor(ys, 16, 64);
         ys += __shfl_xor(ys, 32, 64);
         ms_st(rY, y_off + 4 * (t0 + 16 * tt) * KP, ys + b1);  // window t0 + 16 tt + l15 (dropped at or past B)
       }
     }
-    ms_st(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), w1_off, w1A);
+    ms_st(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), w1_off, cur.w1A);
+    cur = nxt;
   }
 }
 
@@ -902,61 +927,83 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
   float* Dg = Wt + 64 * NK4;  // dL/dG row of the network (adjacency L1), then its group norms G
   float* Gn = Dg + 64;
   const int u_off = g == 0 ? 4 * l15 : MS_OOB;  // output-layer updates: group 0, unit l15
-  // lane-linear epilogue elements e = lane + 64 k of the block's run: (row, column) = (e / Q, e % Q)
+  // lane-linear epilogue elements e = lane + 64 k of the block's run: column q = e % Q
   const int q0 = lane % Q, dq = 64 % Q;
+  // the recompute operands of a block (its W0 run, b0 and the W1 snapshot of unit l15), requested
+  // one block ahead so their latency overlaps the previous block's matrix-core work
+  struct Ops {
+    float wt[NK4], bu, w1;
+  };
+  auto issue = [&](int cb, Ops& o) {
+    if (cb >= NB) return;
+    const int kj = cb / nU, u0 = (cb - kj * nU) * 16, nu = min(16, h - u0);
+    ms_load_tile<NK4>(ms_rsrc(P + c.fo.W0 + ((int64_t)kj * h + u0) * Q, nu * Q), lane, o.wt);
+    o.bu = ms_ld(ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu), 4 * l15);              // 0 past h
+    o.w1 = ms_ld(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), 4 * l15);             // pre-update snapshot
+  };
+  Ops cur, nxt;
+  issue(cb_lo + wv, cur);
   for (int i = 0; i < bpw; ++i) {
     const int cb = cb_lo + 4 * i + wv;
     if (cb >= NB) break;
     const int kj = cb / nU, u0 = (cb - kj * nU) * 16;
-    const int nu = min(16, h - u0), uL = u0 + l15;
+    const int nu = min(16, h - u0);
     const int64_t wofs = c.fo.W0 + ((int64_t)kj * h + u0) * Q;
     const auto rW = ms_rsrc(P + wofs, nu * Q);
     const auto rB0 = ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu);
     const auto rW1 = ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu);
-    // ---- the block's operands, all requested together: recompute operands first
-    float wt[NK4], mt[NK4], vt[NK4], wB[NK4];
-    ms_load_tile<NK4>(rW, lane, wt);
-    const float tbu = ms_ld(rB0, 4 * l15);                                               // 0 past h
-    const float tw1 = ms_ld(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), 4 * l15);  // pre-update snapshot
-    // issue order = arrival order: the tile loop then waits only for the operands above
-    asm volatile("" ::: "memory");
+    float wB[NK4], mt[NK4], vt[NK4];
+    ms_tile_operands<NK4>(Wt, cur.wt, lane, l15, g, Q, wB);
+    // this block's epilogue operands (Adam moments of the run, adjacency rows, output-layer
+    // state), then the next block's recompute operands: issue order = arrival order
     ms_load_tile<NK4>(ms_rsrc(PMr + wofs, nu * Q), lane, mt);
     ms_load_tile<NK4>(ms_rsrc(PVr + wofs, nu * Q), lane, vt);
     const float dgv = ms_ld(ms_rsrc(ws + c.wo.dgs + (int64_t)kj * Q, Q), 4 * lane);
     const float gnv = ms_ld(ms_rsrc(ws + c.wo.G + (int64_t)kj * Q, Q), 4 * lane);
     const auto rMb = ms_rsrc(PMr + c.fo.b0 + (int64_t)kj * h + u0, nu), rVb = ms_rsrc(PVr + c.fo.b0 + (int64_t)kj * h + u0, nu);
     const auto rMw = ms_rsrc(PMr + c.fo.W1 + (int64_t)kj * h + u0, nu), rVw = ms_rsrc(PVr + c.fo.W1 + (int64_t)kj * h + u0, nu);
-    float sb[6] = {tbu, ms_ld(rMb, 4 * l15), ms_ld(rVb, 4 * l15), ms_ld(rW1, 4 * l15), ms_ld(rMw, 4 * l15), ms_ld(rVw, 4 * l15)};
-    ms_tile_operands<NK4>(Wt, wt, lane, l15, g, Q, wB);
-    const float bu = tbu, w1 = tw1;  // 0 past h
+    float sb[6] = {cur.bu, ms_ld(rMb, 4 * l15), ms_ld(rVb, 4 * l15), ms_ld(rW1, 4 * l15), ms_ld(rMw, 4 * l15), ms_ld(rVw, 4 * l15)};
+    issue(cb + 4, nxt);
+    const float bu = cur.bu, w1 = cur.w1;  // 0 past h
     f32x4 acc[NQT];
 #pragma unroll
     for (int t = 0; t < NQT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float pa = 0.f, pb = 0.f;
     const float* dyn = Dys + (kj - kjlo) * rows + 4 * g;
-    for (int t0 = 0; t0 < B; t0 += 16) {
-      const f32x4 dy = *reinterpret_cast<const f32x4*>(dyn + t0);  // windows t0 + 4 g + reg
-      f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    // two 16-window tiles per pass (independent recompute chains); rows past B are zero windows
+    // with zero dL/dy, which add exact zeros, and the tile pairs run to a multiple of 32 <= rows
+    for (int t0 = 0; t0 < B; t0 += 32) {
+      f32x4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       const float* xr = Xs + (t0 + l15) * S + g;
 #pragma unroll
-      for (int s = 0; s < NK4; ++s) z = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], wB[s], z, 0, 0, 0);
-      float dz[4];
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-#pragma clang fp contract(off)
-        const float a = fmaxf(z[reg] + bu, 0.f);
-        // dZ = [a > 0] dL/dy W1; the output-layer sums take the same rounded product (a zero
-        // dZ adds nothing whatever its sign)
-        dz[reg] = a > 0.f ? dy[reg] * w1 : 0.f;
-        pa = pa + dy[reg] * a;
-        pb = pb + dz[reg];
+      for (int s = 0; s < NK4; ++s) {
+        z[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], wB[s], z[0], 0, 0, 0);
+        z[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[16 * S + 4 * s], wB[s], z[1], 0, 0, 0);
       }
-      const float* xq = Xs + (t0 + 4 * g) * S + l15;
+      float dz[2][4];
 #pragma unroll
-      for (int reg = 0; reg < 4; ++reg)
+      for (int tt = 0; tt < 2; ++tt) {
+        const f32x4 dy = *reinterpret_cast<const f32x4*>(dyn + t0 + 16 * tt);  // windows t0 + 16 tt + 4 g + reg
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt)
-          acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[reg], xq[reg * S + 16 * qt], acc[qt], 0, 0, 0);
+        for (int reg = 0; reg < 4; ++reg) {
+#pragma clang fp contract(off)
+          const float a = fmaxf(z[tt][reg] + bu, 0.f);
+          // dZ = [a > 0] dL/dy W1; the output-layer sums take the same rounded product (a zero
+          // dZ adds nothing whatever its sign)
+          dz[tt][reg] = a > 0.f ? dy[reg] * w1 : 0.f;
+          pa = pa + dy[reg] * a;
+          pb = pb + dz[tt][reg];
+        }
+      }
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt) {
+        const float* xq = Xs + (t0 + 16 * tt + 4 * g) * S + l15;
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+#pragma unroll
+          for (int qt = 0; qt < NQT; ++qt)
+            acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[tt][reg], xq[reg * S + 16 * qt], acc[qt], 0, 0, 0);
+      }
     }
     {  // output layer / hidden bias of the lane's unit: the four groups' partial sums in order
       const float a1 = __shfl(pa, l15 + 16, 64), a2 = __shfl(pa, l15 + 32, 64), a3 = __shfl(pa, l15 + 48, 64);
@@ -977,7 +1024,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
       }
     }
     // ---- gradient tile (row stride Q) into the wave's LDS tile: the weight operands were read
-    // from it before the tile loop; the pre-update weights stay in wt[]
+    // from it before the tile loop; the pre-update weights stay in cur.wt
     Dg[lane] = dgv;
     Gn[lane] = gnv;
 #pragma unroll
@@ -995,7 +1042,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
     for (int k = 0; k < NK4; ++k) {
       const int e = lane + 64 * k;  // gradient tile element (row e / Q, column q = e % Q)
       float gr = Wt[e];
-      const float dg = Dg[q], gn = Gn[q], pw = wt[k];
+      const float dg = Dg[q], gn = Gn[q], pw = cur.wt[k];
       if (adj_grad && gn > 0.f) gr += dg * (pw / gn);
       if (!adam) {
         ms_st(rG, 4 * e, gr);
@@ -1009,6 +1056,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
       q += dq;
       q = q >= Q ? q - Q : q;
     }
+    cur = nxt;
   }
 }
 

@@ -9,7 +9,7 @@ models/cmlp.py:13-27) so seeded models are bit-identical.  ``forward``, ``GC`` a
 import torch
 import torch.nn as nn
 
-from . import kernels
+from . import kernels, wavelets
 
 
 class MLP(nn.Module):
@@ -40,15 +40,19 @@ class MLP(nn.Module):
 
 class cMLP(nn.Module):
     def __init__(self, num_chans, lag, hidden, wavelet_level=None, save_path=None):
+        """wavelet_level = l: num_chans * (l + 1) wavelet series and the ranking mask of
+        models/cmlp.py:57-82 (redcliff_amd.wavelets; the mask heat-map plot is not drawn)."""
         super().__init__()
-        if wavelet_level is not None:
-            raise NotImplementedError("wavelet_level != None (wavelet-decomposed inputs) is outside the MI355X path")
         self.num_chans = num_chans
-        self.wavelet_level = None
-        self.wavelet_mask = None
+        self.wavelet_level = wavelet_level
         self.lag = lag
         self.hidden = list(hidden)
-        self.num_series = num_chans
+        if wavelet_level is None:
+            self.num_series = num_chans
+            self.wavelet_mask = None
+        else:
+            self.num_series = int(num_chans * (wavelet_level + 1))
+            self.wavelet_mask = wavelets.factor_mask(num_chans, wavelet_level)
         self.activation = torch.nn.ReLU()
         self.networks = nn.ModuleList([MLP(self.num_series, lag, hidden) for _ in range(self.num_series)])
 
@@ -63,10 +67,17 @@ class cMLP(nn.Module):
         kernels.cmlp_prox([self], lam, lr, penalty)
 
     def GC(self, threshold=True, ignore_lag=True, combine_wavelet_representations=False, rank_wavelets=False):
-        """Group norms of layer-0 weights: (p, p) or (p, p, lag) (models/cmlp.py:147-203)."""
-        if rank_wavelets:
-            raise NotImplementedError("rank_wavelets needs wavelet_level != None")
+        """Group norms of layer-0 weights: (p, p) or (p, p, lag), then the wavelet ranking /
+        combination and the threshold (models/cmlp.py:147-203)."""
         from . import autograd as AG
         G, G0 = AG.group_norms([self]) if not threshold else kernels.cmlp_gc_norms([self])
         out = G0[0] if ignore_lag else G[0]
+        out = self.gc_post(out, ignore_lag, combine_wavelet_representations, rank_wavelets)
         return (out > 0).int() if threshold else out
+
+    def gc_post(self, G, ignore_lag, combine, rank):
+        """Ranking mask and wavelet combination of one (un-thresholded) estimate."""
+        if not rank and not (self.wavelet_level is not None and combine):
+            return G
+        return wavelets.gc_post(G, self.wavelet_mask, self.wavelet_level, self.num_chans, self.num_series, self.lag,
+                                ignore_lag, combine, rank)

@@ -289,58 +289,64 @@ class GenericPath:
         return ys
 
     # -------------------------------------------------------------- GC
-    def factor_gcs(self, threshold, ignore_lag):
-        m = self.m
+    def factor_gcs(self, threshold, ignore_lag, combine=False, rank=False):
+        """cMLP.GC of every factor: norms, wavelet ranking / combination (models/cmlp.py:169-200),
+        threshold, (n, n, 1) when lag-free (:450-454)."""
         out = []
-        for f in m.factors:
-            G = group_norms([net.layers[0].weight for net in f.networks], ignore_lag)
+        for f in self.m.factors:
+            G = f.gc_post(group_norms([net.layers[0].weight for net in f.networks], ignore_lag), ignore_lag, combine,
+                          rank)
             if G.dim() != 3:
-                G = G.view(m.num_series, m.num_series, 1)
+                G = G.view(G.size(0), G.size(0), 1)
             out.append((G > 0).int() if threshold else G)
         return out
 
-    def raw_embedder_gc(self, threshold, ignore_lag, combine):
+    def raw_embedder_gc(self, threshold, ignore_lag, combine, rank=False):
         m = self.m
         emb = m.factor_score_embedder
         if m.factor_score_embedder_type == "cEmbedder":
-            G = group_norms([net.layers[0].weight for net in emb.networks], ignore_lag)
+            G = emb.gc_post(group_norms([net.layers[0].weight for net in emb.networks], ignore_lag), ignore_lag, combine,
+                            rank)
             if G.dim() != 3:
+                assert G.size(0) == m.num_factors_nK  # :476 (a combined wavelet graph fails here, as in the reference)
                 G = G.view(m.num_factors_nK, G.size(1), 1)
         elif m.factor_score_embedder_type == "DGCNN":
-            A = emb.dgcnn.dgcnn.A
-            G = (torch.abs(A) if combine else A).t()  # models/dgcnn.py:47-61
+            G = emb.dgcnn.GC(threshold=False, combine_node_feature_edges=combine)  # models/dgcnn.py:47-61
+            assert G.size(0) == m.num_series  # :472
             G = G.reshape(m.num_series, m.num_series, 1)
         else:
             raise ValueError("raw_embedder GC needs a causal embedder (cEmbedder / DGCNN)")
         return (G > 0).int() if threshold else G
 
-    def fixed_embedder_gc(self, threshold, ignore_lag, combine):
-        G = self.raw_embedder_gc(threshold, ignore_lag, combine)
+    def fixed_embedder_gc(self, threshold, ignore_lag, combine, rank=False):
+        G = self.raw_embedder_gc(threshold, ignore_lag, combine, rank)
         if self.m.factor_score_embedder_type == "DGCNN":
             return G
+        assert G.size(0) == self.m.num_factors_nK  # :513
         Gt = G.float().transpose(0, 2).contiguous()  # (L, p, K): sum_k g_k g_k^T per lag (:514)
         out = bmm(Gt, Gt.transpose(1, 2)).transpose(0, 2)
         return out.int() if threshold else out
 
-    def GC(self, mode, X=None, threshold=True, ignore_lag=True, combine=False):
+    def GC(self, mode, X=None, threshold=True, ignore_lag=True, combine=False, rank=False):
         m = self.m
         ls = min(m.gen_lag, m.embed_lag)
         K = m.num_factors_nK
         if mode == "fixed_factor_exclusive":
-            return [self.factor_gcs(threshold, ignore_lag)]
+            return [self.factor_gcs(threshold, ignore_lag, combine, rank)]
         if mode == "raw_embedder":
-            return [[self.raw_embedder_gc(threshold, ignore_lag, combine)]]
+            return [[self.raw_embedder_gc(threshold, ignore_lag, combine, rank)]]
         if mode == "fixed_embedder_exclusive":
-            return [[self.fixed_embedder_gc(threshold, ignore_lag, combine)]]
+            return [[self.fixed_embedder_gc(threshold, ignore_lag, combine, rank)]]
         if mode == "conditional_factor_exclusive":
             fw, _ = self.embed(X)
-            fg = self.factor_gcs(threshold, ignore_lag)
+            fg = self.factor_gcs(threshold, ignore_lag, combine, rank)
             return [[fw[b, k] * fg[k] for k in range(fw.size(1))] for b in range(fw.size(0))]
         if mode == "conditional_embedder_exclusive":
             if m.factor_score_embedder_type == "DGCNN":
                 raise ValueError("conditional_embedder_exclusive is not supported for model with DGCNN factor "
                                  "score embedder type")
-            raw = self.raw_embedder_gc(threshold, ignore_lag, combine).float()
+            raw = self.raw_embedder_gc(threshold, ignore_lag, combine, rank).float()
+            assert raw.size(0) == K  # :532
             nv, nl = raw.size(1), raw.size(2)
             fw, _ = self.embed(X)
             prods = []
@@ -349,23 +355,23 @@ class GenericPath:
                 prods.append(bmm(g, g.transpose(1, 2)).transpose(0, 2))
             return [[fw[b, k] * prods[k] for k in range(fw.size(1))] for b in range(fw.size(0))]
         if mode == "fixed_factor_fixed_embedder":
-            fg = self.factor_gcs(threshold, ignore_lag)
-            eg = self.fixed_embedder_gc(threshold, ignore_lag, combine)
+            fg = self.factor_gcs(threshold, ignore_lag, combine, rank)
+            eg = self.fixed_embedder_gc(threshold, ignore_lag, combine, rank)
             if not ignore_lag:
                 return [[g[:, :, -ls:] + eg[:, :, -ls:] for g in fg]]
             return [[g + eg for g in fg]]
         if mode == "conditional_factor_fixed_embedder":
-            cond = self.GC("conditional_factor_exclusive", X, threshold, ignore_lag, combine)
-            eg = self.fixed_embedder_gc(threshold, ignore_lag, combine)
+            cond = self.GC("conditional_factor_exclusive", X, threshold, ignore_lag, combine, rank)
+            eg = self.fixed_embedder_gc(threshold, ignore_lag, combine, rank)
             return [[(c + eg) if ignore_lag else (c[:, :, -ls:] + eg[:, :, -ls:]) for c in row] for row in cond]
         if mode == "fixed_factor_conditional_embedder":
-            fg = self.factor_gcs(threshold, ignore_lag)
-            cond = self.GC("conditional_embedder_exclusive", X, threshold, ignore_lag, combine)
+            fg = self.factor_gcs(threshold, ignore_lag, combine, rank)
+            cond = self.GC("conditional_embedder_exclusive", X, threshold, ignore_lag, combine, rank)
             return [[(c + fg[k]) if ignore_lag else (c[:, :, -ls:] + fg[k][:, :, -ls:]) for k, c in enumerate(row)]
                     for row in cond]
         if mode == "conditional_factor_conditional_embedder":
-            a = self.GC("conditional_factor_exclusive", X, threshold, ignore_lag, combine)
-            e = self.GC("conditional_embedder_exclusive", X, threshold, ignore_lag, combine)
+            a = self.GC("conditional_factor_exclusive", X, threshold, ignore_lag, combine, rank)
+            e = self.GC("conditional_embedder_exclusive", X, threshold, ignore_lag, combine, rank)
             return [[(a[b][k] + e[b][k]) if ignore_lag else (a[b][k][:, :, -ls:] + e[b][k][:, :, -ls:])
                      for k in range(K)] for b in range(len(a))]
         raise ValueError("GC EST MODE == " + str(mode) + " IS NOT SUPPORTED")

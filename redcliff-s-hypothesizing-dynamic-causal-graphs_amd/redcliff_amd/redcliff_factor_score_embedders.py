@@ -9,6 +9,7 @@ training) on the generic HIP-GEMM path (redcliff_amd.generic).
 import torch
 import torch.nn as nn
 
+from . import wavelets
 from .cmlp import MLP
 from .dgcnn import DGCNN_Model
 
@@ -67,13 +68,11 @@ class DGCNN_Embedder(nn.Module):
 
 
 class cEmbedder(nn.Module):
-    """models/redcliff_factor_score_embedders.py:183-331 (wavelet_level=None)."""
+    """models/redcliff_factor_score_embedders.py:183-331."""
 
     def __init__(self, num_chans, num_class_preds, num_factor_preds, use_sigmoid_restriction,
                  sigmoid_eccentricity_coeff, lag, hidden, wavelet_level=None, save_path=None):
         super().__init__()
-        if wavelet_level is not None:
-            raise NotImplementedError("wavelet_level != None is outside the MI355X path")
         self.num_chans = num_chans
         self.num_class_preds = num_class_preds
         self.num_factor_preds = num_factor_preds
@@ -81,9 +80,14 @@ class cEmbedder(nn.Module):
         self.sigmoid_eccentricity_coeff = sigmoid_eccentricity_coeff if use_sigmoid_restriction else None
         self.lag = lag
         self.hidden = hidden
-        self.wavelet_level = None
-        self.num_series = num_chans
-        self.wavelet_mask = None
+        self.wavelet_level = wavelet_level
+        if wavelet_level is None:
+            self.num_series = num_chans
+            self.wavelet_mask = None
+        else:  # :206-224 (the mask heat-map plot is not drawn)
+            self.num_series = int(num_chans * (wavelet_level + 1))
+            self.wavelet_mask = wavelets.embedder_mask(num_chans, num_factor_preds, wavelet_level)
+        self.save_path = save_path
         self.activation = torch.nn.ReLU()
         self.sigmoid = nn.Sigmoid() if use_sigmoid_restriction else None
         self.networks = nn.ModuleList([MLP(self.num_series, lag, hidden) for _ in range(num_factor_preds)])
@@ -101,7 +105,15 @@ class cEmbedder(nn.Module):
         dims_owner = _Wrap(self.networks)
         G, G0 = kernels.cmlp_gc_norms([dims_owner])
         out = G0[0] if ignore_lag else G[0]
+        out = self.gc_post(out, ignore_lag, combine_wavelet_representations, rank_wavelets)
         return (out > 0).int() if threshold else out
+
+    def gc_post(self, G, ignore_lag, combine, rank):
+        """Ranking mask and wavelet combination (models/redcliff_factor_score_embedders.py:297-326)."""
+        if not rank and not (self.wavelet_level is not None and combine):
+            return G
+        return wavelets.gc_post(G, self.wavelet_mask, self.wavelet_level, self.num_chans, self.num_series, self.lag,
+                                ignore_lag, combine, rank)
 
 
 class _Wrap:

@@ -59,13 +59,12 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
                  training_mode="pretrain_embedder_and_pretrain_factor_then_combined", num_pretrain_epochs=0,
                  num_acclimation_epochs=0, STATE_SCORE_SMOOTHING_EPSILON=0.0001):
         super().__init__()
-        if wavelet_level is not None:
-            raise NotImplementedError("wavelet_level != None (wavelet-decomposed inputs) is outside the MI355X path")
         self.MAX_NUM_SAMPS_FOR_GC_VIS = 5
         self.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING = 40
         self.STATE_SCORE_SMOOTHING_EPSILON = STATE_SCORE_SMOOTHING_EPSILON
         self.num_chans = num_chans
-        self.num_series = num_chans
+        # wavelet-decomposed inputs: num_chans * (wavelet_level + 1) series (:31-35)
+        self.num_series = num_chans if wavelet_level is None else num_chans * (wavelet_level + 1)
         self.gen_lag = gen_lag
         self.gen_hidden = gen_hidden
         self.num_gen_hiddens = len(gen_hidden)
@@ -113,7 +112,8 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         elif factor_score_embedder_type == "DGCNN":
             assert primary_gc_est_mode != "conditional_embedder_exclusive"
             assert len(factor_score_embedder_args) == 4
-            self.factor_score_embedder = DGCNN_Embedder(num_chans, 1, *args, use_sigmoid_restriction, num_factors,
+            wl = 0 if wavelet_level is None else wavelet_level  # num_wavelets_per_chan (:119-122)
+            self.factor_score_embedder = DGCNN_Embedder(num_chans, wl + 1, *args, use_sigmoid_restriction, num_factors,
                                                         num_supervised_factors)
         else:
             if num_supervised_factors > 0:
@@ -257,28 +257,32 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         return xs.unsqueeze(1), preds, [w], [logits for _ in range(self.num_sims)]
 
     # ------------------------------------------------------------------ GC
-    def _factor_gcs(self, threshold, ignore_lag):
+    def _factor_gcs(self, threshold, ignore_lag, combine=False, rank=False):
+        """cMLP.GC of every factor (models/cmlp.py:147-203: norms, wavelet ranking / combination,
+        threshold), each viewed as (n, n, 1) when lag-free (:450-454)."""
         eng = self.engine()
         W0s = [net.layers[0].weight for f in self.factors for net in f.networks]
         if AG.grad_needed(W0s) and not threshold:
             G, G0 = AG.group_norms(list(self.factors))  # differentiable (cmlp.py:147-167)
         else:
             G, G0 = eng.gc_norms()
-        ests = [G0[k].view(self.num_series, self.num_series, 1) if ignore_lag else G[k]
+        ests = [self.factors[k].gc_post(G0[k] if ignore_lag else G[k], ignore_lag, combine, rank)
                 for k in range(self.num_factors_nK)]
+        ests = [e.view(e.size(0), e.size(0), 1) if e.dim() == 2 else e for e in ests]
         return [(e > 0).int() for e in ests] if threshold else ests
 
     def _embedder_gc(self, threshold, combine):
         G = self.factor_score_embedder.GC(threshold=threshold, combine_node_feature_edges=combine)
+        assert G.size(0) == self.num_series  # :472 (a combined wavelet graph fails here, as in the reference)
         return G.view(self.num_series, self.num_series, 1)
 
-    def _conditional_gc_stack(self, gc_est_mode, X, threshold, ignore_lag, comb):
+    def _conditional_gc_stack(self, gc_est_mode, X, threshold, ignore_lag, comb, rank=False):
         """The conditional GC estimates of every window as one (B, K, p, p, L') tensor: the
         reference's per-(sample, factor) products (:481-498, :565-580) as one broadcast (the
         same element-wise operations, so the same values)."""
         ls = min(self.gen_lag, self.embed_lag)
         w, _ = self.factor_score_embedder(torch.transpose(X[:, -self.embed_lag:, :], 1, 2))
-        fg = torch.stack(self._factor_gcs(threshold, ignore_lag))  # (K, p, p, L')
+        fg = torch.stack(self._factor_gcs(threshold, ignore_lag, comb, rank))  # (K, p, p, L')
         est = w[:, :, None, None, None] * fg[None]
         if gc_est_mode == "conditional_factor_fixed_embedder":
             eg = self._embedder_gc(threshold, comb)
@@ -288,18 +292,17 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
     def GC(self, gc_est_mode, X=None, threshold=True, ignore_lag=True, combine_wavelet_representations=False,
            rank_wavelets=False):
         """The nine GC estimate modes of ...withStateSmoothing.py:415-620 (DGCNN embedder)."""
-        if rank_wavelets:
-            raise NotImplementedError("rank_wavelets needs wavelet_level != None")
         if not self.fused_supported():
             Xd = None if X is None else X.to(self._device(), torch.float32)
-            return self._generic().GC(gc_est_mode, Xd, threshold, ignore_lag, combine_wavelet_representations)
+            return self._generic().GC(gc_est_mode, Xd, threshold, ignore_lag, combine_wavelet_representations,
+                                      rank_wavelets)
         if self.factor_score_embedder_type != "DGCNN":
             raise NotImplementedError("GC on the fused path is implemented for the DGCNN embedder")
         self.engine()  # binds the embedder to this model's kernels (a fresh / loaded model may call GC first)
         ls = min(self.gen_lag, self.embed_lag)
-        comb = combine_wavelet_representations
+        comb, rank = combine_wavelet_representations, rank_wavelets
         if gc_est_mode == "fixed_factor_exclusive":
-            return [self._factor_gcs(threshold, ignore_lag)]
+            return [self._factor_gcs(threshold, ignore_lag, comb, rank)]
         if gc_est_mode in ("raw_embedder", "fixed_embedder_exclusive"):
             return [[self._embedder_gc(threshold, comb)]]
         if gc_est_mode in ("conditional_embedder_exclusive", "fixed_factor_conditional_embedder",
@@ -307,13 +310,13 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
             raise ValueError("conditional_embedder_exclusive is not supported for model with DGCNN factor score "
                              "embedder type")
         if gc_est_mode == "fixed_factor_fixed_embedder":
-            fg = self._factor_gcs(threshold, ignore_lag)
+            fg = self._factor_gcs(threshold, ignore_lag, comb, rank)
             eg = self._embedder_gc(threshold, comb)
             if not ignore_lag:
                 return [[g[:, :, -ls:] + eg[:, :, -ls:] for g in fg]]
             return [[g + eg for g in fg]]
         if gc_est_mode in ("conditional_factor_exclusive", "conditional_factor_fixed_embedder"):
-            est = self._conditional_gc_stack(gc_est_mode, X, threshold, ignore_lag, comb)
+            est = self._conditional_gc_stack(gc_est_mode, X, threshold, ignore_lag, comb, rank)
             return [[est[b, k] for k in range(est.size(1))] for b in range(est.size(0))]
         raise ValueError("GC EST MODE == " + str(gc_est_mode) + " IS NOT SUPPORTED")
 

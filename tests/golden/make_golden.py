@@ -75,7 +75,7 @@ def build(cfg):
         eargs = []
     coeff = reference_coeffs(cfg["K"], cfg["p"], smooth=cfg.get("smooth", 0.0))
     cls = REF.redcliff_smooth.REDCLIFF_S_CMLP_withStateSmoothing if cfg["smoothing_class"] else REF.redcliff.REDCLIFF_S_CMLP
-    kw = dict(num_sims=cfg["S"], wavelet_level=None, save_path=None, training_mode=cfg["training_mode"],
+    kw = dict(num_sims=cfg["S"], wavelet_level=cfg.get("wl"), save_path=None, training_mode=cfg["training_mode"],
               num_pretrain_epochs=cfg["pre"], num_acclimation_epochs=cfg["acc"])
     if cfg["smoothing_class"]:
         kw["STATE_SCORE_SMOOTHING_EPSILON"] = 0.0001
@@ -105,13 +105,21 @@ def record_eval(m, cfg, Xb, Yb, out, prefix):
         for k, fp in enumerate(fpreds):
             out[prefix + "/fpred%d" % k] = _np(fp)
     if prefix == "eval":
+        wl = cfg.get("wl") is not None
         for mode in valid_gc_modes(cfg):
             for ign in (True, False):
                 for comb in (False, True):
-                    gcs = m.GC(mode, X=Xb[:, :Lm, :], threshold=False, ignore_lag=ign,
-                               combine_wavelet_representations=comb)
-                    arr = np.stack([np.stack([_np(g) for g in row]) for row in gcs])
-                    out["%s/gc/%s/ign%d/comb%d" % (prefix, mode, int(ign), int(comb))] = arr
+                    for rank in ((False, True) if wl else (False,)):
+                        key = "%s/gc/%s/ign%d/comb%d" % (prefix, mode, int(ign), int(comb)) + ("/rank%d" % rank if wl else "")
+                        try:
+                            gcs = m.GC(mode, X=Xb[:, :Lm, :], threshold=False, ignore_lag=ign,
+                                       combine_wavelet_representations=comb, rank_wavelets=rank)
+                        except Exception as e:  # the reference's own failure for this combination
+                            if not wl:
+                                raise
+                            out[key + "/err"] = np.asarray(type(e).__name__)
+                            continue
+                        out[key] = np.stack([np.stack([_np(g) for g in row]) for row in gcs])
         tgt = Xb[:, Lm:Lm + cfg["S"], :]
         for flag in ("combined", "emb", "fac"):
             combo, terms = m.compute_loss(Xb[:, :cfg["F"], :], x_sim, tgt, labels, Yb, cfg["gc_mode"],
@@ -125,9 +133,14 @@ def record_eval(m, cfg, Xb, Yb, out, prefix):
 def run_scenario(name, cfg):
     out = {}
     m, coeff = build(cfg)
-    X, Y = make_data(cfg["N"], cfg["T"], cfg["p"], cfg["K"], cfg["label_T"], cfg["data_seed"])
+    ns = cfg["p"] * (cfg["wl"] + 1) if cfg.get("wl") is not None else cfg["p"]  # wavelet series
+    X, Y = make_data(cfg["N"], cfg["T"], ns, cfg["K"], cfg["label_T"], cfg["data_seed"])
     out["X"], out["Y"] = X, Y
     _sd("init", m, out)
+    if cfg.get("wl") is not None:  # the ranking masks (plain attributes, not in the state_dict)
+        out["wavelet_mask/factor"] = _np(m.factors[0].wavelet_mask)
+        if cfg["emb"] == "cEmbedder":
+            out["wavelet_mask/embedder"] = _np(m.factor_score_embedder.wavelet_mask)
     B = cfg["B"]
     batches = [(torch.from_numpy(X[i:i + B]), torch.from_numpy(Y[i:i + B])) for i in range(0, cfg["N"], B)]
     # eval-mode probes on a deep copy (BN running stats untouched in the main model)
@@ -149,7 +162,7 @@ def run_scenario(name, cfg):
             _sd("step%d" % step, m, out)
     out["nsteps"] = np.asarray(step)
     hist = [[] for _ in range(5)] if cfg["nsup"] > 0 else [None] * 5
-    vals = m.validate_training(batches, 1, cfg["p"], *hist)
+    vals = m.validate_training(batches, 1, ns, *hist)
     names = ["forecast", "factor", "cos", "fw_l1", "smooth", "adj", "dag_reg", "dag_lag", "dag_node", "combo"]
     if not cfg["smoothing_class"]:
         names = ["forecast", "factor", "cos", "fw_l1", "adj", "dag_reg", "dag_lag", "dag_node", "combo"]
@@ -202,7 +215,8 @@ def run_fit():
                training_mode="pretrain_embedder_then_acclimate_factors_then_combined", pre=1, acc=1,
                N=48, T=10, label_T=10, data_seed=11, B=16)
     m, coeff = build(cfg)
-    X, Y = make_data(cfg["N"], cfg["T"], cfg["p"], cfg["K"], cfg["label_T"], cfg["data_seed"])
+    ns = cfg["p"] * (cfg["wl"] + 1) if cfg.get("wl") is not None else cfg["p"]  # wavelet series
+    X, Y = make_data(cfg["N"], cfg["T"], ns, cfg["K"], cfg["label_T"], cfg["data_seed"])
     Xv, Yv = make_data(32, cfg["T"], cfg["p"], cfg["K"], cfg["label_T"], 12)
     B = cfg["B"]
     train = [(torch.from_numpy(X[i:i + B]), torch.from_numpy(Y[i:i + B])) for i in range(0, len(X), B)]
@@ -343,6 +357,10 @@ SCENARIOS = {
     # Vanilla embedder (multiple objectives)
     "vanilla": dict(BASE, emb="Vanilla_Embedder", F=5, eh=6, nsup=2, gc_mode="conditional_factor_exclusive",
                     data_seed=10, seed=9),
+    # wavelet-decomposed inputs (wavelet_level = 3: 4 series per channel, the only supported
+    # count), DGCNN over p * 4 nodes and the cEmbedder with its ranking mask
+    "dgcnn_wavelet": dict(BASE, wl=3, p=2, data_seed=11, seed=10),
+    "cemb_wavelet": dict(BASE, emb="cEmbedder", wl=3, p=2, F=4, eh=5, nsup=2, data_seed=12, seed=11),
 }
 
 if __name__ == "__main__":

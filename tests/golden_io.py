@@ -34,7 +34,7 @@ def ctor_args(meta):
     """Positional + keyword arguments of the reference constructor for a fixture."""
     args = (meta["p"], meta["L"], [meta["h"]], meta["F"], [meta.get("eh", 0)], meta["L"], 1, meta["K"], meta["nsup"],
             meta["coeff"], meta["sigmoid"], meta["emb"], embedder_args(meta), meta["gc_mode"], meta["fwd_mode"])
-    kw = dict(num_sims=meta["S"], wavelet_level=None, save_path=None, training_mode=meta["training_mode"],
+    kw = dict(num_sims=meta["S"], wavelet_level=meta.get("wl"), save_path=None, training_mode=meta["training_mode"],
               num_pretrain_epochs=meta["pre"], num_acclimation_epochs=meta["acc"])
     return args, kw
 

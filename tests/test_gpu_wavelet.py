@@ -1,0 +1,66 @@
+"""Wavelet-decomposed inputs (wavelet_level = 3, 4 series per channel) on the GPU against the
+reference's own outputs (tests/golden/{dgcnn,cemb}_wavelet.npz, tests/golden/make_golden.py):
+seeded construction, the eval forward, every GC mode with every ignore_lag / combine /
+rank_wavelets combination (values, or the reference's own AssertionError where it fails),
+the three-phase batch_update schedule and validation.  DGCNN runs on the fused kernels with
+p = num_chans * 4 nodes; the cEmbedder on the generic HIP-GEMM path."""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import assert_close, batches, load, state
+from test_gpu_parity import RTOL, build, compare_state, make_opts
+
+pytestmark = pytest.mark.gpu
+WAVELET_SCENARIOS = ["dgcnn_wavelet", "cemb_wavelet"]
+
+
+@pytest.mark.parametrize("name", WAVELET_SCENARIOS)
+def test_wavelet_init_forward_and_gc(name):
+    d, meta = load(name)
+    m = build(meta)
+    assert m.num_series == meta["p"] * 4
+    assert m.fused_supported() == (meta["emb"] == "DGCNN")
+    compare_state("init", m, state(d, "init"), 0.0, 0.0)
+    np.testing.assert_array_equal(m.factors[0].wavelet_mask.numpy(), d["wavelet_mask/factor"])
+    m.eval()
+    Xb, _ = batches(d, meta)[0]
+    Lm = max(meta["L"], meta["F"])
+    X = Xb[:, :Lm, :].cuda()
+    with torch.no_grad():
+        x_sim, _, fws, _ = m(X)
+    assert_close("x_sim", x_sim.cpu().numpy(), d["eval/x_sim"], RTOL, 1e-5)
+    assert_close("w", fws[0].cpu().numpy(), d["eval/w"], RTOL, 1e-5)
+    keys = sorted(set(k[:-4] if k.endswith("/err") else k for k in d.files if k.startswith("eval/gc/")))
+    assert keys
+    for key in keys:
+        _, _, mode, ign, comb, rank = key.split("/")
+        kw = dict(X=X, threshold=False, ignore_lag=ign == "ign1", combine_wavelet_representations=comb == "comb1",
+                  rank_wavelets=rank == "rank1")
+        if key + "/err" in d.files:
+            with pytest.raises(AssertionError):
+                with torch.no_grad():
+                    m.GC(mode, **kw)
+            continue
+        with torch.no_grad():
+            gcs = m.GC(mode, **kw)
+        arr = np.stack([np.stack([g.detach().cpu().numpy() for g in row]) for row in gcs])
+        assert_close(key, arr, d[key], RTOL, 1e-5)
+
+
+@pytest.mark.parametrize("name", WAVELET_SCENARIOS)
+def test_wavelet_batch_update_schedule(name):
+    d, meta = load(name)
+    m = build(meta)
+    oA, oB = make_opts(m, meta["lrA"], meta["lrB"])
+    bs = batches(d, meta)
+    step = 0
+    for epoch in meta["epochs"]:
+        for bi, (Xb, Yb) in enumerate(bs):
+            m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+            step += 1
+            compare_state("step%d" % step, m, state(d, "step%d" % step))
+    hist = [[] for _ in range(5)]
+    vals = m.validate_training(bs, 1, m.num_series, *hist)
+    for n_, v in zip(["forecast", "factor", "cos", "fw_l1", "smooth", "adj"], vals):
+        assert_close("val/" + n_, v, d["val/" + n_], 1e-4, 1e-6)
