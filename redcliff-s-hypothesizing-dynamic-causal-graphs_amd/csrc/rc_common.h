@@ -451,6 +451,7 @@ __device__ inline void rc_critical_priority() { __builtin_amdgcn_s_setprio(2); }
 // fp32 matrix cores: v_mfma_f32_32x32x2f32 accumulator, and the row of accumulator register
 // `reg` of lane `lane` in its 32x32 tile (columns = lane & 31).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ inline int mf_row(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
 // Block-wide sum; every thread gets the result.  `red` must hold >= RC_BLOCK/64 floats.

@@ -296,6 +296,15 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   float awi[16];                            // dW_i chunk: n*F*HC <= 4096 -> 16 / thread
 #pragma unroll
   for (int k = 0; k < 16; ++k) awi[k] = 0.f;
+  // Matrix-core form of the sub-block products (16-window sub-blocks, fc1 width <= 64, K <= 16,
+  // n*F <= 256): df1, dZ, dT and the dfc1W / dW_i partials as v_mfma_f32_16x16x4_f32 tiles,
+  // each an fmaf chain over its contraction index in ascending order; the partial-record
+  // layout is the vector form's.  Lane l: l15 = l & 15, g = l >> 4; D rows 4 g + reg, column l15.
+  const bool mf = !MULTI && BC == 16 && M1 <= 64 && K <= 16 && nF <= 256;  // single-sub-block workgroups
+  const int lane = tid & 63, l15 = lane & 15, lg = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // (the matrix-core accumulators live in afc (dfc1W rows m in [16 wv, 16 wv + 16)) and awi
+  // (dW_i row tiles wv + 4 i, 4 registers each): one register set for either form)
   const int nwi = (nF * HC + RC_BLOCK - 1) / RC_BLOCK;
   const int nout = K * M1 + K + M1;
   const int nS = (n - 1) * p;
@@ -400,85 +409,190 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     }
   RC_PHASE(c.ws, c.wo.total, pbx, 34);
     for (int e = tid; e < nbc * K; e += RC_BLOCK) dr[e] = draw_value(c, r, dK.mod(e), wrl[e], dwl[e], labl[e]);
-    __syncthreads();
-    // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
-    for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
-      const int s = dM1.div(e), m = e - s * M1;
-      float g = 0.f;
-      if (f1r[e] > 0.f)
-        for (int k = 0; k < K; ++k) g += dr[s * K + k] * fc2s[k * M1 + m];
-      df1c[e] = g;
-    }
-    __syncthreads();
-  RC_PHASE(c.ws, c.wo.total, pbx, 35);
-    // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
-    for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
-      const int s = e / HC, hh = e - s * HC;
-      const float* dfr = df1c + s * M1;
-      float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
-      int m = 0;
-      for (; m + 3 < M1; m += 4) {
-        g0 += dfr[m] * FW[m * HC + hh];
-        g1 += dfr[m + 1] * FW[(m + 1) * HC + hh];
-        g2 += dfr[m + 2] * FW[(m + 2) * HC + hh];
-        g3 += dfr[m + 3] * FW[(m + 3) * HC + hh];
-      }
-      for (; m < M1; ++m) g0 += dfr[m] * FW[m * HC + hh];
-      const float g = (g0 + g1) + (g2 + g3);
-      dZc[e] = Rc[e] > 0.f ? g : 0.f;
-    }
-    // dfc1W chunk partial: afc[m][hh] += sum_s df1[s][m] R[s][hh]
-    for (int s = 0; s < nbc; ++s) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = tid + k * RC_BLOCK;
-        if (e < M1 * HC) afc[k] += df1c[s * M1 + e / HC] * Rc[s * HC + e % HC];
-      }
-    }
-    // group 0: dfc2W[k][m] += sum_s dr[s][k] relu(f1[s][m]); dfc2b[k] += sum_s dr[s][k]; dfc1b[m] += sum_s df1[s][m]
-    if (head_grads) {
-#pragma unroll
-      for (int kk = 0; kk < 5; ++kk) {
-        const int e = tid + kk * RC_BLOCK;
-        if (e >= nout) continue;
-        float g = agf[kk];
-        if (e < K * M1) {
-          const int k = dM1.div(e), m = e - k * M1;
-          for (int s = 0; s < nbc; ++s) g += dr[s * K + k] * fmaxf(f1r[s * M1 + m], 0.f);
-        } else if (e < K * M1 + K) {
-          const int k = e - K * M1;
-          for (int s = 0; s < nbc; ++s) g += dr[s * K + k];
-        } else {
-          const int m = e - K * M1 - K;
-          for (int s = 0; s < nbc; ++s) g += df1c[s * M1 + m];
+    if (mf) {
+      // rows [nbc, 16) of the window tiles the products read are zero windows
+      for (int e = nbc * K + tid; e < 16 * K; e += RC_BLOCK) dr[e] = 0.f;
+      for (int e = nbc * HC + tid; e < 16 * HC; e += RC_BLOCK) Rc[e] = 0.f;
+      for (int e = nbc * nF + tid; e < 16 * nF; e += RC_BLOCK) Tc[e] = 0.f;
+      __syncthreads();
+      // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]: wave w, columns m in [16 w, 16 w + 16)
+      if (16 * wv < M1) {
+        const int m = 16 * wv + l15;
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < K; k0 += 4) {
+          const int k = k0 + lg;
+          const float av = k < K ? dr[l15 * K + k] : 0.f;
+          const float bv = (k < K && m < M1) ? fc2s[k * M1 + m] : 0.f;
+          a = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, a, 0, 0, 0);
         }
-        agf[kk] = g;
+        if (m < M1)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) {
+            const int sw = 4 * lg + reg;
+            df1c[sw * M1 + m] = (sw < nbc && f1r[sw * M1 + m] > 0.f) ? a[reg] : 0.f;
+          }
       }
-    }
-    __syncthreads();
+      __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, pbx, 35);
+      // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]: wave 0
+      if (wv == 0) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        for (int m0 = 0; m0 < M1; m0 += 4) {
+          const int m = m0 + lg;
+          const float av = m < M1 ? df1c[l15 * M1 + m] : 0.f;
+          const float bv = m < M1 ? FW[m * HC + l15] : 0.f;
+          a = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, a, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int e = (4 * lg + reg) * HC + l15;
+          dZc[e] = Rc[e] > 0.f ? a[reg] : 0.f;
+        }
+      }
+      // dfc1W chunk partial: afc[m][hh] += sum_s df1[s][m] R[s][hh]: wave w, rows m in [16 w, 16 w + 16)
+      if (16 * wv < M1) {
+        const int m = 16 * wv + l15;
+        f32x4 accA = {afc[0], afc[1], afc[2], afc[3]};
+#pragma unroll
+        for (int s0 = 0; s0 < 16; s0 += 4) {
+          const int sw = s0 + lg;
+          const float av = m < M1 ? df1c[sw * M1 + m] : 0.f;
+          accA = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Rc[sw * HC + l15], accA, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) afc[reg] = accA[reg];
+      }
+      // group 0: dfc2W[k][m] += sum_s dr[s][k] relu(f1[s][m]); dfc2b[k] += sum_s dr[s][k]; dfc1b[m] += sum_s df1[s][m]
+      if (head_grads) {
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) {
+          const int e = tid + kk * RC_BLOCK;
+          if (e >= nout) continue;
+          float g = agf[kk];
+          if (e < K * M1) {
+            const int k = dM1.div(e), m = e - k * M1;
+            for (int s = 0; s < nbc; ++s) g += dr[s * K + k] * fmaxf(f1r[s * M1 + m], 0.f);
+          } else if (e < K * M1 + K) {
+            const int k = e - K * M1;
+            for (int s = 0; s < nbc; ++s) g += dr[s * K + k];
+          } else {
+            const int m = e - K * M1 - K;
+            for (int s = 0; s < nbc; ++s) g += df1c[s * M1 + m];
+          }
+          agf[kk] = g;
+        }
+      }
+      __syncthreads();
   RC_PHASE(c.ws, c.wo.total, pbx, 36);
-    // dW_i chunk partial: awi[i][f][hh] += sum_s T_i[s][f] dZ[s][hh]
-    for (int s = 0; s < nbc; ++s) {
+      // dW_i chunk partial: awi[q][hh] += sum_s T[s][q] dZ[s][hh], q = (i, f); dT[s][q] =
+      // sum_hh dZ[s][hh] W[q][hh]: wave w, 16-row tiles qt = w + 4 i
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = tid + k * RC_BLOCK;
-        if (k < nwi && e < nF * HC) awi[k] += Tc[s * nF + e / HC] * dZc[s * HC + e % HC];
-      }
-    }
-    // dT_i[s][f] = sum_hh dZ[s][hh] W_i[f][hh]
-    for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
-      const int s = dnF.div(e), rem = e - s * nF;
-      const float* wr = WiC + rem * HP;
-      const float* dz = dZc + s * HC;
-      float t0 = 0.f, t1 = 0.f;
+      for (int i = 0; i < 4; ++i) {
+        const int qt = wv + 4 * i;
+        if (16 * qt >= nF) break;
+        const int q = 16 * qt + l15;
+        f32x4 accW = {awi[4 * i], awi[4 * i + 1], awi[4 * i + 2], awi[4 * i + 3]};
 #pragma unroll
-      for (int hh = 0; hh < HC; hh += 2) {
-        t0 += dz[hh] * wr[hh];
-        t1 += dz[hh + 1] * wr[hh + 1];
+        for (int s0 = 0; s0 < 16; s0 += 4) {
+          const int sw = s0 + lg;
+          const float av = q < nF ? Tc[sw * nF + q] : 0.f;
+          accW = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dZc[sw * HC + l15], accW, 0, 0, 0);
+        }
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) awi[4 * i + reg] = accW[reg];
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int hq = 0; hq < 16; hq += 4) {
+          const int hh = hq + lg;
+          const float bv = q < nF ? WiC[q * HP + hh] : 0.f;
+          a = __builtin_amdgcn_mfma_f32_16x16x4f32(dZc[l15 * HC + hh], bv, a, 0, 0, 0);
+        }
+        if (q < nF)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg) dTc[(4 * lg + reg) * nF + q] = a[reg];
       }
-      dTc[e] = t0 + t1;
+      __syncthreads();
+    } else {
+      __syncthreads();
+      // df1[s][m] = [f1 > 0] sum_k dr[s][k] fc2W[k][m]
+      for (int e = tid; e < nbc * M1; e += RC_BLOCK) {
+        const int s = dM1.div(e), m = e - s * M1;
+        float g = 0.f;
+        if (f1r[e] > 0.f)
+          for (int k = 0; k < K; ++k) g += dr[s * K + k] * fc2s[k * M1 + m];
+        df1c[e] = g;
+      }
+      __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, pbx, 35);
+      // dZ[s][hh] = [R > 0] sum_m df1[s][m] fc1W[m][hh]   (4 independent partial sums)
+      for (int e = tid; e < nbc * HC; e += RC_BLOCK) {
+        const int s = e / HC, hh = e - s * HC;
+        const float* dfr = df1c + s * M1;
+        float g0 = 0.f, g1 = 0.f, g2 = 0.f, g3 = 0.f;
+        int m = 0;
+        for (; m + 3 < M1; m += 4) {
+          g0 += dfr[m] * FW[m * HC + hh];
+          g1 += dfr[m + 1] * FW[(m + 1) * HC + hh];
+          g2 += dfr[m + 2] * FW[(m + 2) * HC + hh];
+          g3 += dfr[m + 3] * FW[(m + 3) * HC + hh];
+        }
+        for (; m < M1; ++m) g0 += dfr[m] * FW[m * HC + hh];
+        const float g = (g0 + g1) + (g2 + g3);
+        dZc[e] = Rc[e] > 0.f ? g : 0.f;
+      }
+      // dfc1W chunk partial: afc[m][hh] += sum_s df1[s][m] R[s][hh]
+      for (int s = 0; s < nbc; ++s) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e = tid + k * RC_BLOCK;
+          if (e < M1 * HC) afc[k] += df1c[s * M1 + e / HC] * Rc[s * HC + e % HC];
+        }
+      }
+      // group 0: dfc2W[k][m] += sum_s dr[s][k] relu(f1[s][m]); dfc2b[k] += sum_s dr[s][k]; dfc1b[m] += sum_s df1[s][m]
+      if (head_grads) {
+#pragma unroll
+        for (int kk = 0; kk < 5; ++kk) {
+          const int e = tid + kk * RC_BLOCK;
+          if (e >= nout) continue;
+          float g = agf[kk];
+          if (e < K * M1) {
+            const int k = dM1.div(e), m = e - k * M1;
+            for (int s = 0; s < nbc; ++s) g += dr[s * K + k] * fmaxf(f1r[s * M1 + m], 0.f);
+          } else if (e < K * M1 + K) {
+            const int k = e - K * M1;
+            for (int s = 0; s < nbc; ++s) g += dr[s * K + k];
+          } else {
+            const int m = e - K * M1 - K;
+            for (int s = 0; s < nbc; ++s) g += df1c[s * M1 + m];
+          }
+          agf[kk] = g;
+        }
+      }
+      __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, pbx, 36);
+      // dW_i chunk partial: awi[i][f][hh] += sum_s T_i[s][f] dZ[s][hh]
+      for (int s = 0; s < nbc; ++s) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const int e = tid + k * RC_BLOCK;
+          if (k < nwi && e < nF * HC) awi[k] += Tc[s * nF + e / HC] * dZc[s * HC + e % HC];
+        }
+      }
+      // dT_i[s][f] = sum_hh dZ[s][hh] W_i[f][hh]
+      for (int e = tid; e < nbc * nF; e += RC_BLOCK) {
+        const int s = dnF.div(e), rem = e - s * nF;
+        const float* wr = WiC + rem * HP;
+        const float* dz = dZc + s * HC;
+        float t0 = 0.f, t1 = 0.f;
+#pragma unroll
+        for (int hh = 0; hh < HC; hh += 2) {
+          t0 += dz[hh] * wr[hh];
+          t1 += dz[hh + 1] * wr[hh + 1];
+        }
+        dTc[e] = t0 + t1;
+      }
+      __syncthreads();
     }
-    __syncthreads();
     if (late_x) {  // f1 / df1 / R / dZ / T are dead: the window tile goes there
       rc_stage_all(rc_seg<16>(nbc * pF, x_ld, x_st));
       __syncthreads();
@@ -519,15 +633,34 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const int pst = rc_emb_pstride(d);
   const int ofs_w = M1 * HC, ofs_s = ofs_w + nF * HC, ofs_g = ofs_s + nS, ofs_h = ofs_g + 2 * F;
   float* part = ws + c.wo.ebp + ((int64_t)grp * nbw_max + wb) * pst;
+  if (mf) {
+    if (16 * wv < M1)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int e = tid + k * RC_BLOCK;
-    if (e < M1 * HC) part[e] = afc[k];
-  }
+      for (int reg = 0; reg < 4; ++reg) {
+        const int m = 16 * wv + 4 * lg + reg;
+        if (m < M1) part[m * HC + l15] = afc[reg];
+      }
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = tid + k * RC_BLOCK;
-    if (k < nwi && e < nF * HC) part[ofs_w + e] = awi[k];
+    for (int i = 0; i < 4; ++i) {
+      const int qt = wv + 4 * i;
+      if (16 * qt >= nF) break;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int q = 16 * qt + 4 * lg + reg;
+        if (q < nF) part[ofs_w + q * HC + l15] = awi[4 * i + reg];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (e < M1 * HC) part[e] = afc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = tid + k * RC_BLOCK;
+      if (k < nwi && e < nF * HC) part[ofs_w + e] = awi[k];
+    }
   }
   if (head_grads) {
 #pragma unroll

@@ -1093,10 +1093,8 @@ bool rc_fac_short(const RedcliffDims& d) {
 int rc_fac_slots(const RedcliffDims& d) { return rc_fac_short(d) ? (d.h + 15) / 16 : mf_nub(d); }
 
 // Launch of the short-contraction kernels: the k-step count picks the instantiation, and the
-// blocks per wave are chosen so the grid is about one round of resident workgroups (the
-// occupancy the runtime computes from the kernel's registers and this launch's LDS, times the
-// CUs): at the D4IC grid (R = 128, 280 blocks per replica) 12 forward / 8 backward workgroups
-// per replica instead of 1.5 rounds with a half-empty tail.  REDCLIFF_FAC_BPW=n overrides.
+// blocks per wave are chosen from the resident workgroups (the occupancy the runtime computes
+// from the kernel's registers and this launch's LDS, times the CUs).  REDCLIFF_FAC_BPW=n overrides.
 typedef void (*MsKern)(StepCtx, int);
 template <int N>
 struct MsTab {
@@ -1159,7 +1157,11 @@ static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
     }
     const int64_t slots = (int64_t)ms_occupancy(k, lds) * ms_cus();
     if (slots > 0) {
-      const int64_t blocks = (int64_t)NB * c.nrep, want = (blocks + 4 * slots - 1) / (4 * slots);
+      // the backward as one round of resident workgroups, the forward (short blocks, a staging
+      // prologue per workgroup) as about two: R = 128 D4IC grid, bpw 4 / 8 / 16 -> forward 114 /
+      // 140 / 145 us, backward 228 / 236 / 266 us against 205 us at one round (12)
+      const int64_t rounds = bwd ? 1 : 2;
+      const int64_t blocks = (int64_t)NB * c.nrep, want = (blocks + 4 * rounds * slots - 1) / (4 * rounds * slots);
       bpw = (int)(want < 1 ? 1 : (want > 16 ? 16 : want));
     }
   }

@@ -6,7 +6,7 @@ source "$(dirname "$0")/gpu_steps.sh"
 HB=$!
 G="python scripts/grid_step.py --replicas 128 --steps 3"
 F="--kernel-include-regex k_fac --output-format csv"
-step p_tests 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_replicas.py tests/test_gpu_pack_fit.py tests/test_gpu_forked.py tests/test_gpu_fit_modes.py tests/test_gpu_data_parallel.py
+step p_tests 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_replicas.py tests/test_gpu_pack_fit.py tests/test_gpu_forked.py tests/test_gpu_fit_modes.py tests/test_gpu_data_parallel.py tests/test_gpu_wavelet.py
 step p_grid 200 python scripts/grid_step.py --replicas 128 --steps 30
 step p_stats 200 rocprofv3 --kernel-trace --stats --kernel-include-regex k_ --output-format csv -d gpurun_out/stats_p -o run -- python scripts/grid_step.py --replicas 128 --steps 20
 step p_sq1 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT $F -d gpurun_out/pmc_p_sq1 -o run -- $G
