@@ -72,7 +72,13 @@ def flops_per_window(c):
                 total=fac_fwd + fac_bwd + emb_fwd + emb_bwd + pen)
 
 
-def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg):
+def short_factor_kernels(c):
+    """The matrix-core factor path runs the 16-unit short-contraction kernels (k_fac_*_s16) when
+    p*L <= 64 (rc_factor_mfma.hip rc_fac_short; REDCLIFF_FAC_SHORT=0 selects the 32-unit ones)."""
+    return c["p"] * c["L"] <= 64 and os.environ.get("REDCLIFF_FAC_SHORT") != "0"
+
+
+def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg, short=False):
     """Roofline object of the dominant kernel: algorithmic FLOPs per launch (SURVEY 8(d)
     per-window counts x the windows one launch processes) / its average HIP-event duration.
     Timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch)
@@ -95,7 +101,8 @@ def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg):
     avg_ms = ktimes[dom][0]
     flops = fl.get(dom, 0) * windows_per_launch
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_mfma", "fac_bwd": "k_fac_bwd_mfma" if mfma else "k_fac_bwd",
+    kname = {"emb_fwd": "k_forward", "fac_fwd": "k_fac_fwd_s16" if short else "k_fac_fwd_mfma",
+             "fac_bwd": ("k_fac_bwd_s16" if short else "k_fac_bwd_mfma") if mfma else "k_fac_bwd",
              "emb_bwd": "k_bwd_merged" if merged else "k_emb_bwd", "emb_final": "k_emb_final",
              "fac_mix": "k_fac_mix"}[dom]
     return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
@@ -292,7 +299,8 @@ def pmc_traffic(kernel_name, cfg):
     import glob
     import re
     base, packed = (cfg.rsplit("_r", 1)[0], True) if "_r" in cfg else (cfg, False)
-    pats = [os.path.join(ROOT, "profiles", "r02_pmc_%s_*counter_collection*.csv" % base)]
+    # the newest round's passes first (kernels change between rounds), then older ones
+    pats = [os.path.join(ROOT, "profiles", "r%02d_pmc_%s_*counter_collection*.csv" % (rnd, base)) for rnd in (3, 2)]
     if base == "d4ic" and not packed:
         pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
     for pat in pats:
@@ -464,7 +472,8 @@ def mode_fit(args, dev, rank, world, dist):
                         "for all R" % B}
         if not args.no_kernel_times:
             gkt = kernel_times_of(gsteps(min(args.grid_steps, 20), 3))
-            grid["roofline"] = roofline_of(gkt, flops_per_window(c), R * B, "%s_r%d" % (args.config, R))
+            grid["roofline"] = roofline_of(gkt, flops_per_window(c), R * B, "%s_r%d" % (args.config, R),
+                                           short_factor_kernels(c))
     fph = None
     if args.fit_replicas > 0:
         fph = fits_per_hour(c, args, dev, rank, dist, world)
