@@ -1051,7 +1051,7 @@ struct EmbWbSum {
 // NR = elements of a p x p matrix per thread (p * p <= NR * RC_BLOCK): staging width and the
 // register prefetch; small adjacencies get the short code (one-shot code is fetched cold).
 template <int NR>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int ept) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
   // the adjacency workgroups (the longest) are dispatched first for ALL replicas: linear
@@ -1086,8 +1086,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
   // workgroup 0 is the adjacency workgroup (the longest; dispatched first), 1..nw the parameters
   if (wx > 0) {
     if (!stepA) return;
-    const int e = (wx - 1) * RC_BLOCK + threadIdx.x;
-    if (e >= total) return;
+    // ept runs of RC_BLOCK consecutive elements per workgroup (1 for a single fit; 4 for packed
+    // replicas, where one element per thread made ~10K short workgroups at R = 128)
+    for (int run = 0; run < ept; ++run) {
+    const int e = ((wx - 1) * ept + run) * RC_BLOCK + threadIdx.x;
+    if (e >= total) break;
     float g = 0.f;
     int64_t idx;
     if (fused) {
@@ -1145,6 +1148,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw) {
       idx = c.eo.fc1W + q;
     }
     rc_update(c, E, Mm, V, c.gE + r * c.es, idx, g, as);
+    }
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
     return;
   }
@@ -1453,17 +1457,18 @@ int rc_launch_emb_combine(const StepCtx& c, hipStream_t s) {
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
-  const int nw = (total + RC_BLOCK - 1) / RC_BLOCK;
+  const int ept = c.nrep >= 8 ? 4 : 1;
+  const int nw = (total + ept * RC_BLOCK - 1) / (ept * RC_BLOCK);
   const size_t lds = sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * (d.p + 1) + 3 * 64);
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   if (d.p * d.p <= 4 * RC_BLOCK) {
     int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw);
+    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw, ept);
   } else {
     int e = rc_lds_optin(k_emb_final<16>, lds, "k_emb_final LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw);
+    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw, ept);
   }
   return rc_check(hipGetLastError(), "k_emb_final");
 }

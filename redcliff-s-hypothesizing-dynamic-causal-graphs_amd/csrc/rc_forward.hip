@@ -126,11 +126,16 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
   RC_PHASE(c.ws, c.wo.total, bx, 4);
   // fc1 weights of the first column step are issued before the graph convolution runs
   const float* W1 = E + c.eo.fc1W;
-  const int lane = tid & 63, wv = tid >> 6;
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int RW = (M1 + 3) / 4, m0 = wv * RW;
-  float wcur[16];
+  // two column steps in flight (the third is requested as the first is multiplied): p*H = 1,000
+  // - 1,200 at C1 / TST is 16 - 19 steps of dependent L2 round trips otherwise
+  float wcur[16], wn1[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) wcur[j] = (j < RW && m0 + j < M1 && lane < pH) ? W1[(int64_t)(m0 + j) * pH + lane] : 0.f;
+  for (int j = 0; j < 16; ++j) {
+    wcur[j] = (j < RW && m0 + j < M1 && lane < pH) ? W1[(int64_t)(m0 + j) * pH + lane] : 0.f;
+    wn1[j] = (j < RW && m0 + j < M1 && lane + 64 < pH) ? W1[(int64_t)(m0 + j) * pH + lane + 64] : 0.f;
+  }
   RC_PHASE(c.ws, c.wo.total, bx, 5);
   // Z = sum_i T_i W_i ; R = relu(Z)
   const float* Wsrc = w_lds ? Wl : gw;
@@ -161,10 +166,10 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc[j][s] = 0.f;
   for (int q = lane; q < pH; q += 64) {
-    float wnext[16];
-    const int qn = q + 64;
+    float wn2[16];
+    const int qn = q + 128;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) wnext[j] = (j < RW && m0 + j < M1 && qn < pH) ? W1[(int64_t)(m0 + j) * pH + qn] : 0.f;
+    for (int j = 0; j < 16; ++j) wn2[j] = (j < RW && m0 + j < M1 && qn < pH) ? W1[(int64_t)(m0 + j) * pH + qn] : 0.f;
     float rv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
@@ -173,7 +178,10 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc[j][s] += wcur[j] * rv[s];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) wcur[j] = wnext[j];
+    for (int j = 0; j < 16; ++j) {
+      wcur[j] = wn1[j];
+      wn1[j] = wn2[j];
+    }
   }
   // reduce-scatter of the 16 row partials over the 64 lanes: 17 shuffles per window instead of
   // 16 full reductions (96); afterwards lane l holds row (l >> 2) & 15 in every lane of its quad
