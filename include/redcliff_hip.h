@@ -213,6 +213,14 @@ int redcliff_adam_apply(const RedcliffDims* d, float* params, float* exp_avg, fl
                         int64_t n, int64_t stride, const RedcliffReplicaHyper* hyper, int32_t group, int32_t t,
                         void* stream);
 
+/* The data-parallel update in one launch: with the step arguments of the RC_GRAD_ONLY shard step
+ * that just ran (after grad_emb / grad_fac were all-reduced), Adam of the RC_STEP_A group
+ * (n_emb floats) and the RC_STEP_B group (n_fac floats), exactly as redcliff_adam_apply with
+ * t = tA / tB, plus the DGCNN Chebyshev supports of the updated A in the workspace, so the next
+ * step needs no RC_REFRESH_SUPPORTS.  Replaces the optimizer steps of batch_update
+ * (models/redcliff_s_cmlp_withStateSmoothing.py:741-759) for summed gradients. */
+int redcliff_dp_update(const RedcliffStepArgs* a, int64_t n_emb, int64_t n_fac, void* stream);
+
 /* Batched fp32 GEMM, row-major: C[b] = alpha * op(A[b]) op(B[b]) + beta * C[b], op = X or X^T
  * (trans flag), A/B/C of batch b at X + b * stride_x.  The contraction of the generic
  * (non-fused) path: cEmbedder / Vanilla embedders (models/redcliff_factor_score_embedders.py:
@@ -252,7 +260,7 @@ int redcliff_gc_track_stats(int32_t n_l1_rows, int64_t l1_len, const float* est,
 /* Per-kernel HIP-event timing for benchmarking: redcliff_kernel_timing(1) brackets every
  * kernel launched by redcliff_train_step with events on its stream; redcliff_kernel_times()
  * synchronises them and returns per-kernel totals (ids 0..7: supports, emb_fwd, fac_fwd,
- * fac_bwd, emb_bwd, emb_final, fac_mix, emb_combine).  Returns the number of kernel ids.
+ * fac_bwd, emb_bwd, emb_final, fac_mix, emb_combine, fac_lead).  Returns the number of kernel ids.
  * When a single fit (R == 1) splits into two kernel chains (GEMM-shaped embedder and / or
  * matrix-core factor path), the factor chain runs on an internal second stream (one per host
  * thread and device) forked from and joined back into `stream` with events, so stream

@@ -9,7 +9,7 @@
 
 // ---- optional per-kernel HIP-event timing (bench / profiling only) -------------------------
 namespace {
-enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_FAC_MIX, KT_EMB_COMB, KT_N };
+enum { KT_SUPPORTS = 0, KT_EMB_FWD, KT_FAC_FWD, KT_FAC_BWD, KT_EMB_BWD, KT_EMB_FINAL, KT_FAC_MIX, KT_EMB_COMB, KT_FAC_LEAD, KT_N };
 struct TimedLaunch {
   int id;
   hipEvent_t a, b;
@@ -49,13 +49,20 @@ int aux_stream(AuxStream** out) {
   if (dev < 0 || dev >= 16) { rc_set_error("device %d outside the auxiliary-stream table", dev); return REDCLIFF_ELIMIT; }
   AuxStream& a = g_aux[dev];
   if (!a.s) {
-    // lowest priority: the embedder chain on the caller's stream is the critical path, the
-    // factor chain's long matrix-core launches fill the CUs it leaves idle
-    int least = 0, greatest = 0;
-    e = rc_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
-    const char* pv = getenv("REDCLIFF_AUX_PRIO");  // tuning knob: low (default) | normal | high
-    const int prio = !pv ? least : (!strcmp(pv, "high") ? greatest : (!strcmp(pv, "normal") ? (least + greatest) / 2 : least));
-    if (!e) e = rc_check(hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, prio), "hipStreamCreateWithPriority");
+    // normal priority (round 3): a low- or high-priority stream needs a hardware queue of its
+    // own class, and once RCCL's streams hold the process's queues (a torch.distributed "nccl"
+    // group) a forked step on such a stream ran 3.5x slower (C1(K=4): 100 -> 353 us per step,
+    // profiles/r03_dp_profile_c1k4_*.log); without RCCL normal and low measure the same (C1(K=4)
+    // 1.29 M windows/s both, C5 288 K vs 281 K)
+    const char* pv = getenv("REDCLIFF_AUX_PRIO");  // tuning knob: low | normal (default) | high
+    if (!pv || (strcmp(pv, "low") && strcmp(pv, "high"))) {
+      e = rc_check(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+    } else {
+      int least = 0, greatest = 0;
+      e = rc_check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+      const int prio = !strcmp(pv, "high") ? greatest : least;
+      if (!e) e = rc_check(hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, prio), "hipStreamCreateWithPriority");
+    }
     for (int i = 0; i < 3 && !e; ++i) e = rc_check(hipEventCreateWithFlags(&a.ev[i], hipEventDisableTiming), "hipEventCreate");
     if (e) return e;
   }
@@ -353,9 +360,29 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   const char* dv0 = getenv("REDCLIFF_DEFER");
   const bool merged = fac && !mfma && !fork && !egemm && emb_grad && !(fl & RC_VALUES) && !(dv0 && strcmp(dv0, "1") != 0) &&
                       (mv ? strcmp(mv, "0") != 0 : rc_bwd_merged_grid(c) > 0);
-  if (!mfma && fac && !merged) {
+  // Split lead (vector factor path when the merged launch does not fit, e.g. TST: K*p = 108
+  // networks): the K*p lead workgroups' records (dL/dw, dL/dA, group norms) are all the embedder
+  // backward needs, and the factor update needs only the forward, so the records get their own
+  // short launch on s and the update runs on the second stream beside the embedder backward,
+  // joined before k_emb_final (which rewrites A, an operand of the update).  Same workgroup
+  // arithmetic as the one launch, so the same bits (tests/test_gpu_forked.py).  Default: single
+  // fits (a pack fills the chip) whose update grid leaves at least half of the CUs to the
+  // embedder backward (C1(K=4): 80 update workgroups, 1.23 -> 1.30 M windows/s; TST: 216, the
+  // embedder backward is slowed by more than the split saves, 1.07 -> 1.01 M).
+  // REDCLIFF_SPLIT_LEAD=0 / 1 overrides.
+  const char* slv = getenv("REDCLIFF_SPLIT_LEAD");
+  const bool split_ok = !mfma && fac && !merged && !fork && emb_grad && (fl & RC_STEP_B);
+  const bool split = split_ok && (slv ? strcmp(slv, "0") != 0
+                                      : c.d.R == 1 && 2 * rc_fac_bwd_grid(c) <= rc_cu_count());
+  if (split) {
+    if ((e = aux_stream(&aux))) return e;
+    sf = aux->s;
+    if ((e = stream_wait(sf, s, aux->ev[1]))) return e;  // the update needs the forward
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf, RC_FB_UPDATE); }))) return e;
+    if ((e = timed(KT_FAC_LEAD, s, [&] { return rc_launch_fac_bwd(c, s, RC_FB_RECORDS); }))) return e;
+  } else if (!mfma && fac && !merged) {
     if (fork && (e = stream_wait(sf, s, aux->ev[1]))) return e;  // the mixing needs the embedder output w
-    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf); }))) return e;
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf, RC_FB_ALL); }))) return e;
     if (fork && (e = stream_wait(s, sf, aux->ev[0]))) return e;
   }
   if ((fl & RC_VALUES) && (e = rc_launch_cos_values(c, s))) return e;  // before the head workgroup
@@ -387,11 +414,31 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }
+  if (split && (e = stream_wait(s, sf, aux->ev[0]))) return e;  // join before A changes
   if (emb_grad || c.nbn > 0) {
     if ((e = timed(KT_EMB_FINAL, s, [&] { return rc_launch_emb_final(c, s); }))) return e;
   }
   if (fork && (e = stream_wait(s, sf, aux->ev[2]))) return e;  // join: the caller's stream sees both chains
   return 0;
+}
+
+// Data-parallel update (reference: the optimizer steps of batch_update, models/redcliff_s_cmlp_
+// withStateSmoothing.py:741-759, applied to gradients summed over the ranks): the same step
+// arguments the shard step ran with, after the all-reduce of grad_emb / grad_fac.
+int redcliff_dp_update(const RedcliffStepArgs* a, int64_t n_emb, int64_t n_fac, void* stream) {
+  if (!a) { rc_set_error("null step arguments"); return REDCLIFF_EINVAL; }
+  StepCtx c;
+  int e = make_ctx(a, c);
+  if (e) return e;
+  if (c.nrep == 0) return 0;
+  const bool sa = a->flags & RC_STEP_A, sb = a->flags & RC_STEP_B;
+  if ((sa && (!a->grad_emb || n_emb < (int64_t)c.d.p * c.d.p || n_emb > c.es)) || (sb && (!a->grad_fac || n_fac < 0 || n_fac > c.fs))) {
+    rc_set_error("dp_update: gradient buffers / group sizes do not match the step arguments");
+    return REDCLIFF_EINVAL;
+  }
+  if (c.eo.A + (int64_t)c.d.p * c.d.p > n_emb && sa) { rc_set_error("dp_update: A outside the embedder group"); return REDCLIFF_EINVAL; }
+  if (!sa && !sb) return 0;
+  return rc_launch_dp_update(c, n_emb, n_fac, (hipStream_t)stream);
 }
 
 int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_t* rows, const int32_t* sizes,
@@ -414,7 +461,7 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
 // Per-kernel timing: while enabled every launch of redcliff_train_step is bracketed by
 // HIP events on its stream.  redcliff_kernel_times() waits for the recorded events,
 // adds the elapsed milliseconds per kernel (ids: supports, emb_fwd, fac_fwd, fac_bwd,
-// emb_bwd, emb_final, fac_mix, emb_combine) into total_ms[]/counts[] and clears the record.
+// emb_bwd, emb_final, fac_mix, emb_combine, fac_lead) into total_ms[]/counts[] and clears the record.
 int redcliff_kernel_timing(int32_t enable) {
   g_timing = enable != 0;
   return 0;

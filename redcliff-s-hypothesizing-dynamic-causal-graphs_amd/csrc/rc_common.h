@@ -537,7 +537,24 @@ int rc_check(hipError_t e, const char* what);
 // embedder forward and / or vector-path factor forward in one launch (rc_forward.hip)
 int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac);
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s);
-int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s);
+// factor backward roles (rc_fac_bwd.h fac_bwd_wg): one launch, or the split-lead pair
+enum { RC_FB_ALL = 0, RC_FB_RECORDS = 1, RC_FB_UPDATE = 2 };
+int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role);
+int rc_fac_bwd_grid(const StepCtx& c);  // workgroups per replica of the update launch
+
+// compute units of the current device (cached per host thread)
+inline int rc_cu_count() {
+  static thread_local int dev_c = -1, n_c = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (dev != dev_c) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 0;
+    dev_c = dev;
+    n_c = n;
+  }
+  return n_c;
+}
 // MFMA path of the factor networks (large p*L): window transpose, GEMM forward, per-network
 // mixing / penalties / small-parameter updates, GEMM dW0 + Adam.
 bool rc_fac_use_mfma(const RedcliffDims& d);
@@ -556,6 +573,7 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);
 int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s);  // factor + embedder backward, one launch
 int rc_bwd_merged_grid(const StepCtx& c);                    // its grid, 0 when not worth it  // window-block partials (c.defer)
+int rc_launch_dp_update(const StepCtx& c, int64_t nE, int64_t nF, hipStream_t s);
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,
                        WsOff wo, hipStream_t s);
 int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,

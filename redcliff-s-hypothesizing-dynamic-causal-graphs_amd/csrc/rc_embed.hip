@@ -982,6 +982,68 @@ __global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const flo
   supports_lds(sm, sm + p * P, ws + r * wss + wo.S, sm + (d.n + 1) * p * P, p, d.n);
 }
 
+// Data-parallel update after the all-reduce (DataParallelFit): Adam of both parameter groups from
+// the summed gradients in one launch, and the Chebyshev supports of the updated adjacency in the
+// workgroup that owns A's elements, so the next shard step starts without a refresh launch.
+// grid (1 + nbE + nbF, R): workgroup 0 = A (p*p elements) + supports when the embedder group
+// steps; then nbE workgroups over the embedder group (A's range skipped) and nbF over the factor
+// group, DPU_EPT coalesced elements per thread (the fp64 bias corrections once per thread).  The
+// per-element arithmetic is rc_adam's, as in k_emb_final / the factor kernels / k_adam_apply.
+#define DPU_EPT 16
+__global__ __launch_bounds__(RC_BLOCK) void k_dp_update(StepCtx c, int64_t nE, int64_t nF, int nbE) {
+  extern __shared__ float sm[];
+  const int r = rc_rep(c, blockIdx.y), tid = threadIdx.x;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const int bx = blockIdx.x;
+  const int p = c.d.p, pp = p * p;
+  if (bx == 0) {
+    if (!(c.flags & RC_STEP_A)) return;
+    const RcAdamScalars s = rc_adam_scalars(hy.A, c.tA);
+    float* P = c.emb + r * c.es;
+    float* M = c.embM + r * c.es;
+    float* V = c.embV + r * c.es;
+    const float* G = c.gE + r * c.es;
+    const int P1 = p + 1;
+    for (int e = tid; e < pp; e += RC_BLOCK) {
+      const int64_t i = c.eo.A + e;
+      float pv = P[i], mv = M[i], vv = V[i];
+      rc_adam(pv, mv, vv, G[i], s);
+      P[i] = pv; M[i] = mv; V[i] = vv;
+      const int a = e / p;
+      sm[a * P1 + (e - a * p)] = pv;
+    }
+    __syncthreads();
+    supports_lds(sm, sm + p * P1, c.ws + r * c.wss + c.wo.S, sm + (c.d.n + 1) * p * P1, p, c.d.n);
+    return;
+  }
+  const bool emb = bx <= nbE;
+  const RcAdamScalars s = rc_adam_scalars(emb ? hy.A : hy.B, emb ? c.tA : c.tB);
+  const int64_t st = emb ? c.es : c.fs, n = emb ? nE : nF;
+  float* P = (emb ? c.emb : c.fac) + r * st;
+  float* M = (emb ? c.embM : c.facM) + r * st;
+  float* V = (emb ? c.embV : c.facV) + r * st;
+  const float* G = (emb ? c.gE : c.gF) + r * st;
+  const int64_t i0 = (int64_t)(emb ? bx - 1 : bx - 1 - nbE) * RC_BLOCK * DPU_EPT + tid;
+  const int64_t a0 = emb ? c.eo.A : -1, a1 = emb ? c.eo.A + pp : -1;
+  float pv[DPU_EPT], mv[DPU_EPT], vv[DPU_EPT], gv[DPU_EPT];
+#pragma unroll
+  for (int k = 0; k < DPU_EPT; ++k) {
+    const int64_t i = i0 + (int64_t)k * RC_BLOCK;
+    const bool on = i < n;
+    pv[k] = on ? P[i] : 0.f;
+    mv[k] = on ? M[i] : 0.f;
+    vv[k] = on ? V[i] : 0.f;
+    gv[k] = on ? G[i] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < DPU_EPT; ++k) {
+    const int64_t i = i0 + (int64_t)k * RC_BLOCK;
+    if (i >= n || (i >= a0 && i < a1)) continue;
+    rc_adam(pv[k], mv[k], vv[k], gv[k], s);
+    P[i] = pv[k]; M[i] = mv[k]; V[i] = vv[k];
+  }
+}
+
 // Window-block partials of k_emb_bwd read in place by k_emb_final (c.defer == 2): element
 // off of (node, chunk) group grp summed over the window blocks in block order -- the sum
 // k_emb_combine forms, so the fused read and the separate launch give the same bits.
@@ -1480,6 +1542,19 @@ int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, floa
   if (e) return e;
   hipLaunchKernelGGL(k_supports, dim3(d.R), dim3(RC_BLOCK), lds, s, d, emb, es, ws, wss, eo, wo);
   return rc_check(hipGetLastError(), "k_supports");
+}
+
+int rc_launch_dp_update(const StepCtx& c, int64_t nE, int64_t nF, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int64_t per = (int64_t)RC_BLOCK * DPU_EPT;
+  const bool sa = c.flags & RC_STEP_A, sb = c.flags & RC_STEP_B;
+  const int64_t nbE = sa ? (nE + per - 1) / per : 0, nbF = sb ? (nF + per - 1) / per : 0;
+  if (1 + nbE + nbF > 0x7fffffff) { rc_set_error("dp_update: parameter groups too large"); return REDCLIFF_ELIMIT; }
+  const size_t lds = sizeof(float) * ((size_t)(d.n + 1) * d.p * (d.p + 1) + 64);
+  int e = rc_lds_optin(k_dp_update, lds, "k_dp_update LDS");
+  if (e) return e;
+  hipLaunchKernelGGL(k_dp_update, dim3((unsigned)(1 + nbE + nbF), c.nrep), dim3(RC_BLOCK), lds, s, c, nE, nF, (int)nbE);
+  return rc_check(hipGetLastError(), "k_dp_update");
 }
 
 int rc_launch_bn_stats(const RedcliffDims& d, const float* X, int64_t xr, int64_t N, int B, double* st, int64_t str,

@@ -48,11 +48,14 @@ __device__ inline void rc_adam_pre(const StepCtx& c, float* P, float* M, float* 
 // (the merged backward launch, k_bwd_merged): the lead workgroup of each network signals, after
 // its dL/dw partials, group norms and dL/dA records are in memory, by an agent-scope release and
 // an increment of *publish (the embedder-backward workgroups of the same launch wait for all K*p).
+// role (split-lead step, rc_capi.hip): RC_FB_ALL = records and update; RC_FB_RECORDS = the lead's
+// records only (one workgroup per network, returns before the update); RC_FB_UPDATE = the update
+// only (no workgroup writes the records).  The arithmetic of every part is the same in each role.
 __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, int kj, int uc, int qc, int r, float* sm,
-                           unsigned* publish) {
+                           unsigned* publish, int role = RC_FB_ALL) {
   const RedcliffDims& d = c.d;
   const int nU = rc_nuchunk(d);
-  const bool lead = (uc == 0 && qc == 0);
+  const bool lead = (uc == 0 && qc == 0) && role != RC_FB_UPDATE;
   const bool sc1 = publish != nullptr;  // payload read inside this launch: write-through stores
   (void)nUl;
   (void)nQ;
@@ -137,7 +140,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       }
     }
   };
-  if (!split) adam_loads();
+  if (!split && role != RC_FB_RECORDS) adam_loads();
   const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
   const float* W1snap = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by the forward
   const int64_t ys_ = (int64_t)d.Bmax * K * p;
@@ -163,7 +166,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
           return q0 + qq < Q ? xwin(c, dL, X, bb, q0 + qq) : 0.f;
         }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
   };
-  if (!split) stage_update(true);
+  if (!split && role != RC_FB_RECORDS) stage_update(true);
   rc_stage_all(
       rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order)
         const int b = dK.div(e), kk = e - b * K;
@@ -328,7 +331,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_WAIT, 1);  // trace builds: the lead's publish time (end slot)
     rc_publish(publish);
   }
-  if (!stepB) return;
+  if (!stepB || role == RC_FB_RECORDS) return;
   if (split) {  // the lead's own update operands, after its records are out
     adam_loads();
     stage_update(true);

@@ -18,13 +18,13 @@
 
 namespace {
 
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ) {
-  // nUl x nQ workgroups per network (1 x 1 when there is no factor update)
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ, int role) {
+  // nUl x nQ workgroups per network (1 x 1 when there is no factor update or only the records)
   extern __shared__ float sm[];
   const int kj = blockIdx.x / (nUl * nQ);
   const int rem0 = blockIdx.x - kj * nUl * nQ;
   const int uc = rem0 / nQ, qc = rem0 - uc * nQ;
-  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, rc_rep(c, blockIdx.y), sm, nullptr);
+  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, rc_rep(c, blockIdx.y), sm, nullptr, role);
 }
 
 }  // namespace
@@ -35,10 +35,21 @@ bool rc_fac_vector_fits(const RedcliffDims& d) {
   return (size_t)fac_bwd_lds_floats(d) <= (size_t)RC_LDS_LIMIT_FLOATS;
 }
 
-int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
+int rc_fac_bwd_grid(const StepCtx& c) {
+  const RedcliffDims& d = c.d;
+  if (!(c.flags & RC_STEP_B)) return d.K * d.p;
+  return d.K * d.p * rc_nuchunk(d) * ((d.p * d.L + FB_QT - 1) / FB_QT);
+}
+
+// role: RC_FB_ALL (one launch), or the split-lead pair RC_FB_RECORDS (K*p lead workgroups: dL/dw,
+// dL/dA, group norms, x_sim, loss values) + RC_FB_UPDATE (every workgroup's dW0 / bias / Adam part),
+// which depend only on the forward and so run concurrently (rc_capi.hip redcliff_train_step)
+int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role) {
   const RedcliffDims& d = c.d;
   const int Q = d.p * d.L;
-  const int nQ = (c.flags & RC_STEP_B) ? (Q + FB_QT - 1) / FB_QT : 1;
+  const bool upd = (c.flags & RC_STEP_B) && role != RC_FB_RECORDS;
+  if (role == RC_FB_UPDATE && !(c.flags & RC_STEP_B)) { rc_set_error("factor update launch without a factor step"); return REDCLIFF_EINVAL; }
+  const int nQ = upd ? (Q + FB_QT - 1) / FB_QT : 1;
   const size_t lds = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
     // only reached when the matrix-core path cannot take over (h > 128) or is overridden
@@ -51,8 +62,8 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s) {
     return REDCLIFF_ELIMIT;
   }
   // without a factor update only the lead workgroup of each network has work
-  const int nUl = (c.flags & RC_STEP_B) ? rc_nuchunk(d) : 1;
-  hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ);
+  const int nUl = upd ? rc_nuchunk(d) : 1;
+  hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, role);
   return rc_check(hipGetLastError(), "k_fac_bwd");
 }
 

@@ -33,10 +33,10 @@ WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
-            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_gemm",
+            "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_dp_update", "redcliff_gemm",
             "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions",
             "redcliff_gc_track_stats", "redcliff_device_status")
-KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine")
+KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine", "fac_lead")
 
 
 class Dims(ctypes.Structure):
@@ -114,6 +114,7 @@ def lib():
     L.redcliff_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i64), ctypes.c_int32]
     L.redcliff_adam_apply.argtypes = [ctypes.POINTER(Dims), _vp, _vp, _vp, _vp, _i64, _i64, _vp, ctypes.c_int32,
                                       ctypes.c_int32, _vp]
+    L.redcliff_dp_update.argtypes = [ctypes.POINTER(StepArgs), _i64, _i64, _vp]
     L.redcliff_gemm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                 ctypes.c_float, _vp, _i64, _i64, _vp, _i64, _i64, ctypes.c_float, _vp, _i64, _i64,
                                 ctypes.c_int32, _vp]

@@ -15,12 +15,14 @@ recordings (TST, many windows per subject) one fit is spread over the GPUs of a 
     identically on every rank;
   * one all-reduce (sum) of one flat fp32 gradient buffer per update (embedder + factor
     groups, 0.4-0.9 MB at the published configs) over RCCL / xGMI, then the replicated Adam
-    update (redcliff_adam_apply) -- every rank ends every step with identical parameters.
+    update of both groups in one launch (redcliff_dp_update, which also refreshes the DGCNN
+    supports of the new A) -- every rank ends every step with identical parameters.
 
 Works with any torch.distributed backend whose all_reduce takes device tensors ("nccl" =
 RCCL on ROCm for the real thing; "gloo" for tests on one GPU).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -43,7 +45,7 @@ def shard_of(B, world, rank):
 class DataParallelFit:
     """One REDCLIFF-S fit sharded over the ranks of `group` (default: the world)."""
 
-    def __init__(self, model, optimizerA, optimizerB, group=None):
+    def __init__(self, model, optimizerA, optimizerB, group=None, fused_update=None):
         if not dist.is_initialized():
             raise RuntimeError("DataParallelFit needs torch.distributed.init_process_group first")
         self.model = model
@@ -64,6 +66,13 @@ class DataParallelFit:
         self.grad = torch.zeros(self.PA + self.PB, device=eng.device, dtype=torch.float32)
         self.gE, self.gF = self.grad[:self.PA], self.grad[self.PA:]
         self.comm_bytes = 0
+        self._bn_pending = 0
+        # fused_update: Adam of both groups + the supports refresh in one launch (redcliff_dp_update);
+        # False: one redcliff_adam_apply per group, supports refreshed by the next step (the
+        # round-2 sequence, kept as the check of the fused launch)
+        if fused_update is None:
+            fused_update = os.environ.get("REDCLIFF_DP_FUSED", "1") != "0"
+        self.fused_update = bool(fused_update)
 
     def cache_dataset(self, loader):
         return self.eng.cache_dataset(loader)
@@ -89,17 +98,37 @@ class DataParallelFit:
         buf = self.grad if (stepA and stepB) else (self.gE if stepA else self.gF)
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group)
         self.comm_bytes += buf.numel() * 4
-        hyp = eng._hyper()
-        d1 = eng.dims(1, ds["T"])  # Adam over the flat groups: only R and the layouts matter
-        for g, on, P, buf_g, n in (("A", stepA, eng.emb, self.gE, self.PA), ("B", stepB, eng.fac, self.gF, self.PB)):
-            if not on:
-                continue
-            st = eng.opt[g]
-            nat.check(nat.lib().redcliff_adam_apply(ctypes.byref(d1), ptr(P), ptr(st["m"]), ptr(st["v"]), ptr(buf_g),
-                                                    n, n, ptr(hyp), 0 if g == "A" else 1, st["t"] + 1, _stream()),
-                      "adam_apply")
-        eng._after(flags, nbn, 1)
-        eng.supports_fresh = False  # A moved after the step's own support refresh
+        if self.fused_update:
+            # Adam of both groups from the summed gradients and the supports of the updated A, one
+            # launch with the shard step's own arguments (t = tA / tB, the same hyper-parameters)
+            nat.check(nat.lib().redcliff_dp_update(ctypes.byref(a), self.PA, self.PB, _stream()), "dp_update")
+        else:
+            hyp = eng._hyper()
+            d1 = eng.dims(1, ds["T"])  # Adam over the flat groups: only R and the layouts matter
+            for g, on, P, buf_g, n in (("A", stepA, eng.emb, self.gE, self.PA), ("B", stepB, eng.fac, self.gF, self.PB)):
+                if on:
+                    st = eng.opt[g]
+                    nat.check(nat.lib().redcliff_adam_apply(ctypes.byref(d1), ptr(P), ptr(st["m"]), ptr(st["v"]),
+                                                            ptr(buf_g), n, n, ptr(hyp), 0 if g == "A" else 1, st["t"] + 1,
+                                                            _stream()), "adam_apply")
+        # step counters (host, and the optimizers' CPU step tensors, which _args reads back to
+        # detect torch-stepped optimizers); BatchNorm's num_batches_tracked, a device tensor the
+        # kernels do not read, is advanced once per run (flush), not with a launch per update
+        if stepA:
+            eng.opt["A"]["t"] += 1
+        if stepB:
+            eng.opt["B"]["t"] += 1
+        eng._sync_steps()
+        self._bn_pending += nbn
+        eng._mark_fresh()  # the fused update refreshed the supports of the new A
+        if stepA and not self.fused_update:
+            eng.supports_fresh = False  # A moved after the step's own support refresh
+
+    def _flush(self):
+        """The BatchNorm update count deferred by _step."""
+        if self._bn_pending:
+            self.eng.dgcnn.BN1.num_batches_tracked.add_(self._bn_pending)
+            self._bn_pending = 0
 
     def run_steps(self, kind, ds, batches):
         """Updates of one kind over the global batches `batches` (indices into ds), back to back:
@@ -107,6 +136,7 @@ class DataParallelFit:
         waits."""
         for bi in batches:
             self._step(kind, ds, bi)
+        self._flush()
 
     def run_epoch(self, epoch, ds, set_modes=True):
         """The batch_update phase of `epoch` (...withStateSmoothing.py:741-759) over every global
@@ -116,6 +146,7 @@ class DataParallelFit:
         for bi in range(int(ds["len"])):
             for kind in kinds:
                 self._step(kind, ds, bi)
+        self._flush()
         if set_modes:
             self.model._set_module_modes(kinds[-1] if kinds else None)
 

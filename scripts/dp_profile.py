@@ -1,6 +1,6 @@
 """Where the time of one data-parallel update goes (one rank over RCCL, TST shape).
 
-    python scripts/dp_profile.py [--batch 128] [--steps 200]
+    python scripts/dp_profile.py [--batch 128] [--steps 200] [--config c4]
 
 Times N updates of DataParallelFit._step (a) as is, (b) with the all-reduce skipped, and
 (c) the host enqueue time alone (the loop returns before the device finishes), next to the
@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "redcliff-s-hypothesizing-dynamic-causal-g
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--config", default="c4")
     ap.add_argument("--steps", type=int, default=200)
     args = ap.parse_args()
     import torch
@@ -31,7 +32,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1)
-    c = dict(bench.CONFIGS["c4"], B=args.batch)
+    c = dict(bench.CONFIGS[args.config], B=args.batch)
     B = c["B"]
     model = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).to(dev)
     oA, oB = bench.adam_pair(model, c)

@@ -226,3 +226,31 @@ def test_two_rank_data_parallel_fit_matches_single_device_fit(tmp_path):
         tol = 5e-6 * max(1.0, np.abs(w).max()) + 2e-4 * np.abs(w)
         bad = np.abs(got - w) > tol
         assert not bad.any(), "%s: %d/%d off, max err %.3e" % (k, int(bad.sum()), w.size, np.abs(got - w).max())
+
+
+def test_fused_update_bitwise_equals_per_group_adam(monkeypatch):
+    """redcliff_dp_update (Adam of both groups + the supports of the new A, one launch) against
+    the per-group redcliff_adam_apply sequence with the supports refreshed by the next step:
+    one rank (gloo), the same batches, bit for bit after every epoch of the schedule."""
+    import torch.distributed as dist
+    from redcliff_amd import DataParallelFit
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        runs = {}
+        for fused in (False, True):
+            m, oA, oB = _model()
+            dp = DataParallelFit(m, oA, oB, fused_update=fused)
+            ds = dp.cache_dataset(_loader())
+            hist = []
+            for epoch in EPOCHS:
+                dp.run_epoch(epoch, ds)
+                torch.cuda.synchronize()
+                hist.append({k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()})
+            runs[fused] = hist
+    finally:
+        dist.destroy_process_group()
+    for e, (want, got) in enumerate(zip(runs[False], runs[True])):
+        for k, w in want.items():
+            np.testing.assert_array_equal(got[k], w, err_msg="epoch %d: %s" % (EPOCHS[e], k))

@@ -114,9 +114,10 @@ def test_forked_pack_bitwise_equals_single_stream_pack(monkeypatch, guard_bands)
             np.testing.assert_array_equal(states["1"][r][k], want, err_msg="replica %d %s" % (r, k))
 
 
-def run_vector(monkeypatch, merge, train, guarded, seed=0):
+def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0"):
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
     monkeypatch.setenv("REDCLIFF_MERGE", merge)
+    monkeypatch.setenv("REDCLIFF_SPLIT_LEAD", split)
     m = make(seed, 10.0, 0.1)
     oA, oB = opts(m, 5e-4, 2e-4)
     eng = m.engine()
@@ -127,7 +128,7 @@ def run_vector(monkeypatch, merge, train, guarded, seed=0):
             m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
     torch.cuda.synchronize()
     if guarded:
-        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s" % merge)
+        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s" % (merge, split))
     return {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
 
 
@@ -143,4 +144,18 @@ def test_merged_backward_bitwise_equals_two_launches(monkeypatch, guard_bands):
     again = run_vector(monkeypatch, "1", train, False)
     for k, want in two.items():
         np.testing.assert_array_equal(one[k], want, err_msg=k)
+        np.testing.assert_array_equal(again[k], want, err_msg=k)
+
+
+def test_split_lead_bitwise_equals_one_launch(monkeypatch, guard_bands):
+    """Split-lead step (the factor leads' records in their own launch, the factor update on the
+    second stream beside the embedder backward, joined before k_emb_final) against the single
+    factor-backward launch on one stream: bit for bit through pretrain -> acclimate -> combined,
+    ragged last batch included, guard bands intact; a second split run repeats the first."""
+    train = data(64 * 2 + 24, seed=9)
+    one = run_vector(monkeypatch, "0", train, True, split="0")
+    two = run_vector(monkeypatch, "0", train, True, split="1")
+    again = run_vector(monkeypatch, "0", train, False, split="1")
+    for k, want in one.items():
+        np.testing.assert_array_equal(two[k], want, err_msg=k)
         np.testing.assert_array_equal(again[k], want, err_msg=k)
