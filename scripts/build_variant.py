@@ -1,5 +1,6 @@
-"""Build an experiment variant of libredcliff_hip.so with extra -D flags into exp/ (timing
-experiments only; select it with REDCLIFF_HIP_LIB=exp/lib_<name>.so)."""
+"""Build an experiment variant of libredcliff_hip.so with extra -D flags into scripts/bin/ (timing
+experiments only, git-ignored but sent to the GPU box; select it with
+REDCLIFF_HIP_LIB=scripts/bin/lib_<name>.so)."""
 import os
 import subprocess
 import sys
@@ -8,7 +9,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "redcliff-s-hyp
 from redcliff_amd import build as b  # noqa: E402
 
 name, flags = sys.argv[1], sys.argv[2:]
-out = os.path.join(os.path.dirname(__file__), "..", "exp", "lib_%s.so" % name)
+out = os.path.join(os.path.dirname(__file__), "bin", "lib_%s.so" % name)
 os.makedirs(os.path.dirname(out), exist_ok=True)
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=%s" % b.ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + b.INCLUDE,
        "-I" + b.CSRC] + flags + b.sources() + ["-o", out]
