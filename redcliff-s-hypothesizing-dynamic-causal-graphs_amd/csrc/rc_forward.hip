@@ -14,6 +14,7 @@
 // and models/cmlp.py:12-35 / :90-101 (MLP: Conv1d(p, h, L) -> ReLU -> Conv1d(h, 1, 1)),
 // models/cmlp.py:147-167 (group norms of layer-0 weights, pre-update).
 #include <cstdlib>
+#include <type_traits>
 
 #include "rc_common.h"
 
@@ -128,14 +129,19 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
   const float* W1 = E + c.eo.fc1W;
   const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int RW = (M1 + 3) / 4, m0 = wv * RW;
-  // two column steps in flight (the third is requested as the first is multiplied): p*H = 1,000
-  // - 1,200 at C1 / TST is 16 - 19 steps of dependent L2 round trips otherwise
-  float wcur[16], wn1[16];
+  // three buffers of column-step weights in rotation (p*H = 1,000 - 1,200 at C1 / TST is 16 - 19
+  // column steps): each buffer is refilled right after it is multiplied and read two steps
+  // later, with no register moves in between (a move of a loading register waits for the load).
+  // Rows past M1 are wave-uniform zeros; a lane past p*H loads a clamped (valid) column that its
+  // masked multiply never uses, so no load sits behind a lane-varying condition.
+  auto ldw = [&](float (&w)[16], int qn) {
+    const int qc = qn < pH ? qn : pH - 1;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    wcur[j] = (j < RW && m0 + j < M1 && lane < pH) ? W1[(int64_t)(m0 + j) * pH + lane] : 0.f;
-    wn1[j] = (j < RW && m0 + j < M1 && lane + 64 < pH) ? W1[(int64_t)(m0 + j) * pH + lane + 64] : 0.f;
-  }
+    for (int j = 0; j < 16; ++j) w[j] = (j < RW && m0 + j < M1) ? W1[(int64_t)(m0 + j) * pH + qc] : 0.f;
+  };
+  float wb0[16], wb1[16], wb2[16];
+  ldw(wb0, lane);
+  ldw(wb1, lane + 64);
   RC_PHASE(c.ws, c.wo.total, bx, 5);
   // Z = sum_i T_i W_i ; R = relu(Z)
   const float* Wsrc = w_lds ? Wl : gw;
@@ -160,58 +166,71 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
   RC_PHASE(c.ws, c.wo.total, bx, 6);
   // fc1: wave wv owns rows [wv*RW, wv*RW+RW) (RW <= 16); lanes split the p*H contraction.
   // The next column step's weights are loaded while the current one is multiplied.
-  float acc[16][4];
-#pragma unroll
-  for (int j = 0; j < 16; ++j)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc[j][s] = 0.f;
-  for (int q = lane; q < pH; q += 64) {
-    float wn2[16];
-    const int qn = q + 128;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) wn2[j] = (j < RW && m0 + j < M1 && qn < pH) ? W1[(int64_t)(m0 + j) * pH + qn] : 0.f;
-    float rv[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
+  // one window per workgroup (the single fit) multiplies only its own column: NB = 1 accumulators
+  auto fc1 = [&](auto nbc) {
+    constexpr int NB = decltype(nbc)::value;
+    float acc[16][NB];
 #pragma unroll
     for (int j = 0; j < 16; ++j)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc[j][s] += wcur[j] * rv[s];
+      for (int s = 0; s < NB; ++s) acc[j][s] = 0.f;
+    // column q of this lane (q ascending per lane: the same chains as one step per iteration)
+    auto mul = [&](const float (&w)[16], int q) {
+      if (q < pH) {
+        float rv[NB];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      wcur[j] = wn1[j];
-      wn1[j] = wn2[j];
+        for (int s = 0; s < NB; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+#pragma unroll
+          for (int s = 0; s < NB; ++s) acc[j][s] += w[j] * rv[s];
+      }
+    };
+    for (int q0 = 0; q0 < pH; q0 += 192) {  // wave-uniform steps of three column blocks
+      const int q = q0 + lane;
+      ldw(wb2, q + 128);
+      mul(wb0, q);
+      if (q0 + 64 >= pH) break;
+      ldw(wb0, q + 192);
+      mul(wb1, q + 64);
+      if (q0 + 128 >= pH) break;
+      ldw(wb1, q + 256);
+      mul(wb2, q + 128);
     }
-  }
-  // reduce-scatter of the 16 row partials over the 64 lanes: 17 shuffles per window instead of
-  // 16 full reductions (96); afterwards lane l holds row (l >> 2) & 15 in every lane of its quad
+    // reduce-scatter of the 16 row partials over the 64 lanes: 17 shuffles per window instead of
+    // 16 full reductions (96); afterwards lane l holds row (l >> 2) & 15 in every lane of its quad
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (s >= nb) break;
-    float v[16];
+    for (int s = 0; s < NB; ++s) {
+      if (s >= nb) break;
+      float v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = acc[j][s];
+      for (int j = 0; j < 16; ++j) v[j] = acc[j][s];
 #pragma unroll
-    for (int half = 8; half >= 1; half >>= 1) {
-      const int off = half * 4;  // lane bit that selects the kept half: 32, 16, 8, 4
-      const bool hi = lane & off;
+      for (int half = 8; half >= 1; half >>= 1) {
+        const int off = half * 4;  // lane bit that selects the kept half: 32, 16, 8, 4
+        const bool hi = lane & off;
 #pragma unroll
-      for (int i = 0; i < half; ++i) {
-        const float send = hi ? v[i] : v[i + half];
-        const float keep = hi ? v[i + half] : v[i];
-        v[i] = keep + __shfl_xor(send, off, 64);
+        for (int i = 0; i < half; ++i) {
+          const float send = hi ? v[i] : v[i + half];
+          const float keep = hi ? v[i + half] : v[i];
+          v[i] = keep + __shfl_xor(send, off, 64);
+        }
+      }
+      float t = v[0];
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 1, 64);
+      const int j = (lane >> 2) & 15, m = m0 + j;
+      if ((lane & 3) == 0 && j < RW && m < M1) {
+        const float val = t + fb1[m];
+        f1l[s * M1 + m] = val;
+        ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = val;
       }
     }
-    float t = v[0];
-    t += __shfl_xor(t, 2, 64);
-    t += __shfl_xor(t, 1, 64);
-    const int j = (lane >> 2) & 15, m = m0 + j;
-    if ((lane & 3) == 0 && j < RW && m < M1) {
-      const float val = t + fb1[m];
-      f1l[s * M1 + m] = val;
-      ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = val;
-    }
-  }
+  };
+  if (SB == 1)
+    fc1(std::integral_constant<int, 1>{});
+  else
+    fc1(std::integral_constant<int, 4>{});
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, bx, 7);
   for (int e = tid; e < nb * K; e += RC_BLOCK) {
