@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 6
+#define REDCLIFF_ABI_VERSION 7
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */

@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
