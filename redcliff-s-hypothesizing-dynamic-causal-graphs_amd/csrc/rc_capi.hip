@@ -386,6 +386,15 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if (fork && (e = stream_wait(s, sf, aux->ev[0]))) return e;
   }
   if ((fl & RC_VALUES) && (e = rc_launch_cos_values(c, s))) return e;  // before the head workgroup
+  // k_emb_combine + k_emb_final as one launch (k_emb_tail) when its grid is resident: the
+  // adjacency chain starts with the combine instead of after it, and one kernel boundary goes.
+  // REDCLIFF_TAIL=0 keeps the two launches.
+  const char* tlv = getenv("REDCLIFF_TAIL");
+  bool tail = false;
+  auto tail_ok = [&]() {
+    return !egemm && emb_grad && c.defer == 1 && !(fl & RC_VALUES) && !(tlv && strcmp(tlv, "0") == 0) &&
+           rc_emb_tail_grid(c) > 0;
+  };
   if (emb_grad && egemm) {
     // GEMM chain, then the fused kernel without node workgroups (head / adjacency-L1 reduce)
     if ((e = timed(KT_EMB_BWD, s, [&] {
@@ -396,7 +405,8 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   } else if (merged) {
     c.defer = 1;
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_bwd_merged(c, s); }))) return e;
-    if ((e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
+    tail = tail_ok();
+    if (!tail && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (emb_grad) {
     // The node blocks' window-block partials are summed by a separate k_emb_combine launch
     // instead of the in-kernel last arriver (ticket + agent-scope fences): the fences cost the
@@ -410,13 +420,14 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     c.defer = dv ? atoi(dv) : 1;
     if (c.defer < 0 || c.defer > 2) c.defer = 1;
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
-    if (c.defer == 1 && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
+    tail = tail_ok();
+    if (c.defer == 1 && !tail && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }
   if (split && (e = stream_wait(s, sf, aux->ev[0]))) return e;  // join before A changes
   if (emb_grad || c.nbn > 0) {
-    if ((e = timed(KT_EMB_FINAL, s, [&] { return rc_launch_emb_final(c, s); }))) return e;
+    if ((e = timed(KT_EMB_FINAL, s, [&] { return tail ? rc_launch_emb_tail(c, s) : rc_launch_emb_final(c, s); }))) return e;
   }
   if (fork && (e = stream_wait(s, sf, aux->ev[2]))) return e;  // join: the caller's stream sees both chains
   return 0;

@@ -31,8 +31,9 @@ struct WsOff {
   int64_t w1;     // [K][p][h]         pre-update snapshot of the factor output weights
   int64_t gq;     // [nU][K][p][p*L]   squared layer-0 group norms, partial over hidden chunks
   int64_t ebp;    // [p*nch][nbw][pst] embedder-backward partials per (node, chunk, window block)
-  int64_t ecnt;   // [p*nch + 1]       arrival counters of those blocks (u32, self-resetting); the last
-                  //                   slot counts published factor-lead workgroups (k_bwd_merged)
+  int64_t ecnt;   // [p*nch + 2]       arrival counters of those blocks (u32, self-resetting); the last
+                  //                   two slots count published factor-lead workgroups (k_bwd_merged) and
+                  //                   combine workgroups (k_emb_tail)
   int64_t gfc1;   // [M1][p*H]         fc1 weight gradient (combined by the node blocks)
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
@@ -182,7 +183,7 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.w1, K * p * d.h);
   put(o.gq, (int64_t)rc_nuchunk(d) * K * p * p * d.L);
   put(o.ebp, (int64_t)p * rc_nchunk(d) * rc_emb_nbw(d) * rc_emb_pstride(d));
-  put(o.ecnt, p * rc_nchunk(d) + 1);  // + the merged backward's factor-lead counter
+  put(o.ecnt, p * rc_nchunk(d) + 2);  // + the merged backward's factor-lead counter + k_emb_tail's
   put(o.gfc1, (int64_t)d.M1 * p * d.H);
   put(o.dwp, p * B * K);
   put(o.dAadj, K * p * p);
@@ -363,6 +364,8 @@ __device__ inline void rc_wait_count(const unsigned* cnt, unsigned target, unsig
 __device__ inline unsigned* rc_fac_lead_cnt(const StepCtx& c, float* ws) {
   return reinterpret_cast<unsigned*>(ws + c.wo.ecnt) + c.d.p * ((c.d.H + EMB_HC - 1) / EMB_HC);
 }
+// k_emb_tail's combine counter of replica slice `ws`
+__device__ inline unsigned* rc_tail_cnt(const StepCtx& c, float* ws) { return rc_fac_lead_cnt(c, ws) + 1; }
 // a consumer of the merged backward waits for `target` published factor leads of replica slice ws
 __device__ inline void rc_wait_leads(const StepCtx& c, float* ws, const unsigned* cnt, unsigned target) {
   rc_wait_count(cnt, target + (c.wait_dbg ? 1u : 0u), reinterpret_cast<unsigned*>(ws + c.wo.errw),
@@ -570,6 +573,8 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
+int rc_emb_tail_grid(const StepCtx& c);
+int rc_launch_emb_tail(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);
 int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s);  // factor + embedder backward, one launch
 int rc_bwd_merged_grid(const StepCtx& c);                    // its grid, 0 when not worth it  // window-block partials (c.defer)

@@ -757,16 +757,18 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
 // (node, chunk) group blockIdx.y summed over the window blocks in block order and scattered
 // exactly as the last arriver does, so both variants give the same bits.
 // grid (ceil(pstride / RC_BLOCK), p * nchunk, R).
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
+// (emb_combine_elem: element e of group grp of replica r; sc1: coherent stores, read inside the
+// same launch by k_emb_tail's parameter workgroups)
+__device__ __forceinline__ bool emb_combine_in(const StepCtx& c, int grp, int e) {
   const RedcliffDims& d = c.d;
-  const int grp = blockIdx.y, r = rc_rep(c, blockIdx.z), e = blockIdx.x * RC_BLOCK + threadIdx.x;
-  const int p = d.p, n = d.n, F = d.F, H = d.H, M1 = d.M1, HC = EMB_HC;
-  const int nch = rc_nchunk(d), node = grp / nch, ch = grp - node * nch;
+  const int ofs_h = d.M1 * EMB_HC + d.n * d.F * EMB_HC + (d.n - 1) * d.p + 2 * d.F;
+  return e < (grp == 0 ? rc_emb_pstride(d) : ofs_h);  // fc2 / fc1-bias partials ride on group 0
+}
+__device__ __forceinline__ float emb_combine_sum(const StepCtx& c, int r, int grp, int e) {
+  const RedcliffDims& d = c.d;
+  if (!emb_combine_in(c, grp, e)) return 0.f;
   const int pst = rc_emb_pstride(d), nbwm = rc_emb_nbw(d), wpb = rc_emb_wpb(d), nbw = (c.B + wpb - 1) / wpb;
-  const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
-  if (e >= (grp == 0 ? pst : ofs_h)) return;  // fc2 / fc1-bias partials ride on group 0
-  float* ws = c.ws + r * c.wss;
-  const float* base = ws + c.wo.ebp + (int64_t)grp * nbwm * pst + e;
+  const float* base = c.ws + r * c.wss + c.wo.ebp + (int64_t)grp * nbwm * pst + e;
   float t = 0.f;
   for (int w0 = 0; w0 < nbw; w0 += 8) {
     float v[8];
@@ -776,20 +778,37 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
     for (int q = 0; q < 8; ++q)
       if (w0 + q < nbw) t += v[q];
   }
+  return t;
+}
+__device__ __forceinline__ void emb_combine_store(const StepCtx& c, int r, int grp, int e, float t, bool sc1) {
+  const RedcliffDims& d = c.d;
+  if (!emb_combine_in(c, grp, e)) return;
+  const int p = d.p, n = d.n, F = d.F, H = d.H, M1 = d.M1, HC = EMB_HC;
+  const int nch = rc_nchunk(d), node = grp / nch, ch = grp - node * nch;
+  const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
+  float* ws = c.ws + r * c.wss;
   const int h0 = ch * HC, hc = min(HC, H - h0);
   if (e < ofs_w) {
     const int m = e / HC, hh = e - m * HC;
-    if (hh < hc) ws[c.wo.gfc1 + (int64_t)m * p * H + node * H + h0 + hh] = t;
+    if (hh < hc) rc_store_payload(ws + c.wo.gfc1 + (int64_t)m * p * H + node * H + h0 + hh, t, sc1);
   } else if (e < ofs_s) {
     const int q = e - ofs_w, qh = q >> 4, i = qh / F, f = qh - i * F, hh = q & 15;  // HC == 16
-    if (hh < hc) ws[c.wo.dWi + (int64_t)node * n * F * H + ((int64_t)i * F + f) * H + h0 + hh] = t;
+    if (hh < hc) rc_store_payload(ws + c.wo.dWi + (int64_t)node * n * F * H + ((int64_t)i * F + f) * H + h0 + hh, t, sc1);
   } else if (e < ofs_g) {
-    ws[c.wo.dS + (int64_t)grp * n * p + p + (e - ofs_s)] = t;
+    rc_store_payload(ws + c.wo.dS + (int64_t)grp * n * p + p + (e - ofs_s), t, sc1);
   } else if (e < ofs_h) {
-    ws[c.wo.dgb + (int64_t)grp * 2 * F + (e - ofs_g)] = t;
+    rc_store_payload(ws + c.wo.dgb + (int64_t)grp * 2 * F + (e - ofs_g), t, sc1);
   } else {
-    ws[c.wo.gfc + (e - ofs_h)] = t;
+    rc_store_payload(ws + c.wo.gfc + (e - ofs_h), t, sc1);
   }
+}
+
+__device__ __forceinline__ void emb_combine_elem(const StepCtx& c, int r, int grp, int e, bool sc1) {
+  emb_combine_store(c, r, grp, e, emb_combine_sum(c, r, grp, e), sc1);
+}
+
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_combine(StepCtx c) {
+  emb_combine_elem(c, rc_rep(c, blockIdx.z), blockIdx.y, blockIdx.x * RC_BLOCK + threadIdx.x, false);
 }
 
 // Adjacency-L1 gradient of A summed over the K factors' records, in place into record 0
@@ -1112,23 +1131,14 @@ struct EmbWbSum {
 // statistics and recomputes the supports for the next step.
 // NR = elements of a p x p matrix per thread (p * p <= NR * RC_BLOCK): staging width and the
 // register prefetch; small adjacencies get the short code (one-shot code is fetched cold).
+// One workgroup of K4 (wx = 0: the adjacency workgroup, wx >= 1: parameter workgroup wx - 1) of
+// replica slot wy.  fused (c.defer == 2): the parameter workgroups sum the window-block partials
+// in place; sc1: they read the combined records with coherent loads (k_emb_tail, where the
+// combine runs in the same launch); adj_inplace: the adjacency workgroup sums its dS partials in
+// place (k_emb_tail, where it does not wait for the combine).
 template <int NR>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int ept) {
-  rc_critical_priority();
+__device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, int ept, bool sc1, bool adj_inplace) {
   const RedcliffDims& d = c.d;
-  // the adjacency workgroups (the longest) are dispatched first for ALL replicas: linear
-  // workgroup i < nrep is replica i's adjacency workgroup, the rest run the parameter updates
-  // (R = 128 D4IC grid: the last replicas' adjacency workgroups no longer start behind ~10K
-  // parameter workgroups)
-  const int lin = blockIdx.x + blockIdx.y * gridDim.x;
-  int wx, wy;
-  if (lin < c.nrep) {
-    wx = 0;
-    wy = lin;
-  } else {
-    wy = (lin - c.nrep) / nw;
-    wx = 1 + (lin - c.nrep) - wy * nw;
-  }
   const int r = rc_rep(c, wy);
   const int p = d.p, n = d.n, F = d.F, H = d.H, K = d.K, M1 = d.M1;
   float* E = c.emb + r * c.es;
@@ -1142,6 +1152,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
   // c.defer == 2: the node blocks' window-block partials are summed here (no combine launch);
   // record layout of emb_bwd_node: fc1 chunk | W_i chunk | dS rows i >= 1 | dgamma dbeta | head
   const bool fused = c.defer == 2;
+  auto ldr = [&](const float* q) { return sc1 ? rc_load_sc1(q) : *q; };
   const int HC = EMB_HC, nch = rc_nchunk(d);
   const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 0);
@@ -1184,11 +1195,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
       }
     } else if (e < nFH) {
 #pragma unroll 8
-      for (int cc = 0; cc < p; ++cc) g += ws[c.wo.dWi + (int64_t)cc * nFH + e];
+      for (int cc = 0; cc < p; ++cc) g += ldr(ws + c.wo.dWi + (int64_t)cc * nFH + e);
       idx = c.eo.gcW + e;
     } else if (e < nFH + nfc) {
       const int q = e - nFH;
-      g = ws[c.wo.gfc + q];
+      g = ldr(ws + c.wo.gfc + q);
       if (q < K * M1) idx = c.eo.fc2W + q;
       else if (q < K * M1 + K) idx = c.eo.fc2b + (q - K * M1);
       else idx = c.eo.fc1b + (q - K * M1 - K);
@@ -1200,13 +1211,13 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
       int pt = 0;
       for (; pt + 3 < c.dgN; pt += 4)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) g4[u] += ws[c.wo.dgb + ((int64_t)(pt + u) * 2 + which) * F + f];
-      for (; pt < c.dgN; ++pt) g4[0] += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
+        for (int u = 0; u < 4; ++u) g4[u] += ldr(ws + c.wo.dgb + ((int64_t)(pt + u) * 2 + which) * F + f);
+      for (; pt < c.dgN; ++pt) g4[0] += ldr(ws + c.wo.dgb + ((int64_t)pt * 2 + which) * F + f);
       g = (g4[0] + g4[1]) + (g4[2] + g4[3]);
       idx = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
     } else {
       const int q = e - nFH - nfc - 2 * F;  // fc1 weight (gradient combined by the node blocks)
-      g = ws[c.wo.gfc1 + q];
+      g = ldr(ws + c.wo.gfc1 + q);
       idx = c.eo.fc1W + q;
     }
     rc_update(c, E, Mm, V, c.gE + r * c.es, idx, g, as);
@@ -1262,7 +1273,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
         rc_seg<NR>((n - 1) * pp2, [&](int e) {
           const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, cc = rem / p, cp = rem - cc * p;
           float t = 0.f;
-          if (fused) {
+          if (fused || adj_inplace) {
             t = EmbWbSum(c, ws).nodes(cc * nch, 1, nch, ofs_s + (i - 1) * p + cp);
           } else {
             for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
@@ -1348,6 +1359,58 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
     c.rv[r * F + tid] = rv;
   }
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
+}
+
+template <int NR>
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int ept) {
+  rc_critical_priority();
+  // the adjacency workgroups (the longest) are dispatched first for ALL replicas: linear
+  // workgroup i < nrep is replica i's adjacency workgroup, the rest run the parameter updates
+  // (R = 128 D4IC grid: the last replicas' adjacency workgroups no longer start behind ~10K
+  // parameter workgroups)
+  const int lin = blockIdx.x + blockIdx.y * gridDim.x;
+  if (lin < c.nrep) {
+    emb_final_wg<NR>(c, 0, lin, ept, false, false);
+  } else {
+    const int wy = (lin - c.nrep) / nw;
+    emb_final_wg<NR>(c, 1 + (lin - c.nrep) - wy * nw, wy, ept, false, false);
+  }
+}
+
+// k_emb_combine + k_emb_final as one launch (single fits with the fused embedder; round 3):
+// workgroup 0 is the adjacency workgroup, which sums its dS partials in place (the sums
+// k_emb_combine forms) and so starts at once; workgroups 1 .. ncomb are the combine's, which
+// store their sums coherently and publish; the parameter workgroups after them wait for all
+// ncomb and then read the combined records coherently.  Producers precede consumers in
+// dispatch order and the whole grid is resident (rc_emb_tail_grid), as in k_bwd_merged; a wait
+// that runs out of polls counts into the status word.  Same sums, same order: the same bits as
+// the two launches (tests/test_gpu_forked.py).  grid (1 + ncomb + nw, R).
+#define TAIL_CE 1   // combine elements per thread in k_emb_tail (4: the grid fits C1(K=4) / TST but is slower)
+#define TAIL_EPT 1  // parameter elements per thread in k_emb_tail (2: slower, r03_emb_tail_variants.jsonl)
+template <int NR>
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_tail(StepCtx c, int ncx, int nw) {
+  rc_critical_priority();
+  const int ncomb = ncx * c.d.p * rc_nchunk(c.d);
+  const int b = blockIdx.x, r = rc_rep(c, blockIdx.y);
+  float* ws = c.ws + r * c.wss;
+  unsigned* cnt = rc_tail_cnt(c, ws);
+  if (b == 0) {
+    emb_final_wg<NR>(c, 0, blockIdx.y, 1, false, true);
+    return;
+  }
+  if (b <= ncomb) {
+    const int q = b - 1, grp = q / ncx, x = q - grp * ncx;
+    float t[TAIL_CE];
+#pragma unroll
+    for (int u = 0; u < TAIL_CE; ++u) t[u] = emb_combine_sum(c, r, grp, (x * TAIL_CE + u) * RC_BLOCK + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < TAIL_CE; ++u) emb_combine_store(c, r, grp, (x * TAIL_CE + u) * RC_BLOCK + threadIdx.x, t[u], true);
+    rc_publish(cnt);
+    return;
+  }
+  if (!(c.flags & RC_STEP_A)) return;
+  rc_wait_count(cnt, (unsigned)ncomb, reinterpret_cast<unsigned*>(ws + c.wo.errw), RC_WAIT_POLLS);
+  emb_final_wg<NR>(c, b - ncomb, blockIdx.y, TAIL_EPT, true, false);
 }
 
 // BatchNorm batch statistics for consecutive batches: one workgroup per (batch, feature),
@@ -1516,12 +1579,52 @@ int rc_launch_emb_combine(const StepCtx& c, hipStream_t s) {
   return rc_check(hipGetLastError(), "k_emb_combine");
 }
 
+static size_t rc_emb_final_lds(const RedcliffDims& d) {
+  return sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * (d.p + 1) + 3 * 64);
+}
+
+// Workgroups of k_emb_tail per replica, or 0 when the two launches should be used: single fits
+// (R = 1) whose whole grid is resident at the kernel's occupancy (runtime occupancy x CUs).
+int rc_emb_tail_grid(const StepCtx& c) {
+  const RedcliffDims& d = c.d;
+  if (c.nrep != 1 || d.p * d.p > 4 * RC_BLOCK) return 0;
+  const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
+  const int nw = (total + TAIL_EPT * RC_BLOCK - 1) / (TAIL_EPT * RC_BLOCK);
+  const int ncx = (rc_emb_pstride(d) + TAIL_CE * RC_BLOCK - 1) / (TAIL_CE * RC_BLOCK);
+  const int grid = 1 + ncx * d.p * rc_nchunk(d) + nw;
+  const size_t lds = rc_emb_final_lds(d);
+  static thread_local size_t cached_lds = (size_t)-1;
+  static thread_local int occ = 0;
+  if (lds != cached_lds) {
+    occ = 0;
+    if (rc_lds_optin(k_emb_tail<4>, lds, "k_emb_tail LDS") != 0 ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_emb_tail<4>, RC_BLOCK, lds) != hipSuccess)
+      occ = 0;
+    cached_lds = lds;
+  }
+  return grid <= occ * rc_cu_count() ? grid : 0;
+}
+
+int rc_launch_emb_tail(const StepCtx& c, hipStream_t s) {
+  const RedcliffDims& d = c.d;
+  const int grid = rc_emb_tail_grid(c);
+  if (grid == 0 || c.defer != 1) { rc_set_error("embedder tail launch: grid not resident or defer != 1"); return REDCLIFF_EINVAL; }
+  const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
+  const int nw = (total + TAIL_EPT * RC_BLOCK - 1) / (TAIL_EPT * RC_BLOCK);
+  const int ncx = (rc_emb_pstride(d) + TAIL_CE * RC_BLOCK - 1) / (TAIL_CE * RC_BLOCK);
+  const size_t lds = rc_emb_final_lds(d);
+  int e = rc_lds_optin(k_emb_tail<4>, lds, "k_emb_tail LDS");
+  if (e) return e;
+  hipLaunchKernelGGL(k_emb_tail<4>, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, ncx, nw);
+  return rc_check(hipGetLastError(), "k_emb_tail");
+}
+
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
   const int ept = c.nrep >= 8 ? 4 : 1;
   const int nw = (total + ept * RC_BLOCK - 1) / (ept * RC_BLOCK);
-  const size_t lds = sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * (d.p + 1) + 3 * 64);
+  const size_t lds = rc_emb_final_lds(d);
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   if (d.p * d.p <= 4 * RC_BLOCK) {
     int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");

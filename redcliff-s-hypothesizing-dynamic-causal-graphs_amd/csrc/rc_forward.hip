@@ -348,7 +348,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_l
   extern __shared__ float sm[];
   // every step with an embedder forward re-arms the merged backward's factor-lead counter (the
   // kernel boundary orders this store before k_bwd_merged's polls)
-  if (blockIdx.x == 0 && nemb > 0 && threadIdx.x == 0) *rc_fac_lead_cnt(c, c.ws + rc_rep(c, blockIdx.y) * c.wss) = 0u;
+  if (blockIdx.x == 0 && nemb > 0 && threadIdx.x == 0) {  // the counters of this step's later launches
+    unsigned* lc = rc_fac_lead_cnt(c, c.ws + rc_rep(c, blockIdx.y) * c.wss);
+    lc[0] = 0u;  // merged backward: published factor leads
+    lc[1] = 0u;  // k_emb_tail: published combine workgroups
+  }
   if ((int)blockIdx.x < nemb)
     emb_fwd_body(c, blockIdx.x, SB, w_lds, sm);
   else

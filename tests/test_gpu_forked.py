@@ -114,10 +114,11 @@ def test_forked_pack_bitwise_equals_single_stream_pack(monkeypatch, guard_bands)
             np.testing.assert_array_equal(states["1"][r][k], want, err_msg="replica %d %s" % (r, k))
 
 
-def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0"):
+def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0"):
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
     monkeypatch.setenv("REDCLIFF_MERGE", merge)
     monkeypatch.setenv("REDCLIFF_SPLIT_LEAD", split)
+    monkeypatch.setenv("REDCLIFF_TAIL", tail)
     m = make(seed, 10.0, 0.1)
     oA, oB = opts(m, 5e-4, 2e-4)
     eng = m.engine()
@@ -128,7 +129,7 @@ def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0"):
             m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
     torch.cuda.synchronize()
     if guarded:
-        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s" % (merge, split))
+        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s tail=%s" % (merge, split, tail))
     return {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
 
 
@@ -158,4 +159,20 @@ def test_split_lead_bitwise_equals_one_launch(monkeypatch, guard_bands):
     again = run_vector(monkeypatch, "0", train, False, split="1")
     for k, want in one.items():
         np.testing.assert_array_equal(two[k], want, err_msg=k)
+        np.testing.assert_array_equal(again[k], want, err_msg=k)
+
+
+@pytest.mark.parametrize("merge,split", [("1", "0"), ("0", "0"), ("0", "1")])
+def test_embedder_tail_bitwise_equals_combine_and_final(merge, split, monkeypatch, guard_bands):
+    """k_emb_tail (the window-block combine and the embedder optimizer in one launch: the
+    adjacency workgroup sums its dS partials in place, the parameter workgroups wait for the
+    combine workgroups' published records) against k_emb_combine + k_emb_final: bit for bit
+    through pretrain -> acclimate -> combined on the merged, two-launch and split-lead backward
+    paths, guard bands intact; a second tail run repeats the first (the counter re-arms)."""
+    train = data(64 * 2 + 24, seed=13)
+    two = run_vector(monkeypatch, merge, train, True, split=split, tail="0")
+    one = run_vector(monkeypatch, merge, train, True, split=split, tail="1")
+    again = run_vector(monkeypatch, merge, train, False, split=split, tail="1")
+    for k, want in two.items():
+        np.testing.assert_array_equal(one[k], want, err_msg=k)
         np.testing.assert_array_equal(again[k], want, err_msg=k)
