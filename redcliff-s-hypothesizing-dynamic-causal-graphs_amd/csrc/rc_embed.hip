@@ -13,6 +13,7 @@
 // the three upstream gradients are summed, and the BatchNorm running statistics are
 // advanced n_bn_updates (=3) times.
 #include <cstdlib>
+#include <cstring>
 
 #include "rc_common.h"
 #include "rc_fac_bwd.h"
@@ -1008,7 +1009,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const flo
 // steps; then nbE workgroups over the embedder group (A's range skipped) and nbF over the factor
 // group, DPU_EPT coalesced elements per thread (the fp64 bias corrections once per thread).  The
 // per-element arithmetic is rc_adam's, as in k_emb_final / the factor kernels / k_adam_apply.
-#define DPU_EPT 16
+#define DPU_EPT 4  // (16: ~55 workgroups at TST, 9.6 us; the chip needs more of them)
 __global__ __launch_bounds__(RC_BLOCK) void k_dp_update(StepCtx c, int64_t nE, int64_t nF, int nbE) {
   extern __shared__ float sm[];
   const int r = rc_rep(c, blockIdx.y), tid = threadIdx.x;

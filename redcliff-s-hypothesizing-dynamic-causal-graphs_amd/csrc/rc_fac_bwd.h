@@ -167,35 +167,36 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
         }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
   };
   if (!split && role != RC_FB_RECORDS) stage_update(true);
+  // The two partial sums come last and load every slot unconditionally (slots >= nU read slot 0
+  // and are not added): a guarded load is a branch, and a sum between branches waits for its
+  // loads before the next element's are issued -- one memory round per element otherwise.
   rc_stage_all(
+      rc_seg<4>(B * K, [&](int e) { return ws[c.wo.w + e]; }, [&](int e, float v) { wrl[e] = v; }),
+      rc_seg<1>(tgt ? B : 0, [&](int b) { return X[((c.row0 + b) * d.T + c.Lmax) * p + j]; },
+                [&](int b, float v) { xt[b] = v; }),
+      rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }),
       rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order)
         const int b = dK.div(e), kk = e - b * K;
         const float* yp = ws + c.wo.y + ((int64_t)b * K + kk) * p + j;
         float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = q < nU ? yp[q * ys_] : 0.f;
+        for (int q = 0; q < 8; ++q) v[q] = yp[(q < nU ? q : 0) * ys_];
         float yv = 0.f;
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (q < nU) yv += v[q];
+        for (int q = 0; q < 8; ++q) yv += q < nU ? v[q] : 0.f;
         return yv;
       }, [&](int e, float v) { ybuf[e] = v; }),
-      rc_seg<4>(B * K, [&](int e) { return ws[c.wo.w + e]; }, [&](int e, float v) { wrl[e] = v; }),
-      rc_seg<1>(tgt ? B : 0, [&](int b) { return X[((c.row0 + b) * d.T + c.Lmax) * p + j]; },
-                [&](int b, float v) { xt[b] = v; }),
       rc_seg<1>(Q, [&](int e) {  // the nU (<= 8) partials loaded together, summed in slot order
         const float* gp = ws + c.wo.gq + (int64_t)kj * Q + e;
         const int64_t gs_ = (int64_t)K * p * Q;
         float v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = q < nU ? gp[q * gs_] : 0.f;
+        for (int q = 0; q < 8; ++q) v[q] = gp[(q < nU ? q : 0) * gs_];
         float sq = 0.f;
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (q < nU) sq += v[q];
+        for (int q = 0; q < 8; ++q) sq += q < nU ? v[q] : 0.f;
         return sq;
-      }, [&](int e, float v) { sqs[e] = v; }),
-      rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }));
+      }, [&](int e, float v) { sqs[e] = v; }));
   for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
