@@ -13,6 +13,9 @@ namespace {
 
 #define FB_BT 128   // windows per backward tile (the whole batch at B <= 128)
 #define FB_QT 64    // dW0 columns per backward tile
+#ifndef RC_FB_MFMA
+#define RC_FB_MFMA 1  // activation recompute and dW0 tile on v_mfma_f32_16x16x4_f32 (same chains)
+#endif
 
 __device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
   const int L = c.d.L;
@@ -112,6 +115,12 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   // a merged launch, which stages only what its published records need (predictions, embedder
   // outputs, targets, group-norm partials, A column), publishes, and then stages the operands of
   // its own dW0 / Adam work (the embedder workgroups of the launch wait for the K*p leads)
+  // the dW0 tile elements of this thread: (unit u0 + tu + ..., column q0 + tq + ...); with the
+  // matrix-core products (RC_FB_MFMA) a lane holds the 16x16x4 result layout: units
+  // u0 + 4 (lane >> 4) + jj, column q0 + 16 wave + (lane & 15)
+  const int fl15 = tid & 15, flg = (tid >> 4) & 3, fwv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto tile_u = [&](int jj) { return RC_FB_MFMA ? 4 * flg + jj : (tid >> 4); };
+  auto tile_q = [&](int jj) { return RC_FB_MFMA ? 16 * fwv + fl15 : (tid & 15) + 16 * jj; };
   const int tq = tid & 15, tu = tid >> 4;
   const int64_t kjW0 = c.fo.W0 + (int64_t)kj * h * Q;
   float pw[4] = {0.f, 0.f, 0.f, 0.f}, pm[4] = {0.f, 0.f, 0.f, 0.f}, pv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -120,15 +129,14 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const bool split = lead && publish != nullptr;
   auto adam_loads = [&]() {
     if (stepB && !gonly) {  // Adam state of the parameters this thread updates
-      if (u0 + tu < h)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int q = q0 + tq + 16 * jj;
-          if (q < Q) {
-            const int64_t idx = kjW0 + (int64_t)(u0 + tu) * Q + q;
-            pw[jj] = P[idx]; pm[jj] = PM[idx]; pv[jj] = PV[idx];
-          }
+      for (int jj = 0; jj < 4; ++jj) {
+        const int u = u0 + tile_u(jj), q = q0 + tile_q(jj);
+        if (u < h && q < Q) {
+          const int64_t idx = kjW0 + (int64_t)u * Q + q;
+          pw[jj] = P[idx]; pm[jj] = PM[idx]; pv[jj] = PV[idx];
         }
+      }
       if (qc == 0 && tid < FAC_UC && u0 + tid < h) {
         const int64_t ib = c.fo.b0 + (int64_t)kj * h + u0 + tid, iw = c.fo.W1 + (int64_t)kj * h + u0 + tid;
         sb[0] = P[ib]; sb[1] = PM[ib]; sb[2] = PV[ib];
@@ -344,6 +352,28 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const int uu = tid & 15, part = tid >> 4;  // 3a: 16 slices of the batch per hidden unit
   float dW1u = 0.f, db0u = 0.f, db1 = 0.f;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto recompute_a_mfma = [&](int nb) {
+    // a[b][u] = relu(sum_q Xw[b][q] W0[u][q] + b0[u]) as 16x16x4 tiles (rows b, columns u), a
+    // k-ascending fmaf chain per output from 0: the forward's chain, so the same bits; the
+    // columns q >= Q of the last k step are zeros (exact no-ops).  Wave w: window tiles w, w + 4.
+    for (int bt = fwv; bt < (nb + 15) / 16; bt += 4) {
+      f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      const float* xr = Xs + (16 * bt + fl15) * (FB_QT + 1);
+      const float* wr = Wc + fl15 * (FB_QT + 1);
+      for (int k0 = 0; k0 < Q; k0 += 4) {
+        const int k = k0 + flg;
+        const float av = k < Q ? xr[k] : 0.f, bv = k < Q ? wr[k] : 0.f;
+        z = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, z, 0, 0, 0);
+      }
+      const bool uin = u0 + fl15 < h;
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int b = 16 * bt + 4 * flg + reg;
+        if (b < nb) awl[b * (FAC_UC + 1) + fl15] = uin ? fmaxf(z[reg] + bc0[fl15], 0.f) : 0.f;
+      }
+    }
+    __syncthreads();
+  };
   auto recompute_a = [&](int nb) {  // a = relu(Xw W0^T + b0), rc_forward.hip's chain (q ascending)
     // thread: windows {bp, bp + 64} x units 4*uq .. 4*uq+3 (FB_BT = 128 = 2 x 64, FAC_UC = 16 = 4 x 4):
     // 6 LDS reads per 8 fmaf; every output keeps its own chain z = fmaf(x_q, w_q, z), q ascending
@@ -386,7 +416,12 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
           }, [&](int e, float v) { Xs[(e >> 6) * (FB_QT + 1) + (e & 63)] = v; }));
       __syncthreads();
     }
-    if (recompute) recompute_a(nb);
+    if (recompute) {
+      if (RC_FB_MFMA)
+        recompute_a_mfma(nb);
+      else
+        recompute_a(nb);
+    }
     // 3a (column tile 0): output-layer / bias gradients of the chunk's hidden units
     if (qc == 0) {
       const float w1 = w1s[uu];
@@ -406,12 +441,28 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       awl[bb * (FAC_UC + 1) + u] = av > 0.f ? dyl[bt + bb] * w1s[u] : 0.f;
     }
     __syncthreads();
-    // 3b: dW0 tile partial = dZ^T Xw
-#pragma unroll 8
-    for (int bb = 0; bb < nb; ++bb) {
-      const float zv = awl[bb * (FAC_UC + 1) + tu];
+    // 3b: dW0 tile partial = dZ^T Xw, per element an fmaf chain over the windows in order
+    if (RC_FB_MFMA) {
+      // 16x16x4 tiles: rows u (A[u][b] = dZ[b][u]), columns q = 16 wave + l15, k = the windows
+      // (rows >= nb of the last k step are zeros: exact no-ops); the result layout is tile_u /
+      // tile_q's
+      f32x4 a4 = {acc[0], acc[1], acc[2], acc[3]};
+      const float* xc = Xs + 16 * fwv + fl15;
+      for (int k0 = 0; k0 < nb; k0 += 4) {
+        const int b = k0 + flg;
+        const float av = b < nb ? awl[b * (FAC_UC + 1) + fl15] : 0.f;
+        const float bv = b < nb ? xc[b * (FB_QT + 1)] : 0.f;
+        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, a4, 0, 0, 0);
+      }
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) acc[jj] += zv * Xs[bb * (FB_QT + 1) + tq + 16 * jj];
+      for (int jj = 0; jj < 4; ++jj) acc[jj] = a4[jj];
+    } else {
+#pragma unroll 8
+      for (int bb = 0; bb < nb; ++bb) {
+        const float zv = awl[bb * (FAC_UC + 1) + tu];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[jj] += zv * Xs[bb * (FB_QT + 1) + tq + 16 * jj];
+      }
     }
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 21);
@@ -433,12 +484,11 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 22);
   // dW0 tile: + adjacency-L1 term through the group norms, then Adam
-  const int u = u0 + tu;
-  if (u < h) {
+  {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int q = q0 + tq + 16 * jj;
-      if (q >= Q) continue;
+      const int u = u0 + tile_u(jj), q = q0 + tile_q(jj);
+      if (u >= h || q >= Q) continue;
       const int64_t idx = kjW0 + (int64_t)u * Q + q;
       float g = acc[jj];
       if (adj_grad && Gs[q] > 0.f) g += dGs[q] * ((gonly ? P[idx] : pw[jj]) / Gs[q]);
