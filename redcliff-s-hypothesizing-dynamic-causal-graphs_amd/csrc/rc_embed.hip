@@ -18,6 +18,10 @@
 #include "rc_common.h"
 #include "rc_fac_bwd.h"
 
+#ifndef RC_MERGED_LEAD_SPLIT
+#define RC_MERGED_LEAD_SPLIT 1  // k_bwd_merged: the factor leads' update parts as their own workgroups
+#endif
+
 namespace {
 
 // BatchNorm scale/shift exactly as torch's CPU kernel forms them
@@ -891,10 +895,18 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int
     }
     return;
   }
-  // factor workgroups: the K*p leads first (ids [0, K*p)), the rest after the embedder's
-  int kj, uc = 0, qc = 0;
+  // factor workgroups: the K*p leads first (ids [0, K*p)), the rest after the embedder's.  With
+  // a factor step the leads only write their records (the embedder workgroups' inputs) and
+  // publish; the update part of each network's (0, 0) workgroup is K*p more workgroups at the
+  // end, so no workgroup carries both (the longest workgroups of the launch otherwise)
+  const bool lead_split = RC_MERGED_LEAD_SPLIT && (c.flags & RC_STEP_B);
+  int kj, uc = 0, qc = 0, role = RC_FB_ALL;
   if (e < 0) {
     kj = bx;
+    if (lead_split) role = RC_FB_RECORDS;
+  } else if (lead_split && e - nemb >= KP * (nUl * nQ - 1)) {
+    kj = e - nemb - KP * (nUl * nQ - 1);
+    role = RC_FB_UPDATE;
   } else {
     const int f = e - nemb, per = nUl * nQ - 1;
     int rem;
@@ -914,7 +926,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int
     uc = rem / nQ;
     qc = rem - uc * nQ;
   }
-  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, r, sm, e < 0 ? cnt : nullptr);
+  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, r, sm, e < 0 ? cnt : nullptr, role);
 }
 
 // ---- adjacency algebra for p <= 64 in one workgroup, operands in LDS with row stride P = p + 1
@@ -1530,7 +1542,7 @@ int rc_bwd_merged_grid(const StepCtx& c) {
   const int head = (c.flags & RC_CONFUSION) ? 1 : 0;
   const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
   const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
-  const int grid = d.K * d.p * nUl * nQ + nnode + head + nred;
+  const int grid = d.K * d.p * nUl * nQ + nnode + head + nred + (RC_MERGED_LEAD_SPLIT && (c.flags & RC_STEP_B) ? d.K * d.p : 0);
   const size_t le = rc_emb_bwd_lds(d, false), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
   const int occ = rc_bwd_merged_occupancy(le > lf ? le : lf);
   return (int64_t)grid * c.nrep <= (int64_t)occ * cus ? grid : 0;
@@ -1553,7 +1565,7 @@ int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s) {
   const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
   const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
   const int KP = d.K * d.p;
-  const int grid = KP * nUl * nQ + nnode + head + nred;
+  const int grid = KP * nUl * nQ + nnode + head + nred + (RC_MERGED_LEAD_SPLIT && (c.flags & RC_STEP_B) ? KP : 0);
   if (WPB > BC) {
     int e = rc_lds_optin(k_bwd_merged<true>, lds, "k_bwd_merged LDS");
     if (e) return e;
