@@ -518,11 +518,15 @@ class ReplicaPack:
 
 def _eval_modes(models):
     """The module modes every fit epoch ends in (GC tracking + validate_training call .eval() on
-    the embedder and every factor, ...withStateSmoothing.py:1366-1480)."""
+    the embedder and every factor, ...withStateSmoothing.py:1366-1480).  The flags are written
+    directly (Module.train(False) sets exactly this attribute on every submodule; no module of
+    this package overrides train()): torch's recursive .eval() with its __setattr__ per module
+    cost ~110 ms per 128-fit pack (28,800 modules), a fifth of a packed D4IC fit's wall clock."""
     for m in models:
-        m.factor_score_embedder.eval()
-        for f in m.factors:
-            f.eval()
+        for root in (m.factor_score_embedder, *m.factors):
+            for mod in root.modules():
+                if mod.training:
+                    mod.__dict__["training"] = False
 
 
 class _PackBest:

@@ -46,10 +46,19 @@ def main():
     ap.add_argument("--train-batches", type=int, default=8)
     ap.add_argument("--gc-kernel", action="store_true")
     ap.add_argument("--cprofile", action="store_true", help="host-side cProfile of one unwrapped packed fit")
+    ap.add_argument("--torch-eval", action="store_true",
+                    help="comparison: the end-of-fit module modes set with torch's recursive .eval()")
     args = ap.parse_args()
     import redcliff_amd
     from redcliff_amd import fit_loop, replicas
     from redcliff_amd import metrics as M
+    if args.torch_eval:
+        def torch_eval_modes(models):
+            for m in models:
+                m.factor_score_embedder.eval()
+                for f in m.factors:
+                    f.eval()
+        replicas._eval_modes = torch_eval_modes
     c = bench.CONFIGS[args.config]
     B, R, E = c["B"], args.replicas, args.epochs
     ntr, nva = args.train_batches, 2
