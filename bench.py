@@ -652,14 +652,17 @@ def main():
     if world > 1 or args.mode == "dp" or args.dp_leg_batch > 0:
         import torch.distributed as dist
         backend = "nccl" if cuda else "gloo"  # nccl is RCCL on ROCm; gloo only for the CPU plumbing check
+        kw = {}
         if cuda:
             torch.cuda.set_device(local)
+            # bind the communicator to this rank's GPU explicitly (no guessing from the global rank)
+            kw["device_id"] = torch.device("cuda", local)
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", str(_free_port()))
-            dist.init_process_group(backend, rank=0, world_size=1)
+            dist.init_process_group(backend, rank=0, world_size=1, **kw)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **kw)
         seen = dist.get_world_size()
         if seen != world or (args.gpus > 1 and seen != args.gpus):
             raise SystemExit("%s world size %d != --gpus %d / WORLD_SIZE %d" % (backend, seen, args.gpus, world))

@@ -135,6 +135,10 @@ typedef struct RedcliffStepArgs {
 
 int redcliff_abi_version(void);
 const char* redcliff_last_error(void);
+/* Source hash this library was compiled from: the first 16 hex digits of the SHA-256 over
+ * the .hip / .h files of csrc/ and the .h files of include/ (path-sorted, name + contents) and the compile defines
+ * (redcliff_amd/build.py source_hash).  Ties a pushed binary to the committed sources. */
+const char* redcliff_build_id(void);
 
 /* Workspace bytes for one launch of R replicas (all kernels share one layout). */
 size_t redcliff_workspace_bytes(const RedcliffDims* d);

@@ -127,6 +127,14 @@ extern "C" {
 
 int redcliff_abi_version(void) { return REDCLIFF_ABI_VERSION; }
 
+#ifndef REDCLIFF_BUILD_ID
+#define REDCLIFF_BUILD_ID "unknown"
+#endif
+// build.py reads the id back from the file bytes (after the tag) without loading the library
+__attribute__((used)) static const char kBuildTag[] = "REDCLIFF_BUILD_ID=" REDCLIFF_BUILD_ID;
+
+const char* redcliff_build_id(void) { return kBuildTag + sizeof("REDCLIFF_BUILD_ID=") - 1; }
+
 const char* redcliff_last_error(void) { return g_err; }
 
 size_t redcliff_workspace_bytes(const RedcliffDims* d) {

@@ -35,7 +35,7 @@ EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_b
             "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
             "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_dp_update", "redcliff_gemm",
             "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions",
-            "redcliff_gc_track_stats", "redcliff_device_status")
+            "redcliff_gc_track_stats", "redcliff_device_status", "redcliff_build_id")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine", "fac_lead")
 
 
@@ -126,12 +126,36 @@ def lib():
     L.redcliff_device_status.argtypes = [ctypes.POINTER(Dims), _vp, ctypes.POINTER(ctypes.c_uint32), _vp]
     L.redcliff_workspace_regions.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(_i64), ctypes.c_int32]
     for name in EXPORTED[2:]:
-        if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count"):
+        if name not in ("redcliff_workspace_bytes", "redcliff_emb_param_count", "redcliff_fac_param_count",
+                        "redcliff_build_id"):
             getattr(L, name).restype = ctypes.c_int
+    L.redcliff_build_id.restype = ctypes.c_char_p
     if L.redcliff_abi_version() != ABI_VERSION:
         raise ImportError("libredcliff_hip.so ABI %d != %d" % (L.redcliff_abi_version(), ABI_VERSION))
+    want = tree_build_id()
+    got = L.redcliff_build_id().decode()
+    if want is not None and got != want:
+        raise ImportError("libredcliff_hip.so was built from other sources (build id %s, this tree %s); run "
+                          "__graft_entry__.build()" % (got, want))
     _LIB = L
     return L
+
+
+def tree_build_id():
+    """source_hash of the kernel sources next to this package, when the default in-tree library is
+    the one loaded (REDCLIFF_HIP_LIB experiment builds carry their own defines and are not checked);
+    None when the sources are not present."""
+    if os.environ.get("REDCLIFF_HIP_LIB"):
+        return None
+    from . import build as _b
+    if not _b.sources():
+        return None
+    return _b.source_hash()
+
+
+def build_id():
+    """The source hash compiled into the loaded library (redcliff_build_id)."""
+    return lib().redcliff_build_id().decode()
 
 
 def check(rc, what=""):

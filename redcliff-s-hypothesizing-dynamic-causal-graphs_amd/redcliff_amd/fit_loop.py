@@ -465,6 +465,9 @@ class _SavedState:
                 e.opt[g]["t"] = t
         e._sync_steps()
         e.supports_fresh = False
+        # a hand-off timeout the undone epoch logged must not fail a later check: its gradients
+        # were discarded with it (the word is cleared behind the epoch's launches, same stream)
+        e.status_view().zero_()
 
 
 def _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
@@ -641,7 +644,7 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
         raise NotImplementedError("output_length must be 1")
     fused = model.fused_supported()
     eng = model.engine() if fused else None
-    nsup, p = model.num_supervised_factors, model.num_chans
+    nsup = model.num_supervised_factors
     tr = FitTracker(model, GC, deltaConEps, in_degree_coeff, out_degree_coeff, sc_forecast, sc_factor, sc_cos,
                     lookback, check_every)
     iter_start = tr.resume(fused)
@@ -666,8 +669,12 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
         d_train = eng.workspace(max(train["Bmax"] if runner is None else 1, val["Bmax"]), train["T"])
         plans = {}
 
-    dev_metrics = (fused and 2 <= p <= 64 and model.primary_gc_est_mode in (
-        "conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
+    # The device metrics track num_chans-sized graphs of the uncombined estimates; a wavelet model
+    # (num_series = num_chans * (l + 1)) needs the reference's combine_wavelet_representations GC
+    # calls (:1396-1407), so it takes the host loop, which makes them (and fails where they fail).
+    dev_metrics = (fused and model.wavelet_level is None and 2 <= model.num_series <= 64
+                   and model.primary_gc_est_mode in ("conditional_factor_exclusive",
+                                                     "conditional_factor_fixed_embedder"))
     if dev_metrics:
         _device_epochs(model, eng, tr, train, val, d_train, plans, oA, oB, iter_start, max_iter, save_dir, check_every,
                        verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, save_plots, hook, runner=runner,

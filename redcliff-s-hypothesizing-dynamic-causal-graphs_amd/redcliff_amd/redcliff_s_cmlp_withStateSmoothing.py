@@ -395,7 +395,7 @@ class REDCLIFF_S_CMLP_withStateSmoothing(nn.Module):
         dev = self._device()
         try:
             obj = torch.load(path, map_location=dev, weights_only=True)
-        except (pickle.UnpicklingError, RuntimeError, AttributeError) as e:
+        except pickle.UnpicklingError as e:  # disallowed globals; truncated files etc. raise as they are
             if not allow_pickle:
                 raise RuntimeError(
                     "prior_factors_path %s is not a weights-only file (a pickled module?): pass "

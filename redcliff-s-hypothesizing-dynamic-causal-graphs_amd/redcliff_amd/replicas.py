@@ -217,6 +217,8 @@ class ReplicaPack:
         with torch.no_grad():
             for n, t, dim in self._state_tensors():
                 t.index_copy_(dim, idx, self._prev[n].index_select(dim, idx))
+            # hand-off timeouts logged by the undone epoch go with its gradients
+            nat.status_view(self.ws, self.ws_off, self.R).index_fill_(0, idx, 0)
         for r in reps:
             e = self.engines[r]
             for g, t in zip(("A", "B"), steps_before[r]):
@@ -387,10 +389,11 @@ class ReplicaPack:
         train = self.cache_dataset(X_train)
         val = self.cache_dataset(X_val)
         self._workspace(max(int(train["Bmax"]), int(val["Bmax"]), 1), train["T"])
-        dev_metrics = 2 <= p <= 64 and m0.primary_gc_est_mode in ("conditional_factor_exclusive",
-                                                                   "conditional_factor_fixed_embedder")
+        dev_metrics = (m0.wavelet_level is None and 2 <= p <= 64
+                       and m0.primary_gc_est_mode in ("conditional_factor_exclusive", "conditional_factor_fixed_embedder"))
         if not dev_metrics:
-            raise NotImplementedError("packed fits track GC progress on the device (2 <= p <= 64, conditional modes)")
+            raise NotImplementedError("packed fits track GC progress on the device (no wavelet_level, 2 <= p <= 64, "
+                                      "conditional modes); fit these models one by one")
         best = _PackBest(self)
         active = list(range(R))
         nfirst = min(int(val["sizes"][0]), m0.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING)

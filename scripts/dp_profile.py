@@ -31,7 +31,7 @@ def main():
     os.environ.setdefault("MASTER_PORT", str(bench._free_port()))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     c = dict(bench.CONFIGS[args.config], B=args.batch)
     B = c["B"]
     model = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).to(dev)

@@ -56,6 +56,17 @@ def test_native_library_is_the_compute_path():
     assert os.path.basename(nat.LIB_PATH) in maps
 
 
+def test_loaded_library_was_built_from_this_tree():
+    """The binary this GPU process runs is the one compiled from the committed sources: its
+    embedded build id (redcliff_build_id) equals the hash of csrc/ + include/ on this box."""
+    from redcliff_amd import _native as nat
+    from redcliff_amd import build as b
+    assert not os.environ.get("REDCLIFF_HIP_LIB"), "experiment library selected"
+    assert nat.build_id() == b.source_hash()
+    maps = open("/proc/self/maps").read()
+    assert os.path.realpath(b.LIB) in maps
+
+
 @pytest.mark.parametrize("name", FUSED_SCENARIOS)
 def test_batch_update_schedule_matches_reference(name):
     d, meta = load(name)

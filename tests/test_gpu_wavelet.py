@@ -64,3 +64,23 @@ def test_wavelet_batch_update_schedule(name):
     vals = m.validate_training(bs, 1, m.num_series, *hist)
     for n_, v in zip(["forecast", "factor", "cos", "fw_l1", "smooth", "adj"], vals):
         assert_close("val/" + n_, v, d["val/" + n_], 1e-4, 1e-6)
+
+
+def test_dgcnn_wavelet_fit_fails_where_the_reference_fails():
+    """The reference's fit tracks GC progress with GC(..., ignore_lag=True,
+    combine_wavelet_representations=True) (...withStateSmoothing.py:1396-1407); for a DGCNN
+    wavelet model that call trips the model's size(0) == num_series assertion (the golden
+    '/err' keys record it).  The fit here makes the same call after the first training epoch
+    (it takes the host metrics loop for wavelet models) and fails the same way, instead of
+    tracking uncombined num_series graphs against num_chans-sized true graphs."""
+    d, meta = load("dgcnn_wavelet")
+    mode = meta["gc_mode"]
+    if "eval/gc/%s/ign1/comb1/rank0/err" % mode not in d.files:
+        pytest.skip("the reference's combined lag-free GC works for this scenario")
+    m = build(meta)
+    oA, oB = make_opts(m, meta["lrA"], meta["lrB"])
+    bs = batches(d, meta)
+    p = meta["p"]
+    true_gc = [np.eye(p)[:, :, None].repeat(meta["L"], 2) for _ in range(meta["K"])]
+    with pytest.raises(AssertionError):
+        m.fit(None, bs, oA, oB, meta["L"], 1, 1, 2, bs, lookback=1, check_every=1, verbose=0, GC=true_gc)

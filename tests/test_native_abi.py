@@ -90,3 +90,17 @@ def test_train_step_rejects_null_arguments():
     a.B = 16
     rc = L.redcliff_train_step(ctypes.byref(a), None)
     assert rc == -1 and b"null" in L.redcliff_last_error()
+
+
+def test_build_id_matches_committed_sources():
+    """The library carries the hash of the sources it was compiled from (redcliff_build_id), and
+    build() treats a library as current only when that hash equals the tree's (not by mtime)."""
+    from redcliff_amd import _native as nat
+    from redcliff_amd import build as b
+    want = b.source_hash()
+    assert re.fullmatch(r"[0-9a-f]{16}", want)
+    assert b.embedded_id(b.LIB) == want
+    assert nat.build_id() == want
+    assert not b._stale(b.LIB)
+    # a define changes the id (experiment variants never pass for the product library)
+    assert b.source_hash(["-DRC_TRACE"]) != want
