@@ -330,7 +330,11 @@ def pmc_traffic(kernel_name, cfg):
 
 # --------------------------------------------------------------------------- timing helpers
 def timed(fn, dist, dev):
-    """fn() bracketed by barrier + synchronize on both sides; max over ranks."""
+    """fn() bracketed by barrier + synchronize on both sides; max over ranks.  A one-rank group
+    has nobody to wait for: its barrier (an RCCL launch and a host round trip, ~2 us per step of a
+    20-step region, profiles/r04_steady_state_a.log) is skipped."""
+    if dist is not None and dist.get_world_size() == 1:
+        dist = None
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -347,6 +351,21 @@ def timed(fn, dist, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
+
+
+def preheat(plan, start, seconds):
+    """Untimed steps, after the W warm-up steps, until the device has been busy for `seconds`: a
+    GPU that idled through the host-side setup runs its first timed region ~7 % slower than the
+    next one (clock ramp; profiles/r04_steady_state_a.log: 20-step regions 0.0651 -> 0.0610 ->
+    0.0605 ms per step, 300 steps 0.0586).  Returns the number of extra steps."""
+    if seconds <= 0:
+        return 0
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        plan(20, start + n).run()
+        torch.cuda.synchronize()
+        n += 20
+    return n
 
 
 def single_fit(c, args, dev, rank, nbatch=32):
@@ -448,7 +467,8 @@ def mode_fit(args, dev, rank, world, dist):
     B = c["B"]
     eng, plan = single_fit(c, args, dev, rank)
     plan(args.warmup, 0).run()
-    p_timed = plan(args.steps, args.warmup)
+    extra = preheat(plan, args.warmup, args.preheat_s)
+    p_timed = plan(args.steps, args.warmup + extra)
     elapsed = timed(p_timed.run, dist, dev)
     value = world * args.steps * B / elapsed
 
@@ -456,6 +476,9 @@ def mode_fit(args, dev, rank, world, dist):
            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
            "data": "synthetic (D4IC/sVAR-shaped windows; datasets not in image)",
+           "preheat": {"seconds": args.preheat_s, "extra_untimed_steps": extra,
+                       "note": "untimed steps after the W warm-up steps until the device has been busy this long "
+                               "(clock ramp after the host-side setup); the timed region is exactly `steps` steps"},
            "config": {"workload": c["workload"], "global_batch": B * world, "windows_per_step_per_gpu": B,
                       "parallelism": "replicas%d (one independent fit per GPU, no collective)" % world,
                       "ranks": world, "flops_per_window": flops_per_window(c)["total"]}}
@@ -496,8 +519,9 @@ def mode_fit(args, dev, rank, world, dist):
         cn = CONFIGS["c1k4"]
         _, nplan = single_fit(cn, args, dev, rank)
         nplan(args.warmup, 0).run()
+        nextra = preheat(nplan, args.warmup, args.preheat_s)
         nsteps = max(args.steps, 50)
-        nel = timed(nplan(nsteps, args.warmup).run, None, dev)
+        nel = timed(nplan(nsteps, args.warmup + nextra).run, None, dev)
         ns = {"workload": cn["workload"], "windows_per_s": round(nsteps * cn["B"] / nel, 1),
               "ms_per_step": round(1e3 * nel / nsteps, 4), "steps": nsteps, "target_gpu_over_cpu": 50.0}
 
@@ -623,6 +647,8 @@ def main():
     ap.add_argument("--mode", default="fit", choices=("fit", "dp"))
     ap.add_argument("--config", default="d4ic", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--preheat-s", type=float, default=0.3,
+                    help="untimed device-busy seconds after the warm-up steps (0: none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-north-star", action="store_true")

@@ -37,7 +37,7 @@ struct WsOff {
   int64_t gfc1;   // [M1][p*H]         fc1 weight gradient (combined by the node blocks)
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
-  int64_t dWi;    // [p][n][F][H]      graph-conv weight gradient partials (per node)
+  int64_t dWi;    // [max(p, Bmax/16)][n][F][H] graph-conv weight gradient partials (per node / tile)
   int64_t dS;     // [p][nch][n][p]    gradient wrt Chebyshev supports (row c, partial per column chunk)
   int64_t dgb;    // [p][nch][2][F]    BatchNorm affine gradient partials (per node and chunk)
   int64_t S;      // [n][p][p]         supports (S_0 = I)
@@ -187,7 +187,8 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.gfc1, (int64_t)d.M1 * p * d.H);
   put(o.dwp, p * B * K);
   put(o.dAadj, K * p * p);
-  put(o.dWi, p * d.n * d.F * d.H);
+  // per-node slices (node-chunk / GEMM paths) or per-16-window-tile records (rc_embed_batched.hip)
+  put(o.dWi, (p > (B + 15) / 16 ? p : (B + 15) / 16) * d.n * d.F * d.H);
   put(o.dS, (rc_nchunk(d) > 64 ? rc_nchunk(d) : 64) * d.n * p * p);
   put(o.dgb, (p * rc_nchunk(d) > 64 ? p * rc_nchunk(d) : 64) * 2 * d.F);
   put(o.S, d.n * p * p);
@@ -248,8 +249,9 @@ struct StepCtx {
   int* conf;
   float *gE, *gF;  // RC_GRAD_ONLY gradient outputs (emb / fac layouts)
   // layout of the embedder-backward partials the final kernel reduces (node-chunk kernel vs GEMM path):
-  // dS_i[cc][c'] = sum_s ws.dS[cc*dsCC + s*dsS + i*dsI + c'], s < dsN;  BN affine: ws.dgb[s][2][F], s < dgN
-  int dsN, dgN;
+  // dS_i[cc][c'] = sum_s ws.dS[cc*dsCC + s*dsS + i*dsI + c'], s < dsN;  BN affine: ws.dgb[s][2][F], s < dgN;
+  // graph-conv weights: dW_i = sum_s ws.dWi[s][n][F][H], s < dwN (p node slices, or 1: rc_embed_batched.hip)
+  int dsN, dgN, dwN;
   int64_t dsCC, dsS, dsI;
   // matrix-core factor path: y / group-norm partial slots the forward writes (rc_fac_slots)
   int fslots;
@@ -532,9 +534,43 @@ __device__ inline void rc_update(const StepCtx& c, float* P, float* M, float* V,
   P[idx] = pp; M[idx] = mm; V[idx] = vv;
 }
 
+// dL/d(raw embedder output w[b][k]) from the factor side's dL/dw (gw, channel partials summed by
+// the caller) and the batch_update loss terms on the embedder output (...withStateSmoothing.py:
+// 633-666): the factor-score MSE against label y on the first nsup columns (mean over B_global *
+// nsup), the fw-L1 sign, both through the optional sigmoid restriction (:383-386).
+__device__ inline float rc_emb_draw(const StepCtx& c, int r, int k, float raw, float gw, float y) {
+  const RedcliffDims& d = c.d;
+  const int K = d.K, nsup = d.nsup;
+  const RedcliffReplicaHyper& hy = c.hyp[r];
+  const bool sig = d.use_sigmoid;
+  const float ecc = d.sigmoid_ecc;
+  const int ncol = nsup > 0 ? nsup : K;
+  const float weff = sig ? rc_sigmoid(ecc * raw) : raw;
+  float graw = sig ? gw * ecc * weff * (1.f - weff) : gw;
+  if (k < ncol) {
+    const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
+    float gsl = 0.f;
+    if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) gsl += hy.c_factor * (2.f / (float)(c.Bg * nsup)) * (sl - y);
+    if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
+    if (nsup > 0)
+      graw += sig ? gsl * sl * (1.f - sl) : gsl;
+    else
+      graw += sig ? gsl * ecc * weff * (1.f - weff) : gsl;
+  }
+  return graw;
+}
+
 // Shared host-side helpers (defined in rc_capi.hip).
 void rc_set_error(const char* fmt, ...);
 int rc_check(hipError_t e, const char* what);
+
+// Dynamic LDS above 64 KiB (up to the CU's 160 KiB) must be opted into per kernel.
+template <class Kern>
+inline int rc_lds_optin(Kern k, size_t bytes, const char* what) {
+  if (bytes <= RC_LDS_LIMIT_FLOATS * sizeof(float)) return 0;
+  return rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)bytes), what);
+}
 
 // Launchers implemented in the kernel translation units.
 // embedder forward and / or vector-path factor forward in one launch (rc_forward.hip)
@@ -567,6 +603,10 @@ int rc_launch_cos_values(const StepCtx& c, hipStream_t s);  // per-window cos-si
 int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);
+bool rc_emb_use_batched(const RedcliffDims& d);   // rc_embed_batched.hip
+int rc_launch_emb_fwd_batched(const StepCtx& c, hipStream_t s);
+int rc_launch_emb_bwd_batched(const StepCtx& c, hipStream_t s);
+int rc_emb_batched_slots(int B);
 int rc_fac_slots(const RedcliffDims& d);  // rc_factor_mfma.hip
 void rc_emb_partial_layout(StepCtx& c, bool gemm);
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);

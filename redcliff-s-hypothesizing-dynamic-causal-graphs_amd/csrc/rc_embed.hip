@@ -1208,7 +1208,7 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
       }
     } else if (e < nFH) {
 #pragma unroll 8
-      for (int cc = 0; cc < p; ++cc) g += ldr(ws + c.wo.dWi + (int64_t)cc * nFH + e);
+      for (int cc = 0; cc < c.dwN; ++cc) g += ldr(ws + c.wo.dWi + (int64_t)cc * nFH + e);
       idx = c.eo.gcW + e;
     } else if (e < nFH + nfc) {
       const int q = e - nFH;
@@ -1464,13 +1464,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_bn_stats(RedcliffDims d, const flo
 
 // ------------------------------------------------------------------------------------------
 // host launchers
-// Dynamic LDS above 64 KiB (up to the CU's 160 KiB) must be opted into per kernel.
-template <class Kern>
-static int rc_lds_optin(Kern k, size_t bytes, const char* what) {
-  if (bytes <= RC_LDS_LIMIT_FLOATS * sizeof(float)) return 0;
-  return rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)bytes), what);
-}
 
 size_t rc_emb_bwd_lds(const RedcliffDims& d, bool late) {
   const size_t head = 32 + (size_t)d.nsup * d.nsup;

@@ -110,30 +110,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   if (lane < K) ws[c.wo.w + (int64_t)b * K + lane] = a + E[c.eo.fc2b + lane];
 }
 
-// dL/d(raw embedder output) (the same rule as the node-chunk kernel, rc_embed.hip), dL/df1,
-// and the fc2 weight / fc2 bias / fc1 bias gradients.  grid (1, R): one workgroup per replica.
-__device__ inline float lemb_draw(const StepCtx& c, int r, int k, float raw, float gw, float y) {
-  const RedcliffDims& d = c.d;
-  const int K = d.K, nsup = d.nsup;
-  const RedcliffReplicaHyper& hy = c.hyp[r];
-  const bool sig = d.use_sigmoid;
-  const float ecc = d.sigmoid_ecc;
-  const int ncol = nsup > 0 ? nsup : K;
-  const float weff = sig ? rc_sigmoid(ecc * raw) : raw;
-  float graw = sig ? gw * ecc * weff * (1.f - weff) : gw;
-  if (k < ncol) {
-    const float sl = nsup > 0 ? (sig ? rc_sigmoid(raw) : raw) : weff;
-    float gsl = 0.f;
-    if ((c.flags & RC_LOSS_FACTOR) && nsup > 0) gsl += hy.c_factor * (2.f / (float)(c.Bg * nsup)) * (sl - y);
-    if (c.flags & RC_LOSS_FWL1) gsl += hy.c_fwl1 * rc_sign(sl);
-    if (nsup > 0)
-      graw += sig ? gsl * sl * (1.f - sl) : gsl;
-    else
-      graw += sig ? gsl * ecc * weff * (1.f - weff) : gsl;
-  }
-  return graw;
-}
-
 // grid (ceil(B / WPW), R), WPW = 64 / K windows per workgroup: lanes (item = (window, k), g),
 // g sums every 4th channel partial of the factor-side dL/dw (all loads in flight); then dL/df1
 // of the workgroup's windows.  dr -> ws.edr, df1 -> ws.edf1.
@@ -164,7 +140,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   t += __shfl_xor(t, 2);
   if (ok && g == 0) {
     const float y = lab_on ? c.lab[r * c.labr + (c.row0 + b) * K + k] : 0.f;
-    const float v = lemb_draw(c, r, k, ws[c.wo.w + (int64_t)b * K + k], t, y);
+    const float v = rc_emb_draw(c, r, k, ws[c.wo.w + (int64_t)b * K + k], t, y);
     drs[item] = v;
     ws[c.wo.edr + (int64_t)b * K + k] = v;
   }
@@ -503,7 +479,7 @@ int ds_splits(int B) {
 #endif
 bool rc_emb_use_gemm(const RedcliffDims& d) {
   const char* v = getenv("REDCLIFF_EMB_PATH");  // read per call: tests switch paths in-process
-  if (v && !strcmp(v, "gemm")) return d.F <= 64;
+  if (v && (!strcmp(v, "gemm") || !strcmp(v, "batched"))) return d.F <= 64 && d.M1 <= 64;
   if (v && !strcmp(v, "fused")) return false;
   return (d.p >= 32 || d.R >= RC_EMB_GEMM_R) && d.F <= 64 && d.M1 <= 64;
 }
@@ -519,6 +495,14 @@ static int lemb_win_step(const StepCtx& c) {
 void rc_emb_partial_layout(StepCtx& c, bool gemm) {
   const RedcliffDims& d = c.d;
   const int nch = rc_nchunk(d), n = d.n, p = d.p;
+  c.dwN = p;
+  if (gemm && rc_emb_use_batched(d)) {  // one record of each per 16-window tile (rc_embed_batched.hip)
+    c.dsN = c.dgN = c.dwN = rc_emb_batched_slots(c.B);
+    c.dsCC = p;
+    c.dsS = (int64_t)n * p * p;
+    c.dsI = (int64_t)p * p;
+    return;
+  }
   const int wb = gemm ? lemb_win_step(c) : 0;
   if (wb) {  // k_lemb_win_bwd: one dS / BN record [s][i][cc][c'] / [s][2][F] per window group
     c.dsN = c.dgN = (c.B + wb - 1) / wb;
@@ -546,6 +530,7 @@ void rc_emb_partial_layout(StepCtx& c, bool gemm) {
 // output keeps the in-order fmaf chain of the one-replica launch, so packed and single fits agree
 // bit for bit.
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
+  if (rc_emb_use_batched(c.d)) return rc_launch_emb_fwd_batched(c, s);
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F;
@@ -588,6 +573,7 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
 }
 
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
+  if (rc_emb_use_batched(c.d)) return rc_launch_emb_bwd_batched(c, s);
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F, pH = (int64_t)p * H;

@@ -678,8 +678,13 @@ __global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(NBW ==
 // ------------------------------------------------------------------------------------------
 // Short contractions (p*L <= 64, mf_recompute; the D4IC grid): layer 0 forward and backward on
 // v_mfma_f32_16x16x4_f32 with 16-UNIT blocks (h = 100 pads to 112 units, not 128).  A workgroup
-// stages its replica's batch of windows ONCE in LDS, straight from X (Xs[b][c*L + t], row stride
-// S = Qp16 + 4 so the operand reads below are bank-conflict free; no k_xwin, no Xw round trip),
+// stages its replica's batch of windows ONCE in LDS, straight from X (no k_xwin, no Xw round trip):
+// window b's columns q = c*L + t start at b*S + ms_sh(b), row stride S = Qp16 + 4 (S = 4 mod 16)
+// plus a 2-float shift of rows 8..15 of every 16, so that both operand reads below are
+// bank-conflict free (ds_read_b32: lanes 0-31 and 32-63 each hit 32 distinct banks) -- the
+// recompute / forward read rows l15 x columns (g, g + 4s) (rows l15 and l15 + 8 would share banks
+// without the shift), the dW0 product rows 4g + reg x 16 consecutive columns (4S = 16 mod 32 puts
+// g and g + 1 on opposite bank halves);
 // then each wave works through `bpw` 16-unit blocks cb = bx * 4 bpw + 4 i + w with no further
 // barrier.  Lane l: l15 = l & 15, group g = l >> 4; D rows 4 g + reg, column l15.
 //
@@ -705,10 +710,21 @@ __host__ __device__ inline int ms_nk4(const RedcliffDims& d) { return (d.p * d.L
 // networks the 4*bpw consecutive blocks of one workgroup can touch
 __host__ __device__ inline int ms_nnet(int bpw, int nU) { return (4 * bpw - 1) / nU + 2; }
 // per-wave LDS of the backward: the weight / gradient tile (64 NK4 floats) + dL/dG and G rows
-__host__ __device__ inline int ms_wave_floats(int nk4) { return 64 * nk4 + 128; }
+// The wave-private weight / gradient tile: 16 rows of Q floats at row stride ms_qs(Q) = Q + 2..9 with
+// ms_qs = 4 mod 8 and the same 2-float shift of rows 8..15, so the operand read (rows l15, columns
+// g + 4s) and the gradient write (rows 4g + reg, 16 consecutive columns) are conflict-free like Xs;
+// the lane-linear store / epilogue read cross rows with at most a few 2-way conflicts.
+#ifndef RC_MS_TILE_PAD
+#define RC_MS_TILE_PAD 0
+#endif
+constexpr bool kMsTilePad = RC_MS_TILE_PAD;  // 0: the round-3 linear tile (row stride Q), for A/B
+__host__ __device__ inline int ms_qs(int Q) { return Q + 2 + ((2 - Q) & 7); }
+__host__ __device__ inline int ms_sh(int row) { return ((row >> 3) & 1) << 1; }
+__host__ __device__ inline int ms_tile_floats(int nk4) { return 64 * nk4 + 160; }  // >= 16 ms_qs(Q) + 2, Q <= 4 nk4
+__host__ __device__ inline int ms_wave_floats(int nk4) { return ms_tile_floats(nk4) + 128; }
 inline size_t ms_lds(const RedcliffDims& d, int B) { return sizeof(float) * (size_t)ms_rows(B) * (ms_qp16(d) + 4); }
 inline size_t ms_lds_fwd(const RedcliffDims& d, int B) {
-  return ms_lds(d, B) + sizeof(float) * 4 * (size_t)64 * ms_nk4(d);
+  return ms_lds(d, B) + sizeof(float) * 4 * (size_t)ms_tile_floats(ms_nk4(d));
 }
 inline size_t ms_lds_bwd(const RedcliffDims& d, int B, int bpw) {
   return ms_lds(d, B) + sizeof(float) * ((size_t)ms_rows(B) * ms_nnet(bpw, (d.h + 15) >> 4) + 4 * (size_t)ms_wave_floats(ms_nk4(d)));
@@ -724,12 +740,12 @@ __device__ inline void ms_stage_x(const StepCtx& c, int r, float* Xs) {
     return src[(int64_t)b * d.T * p + (e - b * Q)];
   }, [&](int e, float v) {
     const int b = dQ.div(e), k = e - b * Q, t = dp.div(k), ch = k - t * p;
-    Xs[b * S + ch * L + t] = v;
+    Xs[b * S + ms_sh(b) + ch * L + t] = v;
   });
   const int pad = Qp16 - Q;  // zero columns [Q, Qp16) of the batch rows and all of rows [B, rows)
   for (int e = threadIdx.x; e < B * pad; e += RC_BLOCK) {
     const int b = e / pad;
-    Xs[b * S + Q + (e - b * pad)] = 0.f;
+    Xs[b * S + ms_sh(b) + Q + (e - b * pad)] = 0.f;
   }
   for (int e = B * S + threadIdx.x; e < rows * S; e += RC_BLOCK) Xs[e] = 0.f;
 }
@@ -773,12 +789,46 @@ __device__ inline void ms_load_tile(__amdgpu_buffer_rsrc_t r, int lane, float (&
 #pragma unroll
   for (int k = 0; k < NK4; ++k) t[k] = ms_ld(r, 4 * (lane + 64 * k));
 }
+// Walk over the lane-linear elements e = lane + 64 k of a block's run: row e / Q, column e % Q,
+// advanced incrementally (two live integers, not one address per k); addr() is the tile address
+// (-1 for rows past 15, which hold only elements past the run -- never operands)
+// The start (lane / Q, lane % Q) goes through an empty asm statement, so the compiler cannot hoist
+// the NK4 addresses out of the block loop into NK4 live registers (that cost the backward a wave).
+struct MsTileWalk {
+  int rw, cl;
+  const int Q, Qs, dr, dc;
+  __device__ MsTileWalk(int rw0, int cl0, int Q_, int Qs_) : rw(rw0), cl(cl0), Q(Q_), Qs(Qs_), dr(64 / Q_), dc(64 % Q_) {
+    asm volatile("" : "+v"(rw), "+v"(cl));
+  }
+  __device__ inline int addr() const { return rw < 16 ? rw * Qs + ms_sh(rw) + cl : -1; }
+  __device__ inline void next() {
+    cl += dc;
+    rw += dr;
+    if (cl >= Q) {
+      cl -= Q;
+      ++rw;
+    }
+  }
+};
 // ... through the wave's LDS tile into the MFMA operand layout: w[s] = W0[u0 + l15][4 s + g]
 template <int NK4>
 __device__ inline void ms_tile_operands(float* Wt, const float (&t)[NK4], int lane, int l15, int g, int Q, float (&w)[NK4]) {
+  const float* row;
+  if constexpr (kMsTilePad) {
+    const int Qs = ms_qs(Q);
+    MsTileWalk tw(lane / Q, lane % Q, Q, Qs);
 #pragma unroll
-  for (int k = 0; k < NK4; ++k) Wt[lane + 64 * k] = t[k];
-  const float* row = Wt + l15 * Q + g;
+    for (int k = 0; k < NK4; ++k) {
+      const int a = tw.addr();
+      if (a >= 0) Wt[a] = t[k];
+      tw.next();
+    }
+    row = Wt + l15 * Qs + ms_sh(l15) + g;
+  } else {
+#pragma unroll
+    for (int k = 0; k < NK4; ++k) Wt[lane + 64 * k] = t[k];
+    row = Wt + l15 * Q + g;
+  }
 #pragma unroll
   for (int s = 0; s < NK4; ++s) {
     const float v = row[4 * s];
@@ -804,7 +854,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
   __syncthreads();
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  float* Wt = Xs + rows * S + wv * 64 * NK4;
+  float* Wt = Xs + rows * S + wv * ms_tile_floats(NK4);
   const int cbase = (int)blockIdx.x * 4 * bpw + wv;
   // lane offsets of the stores: y of window column l15 (group 0), the W1 snapshot of unit l15
   // (group 0), the group norms of k-step l15 (q = 4 l15 + g)
@@ -853,7 +903,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
     const auto rY = ms_rsrc(ws + c.wo.y + (int64_t)ub * d.Bmax * KP + k * p + j, B * KP);
     for (int t0 = 0; t0 < B; t0 += 32) {
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-      const float* x0 = Xs + (t0 + l15) * S + g;
+      const float* x0 = Xs + (t0 + l15) * S + ms_sh(l15) + g;
       const float* x1 = x0 + 16 * S;
 #pragma unroll
       for (int s = 0; s < NK4; ++s) {
@@ -924,7 +974,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   float* Wt = Dys + ms_nnet(bpw, nU) * rows + wv * ms_wave_floats(NK4);  // weight, then gradient tile
-  float* Dg = Wt + 64 * NK4;  // dL/dG row of the network (adjacency L1), then its group norms G
+  float* Dg = Wt + ms_tile_floats(NK4);  // dL/dG row of the network (adjacency L1), then its group norms G
   float* Gn = Dg + 64;
   const int u_off = g == 0 ? 4 * l15 : MS_OOB;  // output-layer updates: group 0, unit l15
   // lane-linear epilogue elements e = lane + 64 k of the block's run: column q = e % Q
@@ -974,7 +1024,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
     // with zero dL/dy, which add exact zeros, and the tile pairs run to a multiple of 32 <= rows
     for (int t0 = 0; t0 < B; t0 += 32) {
       f32x4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      const float* xr = Xs + (t0 + l15) * S + g;
+      const float* xr = Xs + (t0 + l15) * S + ms_sh(l15) + g;
 #pragma unroll
       for (int s = 0; s < NK4; ++s) {
         z[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * s], wB[s], z[0], 0, 0, 0);
@@ -997,7 +1047,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
       }
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt) {
-        const float* xq = Xs + (t0 + 16 * tt + 4 * g) * S + l15;
+        const float* xq = Xs + (t0 + 16 * tt + 4 * g) * S + ms_sh(4 * g) + l15;  // rows 4g + reg: shift of row 4g
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg)
 #pragma unroll
@@ -1023,17 +1073,19 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
         ms_st(rVw, u_off, sb[5]);
       }
     }
-    // ---- gradient tile (row stride Q) into the wave's LDS tile: the weight operands were read
+    // ---- gradient tile (the tile layout) into the wave's LDS tile: the weight operands were read
     // from it before the tile loop; the pre-update weights stay in cur.wt
     Dg[lane] = dgv;
     Gn[lane] = gnv;
+    const int Qs = kMsTilePad ? ms_qs(Q) : Q, sh4g = kMsTilePad ? ms_sh(4 * g) : 0;
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt) {
       const int q = 16 * qt + l15;
       if (qt + 1 < NQT || q < Q)
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) Wt[(4 * g + reg) * Q + q] = acc[qt][reg];
+        for (int reg = 0; reg < 4; ++reg) Wt[(4 * g + reg) * Qs + sh4g + q] = acc[qt][reg];
     }
+    MsTileWalk tw(lane / Q, lane % Q, Q, Qs);
     // ---- epilogue, lane-linear: + the adjacency term through the group norms, then Adam (or the
     // gradient); elements past the block's run are computed on zeros and their stores dropped
     const auto rM = ms_rsrc(PMr + wofs, nu * Q), rV = ms_rsrc(PVr + wofs, nu * Q), rG = ms_rsrc(GF + wofs, nu * Q);
@@ -1041,7 +1093,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
 #pragma unroll
     for (int k = 0; k < NK4; ++k) {
       const int e = lane + 64 * k;  // gradient tile element (row e / Q, column q = e % Q)
-      float gr = Wt[e];
+      float gr;
+      if constexpr (kMsTilePad) {
+        const int ta = tw.addr();
+        tw.next();
+        gr = Wt[ta >= 0 ? ta : 0];  // rows past 15: past the run, the stores are dropped
+      } else {
+        gr = Wt[e];
+      }
       const float dg = Dg[q], gn = Gn[q], pw = cur.wt[k];
       if (adj_grad && gn > 0.f) gr += dg * (pw / gn);
       if (!adam) {

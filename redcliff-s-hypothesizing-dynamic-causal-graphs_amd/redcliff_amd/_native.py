@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", os.path.join(_HERE, "lib", "libredcliff_hip.so"))
+DEFAULT_LIB_PATH = os.path.join(_HERE, "lib", "libredcliff_hip.so")
+LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", DEFAULT_LIB_PATH)
 ABI_VERSION = 7
 
 # RC_* step flags (include/redcliff_hip.h)
@@ -143,9 +144,10 @@ def lib():
 
 def tree_build_id():
     """source_hash of the kernel sources next to this package, when the default in-tree library is
-    the one loaded (REDCLIFF_HIP_LIB experiment builds carry their own defines and are not checked);
+    the one loaded (REDCLIFF_HIP_LIB experiment builds and the trace / diagnostic variants carry
+    their own defines and are not checked);
     None when the sources are not present."""
-    if os.environ.get("REDCLIFF_HIP_LIB"):
+    if os.environ.get("REDCLIFF_HIP_LIB") or os.path.abspath(LIB_PATH) != os.path.abspath(DEFAULT_LIB_PATH):
         return None
     from . import build as _b
     if not _b.sources():

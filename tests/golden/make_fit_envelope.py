@@ -1,0 +1,204 @@
+"""The reference's own fp32 spread around a fit fixture (build container only).
+
+    python tests/golden/make_fit_envelope.py run <scenario> <j>     # one realization -> tests/golden/_env/
+    python tests/golden/make_fit_envelope.py merge <scenario> [J]   # realizations 0..J-1 -> tests/golden/<scenario>_envelope.npz
+
+A REALIZATION is the reference's own ``fit`` (models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647)
+on the fixture's model and windows with the rows of every training batch in a different order
+(a fixed permutation per batch, drawn from RandomState(1000 + j), the same every epoch).  The
+mathematics is unchanged -- every batch term is a mean or a sum over its windows, the BatchNorm
+statistics are moments of the same windows, the confusion matrix counts the same pairs -- only
+the fp32 rounding order of torch's CPU reductions over the window axis changes.  So the
+realizations span the spread that fp32 rounding order alone produces around the fixture's
+trajectory, which is what a correct GPU fit (fixed-order reductions of its own) must stay within.
+
+Each realization records, for the fit and for the reference-style resume from the fixture's
+mid-fit checkpoint (fresh optimizers, :209-251, redcliff_s_cmlp.py:245):
+  * the loss histories (HIST_KEYS), best_it, best_loss, the stopping epoch, the fit's return;
+  * the final state_dict.
+Realization 0 keeps the fixture's order but runs torch on one CPU thread where make_fit_golden.py
+used eight: torch's CPU reductions split their work by thread, so that alone changes the last bits
+of the trajectory (measured: 1 ulp in one C1 loss entry) -- another realization of the same
+mathematics, checked to stay within 1e-3 of the fixture as a sanity check of this script.  ``merge`` writes, per
+history key and per state tensor, the realizations' values (histories) and the elementwise
+maximum deviation from the fixture over the realizations (states), each realization's count of
+state entries outside the fixed tolerance, and its leave-one-out count: the entries where it
+leaves max(tolerance, the other realizations' deviation) -- what tests/test_gpu_fit_golden.py
+allows the GPU fit, as one more realization of the same mathematics.
+
+The validation windows are never permuted (GC tracking uses the first validation batch's
+first samples).  Only arrays and JSON leave the script.
+"""
+import json
+import os
+import pickle
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import make_fit_golden as G  # noqa: E402  (imports the reference through oracle/ref_import.py)
+
+OUT = os.path.join(HERE, "_env")
+
+
+def _load(name):
+    d = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)
+    return d, json.loads(str(d["meta"]))
+
+
+def _batches(X, Y, B, j):
+    out = []
+    rng = np.random.RandomState(1000 + j)
+    for i in range(0, len(X), B):
+        xb, yb = X[i:i + B], Y[i:i + B]
+        if j > 0:
+            perm = rng.permutation(len(xb))
+            xb, yb = xb[perm], yb[perm]
+        out.append((torch.from_numpy(np.ascontiguousarray(xb)), torch.from_numpy(np.ascontiguousarray(yb))))
+    return out
+
+
+def _opts(m, cfg):
+    return (torch.optim.Adam(m.gen_model[0].parameters(), lr=cfg["lrA"], betas=(0.9, 0.999), eps=1e-4,
+                             weight_decay=1e-4),
+            torch.optim.Adam(m.gen_model[1].parameters(), lr=cfg["lrB"], betas=(0.9, 0.999), eps=1e-4,
+                             weight_decay=1e-4))
+
+
+def _fit_kw(cfg, true_gc):
+    return dict(lookback=cfg["lookback"], check_every=cfg["check_every"], verbose=0, GC=true_gc, deltaConEps=0.1,
+                in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=10.,
+                stopping_criteria_factor_coeff=100., stopping_criteria_cosSim_coeff=1.)
+
+
+def _record(prefix, loc, ret, m, out):
+    for k in G.HIST_KEYS:
+        out["%s/%s" % (prefix, k)] = np.asarray(loc[k], dtype=np.float64)
+    out[prefix + "/best_it"] = np.asarray(loc["best_it"])
+    out[prefix + "/best_loss"] = np.asarray(float(loc["best_loss"]))
+    out[prefix + "/epoch"] = np.asarray(loc["it"])
+    out[prefix + "/fit_return"] = np.asarray(float(ret))
+    G._sd(prefix + "/final", m, out)
+
+
+def run(name, j):
+    import contextlib
+    import io
+    t0 = time.time()
+    d, cfg = _load(name)
+    X, Y, Xv, Yv = d["X"], d["Y"], d["Xv"], d["Yv"]
+    true_gc = [d["true_gc%d" % k] for k in range(cfg["K"])]
+    B = cfg["B"]
+    train = _batches(X, Y, B, j)
+    val = _batches(Xv, Yv, B, 0)
+    out = {}
+    quiet = contextlib.redirect_stdout(io.StringIO())
+    # ---- the fit from the seeded model
+    m, _ = G.build(cfg)
+    oA, oB = _opts(m, cfg)
+    with tempfile.TemporaryDirectory() as td, G._Capture(), G._FitLocals() as fl, quiet:
+        ret = m.fit(td, train, oA, oB, cfg["L"], 1, 1, cfg["max_iter"], val, **_fit_kw(cfg, true_gc))
+    _record("fit", fl.locals, ret, m, out)
+    # ---- the reference-style resume from the fixture's checkpoint (fresh optimizers)
+    rm, _ = G.build(cfg)
+    sd = dict((k[len("resume/ckpt_model/"):], torch.from_numpy(d[k])) for k in d.files
+              if k.startswith("resume/ckpt_model/"))
+    rm.load_state_dict(sd, strict=False)
+    nsup = cfg["nsup"]
+    meta = dict((k, list(d["resume/ckpt/" + k])) for k in G.HIST_KEYS)
+    meta.update(epoch=int(d["resume/ckpt/epoch"]), best_it=int(d["resume/ckpt/best_it"]),
+                best_loss=float(d["resume/ckpt/best_loss"]))
+    # the GC-progress histories the reference's resume reads; its fit stops restoring them at the
+    # roc_au_OffDiagc typo (:1253), so only their structure matters (make_fit_golden.py docstring)
+    empty = [[] for _ in range(nsup)]
+    for k in ("f1score_histories", "f1score_OffDiag_histories", "roc_auc_histories", "roc_auc_OffDiag_histories"):
+        meta[k] = {0.0: [list(x) for x in empty]}
+    for k in ("factor_score_train_acc_history", "factor_score_train_tpr_history", "factor_score_train_tnr_history",
+              "factor_score_train_fpr_history", "factor_score_train_fnr_history", "factor_score_val_acc_history",
+              "factor_score_val_tpr_history", "factor_score_val_tnr_history", "factor_score_val_fpr_history",
+              "factor_score_val_fnr_history"):
+        meta[k] = []
+    for k in ("gc_factor_l1_loss_histories", "deltacon0_histories", "deltacon0_with_directed_degrees_histories",
+              "deltaffinity_histories"):
+        meta[k] = [list(x) for x in empty]
+    meta["gc_factor_cosine_sim_histories"] = {}
+    meta["gc_factorUnsupervised_cosine_sim_histories"] = {}
+    meta["path_length_mse_histories"] = {}
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "training_meta_data_and_hyper_parameters.pkl")
+        with open(path, "wb") as f:
+            pickle.dump(meta, f)
+        with quiet:
+            rm.resume_training_from_checkpoint(path)
+        rA, rB = _opts(rm, cfg)
+        with G._Capture(), G._FitLocals() as fl2, quiet:
+            rret = rm.fit(td, train, rA, rB, cfg["L"], 1, 1, cfg["max_iter"], val, **_fit_kw(cfg, true_gc))
+    _record("resume", fl2.locals, rret, rm, out)
+    if j == 0:  # the fixture's own order, one CPU thread instead of the fixture's eight: torch's
+        # CPU reductions split differently, so this is a realization too; it must stay close
+        for k in G.HIST_KEYS:
+            np.testing.assert_allclose(out["fit/" + k], d["hist/" + k], rtol=1e-3, atol=1e-6, err_msg=k)
+    os.makedirs(OUT, exist_ok=True)
+    np.savez_compressed(os.path.join(OUT, "%s_%d.npz" % (name, j)), **out)
+    print("%s realization %d: fit stopped at %d (best_it %d), resume stopped at %d (best_it %d), %.0f s"
+          % (name, j, int(out["fit/epoch"]), int(out["fit/best_it"]), int(out["resume/epoch"]),
+             int(out["resume/best_it"]), time.time() - t0), flush=True)
+
+
+RTOL, ATOL = 2e-4, 5e-6  # the fit tests' state tolerance (tests/test_gpu_fit_golden.py compare_state)
+
+
+def merge(name, J):
+    d, cfg = _load(name)
+    reals = [np.load(os.path.join(OUT, "%s_%d.npz" % (name, j))) for j in range(J)]
+    out = {"J": np.asarray(J)}
+    for part, href, sref in (("fit", "hist", "final"), ("resume", "resume/hist", "resume/final")):
+        out["%s/epoch" % part] = np.asarray([int(r[part + "/epoch"]) for r in reals])
+        out["%s/best_it" % part] = np.asarray([int(r[part + "/best_it"]) for r in reals])
+        out["%s/fit_return" % part] = np.asarray([float(r[part + "/fit_return"]) for r in reals])
+        out["%s/best_loss" % part] = np.asarray([float(r[part + "/best_loss"]) for r in reals])
+        for k in G.HIST_KEYS:
+            want = d["%s/%s" % (href, k)]
+            rows = []
+            for r in reals:
+                v = r["%s/%s" % (part, k)]
+                row = np.full(want.shape, np.nan)
+                n = min(len(v), len(want))
+                row[:n] = v[:n]
+                rows.append(row)
+            out["%s/hist/%s" % (part, k)] = np.asarray(rows)
+        keys = sorted(k[len(sref) + 1:] for k in d.files if k.startswith(sref + "/"))
+        for k in keys:
+            want = d["%s/%s" % (sref, k)]
+            if k.endswith("num_batches_tracked"):
+                continue
+            devs = np.asarray([np.abs(r["%s/final/%s" % (part, k)].astype(np.float64) - want) for r in reals])
+            out["%s/env/%s" % (part, k)] = np.max(devs, axis=0).astype(np.float32)
+            scale = max(1.0, float(np.abs(want).max()))
+            bound = RTOL * np.abs(want) + ATOL * scale
+            out["%s/outside/%s" % (part, k)] = np.asarray([int(np.sum(dv > bound)) for dv in devs])
+            # leave-one-out: entries where realization j leaves the envelope of the OTHER realizations
+            # (the allowance an exchangeable extra realization -- the GPU fit -- is held to)
+            loo = []
+            for j in range(len(reals)):
+                others = np.max(np.delete(devs, j, axis=0), axis=0) if len(reals) > 1 else np.zeros_like(bound)
+                loo.append(int(np.sum(devs[j] > np.maximum(bound, others))))
+            out["%s/loo/%s" % (part, k)] = np.asarray(loo)
+    path = os.path.join(HERE, name + "_envelope.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, len(out), "arrays")
+    for part in ("fit", "resume"):
+        print(part, "stop epochs", out[part + "/epoch"].tolist(), "best_it", out[part + "/best_it"].tolist())
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(1)
+    if sys.argv[1] == "run":
+        run(sys.argv[2], int(sys.argv[3]))
+    else:
+        merge(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4)

@@ -71,6 +71,13 @@ SCENARIOS = {
     "fit_d4ic": dict(seed=1, p=10, L=4, K=4, nsup=4, h=100, F=20, n=2, H=30, B=128, N=200, Nv=96, T=21,
                      label="d4ic", pre=2, acc=1, max_iter=40, lookback=1, check_every=2, lrA=1e-3, lrB=1e-3,
                      data_seed=4242, resume_at=None),
+    # configs[1] D4IC shape at the PUBLISHED learning rates (embed 2e-4, factors 5e-4:
+    # train/REDCLIFF_S_CMLP_Smooth_d4IC_BSCgs4ParsimSmo0_cached_args.txt) and the published batch of
+    # 128: one full training batch and 64 validation windows, so that the validation criterion turns
+    # (it stops at epoch 76; with 200 training windows it still improved at epoch 40)
+    "fit_d4ic_pub": dict(seed=1, p=10, L=4, K=4, nsup=4, h=100, F=20, n=2, H=30, B=128, N=128, Nv=64, T=21,
+                         label="d4ic", pre=2, acc=1, max_iter=200, lookback=1, check_every=2, lrA=2e-4, lrB=5e-4,
+                         data_seed=4242, resume_at=None),
 }
 
 

@@ -17,6 +17,19 @@ The HIP fit runs on the same seeded model and the same windows and must give (no
   * final parameters / buffers within rtol 2e-4 (the published-config schedule tolerance of
     tests/test_gpu_parity.py), the final GC estimate within 1e-4 relative, thresholded graphs
     (GC > 0) and get_f1_score identical.
+
+Where a trajectory is long enough for fp32 rounding order to matter -- the resumed fits, whose
+fresh Adam moments make the first post-restart steps near-unit-normalised for every weight, and the
+76-epoch fit at the published D4IC learning rates -- the bound is the REFERENCE's own fp32 spread,
+measured: tests/golden/make_fit_envelope.py reruns the reference's fit with the windows of every
+training batch in other orders (and on one CPU thread instead of eight), which changes nothing but
+the rounding order of torch's reductions.  For the resumed C1 fit those realizations spread by up
+to 2.2e-3 relative on the last fw-L1 entry and leave the 2e-4 state tolerance at up to 91 entries
+(tests/golden/fit_c1_envelope.npz), so no implementation can hold 1e-4 there, the reference
+included.  An entry then passes within max(tolerance, the realizations' largest deviation); the
+GPU fit may leave that bound at no more entries than a reference realization leaves the bound of
+the others (leave-one-out), and never by more than 3x the realizations' deviation.  Stopping epoch
+and best_it are exact everywhere.
 """
 import json
 import os
@@ -81,20 +94,77 @@ def compare_state(tag, model, want, rtol=2e-4, atol=5e-6, outliers=0):
         assert_close("%s/%s" % (tag, k), got[k], want[k], rtol, atol * scale, outliers)
 
 
-def compare_hist(tag, h, d, prefix, rtol=1e-4):
+def load_envelope(name):
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + "_envelope.npz")
+    return np.load(path, allow_pickle=False) if os.path.exists(path) else None
+
+
+def within_envelope(tag, got, want, base, devs_ref, loo_allowed=None):
+    """got / want: arrays; base: the fixed bound per entry; devs_ref: [J, ...] the reference
+    realizations' |deviation| from `want` (NaN where a realization has no entry).  Passes when at
+    most `allowed` entries exceed max(base, max_j devs_ref) -- allowed = the worst leave-one-out
+    count of the realizations themselves (or `loo_allowed`) -- and none exceeds max(base, 3 x it)."""
+    dev = np.abs(np.asarray(got, np.float64) - want)
+    env = np.nanmax(devs_ref, axis=0) if devs_ref.shape[0] else np.zeros_like(dev)
+    env = np.nan_to_num(env, nan=0.0)
+    bound = np.maximum(base, env)
+    if loo_allowed is None:
+        loo = []
+        for j in range(devs_ref.shape[0]):
+            others = np.nan_to_num(np.nanmax(np.delete(devs_ref, j, axis=0), axis=0), nan=0.0) \
+                if devs_ref.shape[0] > 1 else np.zeros_like(dev)
+            loo.append(int(np.sum(np.nan_to_num(devs_ref[j], nan=0.0) > np.maximum(base, others))))
+        loo_allowed = max(loo) if loo else 0
+    n_out = int(np.sum(dev > bound))
+    worst = float(np.max(dev / np.maximum(np.maximum(base, 3.0 * env), 1e-30))) if dev.size else 0.0
+    print("%s: %d entries beyond max(tol, reference spread) (allowed %d); worst %.2f of max(tol, 3 x spread)"
+          % (tag, n_out, loo_allowed, worst))
+    assert n_out <= loo_allowed, (tag, n_out, loo_allowed)
+    assert worst <= 1.0, (tag, worst)
+
+
+def compare_hist(tag, h, d, prefix, rtol=1e-4, env=None, part=None):
     for k in HKEYS:
         got, want = np.asarray(h[k], np.float64), d["%s/%s" % (prefix, k)]
         if got.shape == want.shape and want.size:
             print("%s/%s: max rel err %.2e" % (tag, k, float(np.max(np.abs(got - want) / np.maximum(np.abs(want),
                                                                                                  1e-6)))))
-        assert_close("%s/%s" % (tag, k), got, want, rtol, 1e-6)
+        if env is None:
+            assert_close("%s/%s" % (tag, k), got, want, rtol, 1e-6)
+        else:
+            assert got.shape == want.shape, (tag, k, got.shape, want.shape)
+            rows = env["%s/hist/%s" % (part, k)]
+            within_envelope("%s/%s" % (tag, k), got, want, rtol * np.abs(want) + 1e-6, np.abs(rows - want))
     assert h["best_it"] == int(d[prefix + "/best_it"]), (tag, h["best_it"], int(d[prefix + "/best_it"]))
-    assert_close(tag + "/best_loss", h["best_loss"], d[prefix + "/best_loss"], 1e-4, 1e-6)
+    want_bl = float(d[prefix + "/best_loss"])
+    if env is None:
+        assert_close(tag + "/best_loss", h["best_loss"], want_bl, 1e-4, 1e-6)
+    else:
+        within_envelope(tag + "/best_loss", np.asarray([h["best_loss"]]), np.asarray([want_bl]),
+                        np.asarray([1e-4 * abs(want_bl) + 1e-6]),
+                        np.abs(env["%s/best_loss" % part] - want_bl)[:, None])
 
 
-@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic"])
+def compare_state_envelope(tag, model, want, env, part, rtol=2e-4, atol=5e-6):
+    """compare_state's tolerance, widened entry-wise to the reference realizations' spread with the
+    leave-one-out allowance the merge step recorded (tests/golden/make_fit_envelope.py)."""
+    got = dict((k, v.detach().cpu().numpy()) for k, v in model.state_dict().items() if not k.startswith("gen_model."))
+    assert set(got) == set(want), tag
+    for k in want:
+        if k.endswith("num_batches_tracked"):
+            assert int(got[k]) == int(want[k]), tag + k
+            continue
+        w = want[k].astype(np.float64)
+        scale = max(1.0, float(np.abs(w).max()))
+        base = rtol * np.abs(w) + atol * scale
+        within_envelope("%s/%s" % (tag, k), got[k], w, base, env["%s/env/%s" % (part, k)].astype(np.float64)[None],
+                        loo_allowed=int(np.max(env["%s/loo/%s" % (part, k)])))
+
+
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub"])
 def test_fit_matches_reference_fit(name):
     d, meta = load(name)
+    env = load_envelope(name) if name == "fit_d4ic_pub" else None  # the long published-lr trajectory
     m = build(meta)
     compare_state("init", m, state(d, "init"), rtol=0, atol=0)  # seeded construction: bit-identical
     train, val = data(d, meta)
@@ -104,7 +174,7 @@ def test_fit_matches_reference_fit(name):
     n = int(d["hist/n_epochs"])
     assert len(h["avg_combo_loss"]) == n, (len(h["avg_combo_loss"]), n)
     assert h["stopped_at"] == int(d["hist/epoch"]), (h["stopped_at"], int(d["hist/epoch"]))
-    compare_hist(name, h, d, "hist")
+    compare_hist(name, h, d, "hist", env=env, part="fit")
     nsup = meta["nsup"]
     for key in ("f1score_histories", "f1score_OffDiag_histories", "roc_auc_histories", "roc_auc_OffDiag_histories"):
         got = np.asarray([h[key][0.0][sf] for sf in range(nsup)], np.float64)
@@ -125,8 +195,14 @@ def test_fit_matches_reference_fit(name):
         got = np.asarray(h["factor_score_train_history"][ck], np.float64)
         np.testing.assert_array_equal(np.nan_to_num(got, nan=-1.0), np.nan_to_num(d["hist/" + key], nan=-1.0),
                                       err_msg=key)
-    compare_state("final", m, state(d, "final"))
-    assert_close("fit return", ret, d["fit_return"], 1e-4, 1e-6)
+    if env is None:
+        compare_state("final", m, state(d, "final"))
+        assert_close("fit return", ret, d["fit_return"], 1e-4, 1e-6)
+    else:
+        compare_state_envelope("final", m, state(d, "final"), env, "fit")
+        fr = float(d["fit_return"])
+        within_envelope("fit return", np.asarray([ret]), np.asarray([fr]), np.asarray([1e-4 * abs(fr) + 1e-6]),
+                        np.abs(env["fit/fit_return"] - fr)[:, None])
     m.eval()
     Lm = max(meta["L"], meta["F"])
     with torch.no_grad():
@@ -142,12 +218,16 @@ def test_fit_matches_reference_fit(name):
     np.testing.assert_array_equal(f1, d["f1"])
 
 
-@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic"])
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub"])
 def test_resume_matches_reference_resume(name, tmp_path):
     """The reference's resume: the model saved at a mid-fit checkpoint (best_model) plus its
     metadata, resume_training_from_checkpoint, fit with FRESH Adam objects (the default here,
-    as in the reference) -- histories, best_it and final state as the reference's resumed fit."""
+    as in the reference) -- stopping epoch and best_it exact; histories within 1e-4, final state
+    within 2e-4, both widened to the reference's own fp32 spread where that is larger (module
+    docstring; the restart amplifies rounding order: C1's realizations spread by 2.2e-3)."""
     d, meta = load(name)
+    env = load_envelope(name)
+    assert env is not None, "tests/golden/%s_envelope.npz missing (make_fit_envelope.py)" % name
     m = build(meta)
     with torch.no_grad():
         sd = state(d, "resume/ckpt_model")
@@ -168,12 +248,8 @@ def test_resume_matches_reference_resume(name, tmp_path):
     ret = m.fit(None, train, oA, oB, meta["L"], 1, 1, meta["max_iter"], val, **fit_kw(meta, d))
     h = m.fit_history
     assert h["stopped_at"] == int(d["resume/hist/epoch"])
-    # 2e-4 (the published-config schedule tolerance of test_gpu_parity) on the resumed fit's
-    # histories: its trajectory is the longest here (C1: epochs 0-11, with Adam restarted from
-    # zero moments at epoch 5, whose first steps are near-unit-normalised for every weight);
-    # measured worst 1.2e-4 (fw-L1 of C1's last epoch), every other entry within 1e-4
-    compare_hist(name + "/resume", h, d, "resume/hist", rtol=2e-4)
-    # final state: at most 2 entries per tensor beyond the bound, each within 10x of it (measured:
-    # one graph-conv weight of C1 at 1.03x the bound after the restart; every other entry inside)
-    compare_state("resume/final", m, state(d, "resume/final"), outliers=2)
-    assert_close("resume fit return", ret, d["resume/fit_return"], 1e-4, 1e-6)
+    compare_hist(name + "/resume", h, d, "resume/hist", rtol=1e-4, env=env, part="resume")
+    compare_state_envelope("resume/final", m, state(d, "resume/final"), env, "resume")
+    fr = float(d["resume/fit_return"])
+    within_envelope("resume fit return", np.asarray([ret]), np.asarray([fr]), np.asarray([1e-4 * abs(fr) + 1e-6]),
+                    np.abs(env["resume/fit_return"] - fr)[:, None])

@@ -53,12 +53,13 @@ def data(N, seed):
 
 
 @pytest.mark.parametrize("path,grid,emb", [("vector", GRID, None), ("mfma", GRID, None), ("mfma", GRID8, None),
-                                          ("mfma", GRID, "gemm")])
+                                          ("mfma", GRID, "gemm"), ("mfma", GRID8, "batched")])
 def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
     """Both factor paths (the default picks the matrix cores for packs of >= 8 replicas, so the
     path is pinned here to compare like with like); R = 3 and the packed-only paths at R = 8.
-    emb "gemm": the GEMM-shaped embedder (the default for packs of >= 16 replicas) with its
-    products batched over the replicas, against single fits on the same embedder path."""
+    emb "gemm": the GEMM-shaped embedder with its products batched over the replicas, against
+    single fits on the same embedder path; emb "batched": the replica-batched embedder kernels
+    (the default for D4IC-shaped packs of >= 16 replicas), likewise."""
     monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     if emb:
         monkeypatch.setenv("REDCLIFF_EMB_PATH", emb)
