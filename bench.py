@@ -461,7 +461,7 @@ def fits_per_hour(c, args, dev, rank, dist, world):
 
 
 # --------------------------------------------------------------------------- modes
-def mode_fit(args, dev, rank, world, dist):
+def mode_fit(args, dev, rank, world, dist, holder):
     from redcliff_amd import _native as nat  # noqa: F401
     c = CONFIGS[args.config]
     B = c["B"]
@@ -501,7 +501,25 @@ def mode_fit(args, dev, rank, world, dist):
     if args.fit_replicas > 0:
         fph = fits_per_hour(c, args, dev, rank, dist, world)
 
+    ns = None
+    if world == 1 and not args.no_north_star and args.config != "c1k4":
+        cn = CONFIGS["c1k4"]
+        _, nplan = single_fit(cn, args, dev, rank)
+        nplan(args.warmup, 0).run()
+        nextra = preheat(nplan, args.warmup, args.preheat_s)
+        nsteps = max(args.steps, 50)
+        nel = timed(nplan(nsteps, args.warmup + nextra).run, None, dev)
+        ns = {"workload": cn["workload"], "windows_per_s": round(nsteps * cn["B"] / nel, 1),
+              "ms_per_step": round(1e3 * nel / nsteps, 4), "steps": nsteps, "target_gpu_over_cpu": 50.0}
+
     dpl = None
+    if args.dp_leg_batch > 0 and dist is None and world == 1:
+        # one rank: the RCCL group exists only from here on -- a process with an RCCL communicator
+        # runs the single fit's second stream (split-lead step) serialised behind the first
+        # (C1(K=4): 0.097 -> 0.132 ms per step, profiles/r04_ns_probe.log), so the single-fit legs
+        # above ran without one, as a one-GPU user's fit does
+        dist = init_group(dev, 1, 0)
+        holder["dist"] = dist
     if args.dp_leg_batch > 0 and dist is not None:
         # configs[3] beside the replica numbers: ONE TST-shaped fit data-parallel over all ranks
         # (global batch --dp-leg-batch, RCCL all-reduce of the flat gradient per update), so the
@@ -513,17 +531,6 @@ def mode_fit(args, dev, rank, world, dist):
                "ms_per_update": round(1e3 * del_ / dsteps, 4), "scaling": "strong",
                "allreduce_floats_per_update": int(dpo.PA + dpo.PB),
                "workload": CONFIGS["c4"]["workload"].replace("B=128", "global B=%d" % args.dp_leg_batch)}
-
-    ns = None
-    if world == 1 and not args.no_north_star and args.config != "c1k4":
-        cn = CONFIGS["c1k4"]
-        _, nplan = single_fit(cn, args, dev, rank)
-        nplan(args.warmup, 0).run()
-        nextra = preheat(nplan, args.warmup, args.preheat_s)
-        nsteps = max(args.steps, 50)
-        nel = timed(nplan(nsteps, args.warmup + nextra).run, None, dev)
-        ns = {"workload": cn["workload"], "windows_per_s": round(nsteps * cn["B"] / nel, 1),
-              "ms_per_step": round(1e3 * nel / nsteps, 4), "steps": nsteps, "target_gpu_over_cpu": 50.0}
 
     if rank != 0:
         return None
@@ -567,7 +574,7 @@ def dp_throughput(B, steps, warmup, dev, dist):
     return timed(run(steps, warmup), dist, dev), dp
 
 
-def mode_dp(args, dev, rank, world, dist):
+def mode_dp(args, dev, rank, world, dist, holder=None):
     """BASELINE configs[3]: one TST-shaped fit sharded over the ranks (DataParallelFit)."""
     c = dict(CONFIGS["c4"], B=args.dp_batch)
     B = c["B"]
@@ -621,6 +628,23 @@ def rank_devices(dist, rank, local, world, dev):
 
 
 # --------------------------------------------------------------------------- launch
+def init_group(dev, world, local):
+    """torch.distributed over RCCL ("nccl") on the GPU, bound to this rank's device (no guessing the
+    device from the global rank), or gloo for the CPU plumbing check; 127.0.0.1 rendezvous."""
+    import torch.distributed as dist
+    kw = {}
+    if dev is not None:
+        torch.cuda.set_device(dev)
+        kw["device_id"] = dev
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("nccl" if dev is not None else "gloo", rank=0, world_size=1, **kw)
+    else:
+        dist.init_process_group("nccl" if dev is not None else "gloo", **kw)
+    return dist
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -675,23 +699,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cuda = torch.cuda.is_available()
     dist = None
-    if world > 1 or args.mode == "dp" or args.dp_leg_batch > 0:
-        import torch.distributed as dist
-        backend = "nccl" if cuda else "gloo"  # nccl is RCCL on ROCm; gloo only for the CPU plumbing check
-        kw = {}
-        if cuda:
-            torch.cuda.set_device(local)
-            # bind the communicator to this rank's GPU explicitly (no guessing from the global rank)
-            kw["device_id"] = torch.device("cuda", local)
-        if world == 1:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(_free_port()))
-            dist.init_process_group(backend, rank=0, world_size=1, **kw)
-        else:
-            dist.init_process_group(backend, **kw)
+    # one rank in --mode fit: the group for the data-parallel leg is created when that leg runs (mode_fit)
+    if world > 1 or args.mode == "dp" or (args.dp_leg_batch > 0 and not cuda):
+        dist = init_group(torch.device("cuda", local) if cuda else None, world, local)
         seen = dist.get_world_size()
         if seen != world or (args.gpus > 1 and seen != args.gpus):
-            raise SystemExit("%s world size %d != --gpus %d / WORLD_SIZE %d" % (backend, seen, args.gpus, world))
+            raise SystemExit("world size %d != --gpus %d / WORLD_SIZE %d" % (seen, args.gpus, world))
         world = seen
     if not cuda:
         devices = rank_devices(dist, rank, local, world, None)
@@ -714,13 +727,14 @@ def main():
     if dist is not None:
         dist.barrier()
     devices = rank_devices(dist, rank, local, world, dev)
-    out = (mode_dp if args.mode == "dp" else mode_fit)(args, dev, rank, world, dist)
+    holder = {"dist": dist}
+    out = (mode_dp if args.mode == "dp" else mode_fit)(args, dev, rank, world, dist, holder)
     if out is not None:
         out["config"]["rank_devices"] = devices
         out["config"]["world_size"] = world
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    if holder["dist"]:
+        holder["dist"].destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -378,8 +378,11 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   // embedder backward (C1(K=4): 80 update workgroups, 1.23 -> 1.30 M windows/s; TST: 216, the
   // embedder backward is slowed by more than the split saves, 1.07 -> 1.01 M).
   // REDCLIFF_SPLIT_LEAD=0 / 1 overrides.
+  // Not for data-parallel shard steps (RC_GRAD_ONLY): their process holds an RCCL communicator, and
+  // with one the second stream runs serialised behind the first -- the split step is then slower
+  // than one launch (C1(K=4): 0.104 -> 0.132 ms, profiles/r04_ns_probe.log).
   const char* slv = getenv("REDCLIFF_SPLIT_LEAD");
-  const bool split_ok = !mfma && fac && !merged && !fork && emb_grad && (fl & RC_STEP_B);
+  const bool split_ok = !mfma && fac && !merged && !fork && emb_grad && (fl & RC_STEP_B) && !(fl & RC_GRAD_ONLY);
   const bool split = split_ok && (slv ? strcmp(slv, "0") != 0
                                       : c.d.R == 1 && 2 * rc_fac_bwd_grid(c) <= rc_cu_count());
   if (split) {

@@ -9,12 +9,14 @@ G="python scripts/grid_step.py --replicas 128 --steps 30"
 step c_grid_prev 200 env REDCLIFF_HIP_LIB=scripts/bin/lib_prev.so $G
 step c_grid_xsonly_gemm 200 env REDCLIFF_HIP_LIB=scripts/bin/lib_xsonly.so REDCLIFF_EMB_PATH=gemm $G
 step c_grid_cur_gemm 200 env REDCLIFF_EMB_PATH=gemm $G
-step c_grid_cur 200 $G
+step c_grid_cur 200 env REDCLIFF_EMB_PATH=batched $G
 step c_grid_prev2 200 env REDCLIFF_HIP_LIB=scripts/bin/lib_prev.so $G
 step c_grid_xsonly_gemm2 200 env REDCLIFF_HIP_LIB=scripts/bin/lib_xsonly.so REDCLIFF_EMB_PATH=gemm $G
 step c_grid_cur_gemm2 200 env REDCLIFF_EMB_PATH=gemm $G
-step c_grid_cur2 200 $G
-step c_stats 200 rocprofv3 --kernel-trace --stats --kernel-include-regex k_ --output-format csv -d gpurun_out/stats_c -o run -- python scripts/grid_step.py --replicas 128 --steps 20
-step c_lds 150 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --kernel-include-regex k_ --output-format csv -d gpurun_out/pmc_c_lds -o run -- python scripts/grid_step.py --replicas 128 --steps 3
+step c_grid_cur2 200 env REDCLIFF_EMB_PATH=batched $G
+step c_stats 200 env REDCLIFF_EMB_PATH=batched rocprofv3 --kernel-trace --stats --kernel-include-regex k_ --output-format csv -d gpurun_out/stats_c -o run -- python scripts/grid_step.py --replicas 128 --steps 20
+step c_lds 150 env REDCLIFF_EMB_PATH=batched rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES --kernel-include-regex k_ --output-format csv -d gpurun_out/pmc_c_lds -o run -- python scripts/grid_step.py --replicas 128 --steps 3
 step c_tests2 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_pack_fit.py
+step c_ns 200 python scripts/ns_probe.py
+step c_ns_nccl 200 python scripts/ns_probe.py --nccl
 kill $HB
