@@ -79,8 +79,8 @@ __host__ __device__ inline int gb_lds_fwd(const GbShape& s) {
   return s.p * s.NSt + GB_WT * s.pHs + GB_WT * s.M1h + (s.n - 1) * s.p * s.p + 128;
 }
 __host__ __device__ inline int gb_lds_bwd(const GbShape& s) {
-  return 2 * s.p * s.NSt + GB_WT * s.pHs + s.p * s.NSz + GB_WT * gb_s2(s.M1) + GB_WT * 16 + s.n * s.p * s.p +
-         16 * GB_MAXNT * s.Hs + 2 * GB_THREADS;
+  return 2 * s.p * s.NSt + GB_WT * s.pHs + s.p * s.NSz + GB_WT * gb_s2(s.M1) + GB_WT * s.F * s.p + s.K * s.M1 +
+         GB_WT * 16 + s.n * s.p * s.p + 16 * GB_MAXNT * s.Hs + 2 * GB_THREADS;
 }
 __host__ __device__ inline int gb_ntiles(int B) { return (B + GB_WT - 1) / GB_WT; }
 
@@ -256,8 +256,10 @@ __global__ __launch_bounds__(GB_THREADS) void k_gemb_bwd(StepCtx c) {
   float* DTs = Ts + p * NSt;               // [p][16][nFs], node stride NSt
   float* Rs = DTs + p * NSt;               // [16][pHs]
   float* DZs = Rs + GB_WT * pHs;           // [p][16][Hs], node stride NSz
-  float* DF1 = DZs + p * NSz;              // [16][M1s]
-  float* DR = DF1 + GB_WT * M1s;           // [16][16] dr (K <= 16)
+  float* DF1 = DZs + p * NSz;              // [16][M1s]: f1, then dL/df1 in place
+  float* Xs = DF1 + GB_WT * M1s;           // raw x [16][F][p]
+  float* W2s = Xs + GB_WT * pF;            // fc2W [K][M1]
+  float* DR = W2s + K * M1;                // [16][16] dr (K <= 16)
   float* Ss = DR + GB_WT * 16;             // S_0 .. S_{n-1}
   float* Gs = Ss + n * pp2;                // gcW[(i,f)][h], row stride Hs (the dT B operand)
   float* red = Gs + 16 * GB_MAXNT * Hs;    // [2][GB_THREADS]
@@ -294,6 +296,18 @@ __global__ __launch_bounds__(GB_THREADS) void k_gemb_bwd(StepCtx c) {
                   const int w = e / pH;
                   Rs[w * pHs + (e - w * pH)] = v;
                 }),
+      rc_seg<4>(GB_WT * pF, [&](int e) {
+        const int w = e / pF;
+        return w < nw ? Xg[(int64_t)w * d.T * p + (e - w * pF)] : 0.f;
+      }, [&](int e, float v) { Xs[e] = v; }),
+      rc_seg<4>(GB_WT * M1, [&](int e) {
+        const int w = e / M1;
+        return w < nw ? ws[c.wo.f1 + (int64_t)(b0 + w) * M1 + (e - w * M1)] : 0.f;
+      }, [&](int e, float v) {
+        const int w = e / M1;
+        DF1[w * M1s + (e - w * M1)] = v;
+      }),
+      rc_seg<2>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { W2s[e] = v; }),
       rc_seg<2>(n * pp2, [&](int e) { return ws[c.wo.S + e]; }, [&](int e, float v) { Ss[e] = v; }),
       rc_seg<4>(16 * GB_MAXNT * Hs, [&](int e) {
         const int col = e / Hs, h = e - col * Hs;
@@ -316,12 +330,12 @@ __global__ __launch_bounds__(GB_THREADS) void k_gemb_bwd(StepCtx c) {
     DR[w * 16 + k] = v;
   }
   __syncthreads();
-  // ---- df1 = [f1 > 0] dr fc2W (k ascending)
+  // ---- df1 = [f1 > 0] dr fc2W (k ascending), in place over f1
   for (int e = tid; e < GB_WT * M1; e += GB_THREADS) {
     const int w = e / M1, m = e - w * M1;
     float gg = 0.f;
-    if (w < nw && ws[c.wo.f1 + (int64_t)(b0 + w) * M1 + m] > 0.f)
-      for (int k = 0; k < K; ++k) gg = fmaf(DR[w * 16 + k], E[c.eo.fc2W + k * M1 + m], gg);
+    for (int k = 0; k < K; ++k) gg = fmaf(DR[w * 16 + k], W2s[k * M1 + m], gg);
+    gg = DF1[w * M1s + m] > 0.f ? gg : 0.f;
     DF1[w * M1s + m] = gg;
     if (w < nw) ws[c.wo.edf1 + (int64_t)(b0 + w) * M1 + m] = gg;
   }
@@ -408,29 +422,46 @@ __global__ __launch_bounds__(GB_THREADS) void k_gemb_bwd(StepCtx c) {
     gb_bn(c, r, bf, bmean, binv);
     for (int row = bsl; row < p * GB_WT; row += nbsl) {
       const int ch = row / GB_WT, w = row - ch * GB_WT;
-      if (w >= nw) continue;
       float dx = DTs[ch * NSt + w * nFs + bf];
       for (int i = 1; i < n; ++i)
         for (int cp = 0; cp < p; ++cp) dx = fmaf(Ss[(i * p + cp) * p + ch], DTs[cp * NSt + w * nFs + i * F + bf], dx);
-      const float x = Xg[(int64_t)w * d.T * p + bf * p + ch];  // the raw window (L2)
-      ag += dx * ((x - bmean) * binv);
-      ab += dx;
+      const float x = Xs[(w * F + bf) * p + ch];
+      if (w < nw) {  // windows past the batch have dT = 0: skipped, so their (x - mean) terms add nothing
+        ag += dx * ((x - bmean) * binv);
+        ab += dx;
+      }
     }
   }
   red[tid] = ag;
   red[GB_THREADS + tid] = ab;
-  // ---- dS_i[ch][c'] slot `tile` = sum_w sum_f dT_i[ch][w][f] x_bn[c'][w][f]  (w, then f ascending)
-  for (int e = tid; e < (n - 1) * pp2; e += GB_THREADS) {
-    const int i = 1 + e / pp2, rem = e - (i - 1) * pp2, ch = rem / p, cp = rem - ch * p;
-    float t = 0.f;
-    for (int w = 0; w < nw; ++w) {
-      const float* a = DTs + ch * NSt + w * nFs + i * F;
-      const float* bq = Ts + cp * NSt + w * nFs;
-      for (int f = 0; f < F; ++f) t = fmaf(a[f], bq[f], t);
+  // ---- dS_i[ch][c'] slot `tile` = sum_w sum_f dT_i[ch][w][f] x_bn[c'][w][f] on the matrix cores: one
+  // 16 x 16 tile per power (A = dT_i rows ch, B = x_bn^T columns c', k = (w, f), F % 4 == 0), wave wv
+  // over windows 4 wv .. 4 wv + 3 (w, then f ascending), the four waves' partials added in wave order
+  {
+    const int chA = l15 < p ? l15 : p - 1;
+    const float ma = l15 < p ? 1.f : 0.f;
+    float* dsx = DZs;  // [GB_WAVES][n - 1][256], DZs is dead now
+    for (int i = 1; i < n; ++i) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int w = 4 * wv; w < 4 * wv + 4; ++w) {
+        const float* a = DTs + chA * NSt + w * nFs + i * F + g;
+        const float* bq = Ts + chA * NSt + w * nFs + g;
+        for (int j = 0; j < F / 4; ++j) acc = gb_mfma(ma * a[4 * j], ma * bq[4 * j], acc);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) dsx[(wv * (n - 1) + (i - 1)) * 256 + reg * 64 + lane] = acc[reg];
     }
-    ws[c.wo.dS + (int64_t)tile * c.dsS + pp2 + e] = t;
   }
   __syncthreads();
+  for (int e = tid; e < (n - 1) * 256; e += GB_THREADS) {
+    const int i1 = e >> 8, reg = (e >> 6) & 3, ln = e & 63;
+    const int ch = 4 * (ln >> 4) + reg, cp = ln & 15;
+    if (ch < p && cp < p) {
+      float t = 0.f;
+      for (int w = 0; w < GB_WAVES; ++w) t += DZs[(w * (n - 1) + i1) * 256 + reg * 64 + ln];
+      ws[c.wo.dS + (int64_t)tile * c.dsS + pp2 + i1 * pp2 + ch * p + cp] = t;
+    }
+  }
   if (tid < F) {
     float ga = 0.f, gb = 0.f;
     for (int q = 0; q < nbsl; ++q) {
@@ -506,24 +537,41 @@ __global__ __launch_bounds__(GB_DFC_THREADS) void k_gemb_dfc1(StepCtx c) {
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) ws[c.wo.gfc1 + (int64_t)(16 * mi + 4 * g + reg) * pH + q] = acc[mi][j][reg];
   }
-  // fc2 / fc2-bias / fc1-bias (lanes: consecutive m, so the f1 / df1 reads of a window are one row)
+  // fc2 / fc2-bias / fc1-bias, windows ascending, through 32-window chunks staged in LDS
   const float* dr = ws + c.wo.edr;
   const float* f1 = ws + c.wo.f1;
   const int nfc = K * M1 + K + M1;
-  for (int e = tid; e < nfc; e += GB_DFC_THREADS) {
-    float t = 0.f;
+  __shared__ float cdr[32 * 16], cf1[32 * 64], cdf[32 * 64];
+  float t0 = 0.f, t1 = 0.f, t2 = 0.f;  // outputs tid, tid + 512, tid + 1024 (nfc <= 16 * 64 + 80)
+  auto acc_out = [&](int e, int nb, float& t) {
+    if (e >= nfc) return;
     if (e < K * M1) {
       const int k = e / M1, m = e - k * M1;
-      for (int b = 0; b < B; ++b) t = fmaf(dr[(int64_t)b * K + k], fmaxf(f1[(int64_t)b * M1 + m], 0.f), t);
+      for (int b = 0; b < nb; ++b) t = fmaf(cdr[b * 16 + k], cf1[b * 64 + m], t);
     } else if (e < K * M1 + K) {
       const int k = e - K * M1;
-      for (int b = 0; b < B; ++b) t += dr[(int64_t)b * K + k];
+      for (int b = 0; b < nb; ++b) t += cdr[b * 16 + k];
     } else {
       const int m = e - K * M1 - K;
-      for (int b = 0; b < B; ++b) t += df1[(int64_t)b * M1 + m];
+      for (int b = 0; b < nb; ++b) t += cdf[b * 64 + m];
     }
-    ws[c.wo.gfc + e] = t;
+  };
+  for (int b0 = 0; b0 < B; b0 += 32) {
+    const int nb = min(32, B - b0);
+    __syncthreads();
+    for (int e = tid; e < nb * K; e += GB_DFC_THREADS) cdr[(e / K) * 16 + e % K] = dr[(int64_t)b0 * K + e];
+    for (int e = tid; e < nb * M1; e += GB_DFC_THREADS) {
+      cf1[(e / M1) * 64 + e % M1] = fmaxf(f1[(int64_t)b0 * M1 + e], 0.f);
+      cdf[(e / M1) * 64 + e % M1] = df1[(int64_t)b0 * M1 + e];
+    }
+    __syncthreads();
+    acc_out(tid, nb, t0);
+    acc_out(tid + GB_DFC_THREADS, nb, t1);
+    acc_out(tid + 2 * GB_DFC_THREADS, nb, t2);
   }
+  if (tid < nfc) ws[c.wo.gfc + tid] = t0;
+  if (tid + GB_DFC_THREADS < nfc) ws[c.wo.gfc + tid + GB_DFC_THREADS] = t1;
+  if (tid + 2 * GB_DFC_THREADS < nfc) ws[c.wo.gfc + tid + 2 * GB_DFC_THREADS] = t2;
 }
 
 }  // namespace
@@ -535,7 +583,8 @@ bool rc_emb_batched_fits(const RedcliffDims& d) {
   const GbShape s(d);
   return d.p <= 16 && d.M1 == 64 && d.K <= 16 && s.nF <= 16 * GB_MAXNT && d.H <= 4 * GB_MAXKH &&
          s.nqt <= GB_WAVES * GB_MAXNQ && s.nqt <= GB_DFC_WAVES * GB_DFC_NQ && s.nkf <= GB_MAXKF && d.F <= GB_THREADS &&
-         gb_ntiles(d.Bmax) <= 64 && (int64_t)gb_lds_bwd(s) <= RC_LDS_MAX_FLOATS &&
+         gb_ntiles(d.Bmax) <= 64 && (int64_t)gb_lds_bwd(s) <= RC_LDS_MAX_FLOATS && d.F % 4 == 0 &&
+         (d.n - 1) * 256 * GB_WAVES <= d.p * s.NSz &&  // dS partials over DZs
          GB_WAVES * GB_MAXNT * 2 * 256 <= GB_WT * s.pHs + s.p * s.NSz &&  // xw over Rs + DZs
          (int64_t)gb_lds_fwd(s) <= RC_LDS_MAX_FLOATS;
 }
