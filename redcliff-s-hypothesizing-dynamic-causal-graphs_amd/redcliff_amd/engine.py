@@ -638,7 +638,7 @@ class StepPlan:
         self._fn = nat.lib().redcliff_train_steps
         self._bn_step = 2 * eng.F
 
-    def run(self, stream=None):
+    def run(self):
         eng, a = self.eng, self.a
         if self.flags == 0:
             return
@@ -647,12 +647,16 @@ class StepPlan:
         a.tA = (stA["t"] + 1) if stA else 1
         a.tB = (stB["t"] + 1) if stB else 1
         a.flags = self.flags | (0 if eng.supports_fresh else nat.REFRESH_SUPPORTS)
-        rc = self._fn(ctypes.byref(a), self.n, self._rows_p, self._sizes_p, self._bn_step,
-                      stream if stream is not None else _stream())
+        if self.nbn:
+            # BatchNorm's num_batches_tracked, which no kernel reads, advanced ahead of the chain (same
+            # stream): its tiny launch runs while the host still enqueues the steps, not after them
+            eng.dgcnn.BN1.num_batches_tracked.add_(self.nbn * self.n)
+        rc = self._fn(ctypes.byref(a), self.n, self._rows_p, self._sizes_p, self._bn_step, _stream())
         if rc != 0:
             nat.check(rc, "train_steps (plan)")
-        eng._after(self.flags, self.nbn, self.n)
+        eng._after(self.flags, self.nbn, self.n, bn=False)
 
 
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
