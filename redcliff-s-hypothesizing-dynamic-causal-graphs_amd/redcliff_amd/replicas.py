@@ -26,6 +26,7 @@ methods keep working on it between packed epochs.
 import ctypes
 import gc
 import os
+import time
 
 import numpy as np
 import torch
@@ -427,11 +428,17 @@ class ReplicaPack:
             self.conf.zero_()
             self.run_epoch(ep, train, active, set_modes=False)
 
+        # REDCLIFF_PACK_PROFILE=1: host seconds per epoch in (enqueue of the evaluation, enqueue of
+        # the next epoch's training, waiting for the device, digesting the epoch) -> self.last_profile
+        prof = [] if os.environ.get("REDCLIFF_PACK_PROFILE", "0") != "0" else None
+        self.last_profile = prof
         try:
             it = 0
             if max_iter > 0:
                 launch_train(0)
             while it < max_iter and active:
+                if prof is not None:
+                    tp = [time.perf_counter()]
                 if verbose:
                     print("ReplicaPack.fit: epoch %d, %d of %d replicas active" % (it, len(active), R), flush=True)
                 tr_act = [trackers[r] for r in active]
@@ -457,13 +464,19 @@ class ReplicaPack:
                     pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d,
                                              nat.status_view(self.ws, self.ws_off, R)] +
                                             ([vals_d] if vals_d is not None else []))
+                if prof is not None:
+                    tp.append(time.perf_counter())
                 spec = (it + 1 < max_iter and not (dirs is not None and it % check_every == 0)
                         and it + 1 != reorder_at)
                 if spec:
                     self._save_state()
                     steps_before = [self._step_counts(r) for r in range(R)]
                     launch_train(it + 1)
+                if prof is not None:
+                    tp.append(time.perf_counter())
                 got = pending.wait()
+                if prof is not None:
+                    tp.append(time.perf_counter())
                 cms, l1, dots, acc, conf = got[:5]
                 nat.raise_on_status(got[5], nat.status_view(self.ws, self.ws_off, R), "packed fit epoch %d" % it)
                 vals = got[6].reshape(Ra, S, *got[6].shape[1:]) if vals_d is not None else None
@@ -497,6 +510,9 @@ class ReplicaPack:
                 it += 1
                 if not spec and it < max_iter and active:
                     launch_train(it)
+                if prof is not None:
+                    tp.append(time.perf_counter())
+                    prof.append([b - a for a, b in zip(tp, tp[1:])])
         finally:
             self._bound_this_epoch = False
         _eval_modes(models)

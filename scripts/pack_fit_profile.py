@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--train-batches", type=int, default=8)
     ap.add_argument("--gc-kernel", action="store_true")
     ap.add_argument("--cprofile", action="store_true", help="host-side cProfile of one unwrapped packed fit")
+    ap.add_argument("--host-split", action="store_true",
+                    help="one more fit with REDCLIFF_PACK_PROFILE=1: host ms per epoch enqueueing the evaluation, "
+                         "enqueueing the next training epoch, waiting for the device, digesting the epoch")
     ap.add_argument("--torch-eval", action="store_true",
                     help="comparison: the end-of-fit module modes set with torch's recursive .eval()")
     args = ap.parse_args()
@@ -88,6 +91,21 @@ def main():
     fit(pack)
     torch.cuda.synchronize()
     unwrapped = time.perf_counter() - t0
+    host_split = None
+    if args.host_split:
+        os.environ["REDCLIFF_PACK_PROFILE"] = "1"
+        pack = make_pack()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fit(pack)
+        torch.cuda.synchronize()
+        tot = time.perf_counter() - t0
+        os.environ.pop("REDCLIFF_PACK_PROFILE")
+        pr = np.asarray(pack.last_profile) * 1e3  # [epochs][4] ms
+        phases = {"pretrain": (0, pre), "acclimation": (pre, pre + acc), "combined": (pre + acc, E)}
+        host_split = {"fit_s": round(tot, 4), "columns": ["enqueue_eval", "enqueue_train", "wait_device", "digest"]}
+        for k, (a, b) in phases.items():
+            host_split[k] = [round(float(x), 3) for x in pr[a:b].mean(axis=0)] if b > a else None
     if args.cprofile:
         import cProfile
         import pstats
@@ -142,6 +160,8 @@ def main():
            "breakdown_ms_per_epoch": dict((k, round(1e3 * v / E, 3)) for k, v in sorted(times.items()))}
     if args.gc_kernel:
         out["gc_progress_kernel"] = gc_kernel_time(c)
+    if host_split is not None:
+        out["host_split_ms_per_epoch"] = host_split
     print(json.dumps(out), flush=True)
 
 
