@@ -78,69 +78,72 @@ __device__ inline float draw_value(const StepCtx& c, int r, int k, float raw, fl
 // Cosine similarity of the lag-free conditional GC estimates (metrics.py:342-381), a value
 // only (the reference's torch.Tensor(list) drops its gradient):
 //   v_bk[r][c] = w_bk * G0[k][r][c] + A[c][r] - I[r][c],  cosb[b] = sum_{k1<k2} cos(v_bk1, v_bk2)
-// grid (B, R): one window per workgroup; per pair, lanes take strided elements, wave sums go to
-// LDS and one thread per pair combines the four waves in order.
+// grid (ceil(B / COS_WPW), R), one WAVE per window: the workgroup stages the replica's G0 stack
+// and A^T in LDS once (K p^2 + p^2 floats; read from global memory when they do not fit), then
+// each wave runs its window with no further barrier.  The arithmetic is that of a 256-thread
+// workgroup per window: virtual thread (vw, lane) sums the elements e = 64 vw + lane + 256 i,
+// each virtual wave's sum is lane 0's butterfly sum, the four are added in order, the pairs'
+// cosines in order in double -- bit for bit the one-window-per-workgroup form.
+#define COS_WPW (RC_BLOCK / 64)
+#define COS_LDS 8192  // staged floats
 __global__ __launch_bounds__(RC_BLOCK) void k_cos_values(StepCtx c) {
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.y), b = blockIdx.x, K = d.K, p = d.p, pp2 = p * p;
+  const int r = rc_rep(c, blockIdx.y), K = d.K, p = d.p, pp2 = p * p;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
-  const float* G0 = ws + c.wo.G0;
+  const float* G0g = ws + c.wo.G0;
   const float* A = E + c.eo.A;
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const int npair = K * (K - 1) / 2;
-  __shared__ float part[120][4][3];  // K <= 16: at most 120 pairs
-  __shared__ float wk[16];
+  extern __shared__ float st[];  // (K + 1) p^2 floats when staged (rc_launch_cos_values)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < K) {
-    const float raw = ws[c.wo.w + (int64_t)b * K + tid];
-    wk[tid] = sig ? rc_sigmoid(ecc * raw) : raw;
+  const bool staged = (K + 1) * pp2 <= COS_LDS;
+  const float* G0 = staged ? st : G0g;
+  float* At = st + K * pp2;  // At[e] = A[c][r] for e = r * p + c (staged)
+  if (staged) {
+    for (int e = tid; e < K * pp2; e += RC_BLOCK) st[e] = G0g[e];
+    for (int e = tid; e < pp2; e += RC_BLOCK) {
+      const int rr = e / p, cc = e - rr * p;
+      At[e] = A[cc * p + rr];
+    }
   }
   __syncthreads();
+  const int b = blockIdx.x * COS_WPW + wv;
+  if (b >= c.B) return;
+  float wl = 0.f;  // lane k < K: w_bk
+  if (lane < K) {
+    const float raw = ws[c.wo.w + (int64_t)b * K + lane];
+    wl = sig ? rc_sigmoid(ecc * raw) : raw;
+  }
+  double t = 0.0;
   for (int q = 0; q < npair; ++q) {
     int k1 = 0, rem = q;
     while (rem >= K - 1 - k1) { rem -= K - 1 - k1; ++k1; }
     const int k2 = k1 + 1 + rem;
-    const float w1 = wk[k1], w2 = wk[k2];
+    const float w1 = __shfl(wl, k1, 64), w2 = __shfl(wl, k2, 64);
     float dot = 0.f, n1 = 0.f, n2 = 0.f;
-    for (int e = tid; e < pp2; e += RC_BLOCK) {
-      const int rr = e / p, cc = e - rr * p;
-      const float at = A[cc * p + rr];
-      const float eye = (rr == cc ? 1.f : 0.f);
-      const float v1 = (w1 * G0[(int64_t)k1 * pp2 + e] + at) - eye;
-      const float v2 = (w2 * G0[(int64_t)k2 * pp2 + e] + at) - eye;
-      dot += v1 * v2;
-      n1 += v1 * v1;
-      n2 += v2 * v2;
-    }
-    dot = rc_wave_sum(dot);
-    n1 = rc_wave_sum(n1);
-    n2 = rc_wave_sum(n2);
-    if (lane == 0) {
-      part[q][wv][0] = dot;
-      part[q][wv][1] = n1;
-      part[q][wv][2] = n2;
-    }
-  }
-  __syncthreads();
-  __shared__ double cq[120];
-  if (tid < npair) {
-    float dot = 0.f, n1 = 0.f, n2 = 0.f;
-    for (int w = 0; w < RC_BLOCK / 64; ++w) {
-      dot += part[tid][w][0];
-      n1 += part[tid][w][1];
-      n2 += part[tid][w][2];
+#pragma unroll
+    for (int vw = 0; vw < RC_BLOCK / 64; ++vw) {
+      float pd = 0.f, p1 = 0.f, p2 = 0.f;
+      for (int e = vw * 64 + lane; e < pp2; e += RC_BLOCK) {
+        const int rr = e / p, cc = e - rr * p;
+        const float at = staged ? At[e] : A[cc * p + rr];
+        const float eye = (rr == cc ? 1.f : 0.f);
+        const float v1 = (w1 * G0[(int64_t)k1 * pp2 + e] + at) - eye;
+        const float v2 = (w2 * G0[(int64_t)k2 * pp2 + e] + at) - eye;
+        pd += v1 * v2;
+        p1 += v1 * v1;
+        p2 += v2 * v2;
+      }
+      dot += __shfl(rc_wave_sum(pd), 0, 64);
+      n1 += __shfl(rc_wave_sum(p1), 0, 64);
+      n2 += __shfl(rc_wave_sum(p2), 0, 64);
     }
     const float eps2 = 1e-16f;
-    cq[tid] = (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
+    t += (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
   }
-  __syncthreads();
-  if (tid == 0) {
-    double t = 0.0;
-    for (int q = 0; q < npair; ++q) t += cq[q];
-    reinterpret_cast<double*>(ws + c.wo.cosb)[b] = t;
-  }
+  if (lane == 0) reinterpret_cast<double*>(ws + c.wo.cosb)[b] = t;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1573,7 +1576,9 @@ int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s) {
 
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {
   if (c.d.K < 2 || !(c.flags & RC_VALUES)) return 0;
-  hipLaunchKernelGGL(k_cos_values, dim3(c.B, c.nrep), dim3(RC_BLOCK), 0, s, c);
+  const int st = (c.d.K + 1) * c.d.p * c.d.p;
+  const size_t lds = st <= COS_LDS ? sizeof(float) * st : 0;
+  hipLaunchKernelGGL(k_cos_values, dim3((c.B + COS_WPW - 1) / COS_WPW, c.nrep), dim3(RC_BLOCK), lds, s, c);
   return rc_check(hipGetLastError(), "k_cos_values");
 }
 

@@ -487,30 +487,45 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_l1(const float* x, int64_t n, d
   if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
-// grid (K(K+1)/2 pairs, nsamp): rows i1 <= i2 of sample s (K rows of n floats), each divided by its
-// own max in float64: out[s][i1][i2] = sum_e f1_e f2_e (the diagonal is the squared norm)
-__global__ __launch_bounds__(RC_BLOCK) void k_gc_dots(const float* x, int K, int64_t n, double* out) {
-  int q = blockIdx.x, i1 = 0;
-  while (q >= K - i1) {
-    q -= K - i1;
-    ++i1;
+// grid (ceil(nsamp / 4)), one WAVE per sample: the K rows of sample s (n floats each), each
+// divided by its own max in float64: out[s][i1][i2] = sum_e f1_e f2_e for i1 <= i2 (the diagonal
+// is the squared norm).  The sums are those of a 256-thread workgroup per (sample, pair):
+// virtual thread (vw, lane) sums e = 64 vw + lane + 256 i, each virtual wave's sum is lane 0's
+// butterfly sum, the four are added in order -- the same bits without a block barrier (one
+// workgroup per pair made ~50K tiny workgroups at a packed grid's 5,120 samples).
+#define GD_VW (RC_BLOCK / 64)
+__global__ __launch_bounds__(RC_BLOCK) void k_gc_dots(const float* x, int K, int64_t n, int nsamp, double* out) {
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * (RC_BLOCK / 64) + (threadIdx.x >> 6);
+  if (s >= nsamp) return;
+  const float* xs = x + (int64_t)s * K * n;
+  double mine = 0.0;  // lane i < K: row i's max
+  for (int i = 0; i < K; ++i) {
+    const float* a = xs + (int64_t)i * n;
+    float m = -INFINITY;
+    for (int64_t e = lane; e < n; e += 64) m = fmaxf(m, a[e]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == i) mine = (double)m;
   }
-  const int i2 = i1 + q;
-  const int s = blockIdx.y;
-  const float* a = x + ((int64_t)s * K + i1) * n;
-  const float* b = x + ((int64_t)s * K + i2) * n;
-  __shared__ float redf[RC_BLOCK / 64];
-  __shared__ double redd[RC_BLOCK / 64];
-  float ma = -INFINITY, mb = -INFINITY;
-  for (int64_t i = threadIdx.x; i < n; i += RC_BLOCK) {
-    ma = fmaxf(ma, a[i]);
-    mb = fmaxf(mb, b[i]);
+  for (int i1 = 0; i1 < K; ++i1) {
+    const float* a = xs + (int64_t)i1 * n;
+    const double da = __shfl(mine, i1, 64);
+    for (int i2 = i1; i2 < K; ++i2) {
+      const float* b = xs + (int64_t)i2 * n;
+      const double db = __shfl(mine, i2, 64);
+      double acc = 0.0;
+#pragma unroll
+      for (int vw = 0; vw < GD_VW; ++vw) {
+        double v = 0.;
+        for (int64_t e = vw * 64 + lane; e < n; e += RC_BLOCK) v += ((double)a[e] / da) * ((double)b[e] / db);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc += __shfl(v, 0, 64);
+      }
+      if (lane == 0) out[((int64_t)s * K + i1) * K + i2] = acc;
+    }
   }
-  const double da = (double)gp_block_maxf(ma, redf), db = (double)gp_block_maxf(mb, redf);
-  double acc = 0.;
-  for (int64_t i = threadIdx.x; i < n; i += RC_BLOCK) acc += ((double)a[i] / da) * ((double)b[i] / db);
-  acc = rc_block_sum_d(acc, redd);
-  if (threadIdx.x == 0) out[((int64_t)s * K + i1) * K + i2] = acc;
 }
 
 }  // namespace
@@ -557,7 +572,8 @@ extern "C" int redcliff_gc_track_stats(int32_t n_l1_rows, int64_t l1_len, const 
     if (e) return e;
   }
   if (n_samples > 0) {
-    hipLaunchKernelGGL(k_gc_dots, dim3(K * (K + 1) / 2, n_samples), dim3(RC_BLOCK), 0, s, nolag, K, row_len, dots_out);
+    hipLaunchKernelGGL(k_gc_dots, dim3((n_samples + GD_VW - 1) / GD_VW), dim3(RC_BLOCK), 0, s, nolag, K, row_len,
+                       n_samples, dots_out);
     return rc_check(hipGetLastError(), "k_gc_dots");
   }
   return 0;

@@ -57,10 +57,12 @@ class ParamSnapshot:
     would hold (checkpoints); ``restore_into`` is restore_parameters (parameters only)."""
 
     def __init__(self, model, emb=None, fac=None, bn=None):
-        eng = model.engine()
-        if emb is None or fac is None or bn is None:  # copies of the live buffers: bindings must be current
-            eng.ensure_bound()
         self.model = model
+        if emb is not None and fac is not None and bn is not None:  # rows a packed fit keeps (replicas._PackBest)
+            self.emb, self.fac, self.bn = emb, fac, bn
+            return
+        eng = model.engine()
+        eng.ensure_bound()  # copies of the live buffers: bindings must be current
         with torch.no_grad():
             self.emb = eng.emb.clone() if emb is None else emb
             self.fac = eng.fac.clone() if fac is None else fac
@@ -289,18 +291,133 @@ def confusion_rates_many(cms):
         return TP / (TP + FN), TN / (TN + FP), FP / (FP + TN), FN / (TP + FN), (TP + TN) / (TP + FP + FN + TN)
 
 
-def train_confusion_many(trackers, cms):
+def train_confusion_many(trackers, cms, log=None, cols=None):
     """FitTracker.train_confusion of several fits (cms [Ra][nsup][nsup] integer counts): the
-    confusion rates of all of them in one vectorised pass (exact: integer-valued sums)."""
+    confusion rates of all of them in one vectorised pass (exact: integer-valued sums).  log: a
+    DeferredHistories that holds the rates until its flush (nothing reads cm_train mid-fit)."""
     if not trackers or trackers[0].nsup <= 0:
         return
     TPR, TNR, FPR, FNR, ACC = confusion_rates_many(cms)
+    if log is not None:
+        log.add_confusion(trackers, np.stack([ACC, TPR, TNR, FPR, FNR], axis=1), cols)
+        return
     for i, t in enumerate(trackers):
         for key, v in zip(CM_KEYS, (ACC, TPR, TNR, FPR, FNR)):
             t.cm_train[key].append(v[i].copy())
 
 
-def gc_progress_many(trackers, vals, l1, nrm, dots):
+def _extend_per_graph(hists, cols, G):
+    """_per_graph_appends over a stack of epochs: cols = the epochs' run / n as G python lists
+    (graph-major); returns whether the lengths match."""
+    L = len(hists)
+    if L != G:
+        if G == 1 and L > 1:
+            for h in hists:
+                h.extend(cols[0])
+            return False
+        assert L < G
+    for j in range(L):
+        hists[j].extend(cols[j])
+    return L == G
+
+
+def _stack_log(entries, pick):
+    """Entries [(trackers, cols, arrays...)] of a DeferredHistories log as one [E][T][...] array
+    (T = the fits, by their column -- the pack's replica index, or order of first appearance;
+    NaN where a fit was not active) plus, per fit, its epoch rows (a slice when they are
+    consecutive, as a pack's always are)."""
+    order, colof, bycol = [], {}, {}
+    for e in entries:
+        if e[1] is None:
+            for t in e[0]:
+                if id(t) not in colof:
+                    colof[id(t)] = len(order)
+                    order.append(t)
+        else:
+            bycol.update(zip(e[1], e[0]))
+    if bycol:
+        order = [bycol.get(c) for c in range(max(bycol) + 1)]
+    first = next(pick(e) for e in entries if pick(e) is not None)
+    V = np.full((len(entries), len(order)) + first.shape[1:], np.nan, dtype=first.dtype)
+    present = np.zeros((len(entries), len(order)), dtype=bool)
+    for i, e in enumerate(entries):
+        a = pick(e)
+        if a is None:
+            continue
+        cols = e[1] if e[1] is not None else [colof[id(t)] for t in e[0]]
+        V[i, cols] = a
+        present[i, cols] = True
+    rows = []
+    for j in range(len(order)):
+        idx = np.flatnonzero(present[:, j])
+        if idx.size and idx[-1] - idx[0] + 1 == idx.size:
+            rows.append(slice(int(idx[0]), int(idx[-1]) + 1))
+        else:
+            rows.append(idx)
+    return V, order, rows
+
+
+class DeferredHistories:
+    """The per-epoch history appends of a packed fit that no decision of the fit reads -- the
+    GC-progress histories (f1 / ROC / DeltaCon / path-length / factor-L1) and the train confusion
+    rates -- logged as arrays per epoch and appended to every fit's tracker lists at flush(): the
+    same values in the same order as gc_progress_many / train_confusion_many append them each
+    epoch (the cosine-similarity histories, which the stopping rule reads, stay per epoch).
+    flush() stacks the log into [epoch][fit][...] arrays, divides once, and extends each history
+    list with its fit's column -- one list extend per (fit, history) instead of one python append
+    per (fit, history, epoch).  The packed fit flushes before every checkpoint and at the end."""
+
+    def __init__(self):
+        self.gc, self.cm = [], []
+
+    def add_gc(self, trackers, run, n, l1m, cols=None):
+        """cols: the fits' fixed column indices (a pack's replica indices), else by first appearance."""
+        self.gc.append((list(trackers), None if cols is None else list(cols), run, float(n), l1m))
+
+    def add_confusion(self, trackers, rates, cols=None):
+        self.cm.append((list(trackers), None if cols is None else list(cols), rates))
+
+    def flush(self):
+        if any(e[2] is not None for e in self.gc):
+            V, order, rows = _stack_log(self.gc, lambda e: e[2])  # [E][T][G][6 + p] running sums
+            n = np.asarray([e[3] for e in self.gc], dtype=np.float64)
+            W = V / n[:, None, None, None]  # run / n, as the per-epoch appends divide
+            G, pv = W.shape[2], W.shape[3] - 6
+            for j, (t, rw) in enumerate(zip(order, rows)):
+                if t is None:
+                    continue
+                cols = np.transpose(W[rw, j], (2, 1, 0)).tolist()  # [6 + p][G][E] python floats
+                for c, f1h, roch in ((0, t.f1_hist, t.roc_hist), (2, t.f1_off, t.roc_off)):
+                    for thresh in f1h.keys():
+                        _extend_per_graph(f1h[thresh], cols[c], G)
+                        _extend_per_graph(roch[thresh], cols[c + 1], G)
+                full = _extend_per_graph(t.dc_hist, cols[4], G)
+                _extend_per_graph(t.dcdd_hist, cols[5], G)
+                _extend_per_graph(t.daff_hist, cols[6], G)
+                if full:
+                    for pl in range(1, min(t.p, pv)):
+                        for g in range(len(t.dc_hist)):
+                            t.plm_hist[pl][g].extend(cols[6 + pl][g])
+        if any(e[4] is not None for e in self.gc):
+            V, order, rows = _stack_log(self.gc, lambda e: e[4])  # [E][T][K] factor-L1 means
+            for j, (t, rw) in enumerate(zip(order, rows)):
+                if t is None:
+                    continue
+                X = V[rw, j].T.tolist()
+                for k in range(len(t.l1_hist)):
+                    t.l1_hist[k].extend(X[k])
+        if self.cm:
+            V, order, rows = _stack_log(self.cm, lambda e: e[2])  # [E][T][5][nsup] confusion rates
+            for j, (t, rw) in enumerate(zip(order, rows)):
+                if t is None:
+                    continue
+                C = np.array(V[rw, j])  # one private array per fit: its rows are the appended vectors
+                for k, key in enumerate(CM_KEYS):
+                    t.cm_train[key].extend(list(C[:, k]))
+        self.gc, self.cm = [], []
+
+
+def gc_progress_many(trackers, vals, l1, nrm, dots, log=None, cols=None):
     """FitTracker.gc_progress (device-metrics path) of several fits at once -- a packed grid search
     updates every replica's trackers in a few array operations instead of R python loops.
 
@@ -309,44 +426,52 @@ def gc_progress_many(trackers, vals, l1, nrm, dots):
     (device) or metrics.track_values_host; trackers share GC, nsup, K and p.  With the host
     statistics every appended value is bit-identical to the per-fit trackers' (metrics.track_*):
     the reference's python-float running sums over samples are left-to-right float64 cumulative
-    sums, the history length rules are model_utils.py:63-84 / :136-158."""
+    sums, the history length rules are model_utils.py:63-84 / :136-158.  log: a DeferredHistories
+    that takes every history but the cosine ones until its flush (cols: the fits' columns there)."""
     t0 = trackers[0]
     GC, nsup, K = t0.GC, t0.nsup, t0.K
     S = l1.shape[1]
+    run, n = None, float(S)
     if GC is not None and nsup > 0 and vals is not None and S > 0:
-        n = float(S)
         run = np.cumsum(vals, axis=1)[:, -1]  # (Ra, G, C): _running over samples
-        G = run.shape[1]
-        pv = vals.shape[3] - 6
-        for i, t in enumerate(trackers):
-            for col, f1h, roch in ((0, t.f1_hist, t.roc_hist), (2, t.f1_off, t.roc_off)):
-                for thresh in f1h.keys():
-                    if thresh != 0.0:
-                        raise ValueError("device GC-progress metrics cover the fit's threshold 0.0 only")
-                    f1v, _ = _per_graph_appends(f1h[thresh], run[i, :, col].tolist(), n, G)
-                    rov, _ = _per_graph_appends(roch[thresh], run[i, :, col + 1].tolist(), n, G)
-                    for j in range(len(f1h[thresh])):
-                        f1h[thresh][j].append(f1v[j])
-                        roch[thresh][j].append(rov[j])
-            ri = run[i].tolist()
-            dcv, full = _per_graph_appends(t.dc_hist, [r[4] for r in ri], n, G)
-            dddv, _ = _per_graph_appends(t.dcdd_hist, [r[5] for r in ri], n, G)
-            dafv, _ = _per_graph_appends(t.daff_hist, [r[6] for r in ri], n, G)
-            for j in range(len(t.dc_hist)):
-                t.dc_hist[j].append(dcv[j])
-                t.dcdd_hist[j].append(dddv[j])
-                t.daff_hist[j].append(dafv[j])
-                if full:
-                    for pl in range(1, min(t.p, pv)):
-                        t.plm_hist[pl][j].append(ri[j][6 + pl] / n)
+        for hist in (t0.f1_hist, t0.f1_off):
+            if any(thresh != 0.0 for thresh in hist.keys()):
+                raise ValueError("device GC-progress metrics cover the fit's threshold 0.0 only")
+    l1m = None
     if nsup > 0:  # track_l1_stats over every (sample, factor) estimate
         if S == 0:
             raise IndexError("list index out of range")  # track_l1_stats on an empty sample list
         l1m = np.cumsum(l1, axis=1)[:, -1] / float(S)  # (Ra, K)
-        for i, t in enumerate(trackers):
-            li = l1m[i].tolist()
-            for j in range(len(t.l1_hist)):
-                t.l1_hist[j].append(li[j])
+    if log is not None:
+        log.add_gc(trackers, run, n, l1m, cols)
+    else:
+        if run is not None:
+            G = run.shape[1]
+            pv = vals.shape[3] - 6
+            for i, t in enumerate(trackers):
+                for col, f1h, roch in ((0, t.f1_hist, t.roc_hist), (2, t.f1_off, t.roc_off)):
+                    for thresh in f1h.keys():
+                        f1v, _ = _per_graph_appends(f1h[thresh], run[i, :, col].tolist(), n, G)
+                        rov, _ = _per_graph_appends(roch[thresh], run[i, :, col + 1].tolist(), n, G)
+                        for j in range(len(f1h[thresh])):
+                            f1h[thresh][j].append(f1v[j])
+                            roch[thresh][j].append(rov[j])
+                ri = run[i].tolist()
+                dcv, full = _per_graph_appends(t.dc_hist, [r[4] for r in ri], n, G)
+                dddv, _ = _per_graph_appends(t.dcdd_hist, [r[5] for r in ri], n, G)
+                dafv, _ = _per_graph_appends(t.daff_hist, [r[6] for r in ri], n, G)
+                for j in range(len(t.dc_hist)):
+                    t.dc_hist[j].append(dcv[j])
+                    t.dcdd_hist[j].append(dddv[j])
+                    t.daff_hist[j].append(dafv[j])
+                    if full:
+                        for pl in range(1, min(t.p, pv)):
+                            t.plm_hist[pl][j].append(ri[j][6 + pl] / n)
+        if l1m is not None:
+            for i, t in enumerate(trackers):
+                li = l1m[i].tolist()
+                for j in range(len(t.l1_hist)):
+                    t.l1_hist[j].append(li[j])
     Ra, Sn = dots.shape[0], dots.shape[1]
     for lo, hi, attr in ((0, nsup, "cos_hist"), (nsup, K, "cos_unsup")):  # track_cosine_stats_batched
         if hi - lo < 2 or Sn == 0:

@@ -34,8 +34,8 @@ import torch
 from . import _native as nat
 from . import metrics as M
 from .engine import _stream, flags_for, phase_of_epoch
-from .fit_loop import (FitTracker, ParamSnapshot, conditional_gc_estimates, confusion_rates_many, gc_progress_many,
-                       restore_parameters, standalone_copy, train_confusion_many)
+from .fit_loop import (DeferredHistories, FitTracker, ParamSnapshot, conditional_gc_estimates, confusion_rates_many,
+                       gc_progress_many, restore_parameters, standalone_copy, train_confusion_many)
 
 
 class ReplicaPack:
@@ -84,6 +84,7 @@ class ReplicaPack:
             e.bind_optimizer("B", oB)
         # BatchNorm num_batches_tracked of every replica as a 0-d view of one [R] tensor, so a
         # packed launch chain advances all of them with one add instead of R small launches
+        self._mod_dicts = _module_dicts(self.models)  # for fit()'s end-of-epoch module modes
         self.nbt = torch.zeros(R, device=dev, dtype=torch.long)
         for r, e in enumerate(self.engines):
             bn = e.dgcnn.BN1
@@ -124,6 +125,11 @@ class ReplicaPack:
         return self._dims(self.ws_B, T)
 
     def _hyper(self):
+        if self._bound_this_epoch:
+            # inside fit(): nothing changes a coefficient, learning rate or BatchNorm setting of
+            # a replica, so the [R] hyper-parameter rows built at the fit's first launch stand
+            # (R key computations per launch were ~1 ms of host time per epoch at R = 128)
+            return self._hyper_cat
         parts = [e._hyper() for e in self.engines]
         key = tuple(e.hyper_key for e in self.engines)
         if key != getattr(self, "_hyper_key", None):
@@ -365,6 +371,7 @@ class ReplicaPack:
         model gets ``fit_history`` as a single fit would."""
         if output_length != 1:
             raise NotImplementedError("output_length must be 1")
+        t_in = time.perf_counter()
         R, models = self.R, self.models
         for m in models:
             if not m.fused_supported() or "Freeze" in m.training_mode or m.__dict__.get("_factors_detached"):
@@ -396,6 +403,7 @@ class ReplicaPack:
             raise NotImplementedError("packed fits track GC progress on the device (no wavelet_level, 2 <= p <= 64, "
                                       "conditional modes); fit these models one by one")
         best = _PackBest(self)
+        hlog = DeferredHistories()
         active = list(range(R))
         nfirst = min(int(val["sizes"][0]), m0.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING)
         Xv = val["X"][:nfirst, :Lm, :]
@@ -406,6 +414,8 @@ class ReplicaPack:
         # bindings of all R engines are checked once per fit, not per launch
         self._bound_this_epoch = False
         self._ensure_bound()
+        self._hyper_key = None
+        self._hyper()  # the fit's hyper-parameter rows (fixed from here on, see _hyper)
         self._bound_this_epoch = True
         # Overlap: while the host digests epoch `it` (trackers, stopping rule, snapshots), the GPU
         # already trains epoch it + 1 for the replicas still active (speculatively).  The state
@@ -432,6 +442,7 @@ class ReplicaPack:
         # the next epoch's training, waiting for the device, digesting the epoch) -> self.last_profile
         prof = [] if os.environ.get("REDCLIFF_PACK_PROFILE", "0") != "0" else None
         self.last_profile = prof
+        t_loop = time.perf_counter()
         try:
             it = 0
             if max_iter > 0:
@@ -481,8 +492,8 @@ class ReplicaPack:
                 nat.raise_on_status(got[5], nat.status_view(self.ws, self.ws_off, R), "packed fit epoch %d" % it)
                 vals = got[6].reshape(Ra, S, *got[6].shape[1:]) if vals_d is not None else None
                 if nsup > 0:
-                    train_confusion_many(tr_act, cms.reshape(R, nsup, nsup)[active])
-                gc_progress_many(tr_act, vals, *M.track_values_finish(l1, dots))
+                    train_confusion_many(tr_act, cms.reshape(R, nsup, nsup)[active], log=hlog, cols=active)
+                gc_progress_many(tr_act, vals, *M.track_values_finish(l1, dots), log=hlog, cols=active)
                 ns = max(nsup, 1)
                 conf = conf.reshape(R, ns, ns)
                 nb = float(val["len"])
@@ -504,7 +515,8 @@ class ReplicaPack:
                     self._roll_back(stopped, steps_before)
                 active = [r for r in active if r not in stopped]
                 if dirs is not None and it % check_every == 0:
-                    _eval_modes(models)
+                    hlog.flush()
+                    _eval_modes(models, self._mod_dicts)
                     for r in active:
                         trackers[r].checkpoint(dirs[r], it, optimizers=self.optimizers[r], save_plots=save_plots)
                 it += 1
@@ -513,18 +525,31 @@ class ReplicaPack:
                 if prof is not None:
                     tp.append(time.perf_counter())
                     prof.append([b - a for a, b in zip(tp, tp[1:])])
+            t_end_loop = time.perf_counter()
+            # ---- restore best parameters and the final validation (:1621-1647), enqueued first
+            # (the bindings checked at the fit's start still hold); the host flushes the deferred
+            # histories and writes the module modes while they run
+            snaps = [t.best_model for t in trackers]
+            if all(isinstance(b, _PackSnapshot) and b._best is best and b._r == r for r, b in enumerate(snaps)):
+                with torch.no_grad():  # every replica's restore_parameters as two row-wise copies
+                    self.emb.copy_(best.emb)
+                    self.fac.copy_(best.fac)
+            else:
+                for r, m in enumerate(models):
+                    restore_parameters(m, snaps[r])
+            for e in self.engines:
+                e.supports_fresh = False
+            final = M.fetch_async(list(self._values(val, host=False)))
         finally:
             self._bound_this_epoch = False
-        _eval_modes(models)
-        # ---- restore best parameters, final files and validation (:1621-1647)
+        hlog.flush()
+        _eval_modes(models, self._mod_dicts)
+        acc, conf = final.wait()
+        conf = conf.astype(np.int32).reshape(R, max(nsup, 1), max(nsup, 1))
         for r, m in enumerate(models):
-            restore_parameters(m, trackers[r].best_model)
             if dirs is not None:
                 os.makedirs(dirs[r], exist_ok=True)
                 torch.save(standalone_copy(m), os.path.join(dirs[r], "final_best_model.bin"))
-        for e in self.engines:
-            e.supports_fresh = False
-        acc, conf = self._values(val)
         nb = float(val["len"])
         finals = []
         for r, m in enumerate(models):
@@ -532,20 +557,36 @@ class ReplicaPack:
             v = m._validation_tuple(acc[r], nb, conf[r], *hist)
             finals.append(v[-6] if nsup > 0 else v[-1])
             m.fit_history = trackers[r].history()
+        if prof is not None:  # host seconds before the epoch loop, in it, after it
+            self.last_profile_edges = (t_loop - t_in, t_end_loop - t_loop, time.perf_counter() - t_end_loop)
         return finals
 
 
-def _eval_modes(models):
+def _module_dicts(models):
+    """The __dict__ of every submodule of the embedders and factors of `models` (the modules
+    whose train flags fit() leaves False), walked once with an explicit stack."""
+    out, stack = [], []
+    for m in models:
+        stack.append(m.factor_score_embedder)
+        stack.extend(m.factors)
+    while stack:
+        d = stack.pop().__dict__
+        out.append(d)
+        stack.extend(c for c in d["_modules"].values() if c is not None)
+    return out
+
+
+def _eval_modes(models, dicts=None):
     """The module modes every fit epoch ends in (GC tracking + validate_training call .eval() on
     the embedder and every factor, ...withStateSmoothing.py:1366-1480).  The flags are written
     directly (Module.train(False) sets exactly this attribute on every submodule; no module of
     this package overrides train()): torch's recursive .eval() with its __setattr__ per module
-    cost ~110 ms per 128-fit pack (28,800 modules), a fifth of a packed D4IC fit's wall clock."""
-    for m in models:
-        for root in (m.factor_score_embedder, *m.factors):
-            for mod in root.modules():
-                if mod.training:
-                    mod.__dict__["training"] = False
+    cost ~110 ms per 128-fit pack (28,800 modules), a fifth of a packed D4IC fit's wall clock.
+    dicts: the modules' __dict__s listed when the pack was built (ReplicaPack._mod_dicts, the
+    pack's fixed module trees), so the fit writes 28,800 flags without walking the trees."""
+    for d in (_module_dicts(models) if dicts is None else dicts):
+        if d["training"]:
+            d["training"] = False
 
 
 class _PackBest:
@@ -564,8 +605,7 @@ class _PackBest:
 
     def mark(self, r):
         self.marked.append(r)
-        return ParamSnapshot(self.pack.models[r], emb=self.emb[r], fac=self.fac[r],
-                             bn=(self.bn[0][r], self.bn[1][r], self.nbt[r]))
+        return _PackSnapshot(self, r)
 
     def copy_marked(self, src=None):
         """src: a dict of [R][...] buffers holding the epoch's state (ReplicaPack._prev while the
@@ -582,6 +622,28 @@ class _PackBest:
             self.bn.index_copy_(1, idx, s["bn"].index_select(1, idx))
             self.nbt.index_copy_(0, idx, s["nbt"].index_select(0, idx))
         self.marked = []
+
+
+class _PackSnapshot(ParamSnapshot):
+    """ParamSnapshot of replica r whose buffers are r's rows of a _PackBest, taken as views when
+    first read (an improving replica's snapshot per epoch is then one small object)."""
+
+    def __init__(self, best, r):  # noqa: super().__init__ is not called: the rows stand for its copies
+        self.model = best.pack.models[r]
+        self._best, self._r = best, r
+
+    @property
+    def emb(self):
+        return self._best.emb[self._r]
+
+    @property
+    def fac(self):
+        return self._best.fac[self._r]
+
+    @property
+    def bn(self):
+        b, r = self._best, self._r
+        return (b.bn[0][r], b.bn[1][r], b.nbt[r])
 
 
 def grid_packs(models_and_opts, max_replicas=64):

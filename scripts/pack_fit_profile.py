@@ -56,7 +56,7 @@ def main():
     from redcliff_amd import fit_loop, replicas
     from redcliff_amd import metrics as M
     if args.torch_eval:
-        def torch_eval_modes(models):
+        def torch_eval_modes(models, dicts=None):
             for m in models:
                 m.factor_score_embedder.eval()
                 for f in m.factors:
@@ -104,6 +104,8 @@ def main():
         pr = np.asarray(pack.last_profile) * 1e3  # [epochs][4] ms
         phases = {"pretrain": (0, pre), "acclimation": (pre, pre + acc), "combined": (pre + acc, E)}
         host_split = {"fit_s": round(tot, 4), "columns": ["enqueue_eval", "enqueue_train", "wait_device", "digest"]}
+        host_split["before_loop_ms"], host_split["loop_ms"], host_split["after_loop_ms"] = [
+            round(1e3 * x, 2) for x in pack.last_profile_edges]
         for k, (a, b) in phases.items():
             host_split[k] = [round(float(x), 3) for x in pr[a:b].mean(axis=0)] if b > a else None
     if args.cprofile:

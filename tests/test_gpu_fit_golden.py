@@ -146,10 +146,17 @@ def compare_hist(tag, h, d, prefix, rtol=1e-4, env=None, part=None):
 
 
 def compare_state_envelope(tag, model, want, env, part, rtol=2e-4, atol=5e-6):
-    """compare_state's tolerance, widened entry-wise to the reference realizations' spread with the
-    leave-one-out allowance the merge step recorded (tests/golden/make_fit_envelope.py)."""
+    """compare_state's tolerance, widened entry-wise to the reference realizations' spread
+    (tests/golden/make_fit_envelope.py).  The GPU fit is held to what the reference's own
+    realizations show against each other over the WHOLE state: its count of entries beyond
+    max(tolerance, the realizations' spread) must not exceed the largest leave-one-out count of a
+    realization (entries where it leaves max(tolerance, the other realizations' spread), summed
+    over every tensor), and no entry may exceed max(tolerance, 3 x spread).  (Per tensor, a count
+    taken over four realizations is too noisy a statistic: the published-lr D4IC resume has
+    realizations with 0 and with 50 such entries.)"""
     got = dict((k, v.detach().cpu().numpy()) for k, v in model.state_dict().items() if not k.startswith("gen_model."))
     assert set(got) == set(want), tag
+    n_out, loo_total, worst = 0, None, 0.0
     for k in want:
         if k.endswith("num_batches_tracked"):
             assert int(got[k]) == int(want[k]), tag + k
@@ -157,8 +164,22 @@ def compare_state_envelope(tag, model, want, env, part, rtol=2e-4, atol=5e-6):
         w = want[k].astype(np.float64)
         scale = max(1.0, float(np.abs(w).max()))
         base = rtol * np.abs(w) + atol * scale
-        within_envelope("%s/%s" % (tag, k), got[k], w, base, env["%s/env/%s" % (part, k)].astype(np.float64)[None],
-                        loo_allowed=int(np.max(env["%s/loo/%s" % (part, k)])))
+        spread = env["%s/env/%s" % (part, k)].astype(np.float64)
+        dev = np.abs(got[k].astype(np.float64) - w)
+        nk = int(np.sum(dev > np.maximum(base, spread)))
+        wk = float(np.max(dev / np.maximum(np.maximum(base, 3.0 * spread), 1e-30))) if dev.size else 0.0
+        if nk:
+            print("%s/%s: %d entries beyond max(tol, reference spread); worst %.2f of max(tol, 3 x spread)"
+                  % (tag, k, nk, wk))
+        n_out += nk
+        worst = max(worst, wk)
+        lk = np.asarray(env["%s/loo/%s" % (part, k)], dtype=np.int64)
+        loo_total = lk if loo_total is None else loo_total + lk
+    allowed = int(np.max(loo_total))
+    print("%s: %d state entries beyond max(tol, reference spread); the realizations' leave-one-out counts %s "
+          "(allowed %d); worst %.2f of max(tol, 3 x spread)" % (tag, n_out, loo_total.tolist(), allowed, worst))
+    assert n_out <= allowed, (tag, n_out, allowed)
+    assert worst <= 1.0, (tag, worst)
 
 
 @pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub"])

@@ -63,3 +63,48 @@ def test_gc_progress_many_bitwise(p, K, nsup, nG, S, Sn, ls):
         assert all(len(h) == epochs for h in sa["cos_hist"].values())
         for k in sa:
             assert _same(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize("with_cols", [False, True])
+@pytest.mark.parametrize("p,K,nsup,nG,S,Sn,ls", [(10, 4, 4, 4, 4, 40, 4), (5, 3, 3, 1, 3, 9, 2), (8, 5, 3, 3, 3, 12, 5)])
+def test_deferred_histories_bitwise(p, K, nsup, nG, S, Sn, ls, with_cols):
+    """DeferredHistories (the packed fit's per-epoch log, flushed before checkpoints and at the
+    end) appends the same values, in the same order, as the per-epoch appends -- with replicas
+    leaving the active set (early stopping) and a flush in the middle (a checkpoint epoch)."""
+    rng = np.random.RandomState(7 * p + K)
+    GC = [(rng.rand(p, p, ls) < 0.3).astype(np.float64) for _ in range(nG)]
+    R, epochs = 4, 6
+    now = [_tracker(p, K, nsup, GC) for _ in range(R)]
+    lazy = [_tracker(p, K, nsup, GC) for _ in range(R)]
+    log = fit_loop.DeferredHistories()
+    G = min(K, nG)
+    active = list(range(R))
+    for e in range(epochs):
+        Ra = len(active)
+        est = rng.rand(Ra, S, K, p, p, ls).astype(np.float32)
+        nolag = (rng.rand(Ra, Sn, K, p, p, 1).astype(np.float32) - 0.1)
+        vals = rng.randn(Ra, S, G, 6 + p)
+        stats = M.track_values_host(est, nolag)
+        fit_loop.gc_progress_many([now[r] for r in active], vals, *stats)
+        cols = active if with_cols else None  # the pack passes its replica indices
+        fit_loop.gc_progress_many([lazy[r] for r in active], vals, *stats, log=log, cols=cols)
+        cms = rng.randint(0, 50, size=(Ra, max(nsup, 1), max(nsup, 1)))
+        fit_loop.train_confusion_many([now[r] for r in active], cms)
+        fit_loop.train_confusion_many([lazy[r] for r in active], cms, log=log, cols=cols)
+        # the cosine histories (the stopping rule reads them) are appended at once
+        for r in active:
+            assert _same(now[r].cos_hist, lazy[r].cos_hist)
+        if e == 2:
+            log.flush()
+            for a, b in zip(now, lazy):
+                assert _same(_state(a), _state(b))
+        if e == 1:
+            active = [0, 1, 3]  # replica 2 stopped at epoch 1
+        if e == 3:
+            active = [1, 3]
+    log.flush()
+    for a, b in zip(now, lazy):
+        sa, sb = _state(a), _state(b)
+        for k in sa:
+            assert _same(sa[k], sb[k]), k
+    assert len(now[2].l1_hist[0]) == 2 and len(now[1].l1_hist[0]) == epochs
