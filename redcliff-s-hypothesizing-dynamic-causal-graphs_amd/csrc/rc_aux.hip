@@ -7,65 +7,43 @@
 
 namespace {
 
-// One workgroup per (factor, network) of a replica: G[e] = ||W0[:, e]|| over the h hidden units
-// (e = c * L + t) and G0[c] = the norm over hidden units and lags.  The h x Q weight block is
-// staged through LDS in chunks of GN_CHUNK floats (one round of coalesced loads per chunk,
-// every thread's loads in flight together); each output keeps its ascending (u[, t]) fmaf
-// order across the chunks, so the sums are the single-pass loop's bit for bit.  Outputs
-// o < Q are G columns, Q <= o < Q + p the G0 channels; thread tid owns o = tid + k * RC_BLOCK.
-#define GN_CHUNK 8192
-#define GN_OUT 8  // outputs per thread (Q + p <= GN_OUT * RC_BLOCK; redcliff_gc_norms checks)
+// One WAVE per (factor, network) of a replica (four per workgroup): G[e] = ||W0[:, e]|| over the
+// h hidden units (e = c * L + t) and G0[c] = the norm over hidden units and lags.  Lane l owns
+// the outputs o = l + 64 k (o < Q: G columns, Q <= o < Q + p: G0 channels) and sums them in
+// ascending (u[, t]) fmaf order straight from global memory (the G lanes' rows are one
+// coalesced 4 Q-byte read per hidden unit; the G0 lanes re-read the same lines from cache).
+// Short waves are dispatch-bound at a packed grid's size: a 256-thread workgroup per network
+// (20,480 waves at R = 128 D4IC) ran 83-94 us, a quarter of the waves is the lever.
+#define GN_WPG (RC_BLOCK / 64)
 __global__ __launch_bounds__(RC_BLOCK) void k_gc_norms(RedcliffDims d, const float* fac, int64_t fs, FacOff fo,
                                                        float* G, float* G0) {
-  extern __shared__ float Ws[];  // uc * Q floats (redcliff_gc_norms)
-  const int r = blockIdx.y, kj = blockIdx.x, tid = threadIdx.x;
+  const int r = blockIdx.y, lane = threadIdx.x & 63;
+  const int kj = blockIdx.x * GN_WPG + (threadIdx.x >> 6);
   const int p = d.p, h = d.h, L = d.L, Q = p * L, nout = Q + p;
+  if (kj >= d.K * p) return;
   const float* W = fac + r * fs + fo.W0 + (int64_t)kj * h * Q;
   float* Gr = G + ((int64_t)r * d.K * p + kj) * Q;
   float* G0r = G0 + ((int64_t)r * d.K * p + kj) * p;
-  const int uc = GN_CHUNK / Q < h ? GN_CHUNK / Q : h;  // hidden units per chunk (>= 1: Q <= GN_CHUNK)
-  const RcDiv dl(L);
-  float s[GN_OUT];
-#pragma unroll
-  for (int k = 0; k < GN_OUT; ++k) s[k] = 0.f;
-  for (int u0 = 0; u0 < h; u0 += uc) {
-    const int nu = (h - u0) < uc ? (h - u0) : uc, n = nu * Q;
-    const float* src = W + (int64_t)u0 * Q;
-    __syncthreads();  // the previous chunk's reads are done
-#pragma unroll 8
-    for (int i = tid; i < n; i += RC_BLOCK) Ws[i] = src[i];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < GN_OUT; ++k) {
-      const int o = tid + k * RC_BLOCK;
-      if (o < Q) {
-        float a = s[k];
-#pragma unroll 8
-        for (int u = 0; u < nu; ++u) {
-          const float x = Ws[u * Q + o];
-          a += x * x;
-        }
-        s[k] = a;
-      } else if (o < nout) {
-        // (u, t) in u-major order as one flat index, so the unrolled LDS reads issue ahead of
-        // the serial fmaf chain (a nested loop over a runtime L kept one read in flight)
-        const float* wr = Ws + (o - Q) * L;
-        float a = s[k];
-#pragma unroll 8
-        for (int j = 0; j < nu * L; ++j) {
-          const int u = dl.div(j);
-          const float x = wr[u * Q + (j - u * L)];
-          a += x * x;
-        }
-        s[k] = a;
+  for (int o = lane; o < nout; o += 64) {
+    float a = 0.f;
+    if (o < Q) {
+#pragma unroll 10
+      for (int u = 0; u < h; ++u) {
+        const float x = W[(int64_t)u * Q + o];
+        a += x * x;
       }
+      Gr[o] = sqrtf(a);
+    } else {
+      const float* wr = W + (o - Q) * L;
+      for (int u = 0; u < h; ++u) {
+#pragma unroll 4
+        for (int t = 0; t < L; ++t) {
+          const float x = wr[(int64_t)u * Q + t];
+          a += x * x;
+        }
+      }
+      G0r[o - Q] = sqrtf(a);
     }
-  }
-#pragma unroll
-  for (int k = 0; k < GN_OUT; ++k) {
-    const int o = tid + k * RC_BLOCK;
-    if (o < Q) Gr[o] = sqrtf(s[k]);
-    else if (o < nout) G0r[o - Q] = sqrtf(s[k]);
   }
 }
 
@@ -139,14 +117,10 @@ extern "C" int redcliff_adam_apply(const RedcliffDims* d, float* params, float* 
 extern "C" int redcliff_gc_norms(const RedcliffDims* d, const float* fac, int64_t fac_stride, float* G, float* G0,
                                  void* stream) {
   if (!d || !fac || !G || !G0) { rc_set_error("gc_norms: null argument"); return REDCLIFF_EINVAL; }
-  if (d->p > 64 || d->h > 4096 || d->p * d->L > GN_CHUNK || d->p * d->L + d->p > GN_OUT * RC_BLOCK) {
-    rc_set_error("gc_norms: p = %d, L = %d, h = %d outside p <= 64, p * (L + 1) <= %d, h <= 4096", d->p, d->L, d->h,
-                 GN_OUT * RC_BLOCK);
-    return REDCLIFF_ELIMIT;
-  }
-  const int Q = d->p * d->L, uc = GN_CHUNK / Q < d->h ? GN_CHUNK / Q : d->h;
-  hipLaunchKernelGGL(k_gc_norms, dim3(d->K * d->p, d->R), dim3(RC_BLOCK), sizeof(float) * uc * Q,
-                     (hipStream_t)stream, *d, fac, fac_stride, rc_fac_off(*d), G, G0);
+  if (d->p > 64 || d->h > 4096) { rc_set_error("gc_norms: p > 64 or h > 4096"); return REDCLIFF_ELIMIT; }
+  const int nwg = (d->K * d->p + GN_WPG - 1) / GN_WPG;
+  hipLaunchKernelGGL(k_gc_norms, dim3(nwg, d->R), dim3(RC_BLOCK), 0, (hipStream_t)stream, *d, fac, fac_stride,
+                     rc_fac_off(*d), G, G0);
   return rc_check(hipGetLastError(), "k_gc_norms");
 }
 

@@ -78,13 +78,14 @@ __device__ inline float draw_value(const StepCtx& c, int r, int k, float raw, fl
 // Cosine similarity of the lag-free conditional GC estimates (metrics.py:342-381), a value
 // only (the reference's torch.Tensor(list) drops its gradient):
 //   v_bk[r][c] = w_bk * G0[k][r][c] + A[c][r] - I[r][c],  cosb[b] = sum_{k1<k2} cos(v_bk1, v_bk2)
-// grid (ceil(B / COS_WPW), R), one WAVE per window: the workgroup stages the replica's G0 stack
-// and A^T in LDS once (K p^2 + p^2 floats; read from global memory when they do not fit), then
-// each wave runs its window with no further barrier.  The arithmetic is that of a 256-thread
+// grid (ceil(B / COS_WPW), R), one WAVE per COS_WPV windows: the workgroup stages the replica's
+// G0 stack and A^T in LDS once (K p^2 + p^2 floats; read from global memory when they do not
+// fit), then each wave runs its windows with no further barrier.  The arithmetic is that of a 256-thread
 // workgroup per window: virtual thread (vw, lane) sums the elements e = 64 vw + lane + 256 i,
 // each virtual wave's sum is lane 0's butterfly sum, the four are added in order, the pairs'
 // cosines in order in double -- bit for bit the one-window-per-workgroup form.
-#define COS_WPW (RC_BLOCK / 64)
+#define COS_WPV 1                             // windows per wave (2: no faster at R = 128 D4IC)
+#define COS_WPW (COS_WPV * (RC_BLOCK / 64))  // windows per workgroup
 #define COS_LDS 8192  // staged floats
 __global__ __launch_bounds__(RC_BLOCK) void k_cos_values(StepCtx c) {
   const RedcliffDims& d = c.d;
@@ -109,41 +110,76 @@ __global__ __launch_bounds__(RC_BLOCK) void k_cos_values(StepCtx c) {
     }
   }
   __syncthreads();
-  const int b = blockIdx.x * COS_WPW + wv;
-  if (b >= c.B) return;
-  float wl = 0.f;  // lane k < K: w_bk
-  if (lane < K) {
-    const float raw = ws[c.wo.w + (int64_t)b * K + lane];
-    wl = sig ? rc_sigmoid(ecc * raw) : raw;
-  }
-  double t = 0.0;
-  for (int q = 0; q < npair; ++q) {
-    int k1 = 0, rem = q;
-    while (rem >= K - 1 - k1) { rem -= K - 1 - k1; ++k1; }
-    const int k2 = k1 + 1 + rem;
-    const float w1 = __shfl(wl, k1, 64), w2 = __shfl(wl, k2, 64);
-    float dot = 0.f, n1 = 0.f, n2 = 0.f;
+  // virtual waves holding elements (the others add exact +0 sums: one +0.f stands for them)
+  const int nvw = (pp2 + 63) / 64 < RC_BLOCK / 64 ? (pp2 + 63) / 64 : RC_BLOCK / 64;
+  // p^2 <= RC_BLOCK: one element per virtual thread, its pair-independent terms kept in registers
+  const bool one = pp2 <= RC_BLOCK;
+  float atv[RC_BLOCK / 64], eyev[RC_BLOCK / 64];
 #pragma unroll
-    for (int vw = 0; vw < RC_BLOCK / 64; ++vw) {
-      float pd = 0.f, p1 = 0.f, p2 = 0.f;
-      for (int e = vw * 64 + lane; e < pp2; e += RC_BLOCK) {
-        const int rr = e / p, cc = e - rr * p;
-        const float at = staged ? At[e] : A[cc * p + rr];
-        const float eye = (rr == cc ? 1.f : 0.f);
-        const float v1 = (w1 * G0[(int64_t)k1 * pp2 + e] + at) - eye;
-        const float v2 = (w2 * G0[(int64_t)k2 * pp2 + e] + at) - eye;
-        pd += v1 * v2;
-        p1 += v1 * v1;
-        p2 += v2 * v2;
-      }
-      dot += __shfl(rc_wave_sum(pd), 0, 64);
-      n1 += __shfl(rc_wave_sum(p1), 0, 64);
-      n2 += __shfl(rc_wave_sum(p2), 0, 64);
+  for (int vw = 0; vw < RC_BLOCK / 64; ++vw) {
+    const int e = vw * 64 + lane;
+    atv[vw] = 0.f;
+    eyev[vw] = 0.f;
+    if (one && e < pp2) {
+      const int rr = e / p, cc = e - rr * p;
+      atv[vw] = staged ? At[e] : A[cc * p + rr];
+      eyev[vw] = (rr == cc ? 1.f : 0.f);
     }
-    const float eps2 = 1e-16f;
-    t += (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
   }
-  if (lane == 0) reinterpret_cast<double*>(ws + c.wo.cosb)[b] = t;
+  for (int b = (blockIdx.x * (RC_BLOCK / 64) + wv) * COS_WPV, bend = min(c.B, b + COS_WPV); b < bend; ++b) {
+    float wl = 0.f;  // lane k < K: w_bk
+    if (lane < K) {
+      const float raw = ws[c.wo.w + (int64_t)b * K + lane];
+      wl = sig ? rc_sigmoid(ecc * raw) : raw;
+    }
+    double t = 0.0;
+    for (int q = 0; q < npair; ++q) {
+      int k1 = 0, rem = q;
+      while (rem >= K - 1 - k1) { rem -= K - 1 - k1; ++k1; }
+      const int k2 = k1 + 1 + rem;
+      const float w1 = __shfl(wl, k1, 64), w2 = __shfl(wl, k2, 64);
+      const float* g1 = G0 + (int64_t)k1 * pp2;
+      const float* g2 = G0 + (int64_t)k2 * pp2;
+      float dot = 0.f, n1 = 0.f, n2 = 0.f;
+#pragma unroll
+      for (int vw = 0; vw < RC_BLOCK / 64; ++vw) {
+        if (vw >= nvw) break;
+        float pd = 0.f, p1 = 0.f, p2 = 0.f;
+        if (one) {
+          const int e = vw * 64 + lane;
+          if (e < pp2) {
+            const float v1 = (w1 * g1[e] + atv[vw]) - eyev[vw];
+            const float v2 = (w2 * g2[e] + atv[vw]) - eyev[vw];
+            pd += v1 * v2;  // fmaf onto +0, as the strided loop's first step (not a bare product)
+            p1 += v1 * v1;
+            p2 += v2 * v2;
+          }
+        } else {
+          for (int e = vw * 64 + lane; e < pp2; e += RC_BLOCK) {
+            const int rr = e / p, cc = e - rr * p;
+            const float at = staged ? At[e] : A[cc * p + rr];
+            const float eye = (rr == cc ? 1.f : 0.f);
+            const float v1 = (w1 * g1[e] + at) - eye;
+            const float v2 = (w2 * g2[e] + at) - eye;
+            pd += v1 * v2;
+            p1 += v1 * v1;
+            p2 += v2 * v2;
+          }
+        }
+        dot += __shfl(rc_wave_sum(pd), 0, 64);
+        n1 += __shfl(rc_wave_sum(p1), 0, 64);
+        n2 += __shfl(rc_wave_sum(p2), 0, 64);
+      }
+      if (nvw < RC_BLOCK / 64) {
+        dot += 0.f;
+        n1 += 0.f;
+        n2 += 0.f;
+      }
+      const float eps2 = 1e-16f;
+      t += (double)(dot / sqrtf(fmaxf(n1, eps2) * fmaxf(n2, eps2)));
+    }
+    if (lane == 0) reinterpret_cast<double*>(ws + c.wo.cosb)[b] = t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------

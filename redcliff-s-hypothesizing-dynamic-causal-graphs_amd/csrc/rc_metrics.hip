@@ -14,13 +14,20 @@
 // affinity matrices and distances float64 (inverses by Gauss-Jordan with partial pivoting where
 // numpy calls LAPACK).  F1 is the float32 arithmetic of get_f1_score on exact counts; ROC-AUC
 // is the Mann-Whitney form of sklearn's trapezoidal area (ties count 1/2), from exact counts.
+#include <cstdlib>
+#include <cstring>
+
 #include "rc_common.h"
 
 namespace {
 
 // Threads per workgroup NT: 1024 for p > 32 (16 waves keep the LDS / FP64 latencies of one
-// (sample, graph) hidden; one workgroup per CU at 36 p^2 bytes of LDS, p = 64), 256 for p <= 32
-// (a D4IC-sized graph has 100 entries: fewer idle lanes per barrier, several workgroups per CU).
+// (sample, graph) hidden; one workgroup per CU at 36 p^2 bytes of LDS, p = 64), 256 for
+// 16 < p <= 32, 64 for p <= 16: one wave per (sample, graph), whose ~300 barriers (four
+// Gauss-Jordan inverses, the path-length powers) are then single-wave barriers -- a D4IC-sized
+// packed grid's 2,048 (sample, graph) workgroups ran 178 us with four waves each.  The NT = 64
+// form sums its float64 terms in the 256-thread form's association (gp_sum_terms), so every
+// metric is the same bits (REDCLIFF_GCP_WAVE=0 keeps the 256-thread form).
 #define GP_NR 4     // matrix elements per thread: p * p <= GP_NR * NT
 
 // numpy's float32 pairwise sum of a contiguous run (loops_utils.h.src, n <= 128)
@@ -88,6 +95,30 @@ __device__ inline float gp_block_max(float v, float* red) {
   for (int i = 1; i < NT / 64; ++i) m = fmaxf(m, red[i]);
   __syncthreads();
   return m;
+}
+
+// Sum of per-element float64 terms tu[u] (element e = tid + u * NT, 0 where e >= p * p) in the
+// arithmetic of the 256-thread workgroup: thread partials, each wave's butterfly sum (lane 0's),
+// the waves in order.  NT = 64 (one wave per (sample, graph), p * p <= 256): the 256-thread
+// workgroup's thread t held exactly element t, so its wave u is this wave's term u -- the same
+// association without a block barrier.
+template <int NT>
+__device__ inline double gp_sum_terms(const double* tu, double* redd) {
+  if (NT == 64) {
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < GP_NR; ++u) {
+      double v = tu[u];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      s += __shfl(v, 0, 64);
+    }
+    return s;
+  }
+  double acc = 0.;
+#pragma unroll
+  for (int u = 0; u < GP_NR; ++u) acc += tu[u];
+  return rc_block_sum_d(acc, redd);
 }
 
 // inverse of the p x p float64 matrix in the left half of Aug[p][2p] (right half := I):
@@ -212,6 +243,7 @@ __global__ __launch_bounds__(NT) void k_gc_progress(int S, int nE, int G, int p,
   __shared__ int cnt[2];
   __shared__ int redi[4];
   __shared__ double degT[64], degE[64];
+  __shared__ double seb[NT == 64 ? GP_NR * 64 : 1];  // NT = 64: per-element terms, element order
 
   // estimate summed over lags: numpy float32 pairwise order
   const float* ep = est + ((int64_t)s * nE + g) * pp * Lt;
@@ -336,17 +368,18 @@ __global__ __launch_bounds__(NT) void k_gc_progress(int S, int nE, int G, int p,
         }
         __syncthreads();
       } else {
-        double acc = 0.;
+        double tu[GP_NR];
 #pragma unroll
         for (int u = 0; u < GP_NR; ++u) {
           const int e = tid + u * NT;
+          tu[u] = 0.;
           if (e < pp) {
             const int i = e / p, j = e - i * p;
             const double df = sqrt(sreg[u]) - sqrt(Aug[i * 2 * p + p + j]);
-            acc += df * df;
+            tu[u] = df * df;
           }
         }
-        const double d = sqrt(rc_block_sum_d(acc, redd));
+        const double d = sqrt(gp_sum_terms<NT>(tu, redd));
         if (dir == 0) d_in = d; else d_out = d;
       }
     }
@@ -430,11 +463,21 @@ __global__ __launch_bounds__(NT) void k_gc_progress(int S, int nE, int G, int p,
           sa1[v] = sa1[v] + ck * tk;
           sa2[v] = sa2[v] + (double)(ckf * ek);
           const double df = tk - (double)ek;
-          se += df * df;
+          if (NT == 64) seb[i * p + jc] = df * df;
+          else se += df * df;
         }
       }
     }
-    se = rc_block_sum_d(se, redd);  // its barriers also order this pass's reads before the next writes
+    if (NT == 64) {  // the terms in element order (the 256-thread workgroup held element t in thread t)
+      __syncthreads();
+      double tu[GP_NR];
+#pragma unroll
+      for (int u = 0; u < GP_NR; ++u) tu[u] = (tid + u * NT < pp) ? seb[tid + u * NT] : 0.;
+      se = gp_sum_terms<NT>(tu, redd);
+      __syncthreads();  // this pass's reads before the next writes
+    } else {
+      se = rc_block_sum_d(se, redd);  // its barriers also order this pass's reads before the next writes
+    }
     if (tid == 0) o[6 + k] = se / (double)pp;
   }
   double acc = 0.;
@@ -444,11 +487,22 @@ __global__ __launch_bounds__(NT) void k_gc_progress(int S, int nE, int G, int p,
       const int i = r0 + v * rpp;
       if (i < p) {
         const double df = sqrt(sa1[v]) - sqrt(sa2[v]);
-        acc += df * df;
+        if (NT == 64) seb[i * p + jc] = df * df;
+        else acc += df * df;
       }
     }
   }
-  const double dd = sqrt(rc_block_sum_d(acc, redd));
+  double dsum;
+  if (NT == 64) {
+    __syncthreads();
+    double tu[GP_NR];
+#pragma unroll
+    for (int u = 0; u < GP_NR; ++u) tu[u] = (tid + u * NT < pp) ? seb[tid + u * NT] : 0.;
+    dsum = gp_sum_terms<NT>(tu, redd);
+  } else {
+    dsum = rc_block_sum_d(acc, redd);
+  }
+  const double dd = sqrt(dsum);
   if (tid == 0) o[6] = 1.0 / (1.0 + dd);
 }
 
@@ -487,43 +541,49 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_l1(const float* x, int64_t n, d
   if (threadIdx.x == 0) out[blockIdx.x] = acc;
 }
 
-// grid (ceil(nsamp / 4)), one WAVE per sample: the K rows of sample s (n floats each), each
+// grid (ceil(nsamp / 8)), one WAVE per GD_SPW samples: the K rows of sample s (n floats each), each
 // divided by its own max in float64: out[s][i1][i2] = sum_e f1_e f2_e for i1 <= i2 (the diagonal
 // is the squared norm).  The sums are those of a 256-thread workgroup per (sample, pair):
 // virtual thread (vw, lane) sums e = 64 vw + lane + 256 i, each virtual wave's sum is lane 0's
 // butterfly sum, the four are added in order -- the same bits without a block barrier (one
 // workgroup per pair made ~50K tiny workgroups at a packed grid's 5,120 samples).
 #define GD_VW (RC_BLOCK / 64)
+#define GD_SPW 1  // samples per wave (2: slower at R = 128 D4IC, 26 -> 34 us)
 __global__ __launch_bounds__(RC_BLOCK) void k_gc_dots(const float* x, int K, int64_t n, int nsamp, double* out) {
   const int lane = threadIdx.x & 63;
-  const int s = blockIdx.x * (RC_BLOCK / 64) + (threadIdx.x >> 6);
-  if (s >= nsamp) return;
-  const float* xs = x + (int64_t)s * K * n;
-  double mine = 0.0;  // lane i < K: row i's max
-  for (int i = 0; i < K; ++i) {
-    const float* a = xs + (int64_t)i * n;
-    float m = -INFINITY;
-    for (int64_t e = lane; e < n; e += 64) m = fmaxf(m, a[e]);
+  const int s0 = (blockIdx.x * (RC_BLOCK / 64) + (threadIdx.x >> 6)) * GD_SPW;
+  for (int s = s0; s < s0 + GD_SPW && s < nsamp; ++s) {
+    const float* xs = x + (int64_t)s * K * n;
+    double mine = 0.0;  // lane i < K: row i's max
+    for (int i = 0; i < K; ++i) {
+      const float* a = xs + (int64_t)i * n;
+      float m = -INFINITY;
+      for (int64_t e = lane; e < n; e += 64) m = fmaxf(m, a[e]);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    if (lane == i) mine = (double)m;
-  }
-  for (int i1 = 0; i1 < K; ++i1) {
-    const float* a = xs + (int64_t)i1 * n;
-    const double da = __shfl(mine, i1, 64);
-    for (int i2 = i1; i2 < K; ++i2) {
-      const float* b = xs + (int64_t)i2 * n;
-      const double db = __shfl(mine, i2, 64);
-      double acc = 0.0;
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      if (lane == i) mine = (double)m;
+    }
+    // virtual waves holding elements; the others add exact +0 sums (one +0.0 stands for them)
+    const int nvw = (int)((n + 63) / 64 < GD_VW ? (n + 63) / 64 : GD_VW);
+    for (int i1 = 0; i1 < K; ++i1) {
+      const float* a = xs + (int64_t)i1 * n;
+      const double da = __shfl(mine, i1, 64);
+      for (int i2 = i1; i2 < K; ++i2) {
+        const float* b = xs + (int64_t)i2 * n;
+        const double db = __shfl(mine, i2, 64);
+        double acc = 0.0;
 #pragma unroll
-      for (int vw = 0; vw < GD_VW; ++vw) {
-        double v = 0.;
-        for (int64_t e = vw * 64 + lane; e < n; e += RC_BLOCK) v += ((double)a[e] / da) * ((double)b[e] / db);
+        for (int vw = 0; vw < GD_VW; ++vw) {
+          if (vw >= nvw) break;
+          double v = 0.;
+          for (int64_t e = vw * 64 + lane; e < n; e += RC_BLOCK) v += ((double)a[e] / da) * ((double)b[e] / db);
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        acc += __shfl(v, 0, 64);
+          for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+          acc += __shfl(v, 0, 64);
+        }
+        if (nvw < GD_VW) acc += 0.0;  // the empty virtual waves' +0 sums (x + 0 + 0 == x + 0)
+        if (lane == 0) out[((int64_t)s * K + i1) * K + i2] = acc;
       }
-      if (lane == 0) out[((int64_t)s * K + i1) * K + i2] = acc;
     }
   }
 }
@@ -540,7 +600,14 @@ extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p,
   }
   if (S * G == 0) return 0;
   const size_t lds = (size_t)36 * p * p;
-  if (p <= 32) {
+  static const bool wave_form = [] {
+    const char* v = getenv("REDCLIFF_GCP_WAVE");
+    return !(v && strcmp(v, "0") == 0);
+  }();
+  if (p <= 16 && wave_form) {  // one wave per (sample, graph): the same bits as the 256-thread form
+    hipLaunchKernelGGL(k_gc_progress<64>, dim3(S * G), dim3(64), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
+                       truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
+  } else if (p <= 32) {
     hipLaunchKernelGGL(k_gc_progress<256>, dim3(S * G), dim3(256), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
                        truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
   } else {
@@ -572,7 +639,8 @@ extern "C" int redcliff_gc_track_stats(int32_t n_l1_rows, int64_t l1_len, const 
     if (e) return e;
   }
   if (n_samples > 0) {
-    hipLaunchKernelGGL(k_gc_dots, dim3((n_samples + GD_VW - 1) / GD_VW), dim3(RC_BLOCK), 0, s, nolag, K, row_len,
+    const int per = GD_VW * GD_SPW;  // samples per workgroup
+    hipLaunchKernelGGL(k_gc_dots, dim3((n_samples + per - 1) / per), dim3(RC_BLOCK), 0, s, nolag, K, row_len,
                        n_samples, dots_out);
     return rc_check(hipGetLastError(), "k_gc_dots");
   }
