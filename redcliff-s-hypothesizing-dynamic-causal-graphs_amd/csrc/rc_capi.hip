@@ -330,13 +330,15 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   AuxStream* aux = &none;
   hipStream_t sf = s;
   // A single fit is latency-bound: the factor chain on a second stream fills idle CUs (C5 201K ->
-  // 233K windows/s).  Packed replicas already fill the chip and the two chains only compete
-  // for it: one stream is faster there (D4IC R=32 grid 6.61M -> 6.78M windows/s).  Forked and
-  // single-stream steps give the same bits (tests/test_gpu_forked.py); the intermittent A
+  // 233K windows/s).  Packs of 32 or more replicas gain as well since round 4 (the chains' launch
+  // tails and short kernels -- head, k_emb_final, supports -- overlap the other chain's work:
+  // D4IC R = 32 / 64 / 128 0.282 / 0.444 / 0.774 -> 0.267 / 0.421 / 0.732 ms per step,
+  // profiles/r04_grid_fork_sweep.log); at R = 8 one stream stays ahead (0.160 vs 0.161).  Forked
+  // and single-stream steps give the same bits (tests/test_gpu_forked.py); the intermittent A
   // mismatch once blamed on the fork was a missing barrier in k_emb_final's adjacency
   // workgroup, which concurrent work only made likelier.  REDCLIFF_FORK=0 / 1 overrides (tuning).
   const char* fv = getenv("REDCLIFF_FORK");
-  const bool two = fv ? strcmp(fv, "0") != 0 : c.d.R == 1;
+  const bool two = fv ? strcmp(fv, "0") != 0 : (c.d.R == 1 || c.nrep >= 32);
   if (fork && two) {
     if ((e = aux_stream(&aux))) return e;
     sf = aux->s;

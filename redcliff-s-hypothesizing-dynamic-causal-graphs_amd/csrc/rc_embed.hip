@@ -1669,7 +1669,10 @@ int rc_launch_emb_tail(const StepCtx& c, hipStream_t s) {
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
-  const int ept = c.nrep >= 8 ? 4 : 1;
+  // parameter elements per thread: 4 from 8 replicas, 8 from 96 (R = 128 D4IC with the forked step:
+  // 0.732 -> 0.728 ms, profiles/r04_grid_fork_sweep.log); REDCLIFF_EMB_FINAL_EPT overrides (tuning)
+  const char* ev = getenv("REDCLIFF_EMB_FINAL_EPT");
+  const int ept = (ev && atoi(ev) > 0) ? atoi(ev) : (c.nrep >= 96 ? 8 : (c.nrep >= 8 ? 4 : 1));
   const int nw = (total + ept * RC_BLOCK - 1) / (ept * RC_BLOCK);
   const size_t lds = rc_emb_final_lds(d);
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
