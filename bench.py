@@ -422,7 +422,13 @@ def run_grid(c, args, dev, rank, dist):
         return lambda: pack.run_steps(["combined"], ds, ds["rows"][idx], ds["sizes"][idx], st)
 
     steps(5, 0)()
-    el = timed(steps(args.grid_steps, 5), dist, dev)
+    extra = 0  # untimed steps until the device has been busy for args.preheat_s (as the single fit)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < getattr(args, "preheat_s", 0.0):
+        steps(20, 5 + extra)()
+        torch.cuda.synchronize()
+        extra += 20
+    el = timed(steps(args.grid_steps, 5 + extra), dist, dev)
     return el, R, steps
 
 
@@ -447,6 +453,14 @@ def fits_per_hour(c, args, dev, rank, dist, world):
     val = [(X[i:i + B], Y[i:i + B]) for i in range(ntr * B, (ntr + nva) * B, B)]
     rng = np.random.RandomState(7)
     true_gc = [(rng.rand(c["p"], c["p"], c["L"]) < 0.2).astype(np.float64) for _ in range(c["K"])]
+    # untimed warm-up: a 3-epoch fit of a copy of the pack (kernels loaded, the caching allocators
+    # holding the pack-sized buffers), as a grid search's later packs find the process
+    import copy
+    wm = [copy.deepcopy(m) for m in models]
+    wpack = redcliff_amd.ReplicaPack(wm, [adam_pair(m, c) for m in wm])
+    wpack.fit(None, train, val, max_iter=3, lookback=10 ** 6, check_every=10 ** 6, GC=true_gc)
+    del wpack, wm
+    torch.cuda.synchronize()
     pack = redcliff_amd.ReplicaPack(models, opts)
 
     def fit():
@@ -456,8 +470,8 @@ def fits_per_hour(c, args, dev, rank, dist, world):
     return {"replicas_per_gpu": R, "epochs_per_fit": E, "train_windows": ntr * B, "val_windows": nva * B,
             "seconds": round(el, 3), "value": round(world * R * 3600.0 / el, 1), "unit": "fits/hour",
             "note": "fixed-epoch D4IC-shaped fits (%d pretrain, %d acclimation, %d combined epochs), early stopping "
-                    "disabled so every fit does the same work; per-epoch GC tracking + validation on the GPU"
-                    % (pre, acc, E - pre - acc)}
+                    "disabled so every fit does the same work; per-epoch GC tracking + validation on the GPU; "
+                    "after an untimed 3-epoch warm-up fit of a copy of the pack" % (pre, acc, E - pre - acc)}
 
 
 # --------------------------------------------------------------------------- modes
