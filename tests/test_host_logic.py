@@ -91,3 +91,27 @@ def test_freeze_decision_raises_like_the_reference():
     x = np.random.RandomState(0).rand(5, 5, 1).astype(np.float32)
     with pytest.raises(ValueError, match="Improper number of dimensions to norm"):
         np.linalg.norm(x / np.max(x), ord=1)
+
+
+def test_packed_fit_module_modes_match_torch_eval():
+    """replicas._eval_modes (the flags a packed fit leaves, written through the module dicts listed
+    when the pack is built) sets exactly the flags torch's recursive .eval() on the embedder and
+    every factor sets (...withStateSmoothing.py:1366-1480), and leaves the other modules alone."""
+    import copy
+    import bench
+    import redcliff_amd
+    from redcliff_amd import replicas
+    c = bench.CONFIGS["d4ic"]
+    ms = [bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=s) for s in range(3)]
+    ref = copy.deepcopy(ms)
+    for m in ref:
+        m.factor_score_embedder.eval()
+        for f in m.factors:
+            f.eval()
+    replicas._eval_modes(ms[:1])                              # walking the trees
+    replicas._eval_modes(ms[1:], replicas._module_dicts(ms[1:]))  # the pack's precomputed list
+    for a, b in zip(ms, ref):
+        flags_a = [(n, x.training) for n, x in a.named_modules()]
+        flags_b = [(n, x.training) for n, x in b.named_modules()]
+        assert flags_a == flags_b
+    assert any(t for _, t in flags_a)  # modules outside the embedder / factors keep their mode
