@@ -300,7 +300,7 @@ def pmc_traffic(kernel_name, cfg):
     import re
     base, packed = (cfg.rsplit("_r", 1)[0], True) if "_r" in cfg else (cfg, False)
     # the newest round's passes first (kernels change between rounds), then older ones
-    pats = [os.path.join(ROOT, "profiles", "r%02d_pmc_%s_*counter_collection*.csv" % (rnd, base)) for rnd in (3, 2)]
+    pats = [os.path.join(ROOT, "profiles", "r%02d_pmc_%s_*counter_collection*.csv" % (rnd, base)) for rnd in (4, 3, 2)]
     if base == "d4ic" and not packed:
         pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
     for pat in pats:
