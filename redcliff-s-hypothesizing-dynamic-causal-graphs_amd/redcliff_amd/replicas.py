@@ -471,8 +471,10 @@ class ReplicaPack:
                     w = torch.sigmoid(emb0.sigmoid_eccentricity_coeff * w_raw) if emb0.use_sigmoid_restriction else w_raw
                     G, G0 = self.gc_norms()
                     A = self.emb[:, :p * p].view(R, p, p)
-                    ai = self._index(active)
-                    est_t, nolag_t = conditional_gc_estimates(w, G[ai], G0[ai], A[ai], nsup, ls, m0.primary_gc_est_mode)
+                    if len(active) < R:  # the active replicas' rows (all of them: no gather needed)
+                        ai = self._index(active)
+                        G, G0, A = G[ai], G0[ai], A[ai]
+                    est_t, nolag_t = conditional_gc_estimates(w, G, G0, A, nsup, ls, m0.primary_gc_est_mode)
                     Ra, S = est_t.shape[0], est_t.shape[1]
                     vals_d = None
                     if GC is not None and nsup > 0 and S > 0:

@@ -3,7 +3,7 @@ fit keeps (losses, GC-progress metrics, cosine similarities, confusion rates), b
 final parameters -- the check for kernel changes on the evaluation side (GC norms, GC-progress
 statistics, validation values) that must not change any bit.
 
-    REDCLIFF_HIP_LIB=scripts/bin/lib_prev.so python scripts/compare_fits.py dump gpurun_out/fprev.npz
+    [COMPARE_FITS_R=8] REDCLIFF_HIP_LIB=scripts/bin/lib_prev.so python scripts/compare_fits.py dump gpurun_out/fprev.npz
     python scripts/compare_fits.py dump gpurun_out/fcur.npz
     python scripts/compare_fits.py compare gpurun_out/fprev.npz gpurun_out/fcur.npz
 """
@@ -39,7 +39,8 @@ def dump(path):
     out = {}
     for cfg in ("d4ic", "c1k4"):
         c = dict(bench.CONFIGS[cfg])
-        R, E = 4, 9
+        # COMPARE_FITS_R=8 or more: the packed (short-contraction matrix-core) factor kernels
+        R, E = int(os.environ.get("COMPARE_FITS_R", "4")), 9
         models, opts = [], []
         for i in range(R):
             m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=50 + i, pre=2, acc=1,
