@@ -347,7 +347,9 @@ def timed(fn, dist, dev):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        # the coordination group of --mode fit is gloo (host tensors); --mode dp's is RCCL
+        on_host = dist.get_backend() == "gloo"
+        t = torch.tensor([el], device=None if on_host else dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
@@ -527,19 +529,24 @@ def mode_fit(args, dev, rank, world, dist, holder):
               "ms_per_step": round(1e3 * nel / nsteps, 4), "steps": nsteps, "target_gpu_over_cpu": 50.0}
 
     dpl = None
+    dpg = None
     if args.dp_leg_batch > 0 and dist is None and world == 1:
         # one rank: the RCCL group exists only from here on -- a process with an RCCL communicator
-        # runs the single fit's second stream (split-lead step) serialised behind the first
-        # (C1(K=4): 0.097 -> 0.132 ms per step, profiles/r04_ns_probe.log), so the single-fit legs
-        # above ran without one, as a one-GPU user's fit does
+        # runs a step's second stream (the split-lead step, forked packs) serialised behind the
+        # first (C1(K=4): 0.097 -> 0.132 ms per step, profiles/r04_ns_probe.log), so the legs
+        # above ran without one, as a one-GPU user's fits do
         dist = init_group(dev, 1, 0)
         holder["dist"] = dist
+    elif args.dp_leg_batch > 0 and dist is not None and world > 1:
+        # several ranks: the legs above were coordinated over gloo; the RCCL group of the
+        # all-reduce is created now, for this leg only (the same reason)
+        dpg = dist.new_group(backend="nccl", device_id=dev)
     if args.dp_leg_batch > 0 and dist is not None:
         # configs[3] beside the replica numbers: ONE TST-shaped fit data-parallel over all ranks
         # (global batch --dp-leg-batch, RCCL all-reduce of the flat gradient per update), so the
         # driver's 1 -> 8 GPU runs record both scaling regimes
         dsteps = max(20, min(args.steps, 200))
-        del_, dpo = dp_throughput(args.dp_leg_batch, dsteps, 5, dev, dist)
+        del_, dpo = dp_throughput(args.dp_leg_batch, dsteps, 5, dev, dist, group=dpg)
         dpl = {"global_batch": args.dp_leg_batch, "windows_per_shard": args.dp_leg_batch // world, "ranks": world,
                "updates": dsteps, "windows_per_s": round(dsteps * args.dp_leg_batch / del_, 1),
                "ms_per_update": round(1e3 * del_ / dsteps, 4), "scaling": "strong",
@@ -568,9 +575,10 @@ def mode_fit(args, dev, rank, world, dist, holder):
     return out
 
 
-def dp_throughput(B, steps, warmup, dev, dist):
+def dp_throughput(B, steps, warmup, dev, dist, group=None):
     """BASELINE configs[3]: one TST-shaped fit sharded over the ranks (DataParallelFit), global
-    batch B per update: (elapsed seconds for `steps` combined-phase updates, the DataParallelFit)."""
+    batch B per update: (elapsed seconds for `steps` combined-phase updates, the DataParallelFit).
+    group: the RCCL group of the all-reduce (default: the world group); timing uses `dist`."""
     import redcliff_amd
     from redcliff_amd.data_parallel import DataParallelFit
     c = dict(CONFIGS["c4"], B=B)
@@ -578,7 +586,7 @@ def dp_throughput(B, steps, warmup, dev, dist):
     oA, oB = adam_pair(model, c)
     nbatch = 16
     X, Y = synth(c, nbatch * B, seed=100)  # every rank holds the whole (identical) data set
-    dp = DataParallelFit(model, oA, oB)
+    dp = DataParallelFit(model, oA, oB, group=group)
     ds = dp.cache_dataset([(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)])
 
     def run(n, start):
@@ -642,20 +650,24 @@ def rank_devices(dist, rank, local, world, dev):
 
 
 # --------------------------------------------------------------------------- launch
-def init_group(dev, world, local):
+def init_group(dev, world, local, coordination=False):
     """torch.distributed over RCCL ("nccl") on the GPU, bound to this rank's device (no guessing the
-    device from the global rank), or gloo for the CPU plumbing check; 127.0.0.1 rendezvous."""
+    device from the global rank), or gloo for the CPU plumbing check; 127.0.0.1 rendezvous.
+    coordination=True: a gloo group for the barriers and the max-over-ranks timing of --mode fit
+    (its legs run no collective on the data path; the data-parallel leg makes its own RCCL group)."""
     import torch.distributed as dist
     kw = {}
     if dev is not None:
         torch.cuda.set_device(dev)
-        kw["device_id"] = dev
+        if not coordination:
+            kw["device_id"] = dev
+    backend = "gloo" if (dev is None or coordination) else "nccl"
     if world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
-        dist.init_process_group("nccl" if dev is not None else "gloo", rank=0, world_size=1, **kw)
+        dist.init_process_group(backend, rank=0, world_size=1, **kw)
     else:
-        dist.init_process_group("nccl" if dev is not None else "gloo", **kw)
+        dist.init_process_group(backend, **kw)
     return dist
 
 
@@ -715,7 +727,8 @@ def main():
     dist = None
     # one rank in --mode fit: the group for the data-parallel leg is created when that leg runs (mode_fit)
     if world > 1 or args.mode == "dp" or (args.dp_leg_batch > 0 and not cuda):
-        dist = init_group(torch.device("cuda", local) if cuda else None, world, local)
+        dist = init_group(torch.device("cuda", local % max(torch.cuda.device_count(), 1)) if cuda else None, world,
+                          local, coordination=(args.mode == "fit"))
         seen = dist.get_world_size()
         if seen != world or (args.gpus > 1 and seen != args.gpus):
             raise SystemExit("world size %d != --gpus %d / WORLD_SIZE %d" % (seen, args.gpus, world))
@@ -730,7 +743,7 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))  # (more ranks than GPUs: rehearsal)
     torch.cuda.set_device(dev)
 
     # the library is built in-tree (a no-op when current); under an external launcher only the
