@@ -1188,6 +1188,7 @@ struct EmbWbSum {
 // in place; sc1: they read the combined records with coherent loads (k_emb_tail, where the
 // combine runs in the same launch); adj_inplace: the adjacency workgroup sums its dS partials in
 // place (k_emb_tail, where it does not wait for the combine).
+#define EF_EPT_MAX 8  // runs per thread of the batched parameter path (k_emb_final's ept <= this)
 template <int NR>
 __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, int ept, bool sc1, bool adj_inplace) {
   const RedcliffDims& d = c.d;
@@ -1211,6 +1212,63 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
   // workgroup 0 is the adjacency workgroup (the longest; dispatched first), 1..nw the parameters
   if (wx > 0) {
     if (!stepA) return;
+    if (!fused && !sc1 && ept > 1 && ept <= EF_EPT_MAX && !(c.flags & RC_GRAD_ONLY)) {
+      // packed replicas (combined records, several runs per thread): every run's gradient, then
+      // the parameters and both moments of all runs requested together and the Adam steps -- one
+      // memory round for the workgroup instead of one per run; the same values and operations
+      float g[EF_EPT_MAX];
+      int64_t ix[EF_EPT_MAX];
+#pragma unroll
+      for (int run = 0; run < EF_EPT_MAX; ++run) {
+        ix[run] = -1;
+        g[run] = 0.f;
+        const int e = ((wx - 1) * ept + run) * RC_BLOCK + threadIdx.x;
+        if (run >= ept || e >= total) continue;
+        if (e < nFH) {
+          float t = 0.f;
+          for (int cc = 0; cc < c.dwN; ++cc) t += ws[c.wo.dWi + (int64_t)cc * nFH + e];
+          g[run] = t;
+          ix[run] = c.eo.gcW + e;
+        } else if (e < nFH + nfc) {
+          const int q = e - nFH;
+          g[run] = ws[c.wo.gfc + q];
+          ix[run] = q < K * M1 ? c.eo.fc2W + q : (q < K * M1 + K ? c.eo.fc2b + (q - K * M1) : c.eo.fc1b + (q - K * M1 - K));
+        } else if (e < nFH + nfc + 2 * F) {
+          const int q = e - nFH - nfc;
+          const int which = q / F, f = q - which * F;
+          float g4[4] = {0.f, 0.f, 0.f, 0.f};
+          int pt = 0;
+          for (; pt + 3 < c.dgN; pt += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g4[u] += ws[c.wo.dgb + ((int64_t)(pt + u) * 2 + which) * F + f];
+          for (; pt < c.dgN; ++pt) g4[0] += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
+          g[run] = (g4[0] + g4[1]) + (g4[2] + g4[3]);
+          ix[run] = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
+        } else {
+          const int q = e - nFH - nfc - 2 * F;
+          g[run] = ws[c.wo.gfc1 + q];
+          ix[run] = c.eo.fc1W + q;
+        }
+      }
+      float pv[EF_EPT_MAX], mv[EF_EPT_MAX], vv[EF_EPT_MAX];
+#pragma unroll
+      for (int run = 0; run < EF_EPT_MAX; ++run) {
+        const int64_t i = ix[run] >= 0 ? ix[run] : 0;
+        pv[run] = E[i];
+        mv[run] = Mm[i];
+        vv[run] = V[i];
+      }
+#pragma unroll
+      for (int run = 0; run < EF_EPT_MAX; ++run) {
+        if (ix[run] < 0) continue;
+        rc_adam(pv[run], mv[run], vv[run], g[run], as);
+        E[ix[run]] = pv[run];
+        Mm[ix[run]] = mv[run];
+        V[ix[run]] = vv[run];
+      }
+      RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FINAL, 1);
+      return;
+    }
     // ept runs of RC_BLOCK consecutive elements per workgroup (1 for a single fit; 4 for packed
     // replicas, where one element per thread made ~10K short workgroups at R = 128)
     for (int run = 0; run < ept; ++run) {
