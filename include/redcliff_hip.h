@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define REDCLIFF_ABI_VERSION 7
+/* 8: the workspace region y is laid out network-major, y[nU][K][p][Bmax] (was y[nU][Bmax][K][p]) */
+#define REDCLIFF_ABI_VERSION 8
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -173,7 +174,7 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
 /* Offsets (floats, per replica) of the workspace regions: T R f1 w a y G G0 w1 dwp dAadj dWi dS
  * dgb S dZ amat lossp xsim gfc total.  Returns the number of offsets available.  The host reads
  * w (raw embedder output), y (per-factor predictions as nU = ceil(h/16) partial sums
- * y[nU][Bmax][K][p] over 16-unit hidden chunks), xsim (mixed forecast), G / G0 (group norms)
+ * y[nU][K][p][Bmax] over 16-unit hidden chunks), xsim (mixed forecast), G / G0 (group norms)
  * back from a step run with RC_STORE_OUTPUTS. */
 int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out);
 
@@ -197,8 +198,8 @@ int redcliff_workspace_regions(const RedcliffDims* d, int64_t* out, int32_t n_pa
 
 /* Stand-alone forward of K cMLPs (models/cmlp.py:90-101) on B windows Xwin[r][B][L][p]
  * (x_rstride floats between replicas).  Per replica (ws_rstride floats) the workspace
- * receives a[K][p][B][h] | y[nU][B][K][p] | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h];
- * sum_u y[u][b][k][j] (nU = ceil(h/16) hidden-chunk partials, output bias in chunk 0) is
+ * receives a[K][p][B][h] | y[nU][K][p][B] | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h];
+ * sum_u y[u][k][j][b] (nU = ceil(h/16) hidden-chunk partials, output bias in chunk 0) is
  * the prediction of network j of factor k for window b. */
 int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride, const float* fac,
                             int64_t fac_stride, float* ws, int64_t ws_rstride, void* stream);

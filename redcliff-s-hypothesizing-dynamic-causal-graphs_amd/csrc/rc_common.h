@@ -382,6 +382,13 @@ __device__ inline float rc_wave_sum(float v) {
 
 // Division by a block-uniform runtime divisor without the ~40-instruction integer divide:
 // q = (n * ceil(2^40 / d)) >> 40, exact for 0 <= n < 2^24 (error term n / 2^40 < 1 / d).
+// Workspace y (the factor forward's per-slot prediction partials): [slot][network kj][Bmax],
+// network-major so that a network's windows are contiguous for the kernels that write them (one
+// network per block) and for the ones that read them (a network's windows per workgroup)
+__host__ __device__ inline int64_t rc_y_idx(const RedcliffDims& d, int slot, int kj, int b) {
+  return ((int64_t)slot * d.K * d.p + kj) * d.Bmax + b;
+}
+
 struct RcDiv {
   unsigned long long m;
   int d;

@@ -76,7 +76,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const int tid = threadIdx.x;
   const int B = c.B;
-  const RcDiv dL(d.L), dK(K);
+  const RcDiv dL(d.L), dB(B);
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const bool fgrad = (c.flags & RC_STEP_B) || (c.flags & RC_STEP_A);
@@ -183,9 +183,9 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       rc_seg<1>(tgt ? B : 0, [&](int b) { return X[((c.row0 + b) * d.T + c.Lmax) * p + j]; },
                 [&](int b, float v) { xt[b] = v; }),
       rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }),
-      rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order)
-        const int b = dK.div(e), kk = e - b * K;
-        const float* yp = ws + c.wo.y + ((int64_t)b * K + kk) * p + j;
+      rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order); e = kk * B + b
+        const int kk = dB.div(e), b = e - kk * B;
+        const float* yp = ws + c.wo.y + rc_y_idx(d, 0, kk * p + j, b);
         float v[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = yp[(q < nU ? q : 0) * ys_];
@@ -193,7 +193,10 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
 #pragma unroll
         for (int q = 0; q < 8; ++q) yv += q < nU ? v[q] : 0.f;
         return yv;
-      }, [&](int e, float v) { ybuf[e] = v; }),
+      }, [&](int e, float v) {
+        const int kk = dB.div(e);
+        ybuf[(e - kk * B) * K + kk] = v;
+      }),
       rc_seg<1>(Q, [&](int e) {  // the nU (<= 8) partials loaded together, summed in slot order
         const float* gp = ws + c.wo.gq + (int64_t)kj * Q + e;
         const int64_t gs_ = (int64_t)K * p * Q;

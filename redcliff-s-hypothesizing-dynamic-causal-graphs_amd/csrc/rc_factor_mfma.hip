@@ -195,8 +195,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
     if (b < c.B) {
       const int l = lane & 31;
       // slot ub holds this block's partial; block 0 also clears the slots past nUB
-      if (l == 0) ws[c.wo.y + (((int64_t)ub * d.Bmax + b) * K + k) * p + j] = ys + b1;
-      else if (ub == 0 && l >= nUB && l < nU) ws[c.wo.y + (((int64_t)l * d.Bmax + b) * K + k) * p + j] = 0.f;
+      if (l == 0) ws[c.wo.y + rc_y_idx(d, ub, kj, b)] = ys + b1;
+      else if (ub == 0 && l >= nUB && l < nU) ws[c.wo.y + rc_y_idx(d, l, kj, b)] = 0.f;
     }
   }
 }
@@ -246,9 +246,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
   const int nUB = c.fslots;  // y / group-norm slots of the forward (16- or 32-unit blocks)
-  // the nUB (<= 8) slot partials of every prediction requested together, summed in slot order
+  // the nUB (<= 8) slot partials of every prediction requested together, summed in slot order;
+  // element e = kk * B + b (consecutive windows of one network: contiguous in y) -> ybuf[b][kk]
+  const RcDiv dB(B);
   rc_stage<2>(B * K, [&](int e) {
-    const float* yp = ws + c.wo.y + (int64_t)e * p + j;  // e = b * K + kk
+    const int kk = dB.div(e), b = e - kk * B;
+    const float* yp = ws + c.wo.y + rc_y_idx(d, 0, kk * p + j, b);
     const int64_t ys_ = (int64_t)d.Bmax * K * p;
     float v[8];
 #pragma unroll
@@ -258,7 +261,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
     for (int ub = 1; ub < 8; ++ub)
       if (ub < nUB) yv += v[ub];
     return yv;
-  }, [&](int e, float v) { ybuf[e] = v; });
+  }, [&](int e, float v) {
+    const int kk = dB.div(e);
+    ybuf[(e - kk * B) * K + kk] = v;
+  });
   __syncthreads();
   float fsum = 0.f;
   for (int b = tid; b < B; b += RC_BLOCK) {
@@ -858,7 +864,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
   const int cbase = (int)blockIdx.x * 4 * bpw + wv;
   // lane offsets of the stores: y of window column l15 (group 0), the W1 snapshot of unit l15
   // (group 0), the group norms of k-step l15 (q = 4 l15 + g)
-  const int y_off = g == 0 ? 4 * l15 * KP : MS_OOB;
+  const int y_off = g == 0 ? 4 * l15 : MS_OOB;
   const int w1_off = g == 0 ? 4 * l15 : MS_OOB;
   const int gq_off = l15 < NK4 ? 4 * (4 * l15 + g) : MS_OOB;
   // a block's operands: its W0 run (lane-linear), b0 / W1 of rows 4 g + reg, W1 of unit l15, b1;
@@ -885,7 +891,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
   for (int i = 0; i < bpw; ++i) {
     const int cb = cbase + 4 * i;
     if (cb >= NB) break;
-    const int kj = cb / nU, ub = cb - kj * nU, u0 = ub * 16, k = kj / p, j = kj - k * p;
+    const int kj = cb / nU, ub = cb - kj * nU, u0 = ub * 16;
     const int nu = min(16, h - u0);
     float wA[NK4];
     ms_tile_operands<NK4>(Wt, cur.wt, lane, l15, g, Q, wA);
@@ -900,7 +906,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
       gsel = l15 == s ? sq : gsel;
     }
     ms_st(ms_rsrc(ws + c.wo.gq + ((int64_t)ub * KP + kj) * Q, Q), gq_off, gsel);
-    const auto rY = ms_rsrc(ws + c.wo.y + (int64_t)ub * d.Bmax * KP + k * p + j, B * KP);
+    const auto rY = ms_rsrc(ws + c.wo.y + rc_y_idx(d, ub, kj, 0), B);
     for (int t0 = 0; t0 < B; t0 += 32) {
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
       const float* x0 = Xs + (t0 + l15) * S + ms_sh(l15) + g;
@@ -918,7 +924,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
         for (int reg = 0; reg < 4; ++reg) ys += cur.w1[reg] * fmaxf(z[reg] + cur.bu[reg], 0.f);  // w1 = 0 past h
         ys += __shfl_xor(ys, 16, 64);
         ys += __shfl_xor(ys, 32, 64);
-        ms_st(rY, y_off + 4 * (t0 + 16 * tt) * KP, ys + b1);  // window t0 + 16 tt + l15 (dropped at or past B)
+        ms_st(rY, y_off + 4 * (t0 + 16 * tt), ys + b1);  // window t0 + 16 tt + l15 (dropped at or past B)
       }
     }
     ms_st(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), w1_off, cur.w1A);

@@ -252,7 +252,7 @@ size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
 
 // ------------------------------------------------------------------------------------------
 // Factor forward of one (factor, channel network, FAC_UC-unit hidden chunk): relu activations
-// a[kj][b][u], partial outputs y[uc][b][k][j] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk
+// a[kj][b][u], partial outputs y[uc][kj][b] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk
 // 0), the chunk's squared layer-0 group norms gq[uc][kj][q] and a snapshot of W1.
 // The whole window block and weight chunk are staged in one pass when p*L <= FQ_MAX.
 __device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
@@ -332,7 +332,7 @@ __device__ void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
       }
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) ys += __shfl_xor(ys, o, 64);
-      if (tu == 0 && b < c.B) ws[c.wo.y + (((int64_t)uc * d.Bmax + b) * K + k) * p + j] = ys + b1;
+      if (tu == 0 && b < c.B) ws[c.wo.y + rc_y_idx(d, uc, kj, b)] = ys + b1;
     }
   }
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 1);

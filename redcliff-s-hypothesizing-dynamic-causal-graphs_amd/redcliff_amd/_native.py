@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB_PATH = os.path.join(_HERE, "lib", "libredcliff_hip.so")
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", DEFAULT_LIB_PATH)
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0

@@ -583,7 +583,9 @@ class FitEngine:
         o = self.ws_off
         w = self.ws[o["w"]:o["w"] + B * self.K].view(B, self.K).clone()
         nU = (self.h + 15) // 16  # the forward kernel leaves per-hidden-chunk partials
-        y = self.ws[o["y"]:o["y"] + nU * d.Bmax * self.K * self.p].view(nU, d.Bmax, self.K, self.p)[:, :B].sum(0)
+        # slots [nU][network k * p + j][Bmax] (rc_y_idx) -> (B, K, p)
+        y = self.ws[o["y"]:o["y"] + nU * d.Bmax * self.K * self.p].view(nU, self.K, self.p, d.Bmax)[..., :B].sum(0)
+        y = y.permute(2, 0, 1).contiguous()
         xs = self.ws[o["xsim"]:o["xsim"] + B * self.p].view(B, self.p).clone()
         return w, y, xs
 

@@ -117,7 +117,8 @@ def factor_forward_packed(flat, K, p, h, L, Xwin):
         nat.check(nat.lib().redcliff_factor_forward(ctypes.byref(dims), nb, ptr(xw), 0, ptr(flat), 0, ptr(ws),
                                                     ws_floats, current_stream()), "factor_forward")
         off = kp * nb * h
-        out[b0:b0 + nb] = ws[off:off + nU * nb * kp].view(nU, nb, K, p).sum(0)
+        # slots [nU][network k * p + j][nb] (rc_y_idx with Bmax = nb)
+        out[b0:b0 + nb] = ws[off:off + nU * nb * kp].view(nU, K, p, nb).sum(0).permute(2, 0, 1)
     return out
 
 
