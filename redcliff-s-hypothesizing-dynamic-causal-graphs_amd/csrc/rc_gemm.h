@@ -35,6 +35,7 @@ struct RcGemm {
   // bases advance by replica r = rmap[i] (or i when rident) times the r-strides.  nrep = 1,
   // strides 0: a plain batched product.
   int batch, nrep, rident;
+  int xcd;  // 1: XCD-aware tile order (rc_gemm_tile)
   int64_t qA, qB, qC, qAux;
   uint8_t rmap[RC_MAX_ACTIVE];
 };
@@ -49,7 +50,7 @@ inline RcGemm rc_gemm_args(int ta, int tb, int M, int N, int K, const float* A, 
   g.alpha = 1.f; g.beta = 0.f;
   g.Kblk = K > 0 ? K : 1; g.rA = 0; g.rB = 0;
   g.epi = RC_EPI_NONE; g.aux = nullptr; g.ldaux = 0; g.sAux = 0;
-  g.batch = 1; g.nrep = 1; g.rident = 1; g.qA = g.qB = g.qC = g.qAux = 0;
+  g.batch = 1; g.nrep = 1; g.rident = 1; g.xcd = 0; g.qA = g.qB = g.qC = g.qAux = 0;
   return g;
 }
 
@@ -61,13 +62,30 @@ inline void rc_gemm_reps(RcGemm& g, const StepCtx& c, int64_t qA, int64_t qB, in
   g.qA = qA; g.qB = qB; g.qC = qC; g.qAux = qAux;
 }
 
+// The output tile (x, y) and grid slice z of this workgroup.  XCD-aware order (g.xcd, slice count
+// a multiple of 8): workgroups are dealt round-robin over the 8 XCDs in dispatch order (observed,
+// used for speed only), so the dispatch index L = x + nx (y + ny z) is remapped such that every
+// tile of one slice -- which share their A rows and B columns -- runs on one XCD (L % 8) and
+// its L2 fetches those operands once, not once per XCD.  A bijection of the grid: the same
+// tiles are computed, with the same bits.
+struct RcTile {
+  int x, y, z;
+};
+__device__ inline RcTile rc_gemm_tile(const RcGemm& g) {
+  const int nx = gridDim.x, ny = gridDim.y, nz = gridDim.z;
+  if (!g.xcd || (nz & 7) != 0) return RcTile{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const int T = nx * ny;
+  const int L = (int)blockIdx.x + nx * ((int)blockIdx.y + ny * (int)blockIdx.z);
+  const int slot = L >> 3, zq = slot / T, t = slot - zq * T, ty = t / nx;
+  return RcTile{t - ty * nx, ty, (L & 7) + 8 * zq};
+}
+
 // The replica of grid slice z and the slice inside it: (replica, zb).
 struct RcGemmZ {
   int64_t r;
   int zb;
 };
-__device__ inline RcGemmZ rc_gemm_z(const RcGemm& g) {
-  const int z = blockIdx.z;
+__device__ inline RcGemmZ rc_gemm_z(const RcGemm& g, int z) {
   if (g.nrep == 1) return RcGemmZ{0, z};
   const int i = z / g.batch, zb = z - i * g.batch;
   return RcGemmZ{g.rident ? i : (int)g.rmap[i], zb};
@@ -81,13 +99,14 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   constexpr int TP = TT / 16;           // outputs per thread along each tile dimension
   constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
   rc_critical_priority();
-  const RcGemmZ zz = rc_gemm_z(g);
+  const RcTile tl = rc_gemm_tile(g);
+  const RcGemmZ zz = rc_gemm_z(g, tl.z);
   const int bz = zz.zb;
   const float* A = g.A + bz * g.sA + zz.r * g.qA;
   const float* B = g.B + bz * g.sB + zz.r * g.qB;
   float* C = g.C + bz * g.sC + zz.r * g.qC;
   const float* aux = g.aux ? g.aux + zz.r * g.qAux : nullptr;
-  const int n0 = blockIdx.x * TT, m0 = blockIdx.y * TT;
+  const int n0 = tl.x * TT, m0 = tl.y * TT;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const RcDiv dkb(g.Kblk);
   __shared__ float As[RC_GEMM_K][TT + 4];  // As[k][m]
@@ -177,13 +196,14 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
   constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
   constexpr int QT = TT / 2;                      // quarter tile per wave
   rc_critical_priority();
-  const RcGemmZ zz = rc_gemm_z(g);
+  const RcTile tl = rc_gemm_tile(g);
+  const RcGemmZ zz = rc_gemm_z(g, tl.z);
   const int bz = zz.zb;
   const float* A = g.A + bz * g.sA + zz.r * g.qA;
   const float* B = g.B + bz * g.sB + zz.r * g.qB;
   float* C = g.C + bz * g.sC + zz.r * g.qC;
   const float* aux = g.aux ? g.aux + zz.r * g.qAux : nullptr;
-  const int n0 = blockIdx.x * TT, m0 = blockIdx.y * TT;
+  const int n0 = tl.x * TT, m0 = tl.y * TT;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wm = QT * (wv >> 1), wn = QT * (wv & 1);
   const RcDiv dkb(g.Kblk);
@@ -289,6 +309,8 @@ inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char
   }();
   const char* core = getenv("REDCLIFF_GEMM_CORE");  // read per launch: the tests switch it
   const bool valu = core != nullptr && core[0] == 'v';
+  const char* xe = getenv("REDCLIFF_GEMM_XCD");  // XCD-aware tile order: default on; 0 = dispatch order
+  g.xcd = !(xe && xe[0] == '0');
   const int64_t t64 = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * batch;
   const bool small = tile_env == 32 || (tile_env != 64 && t64 < 512);
   if (small) {
