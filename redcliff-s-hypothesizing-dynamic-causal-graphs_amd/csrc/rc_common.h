@@ -389,6 +389,18 @@ __host__ __device__ inline int64_t rc_y_idx(const RedcliffDims& d, int slot, int
   return ((int64_t)slot * d.K * d.p + kj) * d.Bmax + b;
 }
 
+// XCD-aware order of a grid of nx workgroups x nz slices (replicas): workgroups are dealt
+// round-robin over the 8 XCDs in dispatch order (observed, used for speed only), so the dispatch
+// index L = x + nx z is remapped such that every workgroup of one slice runs on one XCD (L % 8)
+// and that XCD's L2 serves the operands the slice's workgroups share.  A bijection of the grid
+// when nz is a multiple of 8 (otherwise the identity): the same workgroups, the same bits.
+__device__ inline void rc_xcd_order(int nx, int nz, int& x, int& z) {
+  if ((nz & 7) != 0) return;
+  const int L = x + nx * z, slot = L >> 3, q = slot / nx;
+  x = slot - q * nx;
+  z = (L & 7) + 8 * q;
+}
+
 struct RcDiv {
   unsigned long long m;
   int d;

@@ -207,9 +207,13 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
 //   terms, -> ws.dwp), group norms G / G0, adjacency-L1 value and its gradients wrt the
 //   lagged group norms (-> ws.dgs, used by the dW0 epilogue) and A (-> ws.dAadj), and the
 //   output-layer / hidden-bias gradients + Adam (b0, W1, b1).
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c) {
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.y), kj = blockIdx.x;
+  // xcd: every network of one replica on one XCD (rc_xcd_order): the K networks of a channel
+  // read the same y rows, and the replica's w and window targets are shared by all of them
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) rc_xcd_order(gridDim.x, gridDim.y, bx, by);
+  const int r = rc_rep(c, by), kj = bx;
   const int p = d.p, h = d.h, K = d.K, L = d.L, Q = p * L, B = c.B;
   const int k = kj / p, j = kj - k * p;
   float* P = c.fac + r * c.fs;
@@ -847,10 +851,12 @@ __device__ inline void ms_tile_operands(float* Wt, const float (&t)[NK4], int la
 // over the 4 rows, then the 4 groups in order), + b1 in block 0; group norms of the block; W1
 // snapshot for the backward.
 template <int NK4>
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, int xcd) {
   constexpr int S = ((NK4 + 3) / 4) * 16 + 4;  // == ms_qp16(d) + 4
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.z);
+  int bx = blockIdx.x, bz = blockIdx.z;  // xcd: the replica's workgroups (its window tile) on one XCD
+  if (xcd) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
+  const int r = rc_rep(c, bz);
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU, KP = K * p;
   const int rows = ms_rows(B);
   extern __shared__ float Xs[];
@@ -861,7 +867,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   float* Wt = Xs + rows * S + wv * ms_tile_floats(NK4);
-  const int cbase = (int)blockIdx.x * 4 * bpw + wv;
+  const int cbase = bx * 4 * bpw + wv;
   // lane offsets of the stores: y of window column l15 (group 0), the W1 snapshot of unit l15
   // (group 0), the group norms of k-step l15 (q = 4 l15 + g)
   const int y_off = g == 0 ? 4 * l15 : MS_OOB;
@@ -945,10 +951,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw) {
 // A block costs one memory round trip: its W0 run, Adam moments, adjacency rows and output-layer
 // state are requested together at its start; dL/dy comes from the workgroup's LDS copy.
 template <int NK4>
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
+__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
   constexpr int S = ((NK4 + 3) / 4) * 16 + 4, NQT = (NK4 + 3) / 4;
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.z);
+  int bx = blockIdx.x, bz = blockIdx.z;  // xcd: the replica's workgroups (its window tile) on one XCD
+  if (xcd) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
+  const int r = rc_rep(c, bz);
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
   const int rows = ms_rows(B);
   extern __shared__ float Xs[];
@@ -964,7 +972,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw) {
   // the Adam moments are read only when they exist (RC_GRAD_ONLY steps may run without them)
   float* PMr = adam ? PM : P;
   float* PVr = adam ? PV : P;
-  const int cb_lo = (int)blockIdx.x * 4 * bpw, cb_hi = min(NB, cb_lo + 4 * bpw) - 1;
+  const int cb_lo = bx * 4 * bpw, cb_hi = min(NB, cb_lo + 4 * bpw) - 1;
   const int kjlo = cb_lo / nU, nnet = cb_hi / nU - kjlo + 1;
   float* Dys = Xs + rows * S;
   {  // dL/dy of the workgroup's networks (zero past B), then the window tile
@@ -1160,7 +1168,7 @@ int rc_fac_slots(const RedcliffDims& d) { return rc_fac_short(d) ? (d.h + 15) / 
 // Launch of the short-contraction kernels: the k-step count picks the instantiation, and the
 // blocks per wave are chosen from the resident workgroups (the occupancy the runtime computes
 // from the kernel's registers and this launch's LDS, times the CUs).  REDCLIFF_FAC_BPW=n overrides.
-typedef void (*MsKern)(StepCtx, int);
+typedef void (*MsKern)(StepCtx, int, int);
 template <int N>
 struct MsTab {
   static void fill(MsKern* f, MsKern* b) {
@@ -1238,7 +1246,8 @@ static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
     const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), what);
     if (e) return e;
   }
-  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw);
+  const char* xe = getenv("REDCLIFF_S16_XCD");  // read per launch (A/B); default on
+  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), what);
 }
 
@@ -1261,7 +1270,8 @@ int rc_launch_fac_mix(const StepCtx& c, hipStream_t s) {
   const int KP = d.K * d.p;
   const size_t lds = fac_mix_lds(d, c.Ls);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor mixing: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  hipLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c);
+  const char* xe = getenv("REDCLIFF_MIX_XCD");  // read per launch (A/B); default on
+  hipLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), "k_fac_mix");
 }
 
