@@ -52,6 +52,33 @@ def data(N, seed):
     return [(X[i:i + 64], Y[i:i + 64]) for i in range(0, N, 64)]
 
 
+@pytest.mark.parametrize("emb", [None, "gemm"])
+def test_pack_xcd_orders_bitwise(emb, monkeypatch):
+    """XCD-aware workgroup orders (rc_gemm_tile for the GEMM core, rc_xcd_order for k_fac_mix and the
+    short-contraction factor kernels: every workgroup of one replica on one XCD once the replica
+    count is a multiple of 8) against dispatch order (REDCLIFF_*_XCD=0): a bijection of the same
+    workgroups, so 8 replicas trained through all three phases end bit-identical."""
+    from redcliff_amd import ReplicaPack
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "mfma")
+    if emb:
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", emb)
+    train = data(64 * 2 + 24, seed=9)
+    states = {}
+    for v in ("1", "0"):
+        for k in ("REDCLIFF_GEMM_XCD", "REDCLIFF_MIX_XCD", "REDCLIFF_S16_XCD"):
+            monkeypatch.setenv(k, v)
+        models = [make(s, fc, adj) for s, fc, adj, _, _ in GRID8]
+        pack = ReplicaPack(models, [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA) in zip(models, GRID8)])
+        ds = pack.cache_dataset(train)
+        for epoch in (0, 1, 2, 3):
+            pack.run_epoch(epoch, ds)
+        torch.cuda.synchronize()
+        states[v] = [{k: t.detach().cpu().numpy() for k, t in m.state_dict().items()} for m in models]
+    for r, (a, b) in enumerate(zip(states["1"], states["0"])):
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg="replica %d %s" % (r, k))
+
+
 @pytest.mark.parametrize("path,grid,emb", [("vector", GRID, None), ("mfma", GRID, None), ("mfma", GRID8, None),
                                           ("mfma", GRID, "gemm"), ("mfma", GRID8, "batched")])
 def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
