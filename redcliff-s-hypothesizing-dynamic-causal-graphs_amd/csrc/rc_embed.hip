@@ -1216,24 +1216,59 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
       // packed replicas (combined records, several runs per thread): every run's gradient, then
       // the parameters and both moments of all runs requested together and the Adam steps -- one
       // memory round for the workgroup instead of one per run; the same values and operations
+      // per run: the parameter index and where its gradient comes from (no loads yet): one
+      // combined record (fc / fc1 weights -- all runs of every workgroup but the first), or the
+      // dwN node slices of W_i / the dgN BatchNorm partials (the first parameter workgroup)
       float g[EF_EPT_MAX];
-      int64_t ix[EF_EPT_MAX];
+      int64_t ix[EF_EPT_MAX], go[EF_EPT_MAX];
+      int kind[EF_EPT_MAX];  // 0: past the end, 1: one record at go, 2: W_i slices, 3: BN affine
 #pragma unroll
       for (int run = 0; run < EF_EPT_MAX; ++run) {
         ix[run] = -1;
-        g[run] = 0.f;
+        go[run] = 0;
+        kind[run] = 0;
         const int e = ((wx - 1) * ept + run) * RC_BLOCK + threadIdx.x;
         if (run >= ept || e >= total) continue;
         if (e < nFH) {
-          float t = 0.f;
-          for (int cc = 0; cc < c.dwN; ++cc) t += ws[c.wo.dWi + (int64_t)cc * nFH + e];
-          g[run] = t;
+          kind[run] = 2;
           ix[run] = c.eo.gcW + e;
         } else if (e < nFH + nfc) {
           const int q = e - nFH;
-          g[run] = ws[c.wo.gfc + q];
+          kind[run] = 1;
+          go[run] = c.wo.gfc + q;
           ix[run] = q < K * M1 ? c.eo.fc2W + q : (q < K * M1 + K ? c.eo.fc2b + (q - K * M1) : c.eo.fc1b + (q - K * M1 - K));
         } else if (e < nFH + nfc + 2 * F) {
+          const int q = e - nFH - nfc;
+          kind[run] = 3;
+          ix[run] = (q < F ? c.eo.bnw : c.eo.bnb) + (q < F ? q : q - F);
+        } else {
+          const int q = e - nFH - nfc - 2 * F;
+          kind[run] = 1;
+          go[run] = c.wo.gfc1 + q;
+          ix[run] = c.eo.fc1W + q;
+        }
+      }
+      // the one-record gradients of all runs requested together (the other runs read offset 0)
+#pragma unroll
+      for (int run = 0; run < EF_EPT_MAX; ++run) {
+        const float v = ws[go[run]];
+        g[run] = kind[run] == 1 ? v : 0.f;
+      }
+#pragma unroll
+      for (int run = 0; run < EF_EPT_MAX; ++run) {
+        const int e = ((wx - 1) * ept + run) * RC_BLOCK + threadIdx.x;
+        if (kind[run] == 2) {  // sum of the dwN node slices in slice order, 8 loads per round
+          float t = 0.f;
+          for (int c0 = 0; c0 < c.dwN; c0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = ws[c.wo.dWi + (int64_t)(c0 + u < c.dwN ? c0 + u : 0) * nFH + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (c0 + u < c.dwN) t += v[u];
+          }
+          g[run] = t;
+        } else if (kind[run] == 3) {
           const int q = e - nFH - nfc;
           const int which = q / F, f = q - which * F;
           float g4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1243,11 +1278,6 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
             for (int u = 0; u < 4; ++u) g4[u] += ws[c.wo.dgb + ((int64_t)(pt + u) * 2 + which) * F + f];
           for (; pt < c.dgN; ++pt) g4[0] += ws[c.wo.dgb + ((int64_t)pt * 2 + which) * F + f];
           g[run] = (g4[0] + g4[1]) + (g4[2] + g4[3]);
-          ix[run] = (which == 0 ? c.eo.bnw : c.eo.bnb) + f;
-        } else {
-          const int q = e - nFH - nfc - 2 * F;
-          g[run] = ws[c.wo.gfc1 + q];
-          ix[run] = c.eo.fc1W + q;
         }
       }
       float pv[EF_EPT_MAX], mv[EF_EPT_MAX], vv[EF_EPT_MAX];
