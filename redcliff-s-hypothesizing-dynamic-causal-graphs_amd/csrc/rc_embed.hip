@@ -648,6 +648,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       for (int s = slS; s < nbc; s += nslS) {
         const float* dt = dTc + s * nF + i * F;
         const float* xr = xc + s * pF + cp * F;
+#pragma unroll 4  // (LDS reads of 4 features in flight; the same running sum)
         for (int f = 0; f < F; ++f) aS += dt[f] * (xr[f] * alpha[f] + beta[f]);
       }
     }
@@ -662,6 +663,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
             u = (xs_[node * F] - mu) * iv;
           } else {
             u = 0.f;
+#pragma unroll 4
             for (int cc = 0; cc < p; ++cc) u += Srow[i * p + cc] * ((xs_[cc * F] - mu) * iv);
           }
           const float dt = dTc[s * nF + i * F + f];
@@ -717,6 +719,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   __syncthreads();
   if (tid < nS) {
     float t = 0.f;
+#pragma unroll 4
     for (int q = 0; q < nslS; ++q) t += red[q * nS + tid];
     part[ofs_s + tid] = t;
   }
@@ -725,6 +728,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   __syncthreads();
   if (tid < F) {
     float t = 0.f;
+#pragma unroll 4
     for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
     part[ofs_g + tid] = t;
   }
@@ -733,6 +737,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   __syncthreads();
   if (tid < F) {
     float t = 0.f;
+#pragma unroll 4
     for (int q = 0; q < nslF; ++q) t += red[q * F + tid];
     part[ofs_g + F + tid] = t;
   }

@@ -263,6 +263,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
     if (tid < nsl * B) {
       const float wb = wk[b];
       for (int cc = sl; cc < p; cc += nsl)
+#pragma unroll 4
         for (int i = 0; i < Ls; ++i) {
           const float g = Gs[cc * L + (L - Ls + i)];
           const float val = wb * g + Acol[cc];
@@ -305,7 +306,8 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       const int cc = e / Ls, i = e - cc * Ls;
       const float g = Gs[cc * L + (L - Ls + i)];
       float sw = 0.f, s1v = 0.f;
-      for (int b = sl; b < B; b += nsl) {
+#pragma unroll 8
+      for (int b = sl; b < B; b += nsl) {  // (unrolled: the LDS reads of 8 windows in flight, same order)
         const float sg = rc_sign(wk[b] * g + Acol[cc]);
         sw += sg * wk[b];
         s1v += sg;
