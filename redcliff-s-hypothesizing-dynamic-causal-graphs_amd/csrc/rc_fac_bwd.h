@@ -352,6 +352,10 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   }
   __syncthreads();
 
+  // trace builds: the update part's phases are recorded by the (network 0, chunk 1) workgroup
+  const int tbx = (kj == 0 && uc == 1 && qc == 0 && role == RC_FB_ALL) ? 0 : 1;
+  (void)tbx;
+  RC_PHASE(c.ws, c.wo.total, tbx, 19);
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
   // ---- part 3: over window tiles of FB_BT (one tile when B <= 128; the first is already staged)
   const int uu = tid & 15, part = tid >> 4;  // 3a: 16 slices of the batch per hidden unit
@@ -427,6 +431,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       else
         recompute_a(nb);
     }
+    RC_PHASE(c.ws, c.wo.total, tbx, 20);
     // 3a (column tile 0): output-layer / bias gradients of the chunk's hidden units
     if (qc == 0) {
       const float w1 = w1s[uu];
@@ -470,7 +475,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       }
     }
   }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 21);
+  RC_PHASE(c.ws, c.wo.total, tbx, 21);
   if (qc == 0) {
     rA[tid] = dW1u;
     rB[tid] = db0u;
@@ -487,7 +492,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
     }
     if (uc == 0 && tid == 0) rc_adam_pre(c, P, PM, PV, GF, c.fo.b1 + kj, db1, as, s1[0], s1[1], s1[2]);
   }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 22);
+  RC_PHASE(c.ws, c.wo.total, tbx, 22);
   // dW0 tile: + adjacency-L1 term through the group norms, then Adam
   {
 #pragma unroll
@@ -500,7 +505,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
       rc_adam_pre(c, P, PM, PV, GF, idx, g, as, pw[jj], pm[jj], pv[jj]);
     }
   }
-  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 23);
+  RC_PHASE(c.ws, c.wo.total, tbx, 23);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 1);
 }
 

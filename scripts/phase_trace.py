@@ -56,6 +56,9 @@ def main():
         idx = [i for i in range(hi - lo) if t[i] > 0]
         if len(idx) > 1:
             print(label + ": " + "  ".join("%d->%d %.2f" % (lo + a, lo + b, (t[b] - t[a]) / 100.0) for a, b in zip(idx, idx[1:])))
+    upd = [(i, (ph[i] - t_first) / 100.0) for i in range(19, 24) if ph[i] > 0]
+    if upd:  # the (network 0, chunk 1) factor workgroup's update part (rc_fac_bwd.h, trace builds)
+        print("factor update WG (network 0, chunk 1) phases at: " + "  ".join("%d %.2f us" % x for x in upd))
     for k, name in enumerate(names):
         st, en = tr[k][0::2], tr[k][1::2]
         ok = (st > 0) & (en > 0)
