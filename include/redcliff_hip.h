@@ -30,8 +30,12 @@
 extern "C" {
 #endif
 
-/* 8: the workspace region y is laid out network-major, y[nU][K][p][Bmax] (was y[nU][Bmax][K][p]) */
-#define REDCLIFF_ABI_VERSION 8
+/* 8: the workspace region y is laid out network-major, y[nU][K][p][Bmax] (was y[nU][Bmax][K][p])
+ * 9: redcliff_factor_forward writes finished predictions y_out[r][B][K][p] (callers no longer decode
+ *    the kernel-private workspace); redcliff_factor_forward_workspace_floats sizes its workspace;
+ *    redcliff_step_predictions reads a step's predictions back the same way; RedcliffAdamHyper.t_offset
+ *    (was padding) offsets a replica's Adam step number from the launch's */
+#define REDCLIFF_ABI_VERSION 9
 
 /* error codes (negative) */
 #define REDCLIFF_EINVAL (-1)  /* bad dimension / pointer                        */
@@ -81,7 +85,9 @@ typedef struct RedcliffAdamHyper {
   float beta2_f;            /* (float)beta2                                  */
   float one_minus_beta1_f;  /* (float)(1 - beta1): lerp weight               */
   float one_minus_beta2_f;  /* (float)(1 - beta2): addcmul value             */
-  float pad_;
+  int32_t t_offset;         /* this replica's Adam step number minus the launch's tA / tB (packed
+                               fits whose replicas stepped this group different numbers of times:
+                               mixed phase schedules, ...withStateSmoothing.py:741-759); 0 otherwise */
 } RedcliffAdamHyper;
 
 /* Per-replica hyper-parameters, stored as a device array of R entries. */
@@ -173,10 +179,16 @@ int redcliff_train_steps(const RedcliffStepArgs* a, int32_t nsteps, const int64_
 
 /* Offsets (floats, per replica) of the workspace regions: T R f1 w a y G G0 w1 dwp dAadj dWi dS
  * dgb S dZ amat lossp xsim gfc total.  Returns the number of offsets available.  The host reads
- * w (raw embedder output), y (per-factor predictions as nU = ceil(h/16) partial sums
- * y[nU][K][p][Bmax] over 16-unit hidden chunks), xsim (mixed forecast), G / G0 (group norms)
- * back from a step run with RC_STORE_OUTPUTS. */
+ * w (raw embedder output, [B][K]), xsim (mixed forecast, [B][p]) and G / G0 (group norms) back
+ * from a step run with RC_STORE_OUTPUTS; the per-factor predictions through
+ * redcliff_step_predictions (the y region itself is kernel-private partial sums). */
 int redcliff_workspace_layout(const RedcliffDims* d, int64_t* out, int32_t n_out);
+
+/* Per-factor predictions of the last RC_STORE_OUTPUTS step of the R replicas of workspace ws (sized
+ * for d): y_out[r][b][k][j] (y_rstride floats between replicas), b < B.  The models' per-factor
+ * outputs of forward (...withStateSmoothing.py:326-385). */
+int redcliff_step_predictions(const RedcliffDims* d, int32_t B, const void* ws, float* y_out, int64_t y_rstride,
+                              void* stream);
 
 /* Device status of the R replica slices of a workspace (no reference counterpart: the
  * reference has no device code).  out[r] (host array of R u32) receives replica r's count of
@@ -196,13 +208,15 @@ int redcliff_debug_guard_bands(int32_t floats);
  * order (out[2i], out[2i+1]); returns the region count. */
 int redcliff_workspace_regions(const RedcliffDims* d, int64_t* out, int32_t n_pairs);
 
-/* Stand-alone forward of K cMLPs (models/cmlp.py:90-101) on B windows Xwin[r][B][L][p]
- * (x_rstride floats between replicas).  Per replica (ws_rstride floats) the workspace
- * receives a[K][p][B][h] | y[nU][K][p][B] | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h];
- * sum_u y[u][k][j][b] (nU = ceil(h/16) hidden-chunk partials, output bias in chunk 0) is
- * the prediction of network j of factor k for window b. */
+/* Stand-alone forward of K cMLPs (models/cmlp.py:90-101, MLP.forward :29-35) on B windows
+ * Xwin[r][B][L][p] (x_rstride floats between the R = d->R replicas): y_out[r][b][k][j]
+ * (y_rstride floats between replicas) receives the prediction of network j of factor k for
+ * window b.  ws: scratch of redcliff_factor_forward_workspace_floats(d, B) floats per replica
+ * (ws_rstride floats between replicas; its contents are private to the kernels). */
+size_t redcliff_factor_forward_workspace_floats(const RedcliffDims* d, int32_t B);
 int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride, const float* fac,
-                            int64_t fac_stride, float* ws, int64_t ws_rstride, void* stream);
+                            int64_t fac_stride, float* ws, int64_t ws_rstride, float* y_out, int64_t y_rstride,
+                            void* stream);
 
 /* G[r][k][j][c][t] = ||W0[k][j][:, c, t]||_2, G0[r][k][j][c] = ||W0[k][j][:, c, :]||_F (models/cmlp.py:147-167) */
 int redcliff_gc_norms(const RedcliffDims* d, const float* fac, int64_t fac_stride, float* G, float* G0, void* stream);
@@ -249,6 +263,13 @@ int redcliff_gemm(int32_t trans_a, int32_t trans_b, int32_t M, int32_t N, int32_
 int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt, const float* est,
                          const double* truth, const double* eps_pow, double in_degree_coeff, double out_degree_coeff,
                          double* out, void* stream);
+/* The same with one truth block per group of spt consecutive samples: sample s is scored against
+ * truth[s / spt] ([S / spt][2][G][p][p]) -- a packed grid whose replicas fit different data sets
+ * (train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:66-72: one model over many
+ * datasets, each with its own true graphs).  redcliff_gc_progress is spt = S. */
+int redcliff_gc_progress_grouped(int32_t S, int32_t spt, int32_t nE, int32_t G, int32_t p, int32_t Lt,
+                                 const float* est, const double* truth, const double* eps_pow, double in_degree_coeff,
+                                 double out_degree_coeff, double* out, void* stream);
 
 /* Per-epoch tracker statistics of fit() (replaces the host reductions of
  * general_utils/model_utils.py:163-188 (L1 tracker) and :191-209 (cosine tracker), which the

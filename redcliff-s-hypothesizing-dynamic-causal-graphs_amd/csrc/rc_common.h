@@ -514,6 +514,7 @@ struct RcAdamScalars {
 };
 __device__ inline RcAdamScalars rc_adam_scalars(const RedcliffAdamHyper& h, int t) {
   RcAdamScalars s;
+  t += h.t_offset;  // per-replica step number of a packed launch (0 unless the pack's schedules differ)
   const double bc1 = 1.0 - pow(h.beta1, (double)t);
   const double bc2 = 1.0 - pow(h.beta2, (double)t);
   s.neg_step = (float)(-(h.lr / bc1));

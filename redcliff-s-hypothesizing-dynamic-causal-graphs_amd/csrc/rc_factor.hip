@@ -27,6 +27,22 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ
   fac_bwd_wg(c, nUl, nQ, kj, uc, qc, rc_rep(c, blockIdx.y), sm, nullptr, role);
 }
 
+// Finished predictions of the stand-alone forward: out[r][b][k][j] = sum over the nU hidden-chunk
+// partials y[u][k][j][b] (u ascending from 0, the order every consumer in the training step uses;
+// the output bias sits in chunk 0), one thread per output, windows fastest in the reads.
+// bstride: the window stride of the slots (B for the stand-alone forward, Bmax in a step workspace)
+__global__ __launch_bounds__(256) void k_fac_pred(const float* __restrict__ ws, int64_t wss, int64_t yoff, int B,
+                                                  int bstride, int kp, int nU, float* __restrict__ out,
+                                                  int64_t out_rs) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)kp * B) return;
+  const int kj = (int)(i / B), b = (int)(i - (int64_t)kj * B);
+  const float* y = ws + (int64_t)blockIdx.y * wss + yoff;
+  float s = y[(int64_t)kj * bstride + b];
+  for (int u = 1; u < nU; ++u) s += y[((int64_t)u * kp + kj) * bstride + b];
+  out[(int64_t)blockIdx.y * out_rs + (int64_t)b * kp + kj] = s;
+}
+
 }  // namespace
 
 // The vector factor backward stages per-window terms of the whole batch in LDS; past the
@@ -68,14 +84,32 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role) {
 }
 
 // Stand-alone forward of K cMLPs on B windows Xwin[B][L][p] (cMLP.forward, models/cmlp.py:90-101,
-// and the per-factor predictions of REDCLIFF forward).  Per replica the workspace holds
-// a[K][p][B][h] | y[nU][B][K][p] (partials over hidden chunks) | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h]
-// | gq[nU][K][p][p*L].  G / G0 are left unset (use redcliff_gc_norms).
+// and the per-factor predictions of REDCLIFF forward).  Per replica the (kernel-private) workspace
+// holds a[K][p][B][h] | y[nU][K][p][B] (partials over hidden chunks, network-major: rc_y_idx with
+// Bmax = B) | G[K][p][p][L] | G0[K][p][p] | w1[K][p][h] | gq[nU][K][p][p*L]; k_fac_pred then writes
+// the finished predictions y_out[r][B][K][p].
+static int64_t fac_fwd_ws_floats(const RedcliffDims& d, int B) {
+  const int64_t kp = (int64_t)d.K * d.p, nU = rc_nuchunk(d);
+  return kp * B * d.h + nU * B * kp + kp * d.p * d.L + kp * d.p + kp * d.h + nU * kp * d.p * d.L;
+}
+
+extern "C" size_t redcliff_factor_forward_workspace_floats(const RedcliffDims* d, int32_t B) {
+  if (!d || B < 1 || d->K < 1 || d->p < 1 || d->h < 1 || d->L < 1) return 0;
+  return (size_t)fac_fwd_ws_floats(*d, B);
+}
+
 extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const float* Xwin, int64_t x_rstride,
                                        const float* fac, int64_t fac_stride, float* ws, int64_t ws_rstride,
-                                       void* stream) {
-  if (!d || !Xwin || !fac || !ws || B < 1) { rc_set_error("factor_forward: bad arguments"); return REDCLIFF_EINVAL; }
+                                       float* y_out, int64_t y_rstride, void* stream) {
+  if (!d || !Xwin || !fac || !ws || !y_out || B < 1 || d->R < 1) {
+    rc_set_error("factor_forward: bad arguments");
+    return REDCLIFF_EINVAL;
+  }
   if (d->p > 64 || d->h > 128 || d->L > 64) { rc_set_error("factor_forward: dims outside kernel limits"); return REDCLIFF_ELIMIT; }
+  if (d->R > 1 && (ws_rstride < fac_fwd_ws_floats(*d, B) || y_rstride < (int64_t)B * d->K * d->p)) {
+    rc_set_error("factor_forward: replica strides smaller than one replica's workspace / predictions");
+    return REDCLIFF_EINVAL;
+  }
   StepCtx c;
   memset(&c, 0, sizeof(c));
   c.nrep = d->R;
@@ -101,5 +135,26 @@ extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const f
   c.wo.G0 = c.wo.G + kp * d->p * d->L;
   c.wo.w1 = c.wo.G0 + kp * d->p;
   c.wo.gq = c.wo.w1 + kp * d->h;
-  return rc_launch_fac_fwd(c, (hipStream_t)stream);
+  int rc = rc_launch_fac_fwd(c, (hipStream_t)stream);
+  if (rc) return rc;
+  const int64_t n = kp * B;
+  hipLaunchKernelGGL(k_fac_pred, dim3((unsigned)((n + 255) / 256), d->R), dim3(256), 0, (hipStream_t)stream, ws,
+                     ws_rstride, c.wo.y, B, B, (int)kp, rc_nuchunk(*d), y_out, y_rstride);
+  return rc_check(hipGetLastError(), "k_fac_pred");
+}
+
+// Per-factor predictions of the last RC_STORE_OUTPUTS step (redcliff_train_step) from its workspace
+// (R replica slices): y_out[r][b][k][j] for the step's B windows.
+extern "C" int redcliff_step_predictions(const RedcliffDims* d, int32_t B, const void* ws, float* y_out,
+                                         int64_t y_rstride, void* stream) {
+  if (!d || !ws || !y_out || B < 1 || B > d->Bmax || d->R < 1) {
+    rc_set_error("step_predictions: bad arguments");
+    return REDCLIFF_EINVAL;
+  }
+  const WsOff o = rc_ws_off(*d);
+  const int64_t kp = (int64_t)d->K * d->p, n = kp * B;
+  if (d->R > 1 && y_rstride < n) { rc_set_error("step_predictions: y_rstride < B*K*p"); return REDCLIFF_EINVAL; }
+  hipLaunchKernelGGL(k_fac_pred, dim3((unsigned)((n + 255) / 256), d->R), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)ws, o.total, o.y, B, d->Bmax, (int)kp, rc_nuchunk(*d), y_out, y_rstride);
+  return rc_check(hipGetLastError(), "k_fac_pred");
 }

@@ -225,13 +225,16 @@ __device__ GpRoc gp_roc_f1(const float* xs, const double* t, int pp, double* red
   return o;
 }
 
-// grid (S * G); dynamic LDS 36 p^2 bytes (+ small statics)
+// grid (S * G); dynamic LDS 36 p^2 bytes (+ small statics).  Sample s is scored against truth
+// block s / spt ([2][G][p][p] each): one block for a fit, one per replica for a packed grid whose
+// replicas fit different data sets (each with its own true graphs).
 template <int NT>
-__global__ __launch_bounds__(NT) void k_gc_progress(int S, int nE, int G, int p, int Lt, const float* est,
+__global__ __launch_bounds__(NT) void k_gc_progress(int S, int spt, int nE, int G, int p, int Lt, const float* est,
                                                           const double* truth, const double* eps_pow, double cin,
                                                           double cout, double* out) {
   const int s = blockIdx.x / G, g = blockIdx.x - s * G;
   const int pp = p * p, NM = 6 + p, tid = threadIdx.x;
+  truth += (int64_t)(s / spt) * 2 * G * pp;
   extern __shared__ double smd[];
   double* T = smd;                                   // [pp] truth (with self-connections)
   double* Aug = T + pp;                              // [p][2p] inverse workspace; later Tk | Tn
@@ -590,9 +593,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_gc_dots(const float* x, int K, int
 
 }  // namespace
 
-extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt, const float* est,
-                                    const double* truth, const double* eps_pow, double in_degree_coeff,
-                                    double out_degree_coeff, double* out, void* stream) {
+extern "C" int redcliff_gc_progress_grouped(int32_t S, int32_t spt, int32_t nE, int32_t G, int32_t p, int32_t Lt,
+                                            const float* est, const double* truth, const double* eps_pow,
+                                            double in_degree_coeff, double out_degree_coeff, double* out,
+                                            void* stream) {
+  if (S > 0 && spt < 1) { rc_set_error("gc_progress: samples per truth block must be >= 1"); return REDCLIFF_EINVAL; }
   if (S < 0 || G < 0 || nE < G || p < 2 || p > 64 || Lt < 1 || Lt > 128 || (S * G > 0 && (!est || !truth || !eps_pow || !out))) {
     rc_set_error("gc_progress: bad arguments (S=%d nE=%d G=%d p=%d Lt=%d; need 2 <= p <= 64, Lt <= 128, G <= nE)", S, nE,
                  G, p, Lt);
@@ -605,10 +610,10 @@ extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p,
     return !(v && strcmp(v, "0") == 0);
   }();
   if (p <= 16 && wave_form) {  // one wave per (sample, graph): the same bits as the 256-thread form
-    hipLaunchKernelGGL(k_gc_progress<64>, dim3(S * G), dim3(64), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
+    hipLaunchKernelGGL(k_gc_progress<64>, dim3(S * G), dim3(64), lds, (hipStream_t)stream, S, spt, nE, G, p, Lt, est,
                        truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
   } else if (p <= 32) {
-    hipLaunchKernelGGL(k_gc_progress<256>, dim3(S * G), dim3(256), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
+    hipLaunchKernelGGL(k_gc_progress<256>, dim3(S * G), dim3(256), lds, (hipStream_t)stream, S, spt, nE, G, p, Lt, est,
                        truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
   } else {
     if (lds > 64 * 1024) {
@@ -617,10 +622,17 @@ extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p,
                              "k_gc_progress LDS");
       if (e) return e;
     }
-    hipLaunchKernelGGL(k_gc_progress<1024>, dim3(S * G), dim3(1024), lds, (hipStream_t)stream, S, nE, G, p, Lt, est,
+    hipLaunchKernelGGL(k_gc_progress<1024>, dim3(S * G), dim3(1024), lds, (hipStream_t)stream, S, spt, nE, G, p, Lt, est,
                        truth, eps_pow, in_degree_coeff, out_degree_coeff, out);
   }
   return rc_check(hipGetLastError(), "k_gc_progress");
+}
+
+extern "C" int redcliff_gc_progress(int32_t S, int32_t nE, int32_t G, int32_t p, int32_t Lt, const float* est,
+                                    const double* truth, const double* eps_pow, double in_degree_coeff,
+                                    double out_degree_coeff, double* out, void* stream) {
+  return redcliff_gc_progress_grouped(S, S > 0 ? S : 1, nE, G, p, Lt, est, truth, eps_pow, in_degree_coeff,
+                                      out_degree_coeff, out, stream);
 }
 
 extern "C" int redcliff_gc_track_stats(int32_t n_l1_rows, int64_t l1_len, const float* est, double* l1_out,

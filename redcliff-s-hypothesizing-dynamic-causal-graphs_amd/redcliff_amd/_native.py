@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_LIB_PATH = os.path.join(_HERE, "lib", "libredcliff_hip.so")
 LIB_PATH = os.environ.get("REDCLIFF_HIP_LIB", DEFAULT_LIB_PATH)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # RC_* step flags (include/redcliff_hip.h)
 BN_TRAIN = 1 << 0
@@ -33,9 +33,10 @@ WS_REGIONS = ("T", "R", "f1", "w", "a", "y", "G", "G0", "w1", "gq", "ebp", "ecnt
 
 EXPORTED = ("redcliff_abi_version", "redcliff_last_error", "redcliff_workspace_bytes", "redcliff_emb_param_count",
             "redcliff_fac_param_count", "redcliff_bn_batch_stats", "redcliff_dgcnn_supports", "redcliff_train_step",
-            "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward", "redcliff_gc_norms",
+            "redcliff_train_steps", "redcliff_workspace_layout", "redcliff_factor_forward",
+            "redcliff_factor_forward_workspace_floats", "redcliff_step_predictions", "redcliff_gc_norms",
             "redcliff_prox", "redcliff_kernel_timing", "redcliff_kernel_times", "redcliff_adam_apply", "redcliff_dp_update", "redcliff_gemm",
-            "redcliff_gc_progress", "redcliff_debug_guard_bands", "redcliff_workspace_regions",
+            "redcliff_gc_progress", "redcliff_gc_progress_grouped", "redcliff_debug_guard_bands", "redcliff_workspace_regions",
             "redcliff_gc_track_stats", "redcliff_device_status", "redcliff_build_id")
 KERNEL_IDS = ("supports", "emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix", "emb_combine", "fac_lead")
 
@@ -48,7 +49,7 @@ class Dims(ctypes.Structure):
 class AdamHyper(ctypes.Structure):
     _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
                 ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float), ("beta2_f", ctypes.c_float),
-                ("one_minus_beta1_f", ctypes.c_float), ("one_minus_beta2_f", ctypes.c_float), ("pad_", ctypes.c_float)]
+                ("one_minus_beta1_f", ctypes.c_float), ("one_minus_beta2_f", ctypes.c_float), ("t_offset", ctypes.c_int32)]
 
 
 class ReplicaHyper(ctypes.Structure):
@@ -78,7 +79,7 @@ class StepArgs(ctypes.Structure):
 
 def adam_hyper(lr, betas, eps, weight_decay):
     b1, b2 = float(betas[0]), float(betas[1])
-    return AdamHyper(float(lr), b1, b2, float(eps), float(weight_decay), b2, 1.0 - b1, 1.0 - b2, 0.0)
+    return AdamHyper(float(lr), b1, b2, float(eps), float(weight_decay), b2, 1.0 - b1, 1.0 - b2, 0)
 
 
 _LIB = None
@@ -108,7 +109,11 @@ def lib():
     L.redcliff_train_step.argtypes = [ctypes.POINTER(StepArgs), _vp]
     L.redcliff_train_steps.argtypes = [ctypes.POINTER(StepArgs), ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp]
     L.redcliff_workspace_layout.argtypes = [ctypes.POINTER(Dims), ctypes.POINTER(_i64), ctypes.c_int32]
-    L.redcliff_factor_forward.argtypes = [ctypes.POINTER(Dims), ctypes.c_int32, _vp, _i64, _vp, _i64, _vp, _i64, _vp]
+    L.redcliff_factor_forward.argtypes = [ctypes.POINTER(Dims), ctypes.c_int32, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                                          _i64, _vp]
+    L.redcliff_factor_forward_workspace_floats.restype = ctypes.c_size_t
+    L.redcliff_factor_forward_workspace_floats.argtypes = [ctypes.POINTER(Dims), ctypes.c_int32]
+    L.redcliff_step_predictions.argtypes = [ctypes.POINTER(Dims), ctypes.c_int32, _vp, _vp, _i64, _vp]
     L.redcliff_gc_norms.argtypes = [ctypes.POINTER(Dims), _vp, _i64, _vp, _vp, _vp]
     L.redcliff_prox.argtypes = [ctypes.POINTER(Dims), _vp, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_int32, _vp]
     L.redcliff_kernel_timing.argtypes = [ctypes.c_int32]
@@ -121,6 +126,8 @@ def lib():
                                 ctypes.c_int32, _vp]
     L.redcliff_gc_progress.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp]
+    L.redcliff_gc_progress_grouped.argtypes = [ctypes.c_int32] * 6 + [_vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
+                                                                      _vp, _vp]
     L.redcliff_gc_track_stats.argtypes = [ctypes.c_int32, _i64, _vp, _vp, ctypes.c_int32, ctypes.c_int32, _i64, _vp,
                                           _vp, _vp]
     L.redcliff_debug_guard_bands.argtypes = [ctypes.c_int32]

@@ -582,10 +582,9 @@ class FitEngine:
             self.dgcnn.BN1.num_batches_tracked.add_(bn_updates)
         o = self.ws_off
         w = self.ws[o["w"]:o["w"] + B * self.K].view(B, self.K).clone()
-        nU = (self.h + 15) // 16  # the forward kernel leaves per-hidden-chunk partials
-        # slots [nU][network k * p + j][Bmax] (rc_y_idx) -> (B, K, p)
-        y = self.ws[o["y"]:o["y"] + nU * d.Bmax * self.K * self.p].view(nU, self.K, self.p, d.Bmax)[..., :B].sum(0)
-        y = y.permute(2, 0, 1).contiguous()
+        y = torch.empty(B, self.K, self.p, device=self.device, dtype=torch.float32)
+        nat.check(nat.lib().redcliff_step_predictions(ctypes.byref(d), B, ptr(self.ws), ptr(y), y.numel(), _stream()),
+                  "step_predictions")
         xs = self.ws[o["xsim"]:o["xsim"] + B * self.p].view(B, self.p).clone()
         return w, y, xs
 

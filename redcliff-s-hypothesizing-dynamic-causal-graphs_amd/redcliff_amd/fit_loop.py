@@ -225,11 +225,24 @@ class FitTracker:
             self.h[k].append(v)
         self._vf, self._vfac = vals[0], vals[1]
 
+    def past_warmup(self, it):
+        """Epoch `it` is past pretraining and acclimation: the stopping rule applies (:1483)."""
+        m = self.model
+        return it >= m.num_pretrain_epochs + m.num_acclimation_epochs
+
+    def may_stop(self, it):
+        """step(it) can return True only when this holds (the fit can stop at `it` only past the
+        warm-up and exactly lookback * check_every epochs after its best epoch, :1549-1559).  The
+        packed fit asks it before epoch `it` is decided, to skip saving the Adam moments when no
+        replica can be rolled back; step() itself decides through the same test."""
+        return self.past_warmup(it) and self.best_it is not None and \
+            (it - self.best_it) == self.lookback * self.check_every
+
     def step(self, it, snapshot):
         """Early stopping (:1482-1559).  snapshot() makes the best-model copy; returns True when
         the fit stops at this epoch."""
         m = self.model
-        if it >= m.num_pretrain_epochs + m.num_acclimation_epochs:
+        if self.past_warmup(it):
             with np.errstate(all="ignore"):
                 cos_mean = np.mean([self.cos_hist[key][-1] for key in self.cos_hist.keys()]) if self.cos_hist else np.nan
             if "Freeze" in m.training_mode:  # :1486-1491; raises as the reference's does
@@ -242,7 +255,7 @@ class FitTracker:
                 crit = self.sc_forecast * self._vf
             if crit < self.best_loss:
                 self.best_loss, self.best_it, self.best_model = crit, it, snapshot()
-            elif (it - self.best_it) == self.lookback * self.check_every:
+            elif self.may_stop(it):
                 self.stopped_at = it
                 return True
         else:

@@ -108,17 +108,15 @@ def factor_forward_packed(flat, K, p, h, L, Xwin):
     chunk = 512
     for b0 in range(0, B, chunk):
         nb = min(chunk, B - b0)
-        kp = K * p
-        nU = (h + 15) // 16  # hidden-unit chunks of the forward kernel (FAC_UC)
-        ws_floats = kp * nb * h + nU * nb * kp + kp * p * L + kp * p + kp * h + nU * kp * p * L
-        ws = torch.empty(ws_floats, device=Xwin.device, dtype=torch.float32)
         dims = factor_dims(K, p, L, h, Bmax=nb)
+        ws_floats = nat.lib().redcliff_factor_forward_workspace_floats(ctypes.byref(dims), nb)
+        if ws_floats == 0:
+            nat.check(-1, "factor_forward_workspace_floats")
+        ws = torch.empty(ws_floats, device=Xwin.device, dtype=torch.float32)
         xw = Xwin[b0:b0 + nb].contiguous()
         nat.check(nat.lib().redcliff_factor_forward(ctypes.byref(dims), nb, ptr(xw), 0, ptr(flat), 0, ptr(ws),
-                                                    ws_floats, current_stream()), "factor_forward")
-        off = kp * nb * h
-        # slots [nU][network k * p + j][nb] (rc_y_idx with Bmax = nb)
-        out[b0:b0 + nb] = ws[off:off + nU * nb * kp].view(nU, K, p, nb).sum(0).permute(2, 0, 1)
+                                                    ws_floats, ptr(out[b0:b0 + nb]), nb * K * p, current_stream()),
+                  "factor_forward")
     return out
 
 

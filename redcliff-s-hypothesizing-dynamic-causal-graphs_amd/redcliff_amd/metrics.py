@@ -263,6 +263,41 @@ def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.
     return out.cpu().numpy() if host else out
 
 
+def gc_progress_values_grouped(GCs, est, spt, eps=0.1, in_degree_coeff=1., out_degree_coeff=1., host=True):
+    """gc_progress_values with one list of true graphs per group of `spt` consecutive samples
+    (GCs[i] scores samples i*spt .. i*spt+spt-1): the per-replica true graphs of a packed grid
+    whose replicas fit different data sets.  Every GCs[i] holds the same number of graphs."""
+    import ctypes
+    from . import _native as nat
+    S, nE, p, p2, Lt = est.shape
+    assert p == p2 and S == spt * len(GCs), (S, spt, len(GCs))
+    G = min([nE] + [len(g) for g in GCs])
+    if any(len(g) != len(GCs[0]) for g in GCs):
+        raise ValueError("per-replica true graphs must have one length")
+    dev = est.device
+    est = est.to(torch.float32).contiguous()
+    ids = tuple(id(x) for g in GCs for x in g)
+    hit = None
+    for ent in _TRUTH_CACHE:
+        if ent[0] is GCs and ent[1] == ids and ent[2:6] == (G, p, eps, dev):
+            hit = ent
+            break
+    if hit is None:
+        truth = torch.from_numpy(np.ascontiguousarray(np.stack([_truth_arrays(g, G) for g in GCs]))).to(dev)
+        eps_pow = torch.tensor([eps ** k for k in range(p)], dtype=torch.float64, device=dev)
+        hit = (GCs, ids, G, p, eps, dev, truth, eps_pow)
+        _TRUTH_CACHE.insert(0, hit)
+        del _TRUTH_CACHE[4:]
+    truth, eps_pow = hit[6], hit[7]
+    out = torch.empty(S, G, 6 + p, dtype=torch.float64, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    nat.check(nat.lib().redcliff_gc_progress_grouped(S, spt, nE, G, p, Lt, est.data_ptr(), truth.data_ptr(),
+                                                      eps_pow.data_ptr(), float(in_degree_coeff),
+                                                      float(out_degree_coeff), out.data_ptr(), stream),
+              "gc_progress_grouped")
+    return out.cpu().numpy() if host else out
+
+
 def _running(vals):
     """Per-graph running sums over samples in sample order (python floats), and the count."""
     run = None

@@ -9,9 +9,17 @@ carries the replica on blockIdx.y and every per-fit buffer (parameters, Adam mom
 BatchNorm running statistics, hyper-parameters, workspace, loss accumulators) is a row
 of an [R][...] tensor.  Replicas may differ in everything that is not a shape: seeds,
 coefficient dicts, learning rates / eps / weight decay of both optimizers, BatchNorm
-momentum, stopping-criterion coefficients.  They share the training windows (one dataset
-for the whole grid, as in the reference) and the phase schedule (pretrain / acclimation
-epochs; ``grid_packs`` groups a grid by shape and schedule).
+momentum, stopping-criterion coefficients, the phase schedule (pretrain / acclimation epochs,
+training mode: the TST grid varies them, train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:
+297-298) and the data.  A grid whose points share one dataset (the TST grid) passes one loader;
+a grid of one model over many datasets ("subjects": the synthetic grid is one model config over
+990 dataset variants, train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:66-72)
+passes ``PerReplica`` loaders and true graphs, which become [R][N][T][p] device tensors read
+through the kernels' replica strides.  Every epoch the active replicas are grouped by the update
+kinds their schedules give that epoch and each group is one launch chain; a replica's Adam step
+numbers ride in its hyper-parameter row (``t_offset``), so replicas that stepped a group
+different numbers of times share launches.  ``grid_packs`` groups a grid by shape (and data
+shape), ``shard_grid`` deals whole shape classes to GPUs.
 
 ``ReplicaPack.fit`` is the packed counterpart of ``fit()`` (...withStateSmoothing.py:
 1175-1647): every replica keeps its own histories, GC-progress trackers, best-epoch
@@ -36,6 +44,12 @@ from . import metrics as M
 from .engine import _stream, flags_for, phase_of_epoch
 from .fit_loop import (DeferredHistories, FitTracker, ParamSnapshot, conditional_gc_estimates, confusion_rates_many,
                        gc_progress_many, restore_parameters, standalone_copy, train_confusion_many)
+
+
+class PerReplica(list):
+    """Marks a per-replica argument of ``ReplicaPack.fit`` / ``cache_dataset``: element r belongs
+    to replica r -- its own training or validation loader (a subject / dataset of the grid; every
+    replica's loader must yield the same batch sizes) or its own list of true graphs."""
 
 
 class ReplicaPack:
@@ -129,13 +143,36 @@ class ReplicaPack:
             # inside fit(): nothing changes a coefficient, learning rate or BatchNorm setting of
             # a replica, so the [R] hyper-parameter rows built at the fit's first launch stand
             # (R key computations per launch were ~1 ms of host time per epoch at R = 128)
-            return self._hyper_cat
+            return self._with_offsets(self._hyper_cat)
         parts = [e._hyper() for e in self.engines]
         key = tuple(e.hyper_key for e in self.engines)
         if key != getattr(self, "_hyper_key", None):
             self._hyper_cat = torch.cat(parts).contiguous()
             self._hyper_key = key
-        return self._hyper_cat
+        return self._with_offsets(self._hyper_cat)
+
+    # byte offsets of RedcliffReplicaHyper.{A,B}.t_offset (include/redcliff_hip.h)
+    _HSIZE = ctypes.sizeof(nat.ReplicaHyper)
+    _TOFF = (nat.ReplicaHyper.A.offset + nat.AdamHyper.t_offset.offset,
+             nat.ReplicaHyper.B.offset + nat.AdamHyper.t_offset.offset)
+
+    def _with_offsets(self, base):
+        """The hyper rows `base` with every replica's Adam step offsets (self._toff [R][2], the
+        replica's step number minus its launch's) written in; the device copy is rebuilt only when
+        an offset changes (a replica crosses a phase boundary of a mixed-schedule pack)."""
+        toff = getattr(self, "_toff", None)
+        if toff is None or not toff.any():
+            return base
+        key = (base.data_ptr(), toff.tobytes())
+        cur = getattr(self, "_hyper_off", None)
+        if cur is None or cur[0] != key:
+            raw = base.cpu().numpy().reshape(self.R, self._HSIZE).copy()
+            for gi in (0, 1):
+                o = self._TOFF[gi]
+                raw[:, o:o + 4] = np.ascontiguousarray(toff[:, gi], dtype=np.int32).view(np.uint8).reshape(self.R, 4)
+            cur = (key, torch.from_numpy(raw.reshape(-1)).to(self.device))
+            self._hyper_off = cur
+        return cur[1]
 
     def _active_list(self, active):
         """(host int32 array or None, engines stepped)"""
@@ -150,19 +187,27 @@ class ReplicaPack:
         a.flags = flags | nat.REFRESH_SUPPORTS  # the pack's workspace holds its own supports
         a.n_bn_updates = nbn
         act, engs = self._active_list(active)
-        # the stepped groups' Adam step numbers are shared by the launch (bias corrections); replicas
-        # that stopped early keep theirs and are not in the active list
+        # Adam step numbers: the launch carries the smallest of the active replicas' (+1) and every
+        # replica's hyper row its difference from it (t_offset): replicas of a mixed-schedule pack
+        # may have stepped a group different numbers of times.  Replicas that stopped early keep
+        # theirs and are not in the active list.
         ts = []
-        for g, bit in (("A", nat.STEP_A), ("B", nat.STEP_B)):
-            t = set(e.opt[g]["t"] for e in engs if e.opt[g] is not None) or {0}
-            if (flags & bit) and len(t) != 1:
-                raise RuntimeError("packed replicas must share their Adam step counters (same update schedule)")
-            ts.append(min(t) + 1)
+        idx = list(range(self.R)) if act is None else [int(r) for r in act]
+        for gi, (g, bit) in enumerate((("A", nat.STEP_A), ("B", nat.STEP_B))):
+            t = [e.opt[g]["t"] if e.opt[g] is not None else 0 for e in engs]
+            t0 = min(t) if t else 0
+            ts.append(t0 + 1)
+            if (flags & bit) and any(x != t0 for x in t):
+                if getattr(self, "_toff", None) is None:
+                    self._toff = np.zeros((self.R, 2), dtype=np.int64)
+            if (flags & bit) and getattr(self, "_toff", None) is not None:
+                self._toff[idx, gi] = np.asarray(t, dtype=np.int64) - t0
         a.tA, a.tB = ts
-        a.X, a.x_rstride = ds["X"].data_ptr(), 0  # one dataset for the whole grid
-        a.labels, a.lab_rstride = (ds["lab"].data_ptr() if ds.get("lab") is not None else None), 0
+        # data: one dataset for the whole grid (strides 0), or per-replica data sets (PerReplica)
+        a.X, a.x_rstride = ds["X"].data_ptr(), ds.get("xr", 0)
+        a.labels, a.lab_rstride = (ds["lab"].data_ptr() if ds.get("lab") is not None else None), ds.get("labr", 0)
         a.bn_stats = stats.data_ptr() if stats is not None else None
-        a.bn_stats_rstride = 0
+        a.bn_stats_rstride = ds.get("statsr", 0) if stats is not None else 0
         a.emb, a.emb_stride = self.emb.data_ptr(), self.emb.shape[1]
         a.fac, a.fac_stride = self.fac.data_ptr(), self.fac.shape[1]
         a.emb_m, a.emb_v = self.m["A"].data_ptr(), self.v["A"].data_ptr()
@@ -248,8 +293,71 @@ class ReplicaPack:
                 e.ensure_bound()
 
     def cache_dataset(self, loader):
-        """Upload the (shared) training set once; see FitEngine.cache_dataset."""
+        """Upload a training / validation set once; see FitEngine.cache_dataset.  A ``PerReplica``
+        list of R loaders becomes one [R][N][T][p] window tensor (labels [R][N][K], BatchNorm batch
+        statistics [R][nbatch][2][F], one launch), read through the kernels' replica strides."""
+        if isinstance(loader, PerReplica):
+            return self._cache_per_replica(loader)
         return self.engines[0].cache_dataset(loader)
+
+    def _cache_per_replica(self, loaders):
+        from .engine import select_labels
+        key = tuple(id(x) for x in loaders)
+        cache = self.__dict__.setdefault("_pr_cache", {})
+        if key in cache:
+            return cache[key][1]
+        if len(loaders) != self.R:
+            raise ValueError("PerReplica data: %d loaders for %d replicas" % (len(loaders), self.R))
+        e0 = self.engines[0]
+        xs_all, labs_all, sizes0 = [], [], None
+        for r, loader in enumerate(loaders):
+            xs, ys, sizes = [], [], []
+            for X, Y in loader:
+                xs.append(X.to(torch.float32))
+                ys.append(select_labels(Y, e0.K, e0.Lmax) if Y is not None else torch.zeros(X.shape[0], e0.K))
+                sizes.append(int(X.shape[0]))
+            if sizes0 is None:
+                sizes0 = sizes
+            elif sizes != sizes0:
+                raise ValueError("PerReplica data: replica %d's batches %s differ from replica 0's %s (a pack's "
+                                 "replicas step the same batch sequence)" % (r, sizes, sizes0))
+            xs_all.append(torch.cat(xs, 0))
+            labs_all.append(torch.cat(ys, 0).to(torch.float32))
+        shapes = set(tuple(x.shape) for x in xs_all)
+        if len(shapes) != 1:
+            raise ValueError("PerReplica data: window shapes differ across replicas: %s" % sorted(shapes))
+        X = torch.stack(xs_all).to(self.device).contiguous()  # [R][N][T][p]
+        lab = torch.stack(labs_all).to(self.device).contiguous()  # [R][N][K]
+        R, N, T, p = X.shape
+        if p != e0.p:
+            raise ValueError("expected %d channels, got %d" % (e0.p, p))
+        rows = np.cumsum([0] + sizes0[:-1]).astype(np.int64)
+        nb = len(sizes0)
+        stats = torch.empty(R, nb, 2, e0.F, device=self.device, dtype=torch.float64)
+        d = self._dims(max(sizes0), T)
+        if all(s == sizes0[0] for s in sizes0[:-1]) and sizes0[-1] <= sizes0[0]:
+            nat.check(nat.lib().redcliff_bn_batch_stats(ctypes.byref(d), ctypes.c_void_p(X.data_ptr()), N * T * p, N,
+                                                        sizes0[0], ctypes.c_void_p(stats.data_ptr()), nb * 2 * e0.F,
+                                                        _stream()), "bn_batch_stats (per replica)")
+        else:
+            for i, (r0, s) in enumerate(zip(rows, sizes0)):
+                nat.check(nat.lib().redcliff_bn_batch_stats(
+                    ctypes.byref(d), ctypes.c_void_p(X[0, r0].data_ptr()), N * T * p, s, s,
+                    ctypes.c_void_p(stats[0, i].data_ptr()), nb * 2 * e0.F, _stream()), "bn_batch_stats (per replica)")
+        ds = {"X": X, "lab": lab, "rows": rows, "sizes": np.asarray(sizes0, dtype=np.int32), "stats": stats,
+              "T": int(T), "Bmax": max(sizes0), "len": nb, "loader": loaders, "per_replica": True,
+              "xr": N * T * p, "labr": N * e0.K, "statsr": nb * 2 * e0.F}
+        cache[key] = (loaders, ds)  # the loaders stay referenced, so their ids stay unique
+        return ds
+
+    @staticmethod
+    def _stats_at(ds, b0, nb=None):
+        """The BatchNorm batch statistics of ds from batch b0 on ([R][..] per replica, shared
+        otherwise): the kernels advance 2F doubles per step and a replica stride of ds["statsr"]."""
+        st = ds["stats"]
+        if ds.get("per_replica"):
+            return st[:, b0:] if nb is None else st[:, b0:b0 + nb]
+        return st[b0:] if nb is None else st[b0:b0 + nb]
 
     # ------------------------------------------------------------------ stepping
     def run_steps(self, kinds, ds, rows=None, sizes=None, stats=None, active=None):
@@ -258,7 +366,7 @@ class ReplicaPack:
         self._ensure_bound()
         rows = ds["rows"] if rows is None else rows
         sizes = ds["sizes"] if sizes is None else sizes
-        stats = ds["stats"] if stats is None else stats
+        stats = ds["stats"] if stats is None else stats  # a view starting at the first step's batch
         d = self._workspace(max(int(ds["Bmax"]), 1), ds["T"])
         for kind in kinds:
             flags, nbn = flags_for(kind, self.engines[0].nsup)
@@ -277,24 +385,33 @@ class ReplicaPack:
             for e in self.engines:
                 e.supports_fresh = False  # the single-fit workspace's supports are stale now
 
+    def phase_groups(self, epoch, active=None):
+        """{update kinds: [replicas]} of `epoch` (...withStateSmoothing.py:741-759) for the active
+        replicas, in the order of each group's first replica."""
+        idx = range(self.R) if active is None else sorted(int(r) for r in active)
+        groups = {}
+        for r in idx:
+            groups.setdefault(tuple(phase_of_epoch(self.models[r], epoch)), []).append(r)
+        return groups
+
     def run_epoch(self, epoch, ds, active=None, set_modes=True):
         """The batch_update phase of `epoch` (...withStateSmoothing.py:741-759) over every batch
-        of `ds`, for the active replicas.  All replicas must be in the same phase."""
-        idx = range(self.R) if active is None else active
-        kinds = [tuple(phase_of_epoch(self.models[r], epoch)) for r in idx]
-        if len(set(kinds)) > 1:
-            raise RuntimeError("replicas are in different training phases at epoch %d: %s" % (epoch, kinds))
-        kinds = list(kinds[0]) if kinds else []
-        if len(kinds) <= 1:
-            self.run_steps(kinds, ds, active=active)
-        else:  # several updates per batch: batch-major order as in batch_update
-            for bi, (r, s) in enumerate(zip(ds["rows"], ds["sizes"])):
-                for kind in kinds:
-                    self.run_steps([kind], ds, [r], [s], ds["stats"][bi:bi + 1], active=active)
-        if set_modes:
-            for r in idx:
-                self.models[r]._set_module_modes(kinds[-1] if kinds else None)
-        return kinds
+        of `ds`, for the active replicas.  Replicas whose schedules put them in different phases
+        this epoch run as one launch chain per phase group (the replicas are independent, so the
+        order of the groups changes no result).  Returns {kinds: replicas}."""
+        groups = self.phase_groups(epoch, active)
+        for kinds, reps in groups.items():
+            act = active if len(groups) == 1 else reps
+            if len(kinds) <= 1:
+                self.run_steps(list(kinds), ds, active=act)
+            else:  # several updates per batch: batch-major order as in batch_update
+                for bi, (r, s) in enumerate(zip(ds["rows"], ds["sizes"])):
+                    for kind in kinds:
+                        self.run_steps([kind], ds, [r], [s], self._stats_at(ds, bi, 1), active=act)
+            if set_modes:
+                for r in reps:
+                    self.models[r]._set_module_modes(kinds[-1] if kinds else None)
+        return groups
 
     def _values(self, ds, active=None, host=True):
         """validate_training accumulators of the active replicas: raw acc [R][8], confusion
@@ -324,12 +441,13 @@ class ReplicaPack:
         return acc[:, :7] / nb, conf
 
     def embed_raw(self, X, active=None):
-        """Raw embedder outputs [Ra][B][K] of windows X (B, T >= Lmax, p) for the active replicas
-        (BatchNorm running statistics): one embedder-only launch for all of them."""
+        """Raw embedder outputs [Ra][B][K] of windows X (B, T >= Lmax, p) -- or per replica,
+        X (R, B, T, p) -- for the active replicas (BatchNorm running statistics): one
+        embedder-only launch for all of them."""
         X = X.to(self.device, torch.float32).contiguous()
-        B, T, _ = X.shape
+        B, T, p = X.shape[-3:]
         d = self._workspace(max(B, 1), T)
-        ds = {"X": X, "lab": None}
+        ds = {"X": X, "lab": None, "xr": B * T * p if X.dim() == 4 else 0}
         a, _ = self._args(d, 0, 0, ds, None, active)
         a.B, a.row0 = B, 0
         nat.check(nat.lib().redcliff_train_step(ctypes.byref(a), _stream()), "packed embed")
@@ -372,11 +490,14 @@ class ReplicaPack:
 
         Every replica follows exactly the rules (and the host code, FitTracker) of a single fit:
         its histories, its stopping criterion (per-model stopping_criteria_* may be given as
-        lists), best-epoch snapshot, checkpoints every check_every epochs (save_dir: a list of R
-        directories, or one root that gets replica_<r>/ sub-directories), restore_parameters and
-        final model file.  A stopped replica leaves the active list: nothing of it is launched
-        or updated afterwards.  Returns the final validation combo loss of every replica; each
-        model gets ``fit_history`` as a single fit would."""
+        lists), its own phase schedule (num_pretrain_epochs / num_acclimation_epochs /
+        training_mode of its model), best-epoch snapshot, checkpoints every check_every epochs
+        (save_dir: a list of R directories, or one root that gets replica_<r>/ sub-directories),
+        restore_parameters and final model file.  X_train / X_val / GC may be ``PerReplica``
+        (each replica fits its own data set against its own true graphs).  A stopped replica
+        leaves the active list: nothing of it is launched or updated afterwards.  Returns the
+        final validation combo loss of every replica; each model gets ``fit_history`` as a single
+        fit would."""
         if output_length != 1:
             raise NotImplementedError("output_length must be 1")
         t_in = time.perf_counter()
@@ -384,20 +505,22 @@ class ReplicaPack:
         for m in models:
             if not m.fused_supported() or "Freeze" in m.training_mode or m.__dict__.get("_factors_detached"):
                 raise NotImplementedError("packed fits cover the fused (published) configuration")
-        sched = set((m.num_pretrain_epochs, m.num_acclimation_epochs, m.training_mode) for m in models)
-        if len(sched) != 1:
-            raise ValueError("a pack shares its phase schedule (pretrain / acclimation epochs); group the grid "
-                             "with grid_packs(): %s" % sorted(sched))
+        modes = set(m.primary_gc_est_mode for m in models)
+        if len(modes) != 1:
+            raise ValueError("a packed fit tracks GC progress in one primary_gc_est_mode, got %s" % sorted(modes))
 
         def per(x):
             return list(x) if isinstance(x, (list, tuple)) else [x] * R
+        if isinstance(GC, PerReplica) and len(GC) != R:
+            raise ValueError("PerReplica GC: %d graph lists for %d replicas" % (len(GC), R))
+        gc_of = (lambda r: GC[r]) if isinstance(GC, PerReplica) else (lambda r: GC)
         scf, scfa, scc = per(stopping_criteria_forecast_coeff), per(stopping_criteria_factor_coeff), \
             per(stopping_criteria_cosSim_coeff)
         dirs = None
         if save_dir is not None:
             dirs = list(save_dir) if isinstance(save_dir, (list, tuple)) else \
                 [os.path.join(save_dir, "replica_%d" % r) for r in range(R)]
-        trackers = [FitTracker(m, GC, deltaConEps, in_degree_coeff, out_degree_coeff, scf[r], scfa[r], scc[r],
+        trackers = [FitTracker(m, gc_of(r), deltaConEps, in_degree_coeff, out_degree_coeff, scf[r], scfa[r], scc[r],
                                lookback, check_every) for r, m in enumerate(models)]
         e0, m0 = self.engines[0], models[0]
         nsup, p, K = e0.nsup, e0.p, e0.K
@@ -414,7 +537,17 @@ class ReplicaPack:
         hlog = DeferredHistories()
         active = list(range(R))
         nfirst = min(int(val["sizes"][0]), m0.MAX_NUM_SAMPS_FOR_GC_PROGRESS_TRACKING)
-        Xv = val["X"][:nfirst, :Lm, :]
+        # GC tracking windows: the first validation batch's first samples (:1366-1370), per replica
+        # when every replica has its own validation set
+        Xv = val["X"][:, :nfirst, :Lm, :].contiguous() if val.get("per_replica") else val["X"][:nfirst, :Lm, :]
+        gc_lists = {}  # PerReplica GC: the active replicas' true-graph lists, one list object per active set
+
+        def truths(act):
+            k = tuple(act)
+            if k not in gc_lists:
+                gc_lists.clear()
+                gc_lists[k] = [GC[r] for r in act]
+            return gc_lists[k]
         # The module train/eval flags -- which no fused launch reads -- are set once, to the state
         # the reference leaves after every epoch (eval: GC tracking and validation call .eval()),
         # before checkpoints and at the end, instead of walking R module trees twice per epoch.
@@ -435,12 +568,16 @@ class ReplicaPack:
         # "pretrain_factor" modes re-order each fit's factors before epoch num_pretrain_epochs
         # (...withStateSmoothing.py:1318-1326, initialize_factors_with_prior with fit()'s cost_criteria,
         # unsupervised_start_index and max_factor_prior_batches)
-        reorder_at = m0.num_pretrain_epochs if "pretrain_factor" in m0.training_mode else None
+        reorder_at = dict((r, m.num_pretrain_epochs) for r, m in enumerate(models) if "pretrain_factor" in m.training_mode)
+        reorder_epochs = set(reorder_at.values())
 
         def launch_train(ep):
-            if ep == reorder_at:
+            if ep in reorder_epochs:
                 for r in active:  # with the caller's settings, as each single fit's _prior_hook passes them
-                    models[r].initialize_factors_with_prior(X_train=X_train, cost_criteria=cost_criteria,
+                    if reorder_at.get(r) != ep:
+                        continue
+                    xr = X_train[r] if isinstance(X_train, PerReplica) else X_train
+                    models[r].initialize_factors_with_prior(X_train=xr, cost_criteria=cost_criteria,
                                                             unsupervised_start_index=unsupervised_start_index,
                                                             max_batches=max_factor_prior_batches)
             self.conf.zero_()
@@ -478,8 +615,13 @@ class ReplicaPack:
                     Ra, S = est_t.shape[0], est_t.shape[1]
                     vals_d = None
                     if GC is not None and nsup > 0 and S > 0:
-                        vals_d = M.gc_progress_values(GC, est_t.reshape(Ra * S, *est_t.shape[2:]), deltaConEps,
-                                                      in_degree_coeff, out_degree_coeff, host=False)
+                        est_flat = est_t.reshape(Ra * S, *est_t.shape[2:])
+                        if isinstance(GC, PerReplica):  # each replica scored against its own true graphs
+                            vals_d = M.gc_progress_values_grouped(truths(active), est_flat, S, deltaConEps,
+                                                                  in_degree_coeff, out_degree_coeff, host=False)
+                        else:
+                            vals_d = M.gc_progress_values(GC, est_flat, deltaConEps, in_degree_coeff,
+                                                          out_degree_coeff, host=False)
                     l1_d, dots_d = M.gc_track_values(est_t, nolag_t, host=False)
                     acc_d, confv_d = self._values(val, active, host=False)
                     pending = M.fetch_async([conf_d, l1_d, dots_d, acc_d, confv_d,
@@ -488,13 +630,11 @@ class ReplicaPack:
                 if prof is not None:
                     tp.append(time.perf_counter())
                 spec = (it + 1 < max_iter and not (dirs is not None and it % check_every == 0)
-                        and it + 1 != reorder_at)
+                        and it + 1 not in reorder_epochs)
                 if spec:
                     # a replica can stop at this epoch only after pretraining / acclimation and when
                     # its last improvement is exactly lookback * check_every epochs back (FitTracker.step)
-                    can_stop = any(it >= models[r].num_pretrain_epochs + models[r].num_acclimation_epochs
-                                   and trackers[r].best_it is not None
-                                   and it - trackers[r].best_it == lookback * check_every for r in active)
+                    can_stop = any(trackers[r].may_stop(it) for r in active)
                     self._save_state(full=can_stop)
                     steps_before = [self._step_counts(r) for r in range(R)]
                     launch_train(it + 1)
@@ -661,30 +801,67 @@ class _PackSnapshot(ParamSnapshot):
         return (b.bn[0][r], b.bn[1][r], b.nbt[r])
 
 
-def grid_packs(models_and_opts, max_replicas=64):
-    """Group grid points (model, (optimizerA, optimizerB)) into packs of identical shapes and
-    phase schedules (the reference grid varies embed_lag, graph-conv layers and the pretrain /
-    acclimation epochs, train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:278-309),
-    in the grid's own order, at most max_replicas per pack.  Returns [(models, optimizers)]."""
+def model_shape(m):
+    """The shape key of a model (ReplicaPack._shape of its engine), read from the module tree
+    (no device work): p, gen_lag, K, nsup, h, DGCNN F / layers / hidden, sigmoid restriction."""
+    g = m.factor_score_embedder.dgcnn.dgcnn
+    emb = m.factor_score_embedder
+    return (m.num_series, m.gen_lag, m.num_factors_nK, m.num_supervised_factors, m.gen_hidden[0], g.in_channels,
+            g.num_layers, g.hid_channels, bool(emb.use_sigmoid_restriction),
+            float(emb.sigmoid_eccentricity_coeff or 0.0))
+
+
+def grid_packs(models_and_opts, max_replicas=256, key=None):
+    """Group grid points (model, (optimizerA, optimizerB)) into packs of identical shapes (the
+    reference's TST grid varies embed_lag and the graph-conv layers -- 6 shape classes --, and the
+    pretrain / acclimation epochs, which a pack may mix,
+    train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:278-309), in the grid's own order,
+    at most max_replicas (<= 256, the longest active list of one launch) per pack.  key(i): an
+    extra grouping key of point i -- e.g. the (N, T) shape of its data set, which the replicas of
+    a pack with PerReplica data must share.  Returns [(models, optimizers, point indices)]."""
+    if not 1 <= max_replicas <= 256:
+        raise ValueError("max_replicas must be in 1..256")
     groups = {}
     order = []
-    for m, o in models_and_opts:
-        e = m.engine()
-        key = ReplicaPack._shape(e) + (m.num_pretrain_epochs, m.num_acclimation_epochs, m.training_mode)
-        if key not in groups:
-            groups[key] = []
-            order.append(key)
-        groups[key].append((m, o))
+    for i, (m, o) in enumerate(models_and_opts):
+        k = model_shape(m) + (m.primary_gc_est_mode,) + ((key(i),) if key is not None else ())
+        if k not in groups:
+            groups[k] = []
+            order.append(k)
+        groups[k].append((i, m, o))
     out = []
-    for key in order:
-        g = groups[key]
-        for i in range(0, len(g), max_replicas):
-            chunk = g[i:i + max_replicas]
-            out.append(([m for m, _ in chunk], [o for _, o in chunk]))
+    for k in order:
+        g = groups[k]
+        n = -(-len(g) // max_replicas)  # packs of this class, sized evenly
+        for j in range(n):
+            chunk = g[j * len(g) // n:(j + 1) * len(g) // n]
+            out.append(([m for _, m, _ in chunk], [o for _, _, o in chunk], [i for i, _, _ in chunk]))
     return out
 
 
-def shard_grid(n_points, world, rank):
-    """Grid-point indices of rank `rank`: round-robin over the grid order, as SLURM array tasks
-    map onto nodes (train/...gsSmooth1.py:157-160: task i -> parameters_to_be_parallelized[i-1])."""
-    return list(range(rank, n_points, world))
+def shard_grid(n_points, world, rank, classes=None, cost=None):
+    """Grid-point indices of rank `rank` of `world` GPUs.
+
+    classes=None: round-robin over the grid order, as SLURM array tasks map onto nodes
+    (train/...gsSmooth1.py:157-160: task i -> parameters_to_be_parallelized[i-1]).
+
+    classes (one hashable shape-class key per point, e.g. (K, p) of the synthetic grid or
+    (embed_lag, graph-conv layers) of the TST grid): the points ordered by class (classes in order
+    of first appearance, grid order within a class) and cut into `world` contiguous runs of equal
+    total cost (cost[i], default 1 per point), so every GPU holds whole classes or long runs of one
+    -- few, large packs per GPU instead of ~world-fold thinner packs of every class."""
+    if classes is None:
+        return list(range(rank, n_points, world))
+    if len(classes) != n_points:
+        raise ValueError("one class key per grid point")
+    first = {}
+    for i, c in enumerate(classes):
+        first.setdefault(c, len(first))
+    order = sorted(range(n_points), key=lambda i: (first[classes[i]], i))
+    w = np.ones(n_points) if cost is None else np.asarray(cost, dtype=np.float64)
+    cum = np.cumsum(w[order])
+    total = cum[-1] if n_points else 0.0
+    # run g holds the points whose cumulative cost midpoint falls in [g, g+1) * total / world
+    mid = cum - 0.5 * w[order]
+    owner = np.minimum((mid * world / max(total, 1e-300)).astype(np.int64), world - 1)
+    return sorted(int(order[j]) for j in range(n_points) if owner[j] == rank)

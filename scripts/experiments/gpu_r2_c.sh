@@ -1,0 +1,4 @@
+#!/bin/bash
+source "$(dirname "$0")/../gpu_steps.sh"
+step r2_new_tests 600 python -u -m pytest tests/test_gpu_pack_fit.py tests/test_gpu_checkpoint.py tests/test_gpu_parity.py -v -s --timeout 300 --timeout-method thread
+step r2_bench 600 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 5

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 3: embedder forward graph convolution on the matrix cores + deeper fc1 prefetch -- full GPU
+# suite, D4IC and TST single-fit bench lines, D4IC phase timeline, kernel stats.
+source "$(dirname "$0")/../gpu_steps.sh"
+( while sleep 20; do echo "heartbeat $(date +%s)" >> gpurun_out/heartbeat.txt; done ) &
+HB=$!
+step v_suite 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread --durations=5
+step v_d4ic 300 python bench.py --steps 300 --warmup 30 --replicas 1 --fit-replicas 0 --no-north-star --no-cpu-baseline --dp-leg-batch 0
+step v_c4 300 python bench.py --config c4 --steps 200 --warmup 20 --replicas 1 --fit-replicas 0 --no-north-star --no-cpu-baseline --dp-leg-batch 0
+step v_c1k4 300 python bench.py --config c1k4 --steps 200 --warmup 20 --replicas 1 --fit-replicas 0 --no-north-star --no-cpu-baseline --dp-leg-batch 0
+step v_trace 200 python -u scripts/phase_trace.py --config d4ic
+kill $HB

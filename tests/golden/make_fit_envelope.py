@@ -92,7 +92,7 @@ def run(name, j):
     t0 = time.time()
     d, cfg = _load(name)
     X, Y, Xv, Yv = d["X"], d["Y"], d["Xv"], d["Yv"]
-    true_gc = [d["true_gc%d" % k] for k in range(cfg["K"])]
+    true_gc = [d["true_gc%d" % k] for k in range(int(d["n_true_gc"]) if "n_true_gc" in d.files else cfg["K"])]
     B = cfg["B"]
     train = _batches(X, Y, B, j)
     val = _batches(Xv, Yv, B, 0)

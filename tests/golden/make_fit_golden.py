@@ -78,6 +78,14 @@ SCENARIOS = {
     "fit_d4ic_pub": dict(seed=1, p=10, L=4, K=4, nsup=4, h=100, F=20, n=2, H=30, B=128, N=128, Nv=64, T=21,
                          label="d4ic", pre=2, acc=1, max_iter=200, lookback=1, check_every=2, lrA=2e-4, lrB=5e-4,
                          data_seed=4242, resume_at=None),
+    # configs[3] TST shape (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1_cached_args.txt): p=12,
+    # L=4, K=9 factors of which nsup=3 are supervised (3 system states, per-step one-hot labels
+    # (N, 3, T_rec) with T_rec > Lmax, so the factor loss picks Y[:, :, Lmax] and pads to K,
+    # ...withStateSmoothing.py:637-641), h=25, DGCNN 16/3/100, smoothing coefficient 25, lrs 5e-4.
+    # GC tracking then slices the first nsup SAMPLES (hazard 13, :1379).
+    "fit_tst": dict(seed=2, p=12, L=4, K=9, nsup=3, S=3, h=25, F=16, n=3, H=100, B=128, N=256, Nv=128, T=20,
+                    label="onehot", pre=2, acc=2, max_iter=200, lookback=1, check_every=2, lrA=5e-4, lrB=5e-4,
+                    data_seed=777, smooth=25.0, resume_at=None),
 }
 
 
@@ -99,7 +107,7 @@ def system(rng, S, D, density=0.3):
 
 def make_data(cfg):
     rng = np.random.RandomState(cfg["data_seed"])
-    p, K = cfg["p"], cfg["K"]
+    p, K = cfg["p"], cfg.get("S", cfg["K"])  # K system states (labelled), S of them when S < num_factors
     A = system(rng, K, p)
     N = cfg["N"] + cfg["Nv"]
     freqs = rng.uniform(0.05, 0.2, (p, 1))
@@ -121,7 +129,7 @@ def build(cfg):
     torch.manual_seed(cfg["seed"])
     eargs = [("num_features_per_node", cfg["F"]), ("num_graph_conv_layers", cfg["n"]),
              ("num_hidden_nodes", cfg["H"]), ("sigmoid_eccentricity_coeff", 10.0)]
-    coeff = reference_coeffs(cfg["K"], cfg["p"])
+    coeff = reference_coeffs(cfg["K"], cfg["p"], smooth=cfg.get("smooth", 0.0))
     m = REF.redcliff_smooth.REDCLIFF_S_CMLP_withStateSmoothing(
         cfg["p"], cfg["L"], [cfg["h"]], cfg["F"], [0], cfg["L"], 1, cfg["K"], cfg["nsup"], coeff, False, "DGCNN", eargs,
         "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
@@ -238,6 +246,7 @@ def run(name, cfg):
     out = {"X": X, "Y": Y, "Xv": Xv, "Yv": Yv}
     for k, g in enumerate(true_gc):
         out["true_gc%d" % k] = g
+    out["n_true_gc"] = np.asarray(len(true_gc))
     _sd("init", m, out)
     B = cfg["B"]
     train = [(torch.from_numpy(X[i:i + B]), torch.from_numpy(Y[i:i + B])) for i in range(0, len(X), B)]
@@ -281,7 +290,7 @@ def run(name, cfg):
     out["final_gc"] = arr
     out["final_graphs"] = (arr > 0).astype(np.int8)
     out["f1"] = np.asarray([[REF.metrics.get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), true_gc[k].sum(axis=2))
-                             for k, g in enumerate(row)] for row in arr], dtype=np.float64)
+                             for k, g in enumerate(row[:len(true_gc)])] for row in arr], dtype=np.float64)
 
     # ---- reference-style resume from a mid-fit checkpoint (fresh optimizers)
     ck = [i for i, mm in enumerate(cap.metas) if mm["epoch"] >= cfg["pre"] + cfg["acc"]]

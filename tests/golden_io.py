@@ -54,6 +54,10 @@ def assert_close(name, got, want, rtol=1e-4, atol=1e-5, outliers=0):
     assert got.shape == want.shape, "%s: shape %s vs %s" % (name, got.shape, want.shape)
     if want.size == 0:
         return
+    nan_g, nan_w = np.isnan(got), np.isnan(want)
+    assert np.array_equal(nan_g, nan_w), "%s: NaN pattern differs (%d got, %d want, %d disagree)" % (
+        name, int(nan_g.sum()), int(nan_w.sum()), int((nan_g != nan_w).sum()))
+    got, want = np.where(nan_w, 0.0, got), np.where(nan_w, 0.0, want)
     err = np.abs(got - want)
     tol = atol + rtol * np.abs(want)
     bad = err > tol

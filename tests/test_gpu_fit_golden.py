@@ -78,7 +78,7 @@ def data(d, meta):
 
 def fit_kw(meta, d):
     return dict(lookback=meta["lookback"], check_every=meta["check_every"], verbose=0,
-                GC=[d["true_gc%d" % k] for k in range(meta["K"])], deltaConEps=0.1, in_degree_coeff=1.,
+                GC=true_gc(d, meta), deltaConEps=0.1, in_degree_coeff=1.,
                 out_degree_coeff=1., stopping_criteria_forecast_coeff=10., stopping_criteria_factor_coeff=100.,
                 stopping_criteria_cosSim_coeff=1.)
 
@@ -182,15 +182,29 @@ def compare_state_envelope(tag, model, want, env, part, rtol=2e-4, atol=5e-6):
     assert worst <= 1.0, (tag, worst)
 
 
-@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub"])
+def true_gc(d, meta):
+    """The true graphs the fixture's fit tracked (nsup of them at the TST shape, K otherwise)."""
+    n = int(d["n_true_gc"]) if "n_true_gc" in d.files else meta["K"]
+    return [d["true_gc%d" % k] for k in range(n)]
+
+
+ENV_FIT = ("fit_d4ic_pub", "fit_tst")  # long trajectories: the fit is held to the reference's own spread
+
+
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst"])
 def test_fit_matches_reference_fit(name):
     d, meta = load(name)
-    env = load_envelope(name) if name == "fit_d4ic_pub" else None  # the long published-lr trajectory
+    env = load_envelope(name) if name in ENV_FIT else None
     m = build(meta)
     compare_state("init", m, state(d, "init"), rtol=0, atol=0)  # seeded construction: bit-identical
     train, val = data(d, meta)
     oA, oB = opts(m, meta)
     ret = m.fit(None, train, oA, oB, meta["L"], 1, 1, meta["max_iter"], val, **fit_kw(meta, d))
+    check_fit(name, m, ret, d, meta, env, val)
+
+
+def check_fit(name, m, ret, d, meta, env, val):
+    """Everything the reference's fit recorded (make_fit_golden.py) against model m after its fit."""
     h = m.fit_history
     n = int(d["hist/n_epochs"])
     assert len(h["avg_combo_loss"]) == n, (len(h["avg_combo_loss"]), n)
@@ -238,13 +252,13 @@ def test_fit_matches_reference_fit(name):
     assert_close("final_gc", arr, d["final_gc"], 1e-4, 1e-5)
     np.testing.assert_array_equal((arr > 0).astype(np.int8), d["final_graphs"])
     from redcliff_amd.metrics import get_f1_score
-    true_gc = [d["true_gc%d" % k] for k in range(meta["K"])]
-    f1 = np.asarray([[get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), true_gc[k].sum(axis=2))
-                      for k, g in enumerate(row)] for row in arr])
+    tg = true_gc(d, meta)
+    f1 = np.asarray([[get_f1_score(g.sum(axis=2) / np.max(g.sum(axis=2)), tg[k].sum(axis=2))
+                      for k, g in enumerate(row[:len(tg)])] for row in arr])
     np.testing.assert_array_equal(f1, d["f1"])
 
 
-@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub"])
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst"])
 def test_resume_matches_reference_resume(name, tmp_path):
     """The reference's resume: the model saved at a mid-fit checkpoint (best_model) plus its
     metadata, resume_training_from_checkpoint, fit with FRESH Adam objects (the default here,
@@ -279,3 +293,63 @@ def test_resume_matches_reference_resume(name, tmp_path):
     fr = float(d["resume/fit_return"])
     within_envelope("resume fit return", np.asarray([ret]), np.asarray([fr]), np.asarray([1e-4 * abs(fr) + 1e-6]),
                     np.abs(env["resume/fit_return"] - fr)[:, None])
+
+
+def _dp_fit_worker(rank, world, port, outdir, name):
+    """One rank of the data-parallel fit of fixture `name` (gloo; every rank on cuda:0, the box has
+    one GPU -- the product runs RCCL).  Writes the model state and fit_history of rank `rank`."""
+    import socket  # noqa: F401  (spawned interpreter: the test module's imports are re-run)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "redcliff-s-hypothesizing-dynamic-causal-graphs_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from redcliff_amd import DataParallelFit
+    d, meta = load(name)
+    m = build(meta)
+    oA, oB = opts(m, meta)
+    train, val = data(d, meta)
+    dp = DataParallelFit(m, oA, oB)
+    ret = dp.fit(None, train, 1, meta["max_iter"], val, **fit_kw(meta, d))
+    torch.cuda.synchronize()
+    sd = dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items())
+    with open(os.path.join(outdir, "dp%d.pkl" % rank), "wb") as f:  # this test's own file
+        pickle.dump({"state": sd, "hist": m.fit_history, "ret": float(ret)}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_data_parallel_fit_matches_reference_fit(tmp_path):
+    """configs[3] (TST shape, K = 9 factors of which 3 supervised, per-step labels): the 2-rank
+    data-parallel fit (DataParallelFit.fit: every global batch of 128 split 64 / 64, one all-reduce
+    of the flat gradient per update, replicated Adam) against the REFERENCE's own fit of the same
+    model on the same windows (tests/golden/fit_tst.npz) -- the same checks as the single fit:
+    stopping epoch and best_it exact, histories and final state within 1e-4 / 2e-4 or the
+    reference's own fp32 spread (fit_tst_envelope.npz), final GC within 1e-4, graphs and F1
+    identical.  Both ranks end bit-identical."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    name = "fit_tst"
+    mp.start_processes(_dp_fit_worker, args=(2, port, str(tmp_path), name), nprocs=2, start_method="spawn",
+                       join=True)
+    runs = []
+    for r in range(2):
+        with open(str(tmp_path / ("dp%d.pkl" % r)), "rb") as f:
+            runs.append(pickle.load(f))
+    for k in runs[0]["state"]:
+        np.testing.assert_array_equal(runs[0]["state"][k], runs[1]["state"][k], err_msg="ranks differ: " + k)
+    d, meta = load(name)
+    m = build(meta)
+    with torch.no_grad():
+        m.load_state_dict(dict((k, torch.from_numpy(v)) for k, v in runs[0]["state"].items()))
+    m.fit_history = runs[0]["hist"]
+    _, val = data(d, meta)
+    check_fit(name + "/dp2", m, runs[0]["ret"], d, meta, load_envelope(name), val)

@@ -99,3 +99,60 @@ def test_pack_fit_bitwise_equals_independent_fits(path, save, monkeypatch, tmp_p
     assert len(finals) == len(GRID)
     print("stop epochs:", stops)
     assert any(s is not None for s in stops), "no replica stopped early: the active-list path went untested"
+
+
+# (pretrain epochs, acclimation epochs) per replica: the TST grid's schedule axes
+# (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:297-298), scaled down
+SCHEDULES = [(1, 1), (2, 1), (1, 3), (3, 2)]
+
+
+@pytest.mark.parametrize("path", ["vector", "mfma"])
+def test_mixed_schedule_per_replica_data_pack_fit_bitwise(path, monkeypatch):
+    """The reference's real grids in one pack: every replica has its own phase schedule (the pack
+    launches one chain per phase group each epoch; Adam step numbers per replica through the hyper
+    rows' t_offset) and its own training / validation data and true graphs (PerReplica: the
+    synthetic grid's one-model-many-datasets form, ...BSCgsSmooth3Parsim.py:66-72).  Every replica
+    ends bit-identical to its independent fit(), histories, stopping epoch and Adam state
+    included."""
+    from redcliff_amd import PerReplica, ReplicaPack
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    trains = [data(64 * 2 + 24, seed=30 + r) for r in range(len(GRID))]
+    vals = [data(96, seed=40 + r) for r in range(len(GRID))]
+    gcs = [true_graphs(4, 10, 4, seed=50 + r) for r in range(len(GRID))]
+    max_iter = 10
+    kw = dict(lookback=1, check_every=1, deltaConEps=0.1)
+    solo, solo_opts = [], []
+    for r, (s, fc, adj, lrB, lrA, scf, scfa) in enumerate(GRID):
+        pre, acc = SCHEDULES[r]
+        m = make(s, fc, adj, pre=pre, acc=acc)
+        oA, oB = opts(m, lrB, lrA)
+        solo_opts.append((oA, oB))
+        m.fit(None, trains[r], oA, oB, 4, 1, 1, max_iter, vals[r], verbose=0, GC=gcs[r],
+              stopping_criteria_forecast_coeff=scf, stopping_criteria_factor_coeff=scfa,
+              stopping_criteria_cosSim_coeff=1., **kw)
+        torch.cuda.synchronize()
+        solo.append(m)
+    packed = [make(g[0], g[1], g[2], pre=SCHEDULES[r][0], acc=SCHEDULES[r][1]) for r, g in enumerate(GRID)]
+    pack_opts = [opts(m, g[3], g[4]) for m, g in zip(packed, GRID)]
+    pack = ReplicaPack(packed, pack_opts)
+    # epoch 1: replicas 0 and 2 acclimate while 1 and 3 still pretrain the embedder
+    assert len(pack.phase_groups(1)) == 2
+    pack.fit(None, PerReplica(trains), PerReplica(vals), max_iter, verbose=0, GC=PerReplica(gcs),
+             stopping_criteria_forecast_coeff=[g[5] for g in GRID], stopping_criteria_factor_coeff=[g[6] for g in GRID],
+             stopping_criteria_cosSim_coeff=1., **kw)
+    torch.cuda.synchronize()
+    for r, (a, b) in enumerate(zip(solo, packed)):
+        ha, hb = a.fit_history, b.fit_history
+        assert hb["best_it"] == ha["best_it"] and hb["stopped_at"] == ha["stopped_at"], r
+        for k in HKEYS + ("f1score_histories", "roc_auc_histories", "deltacon0_histories",
+                          "gc_factor_cosine_sim_histories"):
+            assert same(hb[k], ha[k]), "replica %d %s" % (r, k)
+        sa, sb = a.state_dict(), b.state_dict()
+        for k in sa:
+            np.testing.assert_array_equal(sb[k].cpu().numpy(), sa[k].cpu().numpy(), err_msg="replica %d %s" % (r, k))
+        for oa, ob in zip(solo_opts[r], pack_opts[r]):
+            stA, stB = oa.state_dict()["state"], ob.state_dict()["state"]
+            for i in stA:
+                for k in ("exp_avg", "exp_avg_sq", "step"):
+                    np.testing.assert_array_equal(stB[i][k].cpu().numpy(), stA[i][k].cpu().numpy(),
+                                                  err_msg="replica %d optimizer state %s %s" % (r, i, k))

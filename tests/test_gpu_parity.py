@@ -214,7 +214,7 @@ def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
     >= 16 replicas; its window-sized products in the windowed kernels for p < 32),
     "embgemm-products" the same with those products as batched GEMMs (REDCLIFF_EMB_WIN=0, the
     p >= 32 form) onto the published shapes; "embbatched" the replica-batched embedder kernels
-    (rc_embed_batched.hip, normally chosen for a packed D4IC-shaped grid of >= 16 replicas)."""
+    (rc_embed_batched.hip, opt-in through REDCLIFF_EMB_PATH=batched; never chosen by default)."""
     if path == "mfma":
         monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     elif path == "embbatched":

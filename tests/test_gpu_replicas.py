@@ -86,7 +86,7 @@ def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
     path is pinned here to compare like with like); R = 3 and the packed-only paths at R = 8.
     emb "gemm": the GEMM-shaped embedder with its products batched over the replicas, against
     single fits on the same embedder path; emb "batched": the replica-batched embedder kernels
-    (the default for D4IC-shaped packs of >= 16 replicas), likewise."""
+    (opt-in, REDCLIFF_EMB_PATH=batched; packed grids default to the GEMM-shaped embedder), likewise."""
     monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     if emb:
         monkeypatch.setenv("REDCLIFF_EMB_PATH", emb)
@@ -126,15 +126,49 @@ def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
     np.testing.assert_array_equal(g2[3][2].cpu().numpy(), g1[3][2].cpu().numpy())
 
 
-def test_pack_rejects_mixed_shapes_and_phases():
+def test_pack_mixes_phases_and_rejects_mixed_shapes():
+    """Replicas in different phases of their schedules run as one launch chain per phase group,
+    each bit-identical to its own batch_update sequence; differing shapes are refused."""
     from redcliff_amd import ReplicaPack
-    a = make(0, 10.0, 0.1)
-    b = make(1, 10.0, 0.1, pre=2)
-    pack = ReplicaPack([a, b], [opts(a, 5e-4, 5e-4), opts(b, 5e-4, 5e-4)])
-    ds = pack.cache_dataset(data(64, seed=1))
-    pack.run_epoch(0, ds)
-    with pytest.raises(RuntimeError, match="different training phases"):
-        pack.run_epoch(1, ds)
+    train = data(64 + 24, seed=1)
+    solo = [make(0, 10.0, 0.1), make(1, 10.0, 0.1, pre=2)]
+    packed = [make(0, 10.0, 0.1), make(1, 10.0, 0.1, pre=2)]
+    pack = ReplicaPack(packed, [opts(m, 5e-4, 5e-4) for m in packed])
+    ds = pack.cache_dataset(train)
+    solo_opts = [opts(m, 5e-4, 5e-4) for m in solo]
+    for epoch in range(4):
+        groups = pack.run_epoch(epoch, ds)
+        if epoch == 1:  # replica 0 acclimates its factors, replica 1 still pretrains the embedder
+            assert groups == {("acclimate",): [0], ("pretrain_embedder",): [1]}
+        for m, (oA, oB) in zip(solo, solo_opts):
+            for bi, (Xb, Yb) in enumerate(train):
+                m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+    torch.cuda.synchronize()
+    for r, (m, mp) in enumerate(zip(solo, packed)):
+        a, b = m.state_dict(), mp.state_dict()
+        for k in a:
+            np.testing.assert_array_equal(b[k].cpu().numpy(), a[k].cpu().numpy(), err_msg="replica %d %s" % (r, k))
+    c = make(2, 10.0, 0.1)
+    c2 = redcliff_amd_model_with_hidden(50)
+    with pytest.raises(ValueError, match="share every shape"):
+        ReplicaPack([c, c2], [opts(c, 5e-4, 5e-4), opts(c2, 5e-4, 5e-4)])
+
+
+def redcliff_amd_model_with_hidden(h):
+    import redcliff_amd
+    K, p = CFG["K"], CFG["p"]
+    coeff = {"FORECAST_COEFF": 10.0, "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0 / sum(range(1, K)),
+             "FACTOR_WEIGHT_L1_COEFF": 1e-3, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0,
+             "ADJ_L1_REG_COEFF": 0.1 / K / np.sqrt(p * p - 1.0), "DAGNESS_REG_COEFF": 0.0, "DAGNESS_LAG_COEFF": 0.0,
+             "DAGNESS_NODE_COEFF": 0.0}
+    eargs = [("num_features_per_node", CFG["F"]), ("num_graph_conv_layers", CFG["n"]),
+             ("num_hidden_nodes", CFG["H"]), ("sigmoid_eccentricity_coeff", 10.0)]
+    torch.manual_seed(5)
+    return redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(
+        p, CFG["L"], [h], CFG["F"], [0], CFG["L"], 1, K, CFG["nsup"], coeff, False, "DGCNN", eargs,
+        "conditional_factor_fixed_embedder", "apply_factor_weights_after_sim_completion", num_sims=1,
+        training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=1,
+        num_acclimation_epochs=1).cuda()
 
 
 @pytest.mark.parametrize("variant", ["0", "1"])
