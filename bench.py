@@ -476,6 +476,143 @@ def fits_per_hour(c, args, dev, rank, dist, world):
                     "after an untimed 3-epoch warm-up fit of a copy of the pack" % (pre, acc, E - pre - acc)}
 
 
+# --------------------------------------------------------------------------- the reference's grids
+def tst_grid_points():
+    """The TST grid (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:278-309, 1536 points, in
+    itertools.product order): per point the axes that vary -- gen_lr, FORECAST, COS_SIM, SMOOTHING,
+    ADJ_L1, num_pretrain_epochs, num_acclimation_epochs, graph-conv layers, embed_lag, embed_lr."""
+    import itertools
+    axes = (("gen_lr", (5e-4, 1e-4)), ("forecast", (10.0, 1.0)), ("cos", (10.0, 1.0)), ("smooth", (25.0, 0.025)),
+            ("adj", (0.1, 0.01)), ("pre", (100, 50)), ("acc", (15, 100)), ("layers", (2, 3)), ("lag", (16, 32, 64)),
+            ("embed_lr", (5e-4, 1e-4)))
+    return [dict(zip([a for a, _ in axes], v)) for v in itertools.product(*[x for _, x in axes])]
+
+
+def synthetic_grid_points():
+    """(K, p) of the 990 data sets of the synthetic grid in the reference driver's order
+    (train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:140-1131: numF / numN of each
+    name; num_factors = num_supervised_factors = numF, :97-100)."""
+    order = [(10, 12), (10, 6), (9, 12), (9, 6), (8, 12), (8, 6), (7, 12), (7, 6), (6, 12), (6, 6), (5, 12), (5, 6),
+             (5, 3), (4, 12), (4, 6), (4, 3), (3, 12), (3, 6), (3, 3), (2, 12), (2, 6), (2, 3), (1, 12), (1, 6), (1, 3)]
+    counts = {(1, 3): 30, (1, 6): 105, (1, 12): 90, (2, 3): 30, (2, 6): 90, (2, 12): 90, (3, 3): 15, (3, 6): 60,
+              (3, 12): 60, (4, 3): 15, (4, 6): 45, (4, 12): 45, (5, 3): 15, (5, 6): 30, (5, 12): 45, (6, 6): 30,
+              (6, 12): 30, (7, 6): 15, (7, 12): 30, (8, 6): 15, (8, 12): 30, (9, 6): 15, (9, 12): 30, (10, 6): 15,
+              (10, 12): 15}
+    return [kp for kp in order for _ in range(counts[kp])]
+
+
+def reference_grids(args, dev, rank, world, dist):
+    """fits/hour on one GPU's share of the reference's own grids, dealt to an 8-GPU node by class-aware
+    sharding (redcliff_amd.shard_grid; rank r of an N <= 8 GPU run fits share r):
+
+    * TST grid, 1536 points: one TST-shaped data set (p = 12, K = 9, nsup = 3, h = 25, gen_lag 4) for
+      every point; the share's shape classes (embed_lag x graph-conv layers) are packs whose replicas
+      mix the four pretrain / acclimation schedules.  Timed against a control: the same packs with
+      every replica on replica 0's schedule (the uniform-pack figure).
+    * synthetic grid, 990 data sets: one model config (h = 25, gen_lag 4, DGCNN 16 / 3 / 100, K =
+      nsup = numF) per data set; each (K, p) class of the share is a pack with PerReplica data and
+      true graphs (sVAR-shaped windows, one seeded set per replica).
+
+    Every fit runs a fixed schedule scaled 1/10 from the reference's (max_iter 300 -> 30 epochs,
+    pretrain / acclimation epochs / 10, rounded up) over 8 training and 2 validation batches of 128
+    windows, early stopping disabled so every fit does the same work, per-epoch GC tracking and
+    validation on the GPU."""
+    import redcliff_amd
+    from redcliff_amd import PerReplica, ReplicaPack, shard_grid
+    share = rank % 8
+    E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
+    out = {"share": "%d of 8 (class-aware shard_grid)" % share, "epochs_per_fit": E, "train_windows": ntr * B,
+           "val_windows": nva * B}
+
+    def run(packs, warm=True):
+        """[(models, opts, train, val, gc)] -> seconds for all packs, sequentially (after an untimed
+        2-epoch warm-up fit of a copy of the first pack)."""
+        if warm:
+            import copy
+            m0, o0, tr0, va0, gc0 = packs[0]
+            wm = [copy.deepcopy(m) for m in m0]
+            wo = [(torch.optim.Adam(m.gen_model[0].parameters(), lr=1e-4, eps=1e-4, weight_decay=1e-4),
+                   torch.optim.Adam(m.gen_model[1].parameters(), lr=1e-4, eps=1e-4, weight_decay=1e-4)) for m in wm]
+            ReplicaPack(wm, wo).fit(None, tr0, va0, max_iter=2, lookback=10 ** 6, check_every=10 ** 6, GC=gc0)
+            del wm, wo
+            torch.cuda.synchronize()
+        built = [(ReplicaPack(ms, os_), tr, va, gc) for ms, os_, tr, va, gc in packs]
+
+        def go():
+            for pk, tr, va, gc in built:
+                pk.fit(None, tr, va, max_iter=E, lookback=10 ** 6, check_every=10 ** 6, GC=gc)
+        return timed(go, dist, dev)
+
+    # ---- TST grid share
+    pts = tst_grid_points()
+    mine = shard_grid(len(pts), 8, share, classes=[(q["lag"], q["layers"]) for q in pts])
+    classes = {}
+    for i in mine:
+        classes.setdefault((pts[i]["lag"], pts[i]["layers"]), []).append(i)
+    base = CONFIGS["c4"]
+    sched = lambda q: (-(-q["pre"] // 10), -(-q["acc"] // 10))  # noqa: E731  (1/10 of the reference's epochs)
+
+    def tst_packs(uniform):
+        packs = []
+        for (lag, layers), idx in classes.items():
+            c = dict(base, F=lag, n=layers, T=lag + 4)
+            X, Y = synth(c, (ntr + nva) * B, seed=400 + rank)
+            train = [(X[i:i + B], Y[i:i + B]) for i in range(0, ntr * B, B)]
+            val = [(X[i:i + B], Y[i:i + B]) for i in range(ntr * B, (ntr + nva) * B, B)]
+            rng = np.random.RandomState(8)
+            gc = [(rng.rand(c["p"], c["p"], c["L"]) < 0.2).astype(np.float64) for _ in range(c["nsup"])]
+            ms, os_ = [], []
+            for j, i in enumerate(idx):
+                q = pts[i]
+                pre, acc = sched(pts[idx[0]] if uniform else q)
+                m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=7000 + i, pre=pre, acc=acc,
+                                forecast=q["forecast"], adj=q["adj"]).to(dev)
+                ms.append(m)
+                os_.append(adam_pair(m, dict(c, lrA=q["embed_lr"], lrB=q["gen_lr"])))
+            packs.append((ms, os_, train, val, gc))
+        return packs
+
+    el_mixed = run(tst_packs(False))
+    el_uni = run(tst_packs(True), warm=False)
+    n = len(mine)
+    out["tst"] = {"fits": n, "packs": [{"embed_lag": k[0], "graph_conv_layers": k[1], "replicas": len(v),
+                                        "schedules": sorted(set(sched(pts[i]) for i in v))}
+                                       for k, v in classes.items()],
+                  "seconds": round(el_mixed, 3), "fits_per_hour": round(n * 3600.0 / el_mixed, 1),
+                  "uniform_schedule_seconds": round(el_uni, 3),
+                  "uniform_schedule_fits_per_hour": round(n * 3600.0 / el_uni, 1),
+                  "mixed_over_uniform_time": round(el_mixed / el_uni, 3)}
+    # ---- synthetic grid share
+    kp = synthetic_grid_points()
+    mine = shard_grid(len(kp), 8, share, classes=kp, cost=[k * p * p for k, p in kp])
+    by = {}
+    for i in mine:
+        by.setdefault(kp[i], []).append(i)
+    packs = []
+    for (K, p), idx in by.items():
+        c = dict(base, p=p, K=K, nsup=K, F=16, n=3, T=100, label_T=100)
+        trains, vals, gcs, ms, os_ = [], [], [], [], []
+        for i in idx:
+            X, Y = synth(c, (ntr + nva) * B, seed=9000 + i)
+            trains.append([(X[j:j + B], Y[j:j + B]) for j in range(0, ntr * B, B)])
+            vals.append([(X[j:j + B], Y[j:j + B]) for j in range(ntr * B, (ntr + nva) * B, B)])
+            rng = np.random.RandomState(i)
+            gcs.append([(rng.rand(p, p, 2) < 0.3).astype(np.float64) for _ in range(K)])
+            m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=11000 + i, pre=10, acc=10).to(dev)
+            ms.append(m)
+            os_.append(adam_pair(m, c))
+        packs.append((ms, os_, PerReplica(trains), PerReplica(vals), PerReplica(gcs)))
+    el_syn = run(packs)
+    n = len(mine)
+    out["synthetic"] = {"fits": n, "packs": [{"K": k[0], "p": k[1], "replicas": len(v)} for k, v in by.items()],
+                        "seconds": round(el_syn, 3), "fits_per_hour": round(n * 3600.0 / el_syn, 1),
+                        "data": "PerReplica: one sVAR-shaped data set and one set of true graphs per fit"}
+    out["note"] = ("fixed 1/10-scaled schedules (%d epochs; TST pretrain {10, 5} / acclimation {2, 10}; synthetic "
+                   "10 / 10), early stopping disabled, 8 x 128 training + 2 x 128 validation windows per fit; packs "
+                   "of a share run one after another" % E)
+    return out
+
+
 # --------------------------------------------------------------------------- modes
 def mode_fit(args, dev, rank, world, dist, holder):
     from redcliff_amd import _native as nat  # noqa: F401
@@ -516,6 +653,9 @@ def mode_fit(args, dev, rank, world, dist, holder):
     fph = None
     if args.fit_replicas > 0:
         fph = fits_per_hour(c, args, dev, rank, dist, world)
+    refg = None
+    if args.ref_grid_epochs > 0 and world <= 8:
+        refg = reference_grids(args, dev, rank, world, dist)
 
     ns = None
     if world == 1 and not args.no_north_star and args.config != "c1k4":
@@ -560,6 +700,7 @@ def mode_fit(args, dev, rank, world, dist, holder):
     out["roofline_hbm"] = hbm_roofline(c, eng, 1e3 * elapsed / args.steps, out.get("roofline"))
     out["grid_search"] = grid
     out["fits_per_hour"] = fph
+    out["reference_grids"] = refg
     out["data_parallel"] = dpl
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(c, args.cpu_seconds)
@@ -710,6 +851,8 @@ def main():
     ap.add_argument("--fit-replicas", type=int, default=128, help="packed whole fits for fits/hour (0: skip)")
     ap.add_argument("--fit-epochs", type=int, default=40)
     ap.add_argument("--fit-train-batches", type=int, default=8)
+    ap.add_argument("--ref-grid-epochs", type=int, default=30,
+                    help="epochs per fit of the reference-grid fits/hour leg (0: skip)")
     ap.add_argument("--dp-batch", type=int, default=128, help="global batch of --mode dp")
     # 512 = the most windows one launch takes (Bmax), so one rank can run the same global batch
     ap.add_argument("--dp-leg-batch", type=int, default=512,
