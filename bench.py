@@ -78,7 +78,7 @@ def short_factor_kernels(c):
     return c["p"] * c["L"] <= 64 and os.environ.get("REDCLIFF_FAC_SHORT") != "0"
 
 
-def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg, short=False):
+def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg, short=False, chains=()):
     """Roofline object of the dominant kernel: algorithmic FLOPs per launch (SURVEY 8(d)
     per-window counts x the windows one launch processes) / its average HIP-event duration.
     Timing slots: "emb_fwd" = k_forward (embedder + vector-path factor forward in one launch)
@@ -97,7 +97,9 @@ def roofline_of(ktimes, fl, windows_per_launch, traffic_cfg, short=False):
             # k_bwd_merged: the factor and embedder backward in one launch (emb_bwd slot)
             merged = True
             fl["emb_bwd"] += fl["fac_bwd"]
-    dom = max((k for k in ktimes if k in fl and k != "supports"), key=lambda k: ktimes[k][0])
+    # chains: timing slots that hold a chain of launches (the GEMM-shaped embedder's products), not
+    # one kernel -- reported, but not candidates for the dominant KERNEL
+    dom = max((k for k in ktimes if k in fl and k != "supports" and k not in chains), key=lambda k: ktimes[k][0])
     avg_ms = ktimes[dom][0]
     flops = fl.get(dom, 0) * windows_per_launch
     achieved = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -300,7 +302,7 @@ def pmc_traffic(kernel_name, cfg):
     import re
     base, packed = (cfg.rsplit("_r", 1)[0], True) if "_r" in cfg else (cfg, False)
     # the newest round's passes first (kernels change between rounds), then older ones
-    pats = [os.path.join(ROOT, "profiles", "r%02d_pmc_%s_*counter_collection*.csv" % (rnd, base)) for rnd in (4, 3, 2)]
+    pats = [os.path.join(ROOT, "profiles", "r%02d_pmc_%s_*counter_collection*.csv" % (rnd, base)) for rnd in (5, 4, 3, 2)]
     if base == "d4ic" and not packed:
         pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
     for pat in pats:
@@ -647,9 +649,23 @@ def mode_fit(args, dev, rank, world, dist, holder):
                 "note": "R independent fits (grid points) per GPU, each B=%d windows per step; one launch per kernel "
                         "for all R" % B}
         if not args.no_kernel_times:
-            gkt = kernel_times_of(gsteps(min(args.grid_steps, 20), 3))
+            # per-kernel durations with the factor chain on the caller's stream (REDCLIFF_FORK=0, the same
+            # bits): on two streams the HIP-event buckets of concurrent kernels overlap and each one
+            # over-states its kernel.  The GEMM-shaped embedder's slots are chains of launches
+            # (6 products + element-wise kernels), reported but not priced as one kernel.
+            fork_env = os.environ.get("REDCLIFF_FORK")
+            os.environ["REDCLIFF_FORK"] = "0"
+            try:
+                gkt = kernel_times_of(gsteps(min(args.grid_steps, 20), 3))
+            finally:
+                if fork_env is None:
+                    del os.environ["REDCLIFF_FORK"]
+                else:
+                    os.environ["REDCLIFF_FORK"] = fork_env
             grid["roofline"] = roofline_of(gkt, flops_per_window(c), R * B, "%s_r%d" % (args.config, R),
-                                           short_factor_kernels(c))
+                                           short_factor_kernels(c), chains=("emb_fwd", "emb_bwd"))
+            grid["roofline"]["timing"] = ("HIP events per kernel with the factor chain on one stream (REDCLIFF_FORK=0); "
+                                          "emb_fwd / emb_bwd are chains of GEMM-embedder launches")
     fph = None
     if args.fit_replicas > 0:
         fph = fits_per_hour(c, args, dev, rank, dist, world)

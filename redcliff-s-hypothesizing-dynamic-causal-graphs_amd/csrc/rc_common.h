@@ -623,10 +623,6 @@ int rc_launch_cos_values(const StepCtx& c, hipStream_t s);  // per-window cos-si
 int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);
-bool rc_emb_use_batched(const RedcliffDims& d);   // rc_embed_batched.hip
-int rc_launch_emb_fwd_batched(const StepCtx& c, hipStream_t s);
-int rc_launch_emb_bwd_batched(const StepCtx& c, hipStream_t s);
-int rc_emb_batched_slots(int B);
 int rc_fac_slots(const RedcliffDims& d);  // rc_factor_mfma.hip
 void rc_emb_partial_layout(StepCtx& c, bool gemm);
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);

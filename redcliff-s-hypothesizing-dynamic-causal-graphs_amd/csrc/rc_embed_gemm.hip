@@ -479,7 +479,7 @@ int ds_splits(int B) {
 #endif
 bool rc_emb_use_gemm(const RedcliffDims& d) {
   const char* v = getenv("REDCLIFF_EMB_PATH");  // read per call: tests switch paths in-process
-  if (v && (!strcmp(v, "gemm") || !strcmp(v, "batched"))) return d.F <= 64 && d.M1 <= 64;
+  if (v && !strcmp(v, "gemm")) return d.F <= 64 && d.M1 <= 64;
   if (v && !strcmp(v, "fused")) return false;
   return (d.p >= 32 || d.R >= RC_EMB_GEMM_R) && d.F <= 64 && d.M1 <= 64;
 }
@@ -496,13 +496,6 @@ void rc_emb_partial_layout(StepCtx& c, bool gemm) {
   const RedcliffDims& d = c.d;
   const int nch = rc_nchunk(d), n = d.n, p = d.p;
   c.dwN = p;
-  if (gemm && rc_emb_use_batched(d)) {  // one record of each per 16-window tile (rc_embed_batched.hip)
-    c.dsN = c.dgN = c.dwN = rc_emb_batched_slots(c.B);
-    c.dsCC = p;
-    c.dsS = (int64_t)n * p * p;
-    c.dsI = (int64_t)p * p;
-    return;
-  }
   const int wb = gemm ? lemb_win_step(c) : 0;
   if (wb) {  // k_lemb_win_bwd: one dS / BN record [s][i][cc][c'] / [s][2][F] per window group
     c.dsN = c.dgN = (c.B + wb - 1) / wb;
@@ -530,7 +523,6 @@ void rc_emb_partial_layout(StepCtx& c, bool gemm) {
 // output keeps the in-order fmaf chain of the one-replica launch, so packed and single fits agree
 // bit for bit.
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
-  if (rc_emb_use_batched(c.d)) return rc_launch_emb_fwd_batched(c, s);
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F;
@@ -573,7 +565,6 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
 }
 
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
-  if (rc_emb_use_batched(c.d)) return rc_launch_emb_bwd_batched(c, s);
   const RedcliffDims& d = c.d;
   const int p = d.p, F = d.F, n = d.n, H = d.H, M1 = d.M1, B = c.B;
   const int64_t pnF = (int64_t)p * n * F, nF = (int64_t)n * F, pH = (int64_t)p * H;

@@ -205,20 +205,16 @@ def synth(cfg, N, seed):
 
 @pytest.mark.parametrize("cname,path", [(c, "auto") for c in CONFIGS] + [("C1", "mfma"), ("C1K4", "mfma"), ("C4", "mfma"),
                                                                         ("C2", "mfma"), ("C1K4", "embgemm"),
-                                                                        ("C2", "embgemm"), ("C2", "embgemm-products"),
-                                                                        ("C2", "embbatched")])
+                                                                        ("C2", "embgemm"), ("C2", "embgemm-products")])
 def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
     """path "mfma" forces the matrix-core factor kernels (rc_factor_mfma.hip, normally chosen
     for p*L >= 256; C2's h=100 runs as four 32-unit hidden blocks per network), "embgemm" the
     GEMM-shaped embedder (rc_embed_gemm.hip, normally chosen for p >= 32 or a packed grid of
     >= 16 replicas; its window-sized products in the windowed kernels for p < 32),
     "embgemm-products" the same with those products as batched GEMMs (REDCLIFF_EMB_WIN=0, the
-    p >= 32 form) onto the published shapes; "embbatched" the replica-batched embedder kernels
-    (rc_embed_batched.hip, opt-in through REDCLIFF_EMB_PATH=batched; never chosen by default)."""
+    p >= 32 form) onto the published shapes."""
     if path == "mfma":
         monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
-    elif path == "embbatched":
-        monkeypatch.setenv("REDCLIFF_EMB_PATH", "batched")
     elif path.startswith("embgemm"):
         monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
         if path == "embgemm-products":

@@ -80,13 +80,12 @@ def test_pack_xcd_orders_bitwise(emb, monkeypatch):
 
 
 @pytest.mark.parametrize("path,grid,emb", [("vector", GRID, None), ("mfma", GRID, None), ("mfma", GRID8, None),
-                                          ("mfma", GRID, "gemm"), ("mfma", GRID8, "batched")])
+                                          ("mfma", GRID, "gemm"), ("mfma", GRID8, "gemm")])
 def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
     """Both factor paths (the default picks the matrix cores for packs of >= 8 replicas, so the
     path is pinned here to compare like with like); R = 3 and the packed-only paths at R = 8.
     emb "gemm": the GEMM-shaped embedder with its products batched over the replicas, against
-    single fits on the same embedder path; emb "batched": the replica-batched embedder kernels
-    (opt-in, REDCLIFF_EMB_PATH=batched; packed grids default to the GEMM-shaped embedder), likewise."""
+    single fits on the same embedder path (the default of packs of >= 16 replicas)."""
     monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
     if emb:
         monkeypatch.setenv("REDCLIFF_EMB_PATH", emb)
