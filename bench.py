@@ -520,15 +520,16 @@ def reference_grids(args, dev, rank, world, dist):
     windows, early stopping disabled so every fit does the same work, per-epoch GC tracking and
     validation on the GPU."""
     import redcliff_amd
-    from redcliff_amd import PerReplica, ReplicaPack, shard_grid
+    from redcliff_amd import PerReplica, ReplicaPack, fit_packs, shard_grid
     share = rank % 8
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
     out = {"share": "%d of 8 (class-aware shard_grid)" % share, "epochs_per_fit": E, "train_windows": ntr * B,
            "val_windows": nva * B}
 
     def run(packs, warm=True):
-        """[(models, opts, train, val, gc)] -> seconds for all packs, sequentially (after an untimed
-        2-epoch warm-up fit of a copy of the first pack)."""
+        """[(models, opts, train, val, gc)] -> seconds for all packs, fitted concurrently (fit_packs: one
+        stream per pack, every pack's epoch enqueued before the host waits; after an untimed 2-epoch
+        warm-up fit of a copy of the first pack)."""
         if warm:
             import copy
             m0, o0, tr0, va0, gc0 = packs[0]
@@ -541,8 +542,8 @@ def reference_grids(args, dev, rank, world, dist):
         built = [(ReplicaPack(ms, os_), tr, va, gc) for ms, os_, tr, va, gc in packs]
 
         def go():
-            for pk, tr, va, gc in built:
-                pk.fit(None, tr, va, max_iter=E, lookback=10 ** 6, check_every=10 ** 6, GC=gc)
+            fit_packs([(pk, (None, tr, va), dict(max_iter=E, lookback=10 ** 6, check_every=10 ** 6, GC=gc))
+                       for pk, tr, va, gc in built])
         return timed(go, dist, dev)
 
     # ---- TST grid share
@@ -610,8 +611,8 @@ def reference_grids(args, dev, rank, world, dist):
                         "seconds": round(el_syn, 3), "fits_per_hour": round(n * 3600.0 / el_syn, 1),
                         "data": "PerReplica: one sVAR-shaped data set and one set of true graphs per fit"}
     out["note"] = ("fixed 1/10-scaled schedules (%d epochs; TST pretrain {10, 5} / acclimation {2, 10}; synthetic "
-                   "10 / 10), early stopping disabled, 8 x 128 training + 2 x 128 validation windows per fit; packs "
-                   "of a share run one after another" % E)
+                   "10 / 10), early stopping disabled, 8 x 128 training + 2 x 128 validation windows per fit; the "
+                   "packs of a share (one per shape class) run concurrently, one stream each (fit_packs)" % E)
     return out
 
 

@@ -950,12 +950,17 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
 //              adjacency-L1 term through the group norms, Adam (or the gradient).
 // A block costs one memory round trip: its W0 run, Adam moments, adjacency rows and output-layer
 // state are requested together at its start; dL/dy comes from the workgroup's LDS copy.
+// xcd bit 0: XCD-aware workgroup order; bits 1-7: stagger (tuning, REDCLIFF_S16_STAGGER): half of
+// the workgroups start their block loop that many s_sleep(63) later (bit 8 set: the odd ones, else
+// those of the second resident round, blockIdx.x / 256 odd), bit 9: instead of sleeping they run at
+// wave priority 1 -- co-resident waves of the same program otherwise reach their matrix-core and
+// vector phases together (MI355X_MICROARCH.md, "try a stagger").  Timing only: the same bits.
 template <int NK4>
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
   constexpr int S = ((NK4 + 3) / 4) * 16 + 4, NQT = (NK4 + 3) / 4;
   const RedcliffDims& d = c.d;
   int bx = blockIdx.x, bz = blockIdx.z;  // xcd: the replica's workgroups (its window tile) on one XCD
-  if (xcd) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
+  if (xcd & 1) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
   const int r = rc_rep(c, bz);
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
   const int rows = ms_rows(B);
@@ -985,6 +990,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
   }
   ms_stage_x(c, r, Xs);
   __syncthreads();
+  if (const int stg = (xcd >> 1) & 127) {
+    const bool late = (xcd & 256) ? (blockIdx.x & 1) : ((blockIdx.x >> 8) & 1);
+    if (late) {
+      if (xcd & 512) {
+        __builtin_amdgcn_s_setprio(1);
+      } else {
+        for (int i = 0; i < stg; ++i) __builtin_amdgcn_s_sleep(63);
+      }
+    }
+  }
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   float* Wt = Dys + ms_nnet(bpw, nU) * rows + wv * ms_wave_floats(NK4);  // weight, then gradient tile
@@ -1247,7 +1262,16 @@ static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
     if (e) return e;
   }
   const char* xe = getenv("REDCLIFF_S16_XCD");  // read per launch (A/B); default on
-  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
+  int flags = (int)!(xe && xe[0] == '0');
+  if (bwd) {  // REDCLIFF_S16_STAGGER=n[:odd][:prio] (tuning, see k_fac_bwd_s16)
+    const char* sv = getenv("REDCLIFF_S16_STAGGER");
+    if (sv && atoi(sv) > 0) {
+      flags |= (atoi(sv) & 127) << 1;
+      if (strstr(sv, "odd")) flags |= 256;
+      if (strstr(sv, "prio")) flags |= 512;
+    }
+  }
+  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, flags);
   return rc_check(hipGetLastError(), what);
 }
 

@@ -8,9 +8,9 @@ from .redcliff_factor_score_embedders import (DGCNN_Embedder, MLPClassifierForMu
                                               MLPClassifierForSingleObjective, cEmbedder)
 from .redcliff_s_cmlp import REDCLIFF_S_CMLP
 from .redcliff_s_cmlp_withStateSmoothing import REDCLIFF_S_CMLP_withStateSmoothing
-from .replicas import PerReplica, ReplicaPack, grid_packs, shard_grid
+from .replicas import PerReplica, ReplicaPack, fit_packs, grid_packs, shard_grid
 from .data_parallel import DataParallelFit
 
 __all__ = ["MLP", "cMLP", "DGCNN", "DGCNN_Model", "DGCNN_Embedder", "cEmbedder", "MLPClassifierForSingleObjective",
            "MLPClassifierForMultipleObjectives", "REDCLIFF_S_CMLP", "REDCLIFF_S_CMLP_withStateSmoothing", "ReplicaPack",
-           "PerReplica", "grid_packs", "shard_grid", "DataParallelFit"]
+           "PerReplica", "fit_packs", "grid_packs", "shard_grid", "DataParallelFit"]

@@ -238,7 +238,7 @@ def _device_truth(GC, G, p, eps, dev):
     truth = torch.from_numpy(_truth_arrays(GC, G)).to(dev)
     eps_pow = torch.tensor([eps ** k for k in range(p)], dtype=torch.float64, device=dev)
     _TRUTH_CACHE.insert(0, (GC, ids, G, p, eps, dev, truth, eps_pow))
-    del _TRUTH_CACHE[4:]
+    del _TRUTH_CACHE[16:]
     return truth, eps_pow
 
 
@@ -287,7 +287,7 @@ def gc_progress_values_grouped(GCs, est, spt, eps=0.1, in_degree_coeff=1., out_d
         eps_pow = torch.tensor([eps ** k for k in range(p)], dtype=torch.float64, device=dev)
         hit = (GCs, ids, G, p, eps, dev, truth, eps_pow)
         _TRUTH_CACHE.insert(0, hit)
-        del _TRUTH_CACHE[4:]
+        del _TRUTH_CACHE[16:]
     truth, eps_pow = hit[6], hit[7]
     out = torch.empty(S, G, 6 + p, dtype=torch.float64, device=dev)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)

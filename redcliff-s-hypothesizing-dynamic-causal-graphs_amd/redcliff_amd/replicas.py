@@ -474,19 +474,26 @@ class ReplicaPack:
         """R fits of ``fit()`` in one packed launch chain; see ``_fit``.  The host side of an epoch
         is O(R) python, so the cyclic garbage collector is paused for the fit: its full passes
         over R models' module trees cost as much as whole epochs (restored afterwards)."""
-        gc_was = gc.isenabled()
-        gc.disable()
-        try:
-            return self._fit(*args, **kwargs)
-        finally:
-            if gc_was:
-                gc.enable()
+        return fit_packs([(self, args, kwargs)])[0]
 
-    def _fit(self, save_dir, X_train, X_val, max_iter, lookback=5, check_every=50, verbose=0, GC=None,
+    def _fit(self, *args, **kwargs):
+        """The packed fit run to completion (no interleaving with other packs)."""
+        g = self._fit_steps(*args, **kwargs)
+        while True:
+            try:
+                next(g)
+            except StopIteration as e:
+                return e.value
+
+    def _fit_steps(self, save_dir, X_train, X_val, max_iter, lookback=5, check_every=50, verbose=0, GC=None,
              deltaConEps=0.1, in_degree_coeff=1., out_degree_coeff=1., stopping_criteria_forecast_coeff=1.,
              stopping_criteria_factor_coeff=1., stopping_criteria_cosSim_coeff=1., output_length=1, save_plots=False,
              cost_criteria="CosineSimilarity", unsupervised_start_index=0, max_factor_prior_batches=10):
-        """R fits of ``fit()`` (...withStateSmoothing.py:1175-1647) in one packed launch chain.
+        """R fits of ``fit()`` (...withStateSmoothing.py:1175-1647) in one packed launch chain, as a
+        generator: it yields whenever its device work for the next host decision is enqueued and the
+        host would otherwise wait for it (once per epoch, and before the final copy back), so
+        ``fit_packs`` can interleave several packs -- each on its own stream -- and the GPU runs
+        their epochs concurrently.  The return value (StopIteration.value) is the fit's.
 
         Every replica follows exactly the rules (and the host code, FitTracker) of a single fit:
         its histories, its stopping criterion (per-model stopping_criteria_* may be given as
@@ -640,6 +647,7 @@ class ReplicaPack:
                     launch_train(it + 1)
                 if prof is not None:
                     tp.append(time.perf_counter())
+                yield  # the epoch's work is enqueued: let other packs enqueue theirs before waiting
                 got = pending.wait()
                 if prof is not None:
                     tp.append(time.perf_counter())
@@ -699,6 +707,7 @@ class ReplicaPack:
             self._bound_this_epoch = False
         hlog.flush()
         _eval_modes(models, self._mod_dicts)
+        yield
         acc, conf = final.wait()
         conf = conf.astype(np.int32).reshape(R, max(nsup, 1), max(nsup, 1))
         for r, m in enumerate(models):
@@ -715,6 +724,45 @@ class ReplicaPack:
         if prof is not None:  # host seconds before the epoch loop, in it, after it
             self.last_profile_edges = (t_loop - t_in, t_end_loop - t_loop, time.perf_counter() - t_end_loop)
         return finals
+
+
+def fit_packs(jobs):
+    """Several packed fits at once: jobs = [(pack, args, kwargs)] of ``ReplicaPack.fit``.  Each pack
+    runs on its own stream; every pack's epoch is enqueued before any host waits for a result
+    (ReplicaPack._fit_steps yields there), so the device runs the packs' epochs concurrently.  This
+    is for a GPU's share of a grid whose shape classes are small packs -- the synthetic grid's (K, p)
+    classes hold 15 to 105 data sets (train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:
+    140-1131) -- where one small pack's latency-bound epoch leaves most of the chip idle.  Every pack's
+    arithmetic is unchanged (the same launches, on another stream), so each replica ends exactly as
+    in its pack's own fit.  Returns the packs' fit results in job order."""
+    gc_was = gc.isenabled()
+    gc.disable()
+    cur = torch.cuda.current_stream()
+    try:
+        if len(jobs) == 1:
+            pack, args, kwargs = jobs[0]
+            return [pack._fit(*args, **kwargs)]
+        run = []
+        for i, (pack, args, kwargs) in enumerate(jobs):
+            s = torch.cuda.Stream(device=pack.device)
+            s.wait_stream(cur)  # the packs' state was written on the caller's stream
+            with torch.cuda.stream(s):
+                run.append([i, pack, s, pack._fit_steps(*args, **kwargs)])
+        out = [None] * len(jobs)
+        while run:
+            for job in list(run):
+                i, pack, s, g = job
+                with torch.cuda.stream(s):
+                    try:
+                        next(g)
+                    except StopIteration as e:
+                        out[i] = e.value
+                        run.remove(job)
+                        cur.wait_stream(s)  # the caller's stream sees the pack's final state
+        return out
+    finally:
+        if gc_was:
+            gc.enable()
 
 
 def _module_dicts(models):

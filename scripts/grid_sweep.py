@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--config", default="d4ic")
     ap.add_argument("--settings", default=None, help="JSON list of environment dicts (default: the built-in list)")
+    ap.add_argument("--kernel-times", action="store_true",
+                    help="also the per-kernel HIP-event averages (us) of each setting (10 more steps)")
     args = ap.parse_args()
     settings = json.loads(args.settings) if args.settings else SETTINGS
     knobs = sorted(set(k for st in settings for k in st))
@@ -50,8 +52,13 @@ def main():
             steps(5, start)()
             el = bench.timed(steps(args.steps, start + 5), None, dev)
             start += 5 + args.steps
-            print(json.dumps({"replicas": R, "round": rnd, "setting": st, "ms_per_step": round(1e3 * el / args.steps, 4),
-                              "windows_per_s": round(R * args.steps * c["B"] / el, 1)}), flush=True)
+            rec = {"replicas": R, "round": rnd, "setting": st, "ms_per_step": round(1e3 * el / args.steps, 4),
+                   "windows_per_s": round(R * args.steps * c["B"] / el, 1)}
+            if args.kernel_times:
+                kt = bench.kernel_times_of(steps(10, start))
+                start += 10
+                rec["kernel_us"] = dict((k, round(v[0] * 1e3, 2)) for k, v in kt.items() if v[1])
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -156,3 +156,46 @@ def test_mixed_schedule_per_replica_data_pack_fit_bitwise(path, monkeypatch):
                 for k in ("exp_avg", "exp_avg_sq", "step"):
                     np.testing.assert_array_equal(stB[i][k].cpu().numpy(), stA[i][k].cpu().numpy(),
                                                   err_msg="replica %d optimizer state %s %s" % (r, i, k))
+
+
+def test_fit_packs_interleaved_equals_pack_fits(monkeypatch):
+    """fit_packs: two packs of different shapes (K = 4 and K = 3 factors: two shape classes of the
+    synthetic grid) fitted concurrently, one stream each, every epoch of both enqueued before the host
+    waits -- each replica bit-identical to its pack fitted alone."""
+    import redcliff_amd
+    from redcliff_amd import ReplicaPack, fit_packs
+    import test_gpu_replicas as T
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "mfma")
+    train, val = data(64 * 2 + 24, seed=61), data(96, seed=62)
+    gc4 = true_graphs(4, 10, 4, seed=63)
+    kw = dict(lookback=1, check_every=1, deltaConEps=0.1, verbose=0, stopping_criteria_forecast_coeff=10.,
+              stopping_criteria_factor_coeff=100., stopping_criteria_cosSim_coeff=1.)
+
+    def packs():
+        a = [make(s, fc, adj) for s, fc, adj, _, _, _, _ in GRID]
+        oa = [opts(m, g[3], g[4]) for m, g in zip(a, GRID)]
+        saved = dict(T.CFG)
+        T.CFG.update(K=3, nsup=3)
+        try:
+            b = [make(10 + s, fc, adj) for s, fc, adj, _, _, _, _ in GRID[:3]]
+        finally:
+            T.CFG.clear()
+            T.CFG.update(saved)
+        ob = [opts(m, g[3], g[4]) for m, g in zip(b, GRID)]
+        return (ReplicaPack(a, oa), a), (ReplicaPack(b, ob), b)
+    Y3 = [(X, Yb[:, :3]) for X, Yb in train]
+    V3 = [(X, Yb[:, :3]) for X, Yb in val]
+    gc3 = gc4[:3]
+    (pa, ma), (pb, mb) = packs()
+    pa.fit(None, train, val, 8, GC=gc4, **kw)
+    pb.fit(None, Y3, V3, 8, GC=gc3, **kw)
+    torch.cuda.synchronize()
+    (qa, na), (qb, nb) = packs()
+    fit_packs([(qa, (None, train, val, 8), dict(GC=gc4, **kw)), (qb, (None, Y3, V3, 8), dict(GC=gc3, **kw))])
+    torch.cuda.synchronize()
+    for x, y in list(zip(ma, na)) + list(zip(mb, nb)):
+        assert x.fit_history["best_it"] == y.fit_history["best_it"]
+        assert same(x.fit_history["avg_combo_loss"], y.fit_history["avg_combo_loss"])
+        sa, sb = x.state_dict(), y.state_dict()
+        for k in sa:
+            np.testing.assert_array_equal(sb[k].cpu().numpy(), sa[k].cpu().numpy(), err_msg=k)
