@@ -731,7 +731,7 @@ constexpr bool kMsTilePad = RC_MS_TILE_PAD;  // 0: the round-3 linear tile (row 
 __host__ __device__ inline int ms_qs(int Q) { return Q + 2 + ((2 - Q) & 7); }
 __host__ __device__ inline int ms_sh(int row) { return ((row >> 3) & 1) << 1; }
 __host__ __device__ inline int ms_tile_floats(int nk4) { return 64 * nk4 + 160; }  // >= 16 ms_qs(Q) + 2, Q <= 4 nk4
-__host__ __device__ inline int ms_wave_floats(int nk4) { return ms_tile_floats(nk4) + 128; }
+__host__ __device__ inline int ms_wave_floats(int nk4) { return ms_tile_floats(nk4) + 192; }  // + Dg, Gn, 1 / Gn
 inline size_t ms_lds(const RedcliffDims& d, int B) { return sizeof(float) * (size_t)ms_rows(B) * (ms_qp16(d) + 4); }
 inline size_t ms_lds_fwd(const RedcliffDims& d, int B) {
   return ms_lds(d, B) + sizeof(float) * 4 * (size_t)ms_tile_floats(ms_nk4(d));
@@ -1003,8 +1003,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   float* Wt = Dys + ms_nnet(bpw, nU) * rows + wv * ms_wave_floats(NK4);  // weight, then gradient tile
-  float* Dg = Wt + ms_tile_floats(NK4);  // dL/dG row of the network (adjacency L1), then its group norms G
+  float* Dg = Wt + ms_tile_floats(NK4);  // dL/dG row of the network (adjacency L1), its group norms G, 1 / G
   float* Gn = Dg + 64;
+  float* Rg = Gn + 64;
   const int u_off = g == 0 ? 4 * l15 : MS_OOB;  // output-layer updates: group 0, unit l15
   // lane-linear epilogue elements e = lane + 64 k of the block's run: column q = e % Q
   const int q0 = lane % Q, dq = 64 % Q;
@@ -1106,6 +1107,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
     // from it before the tile loop; the pre-update weights stay in cur.wt
     Dg[lane] = dgv;
     Gn[lane] = gnv;
+    // RN(1 / G) of the lane's column for the adjacency term's pw / G (rc_div_recip); NaN where G is
+    // outside [2^-100, 2^100], which sends every element of that column to the IEEE division
+    Rg[lane] = (gnv >= 0x1p-100f && gnv <= 0x1p100f) ? 1.0f / gnv : __builtin_nanf("");
     const int Qs = kMsTilePad ? ms_qs(Q) : Q, sh4g = kMsTilePad ? ms_sh(4 * g) : 0;
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt) {
@@ -1131,7 +1135,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
         gr = Wt[e];
       }
       const float dg = Dg[q], gn = Gn[q], pw = cur.wt[k];
-      if (adj_grad && gn > 0.f) gr += dg * (pw / gn);
+      if (adj_grad && gn > 0.f) gr += dg * rc_div_recip(pw, gn, Rg[q]);
       if (!adam) {
         ms_st(rG, 4 * e, gr);
       } else {
