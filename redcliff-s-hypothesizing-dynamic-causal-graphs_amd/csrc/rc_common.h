@@ -511,8 +511,6 @@ __device__ inline float rc_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
 // then rounded to the fp32 values the element-wise kernels apply.
 struct RcAdamScalars {
   float neg_step, bc2s, eps, wd, b2, omb1, omb2;
-  float rbc2s;  // RN(1 / bc2s): sqrt(v) / bc2s as a reciprocal product plus one exact correction
-  int fast;     // bc2s in [2^-60, 1] (always for beta2 < 1 - 2^-100): the reciprocal form applies
 };
 __device__ inline RcAdamScalars rc_adam_scalars(const RedcliffAdamHyper& h, int t) {
   RcAdamScalars s;
@@ -526,55 +524,7 @@ __device__ inline RcAdamScalars rc_adam_scalars(const RedcliffAdamHyper& h, int 
   s.b2 = h.beta2_f;
   s.omb1 = h.one_minus_beta1_f;
   s.omb2 = h.one_minus_beta2_f;
-  s.rbc2s = 1.0f / s.bc2s;
-  s.fast = s.bc2s >= 0x1p-60f && s.bc2s <= 1.0f;
   return s;
-}
-
-// x / y for y = bc2s through r = RN(1 / y): q = RN(x r), then q + RN((x - q y) r) with the
-// remainder exact in an fma.  That is the correctly rounded quotient -- the IEEE x / y bit for bit --
-// whenever x, the quotient and y lie in [2^-100, 2^100] (Markstein's theorem for a correctly
-// rounded reciprocal; checked exhaustively over every mantissa of y and 5e8 random cases,
-// scripts/fdiv_check.c), and for x = +0.  sqrt(v) is +0 or >= 2^-75 and bc2s in [2^-60, 1], so
-// only sqrt(v) > 2^100 (v past 2^200: never finite) takes the division.  The compiler's IEEE
-// division (div_scale / rcp / 4 fma / div_fmas / div_fixup, with the denormal-mode switches) is
-// twice the vector instructions.
-// x / y given r = RN(1 / y) (NaN when y is outside [2^-100, 2^100]): the same reciprocal form,
-// falling back to the IEEE division unless x and the quotient lie in [2^-100, 2^100] -- so every
-// lane gets x / y bit for bit, and only zeros, tiny operands and extreme divisors pay the division.
-__device__ inline float rc_div_recip(float x, float y, float r) {
-#pragma clang fp contract(off)
-  float q = x * r;
-  q = __builtin_fmaf(__builtin_fmaf(-y, q, x), r, q);
-  const float ax = __builtin_fabsf(x), aq = __builtin_fabsf(q);
-  if (!(ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f)) q = x / y;
-  return q;
-}
-
-// sqrtf(v) bit for bit: v_sqrt_f32 (within 1 ulp) and the round-to-nearest fix-up of its two
-// neighbours by exact fma residuals -- the compiler's own correctly rounded expansion without its
-// denormal scaling and zero / infinity class tests, which v in [2^-96, 2^127) never needs (checked
-// against sqrtf for every exponent in that range with the v_sqrt error at -1 / 0 / +1 ulp,
-// scripts/fdiv_check.c); other v take sqrtf.
-__device__ inline float rc_sqrt_rn(float v) {
-#pragma clang fp contract(off)
-  if (v >= 0x1p-96f && v < 0x1p127f) {
-    const float s = __builtin_amdgcn_sqrtf(v);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-    float t = (__builtin_fmaf(-sm, s, v) <= 0.f) ? sm : s;
-    t = (__builtin_fmaf(-sp, s, v) > 0.f) ? sp : t;
-    return t;
-  }
-  return sqrtf(v);
-}
-
-__device__ inline float rc_div_bc2s(float x, const RcAdamScalars& s) {
-#pragma clang fp contract(off)
-  if (s.fast && x <= 0x1p100f) {
-    const float q = x * s.rbc2s;
-    return __builtin_fmaf(__builtin_fmaf(-s.bc2s, q, x), s.rbc2s, q);
-  }
-  return x / s.bc2s;
 }
 
 // torch.optim.Adam (_single_tensor_adam, coupled L2 weight decay) for one element:
@@ -587,7 +537,7 @@ __device__ inline void rc_adam(float& p, float& m, float& v, float g, const RcAd
   if (s.wd != 0.f) g = __builtin_fmaf(p, s.wd, g);
   m = __builtin_fmaf(s.omb1, g - m, m);
   v = __builtin_fmaf(s.omb2 * g, g, v * s.b2);
-  const float denom = rc_div_bc2s(rc_sqrt_rn(v), s) + s.eps;
+  const float denom = sqrtf(v) / s.bc2s + s.eps;
   p = __builtin_fmaf(s.neg_step, m / denom, p);
 }
 

@@ -731,7 +731,7 @@ constexpr bool kMsTilePad = RC_MS_TILE_PAD;  // 0: the round-3 linear tile (row 
 __host__ __device__ inline int ms_qs(int Q) { return Q + 2 + ((2 - Q) & 7); }
 __host__ __device__ inline int ms_sh(int row) { return ((row >> 3) & 1) << 1; }
 __host__ __device__ inline int ms_tile_floats(int nk4) { return 64 * nk4 + 160; }  // >= 16 ms_qs(Q) + 2, Q <= 4 nk4
-__host__ __device__ inline int ms_wave_floats(int nk4) { return ms_tile_floats(nk4) + 192; }  // + Dg, Gn, 1 / Gn
+__host__ __device__ inline int ms_wave_floats(int nk4) { return ms_tile_floats(nk4) + 128; }
 inline size_t ms_lds(const RedcliffDims& d, int B) { return sizeof(float) * (size_t)ms_rows(B) * (ms_qp16(d) + 4); }
 inline size_t ms_lds_fwd(const RedcliffDims& d, int B) {
   return ms_lds(d, B) + sizeof(float) * 4 * (size_t)ms_tile_floats(ms_nk4(d));
@@ -950,17 +950,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
 //              adjacency-L1 term through the group norms, Adam (or the gradient).
 // A block costs one memory round trip: its W0 run, Adam moments, adjacency rows and output-layer
 // state are requested together at its start; dL/dy comes from the workgroup's LDS copy.
-// xcd bit 0: XCD-aware workgroup order; bits 1-7: stagger (tuning, REDCLIFF_S16_STAGGER): half of
-// the workgroups start their block loop that many s_sleep(63) later (bit 8 set: the odd ones, else
-// those of the second resident round, blockIdx.x / 256 odd), bit 9: instead of sleeping they run at
-// wave priority 1 -- co-resident waves of the same program otherwise reach their matrix-core and
-// vector phases together (MI355X_MICROARCH.md, "try a stagger").  Timing only: the same bits.
 template <int NK4>
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
   constexpr int S = ((NK4 + 3) / 4) * 16 + 4, NQT = (NK4 + 3) / 4;
   const RedcliffDims& d = c.d;
   int bx = blockIdx.x, bz = blockIdx.z;  // xcd: the replica's workgroups (its window tile) on one XCD
-  if (xcd & 1) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
+  if (xcd) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
   const int r = rc_rep(c, bz);
   const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
   const int rows = ms_rows(B);
@@ -990,22 +985,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
   }
   ms_stage_x(c, r, Xs);
   __syncthreads();
-  if (const int stg = (xcd >> 1) & 127) {
-    const bool late = (xcd & 256) ? (blockIdx.x & 1) : ((blockIdx.x >> 8) & 1);
-    if (late) {
-      if (xcd & 512) {
-        __builtin_amdgcn_s_setprio(1);
-      } else {
-        for (int i = 0; i < stg; ++i) __builtin_amdgcn_s_sleep(63);
-      }
-    }
-  }
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   float* Wt = Dys + ms_nnet(bpw, nU) * rows + wv * ms_wave_floats(NK4);  // weight, then gradient tile
-  float* Dg = Wt + ms_tile_floats(NK4);  // dL/dG row of the network (adjacency L1), its group norms G, 1 / G
+  float* Dg = Wt + ms_tile_floats(NK4);  // dL/dG row of the network (adjacency L1), then its group norms G
   float* Gn = Dg + 64;
-  float* Rg = Gn + 64;
   const int u_off = g == 0 ? 4 * l15 : MS_OOB;  // output-layer updates: group 0, unit l15
   // lane-linear epilogue elements e = lane + 64 k of the block's run: column q = e % Q
   const int q0 = lane % Q, dq = 64 % Q;
@@ -1107,9 +1091,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
     // from it before the tile loop; the pre-update weights stay in cur.wt
     Dg[lane] = dgv;
     Gn[lane] = gnv;
-    // RN(1 / G) of the lane's column for the adjacency term's pw / G (rc_div_recip); NaN where G is
-    // outside [2^-100, 2^100], which sends every element of that column to the IEEE division
-    Rg[lane] = (gnv >= 0x1p-100f && gnv <= 0x1p100f) ? 1.0f / gnv : __builtin_nanf("");
     const int Qs = kMsTilePad ? ms_qs(Q) : Q, sh4g = kMsTilePad ? ms_sh(4 * g) : 0;
 #pragma unroll
     for (int qt = 0; qt < NQT; ++qt) {
@@ -1135,7 +1116,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, in
         gr = Wt[e];
       }
       const float dg = Dg[q], gn = Gn[q], pw = cur.wt[k];
-      if (adj_grad && gn > 0.f) gr += dg * rc_div_recip(pw, gn, Rg[q]);
+      if (adj_grad && gn > 0.f) gr += dg * (pw / gn);
       if (!adam) {
         ms_st(rG, 4 * e, gr);
       } else {
@@ -1266,16 +1247,7 @@ static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
     if (e) return e;
   }
   const char* xe = getenv("REDCLIFF_S16_XCD");  // read per launch (A/B); default on
-  int flags = (int)!(xe && xe[0] == '0');
-  if (bwd) {  // REDCLIFF_S16_STAGGER=n[:odd][:prio] (tuning, see k_fac_bwd_s16)
-    const char* sv = getenv("REDCLIFF_S16_STAGGER");
-    if (sv && atoi(sv) > 0) {
-      flags |= (atoi(sv) & 127) << 1;
-      if (strstr(sv, "odd")) flags |= 256;
-      if (strstr(sv, "prio")) flags |= 512;
-    }
-  }
-  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, flags);
+  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), what);
 }
 

@@ -16,9 +16,10 @@ Every contraction -- the K x p (or K) channel MLPs as one batched product, the D
 Chebyshev powers, graph convolutions and fc layers, the Vanilla convolutions as im2col
 products, the cEmbedder conditional GC products -- runs in ``redcliff_gemm`` (HIP, gfx950),
 wrapped in an autograd Function whose backward is two more ``redcliff_gemm`` calls.  The
-element-wise glue (bias, ReLU, BatchNorm normalisation, losses) and the optimizer step are
-torch operations on the GPU tensors.  There is no CPU path: tensors must be on the GPU and
-the HIP library must load.
+optimizer steps are ``redcliff_adam_apply`` (HipAdam: each group's parameters and Adam moments
+are views of flat buffers, one gradient gather and one HIP launch per step).  The element-wise
+glue (bias, ReLU, BatchNorm normalisation, losses) is torch operations on the GPU tensors.
+There is no CPU path: tensors must be on the GPU and the HIP library must load.
 """
 import ctypes
 import math
@@ -191,6 +192,95 @@ def vanilla_forward(emb, X, use_final_activation=True):
     return (torch.sigmoid(ecc * w) if sig else w), None
 
 
+# ----------------------------------------------------------------------------- optimizer
+class HipAdam:
+    """One torch.optim.Adam (a single parameter group, coupled L2 weight decay -- the optimizers
+    call_model_fit_method builds, general_utils/model_utils.py:747-762) stepped by
+    ``redcliff_adam_apply`` (the same per-element update, in torch's operation order, as the
+    fused chain's epilogues): the group's parameters become views of one flat buffer and the
+    optimizer's ``exp_avg`` / ``exp_avg_sq`` / ``step`` state views of flat moment buffers and a
+    shared step tensor, so ``optimizer.state_dict()`` round-trips and a step is one multi-tensor
+    gradient gather plus one launch.  A step where some parameter has no gradient (torch skips
+    those, weight decay included) or an option the kernel does not implement is left to
+    ``optimizer.step()``."""
+
+    def __init__(self, opt):
+        self.opt = opt
+        grp = opt.param_groups[0]
+        self.params = list(grp["params"])
+        self.ok = (len(opt.param_groups) == 1 and not grp.get("amsgrad") and not grp.get("maximize")
+                   and not grp.get("decoupled_weight_decay", False) and len(self.params) > 0
+                   and all(p.is_cuda and p.dtype == torch.float32 for p in self.params))
+        if not self.ok:
+            return
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=dev, dtype=torch.float32)
+        self.m = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.v = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.views, self.gviews = [], []
+        o, t = 0, 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                view = self.flat[o:o + k].view_as(p)
+                view.copy_(p.detach())
+                st = opt.state.get(p)
+                if st and "exp_avg" in st:  # a torch-stepped optimizer: continue from its moments
+                    self.m[o:o + k].copy_(st["exp_avg"].reshape(-1))
+                    self.v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+                    t = int(float(st["step"]))
+                p.data = view
+                self.views.append((o, k))
+                self.gviews.append(self.grad[o:o + k].view_as(p))
+                o += k
+        self.t = t
+        self.step_t = torch.tensor(float(t), dtype=torch.float32)
+        for p, (o, k) in zip(self.params, self.views):
+            opt.state[p] = {"step": self.step_t, "exp_avg": self.m[o:o + k].view_as(p),
+                            "exp_avg_sq": self.v[o:o + k].view_as(p)}
+        self._hkey = None
+        self._dims = nat.Dims(R=1, Bmax=1, T=1, p=1, L=1, K=1, h=1, F=1, n=1, H=1, M1=1, nsup=0, use_sigmoid=0,
+                              sigmoid_ecc=0.0)
+
+    def bound(self):
+        return self.ok and all(p.data_ptr() == self.flat.data_ptr() + 4 * o for p, (o, _) in zip(self.params, self.views))
+
+    def _hyper(self):
+        g = self.opt.param_groups[0]
+        key = (float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"]), float(g["weight_decay"]))
+        if key != self._hkey:
+            h = nat.ReplicaHyper()
+            h.A = nat.adam_hyper(*key)
+            self._hdev = torch.from_numpy(np.frombuffer(bytes(h), dtype=np.uint8).copy()).to(self.flat.device)
+            self._hkey = key
+        return self._hdev
+
+    def release(self):
+        """Hand the optimizer back to torch: every parameter gets its own step tensor (torch's
+        Adam advances each parameter's separately and skips those without a gradient); the moments
+        stay views of the flat buffers."""
+        if self.ok:
+            for p in self.params:
+                self.opt.state[p]["step"] = self.step_t.clone()
+        self.ok = False
+
+    def step(self):
+        if not self.bound() or any(p.grad is None for p in self.params):
+            self.release()
+            return self.opt.step()
+        if int(float(self.step_t)) != self.t:  # stepped by torch in between (or its state edited)
+            self.t = int(float(self.step_t))
+        torch._foreach_copy_(self.gviews, [p.grad for p in self.params])
+        n = self.flat.numel()
+        nat.check(nat.lib().redcliff_adam_apply(ctypes.byref(self._dims), self.flat.data_ptr(), self.m.data_ptr(),
+                                                self.v.data_ptr(), self.grad.data_ptr(), n, n,
+                                                self._hyper().data_ptr(), 0, self.t + 1, _stream()), "adam_apply")
+        self.t += 1
+        self.step_t.fill_(float(self.t))
+
+
 # ----------------------------------------------------------------------------- the model
 class GenericPath:
     """forward / GC / compute_loss / batch_update / validate of one REDCLIFF-S model on the
@@ -198,6 +288,18 @@ class GenericPath:
 
     def __init__(self, model):
         self.m = model
+        self._adams = {}
+
+    def _step(self, opt):
+        """opt.step() through HipAdam (one per optimizer object, built on its first step)."""
+        h = self._adams.get(id(opt))
+        if h is None or h.opt is not opt or (h.ok and not h.bound()):
+            if h is not None and h.opt is opt:
+                h.release()  # its parameters were re-pointed: rebuild on the current ones
+            h = self._adams[id(opt)] = HipAdam(opt) if isinstance(opt, torch.optim.Adam) else None
+        if h is None or not h.ok:  # released optimizers stay with torch (per-parameter step counts)
+            return opt.step()
+        return h.step()
 
     # -------------------------------------------------------------- embedder
     def embed(self, X, use_final_activation=True):
@@ -471,21 +573,21 @@ class GenericPath:
                 optimizerA.zero_grad()
                 (loss, _), labels = self.step_loss(X, Y, output_length, embedder_pretrain_loss=True)
                 loss.backward()
-                optimizerA.step()
+                self._step(optimizerA)
             elif kind in ("pretrain_factor", "acclimate", "post_train"):
                 emb.eval()
                 optimizerB.zero_grad()
                 (loss, _), labels = self.step_loss(X, Y, output_length, factor_pretrain_loss=True)
                 loss.backward()
-                optimizerB.step()
+                self._step(optimizerB)
             elif kind == "combined":
                 emb.train()
                 optimizerA.zero_grad()
                 optimizerB.zero_grad()
                 (loss, _), labels = self.step_loss(X, Y, output_length)
                 loss.backward()
-                optimizerA.step()
-                optimizerB.step()
+                self._step(optimizerA)
+                self._step(optimizerB)
         if confusion is not None and labels is not None and m.num_supervised_factors > 0 and kinds and \
                 kinds[-1] in ("pretrain_embedder", "combined"):
             n = m.num_supervised_factors

@@ -154,3 +154,47 @@ def test_gemm_cores_bitwise(monkeypatch):
                 monkeypatch.setenv("REDCLIFF_GEMM_CORE", "valu")
                 want = _raw_bmm(a, b, ta, tb).cpu().numpy()
                 np.testing.assert_array_equal(got, want, err_msg="M=%d N=%d K=%d ta=%d tb=%d" % (M, N, K, ta, tb))
+
+
+@pytest.mark.parametrize("name", ["cemb", "vanilla"])
+def test_hip_adam_matches_torch_adam(name, monkeypatch):
+    """The generic path's optimizer steps (generic.HipAdam: flat parameter / moment buffers, one
+    redcliff_adam_apply launch per group) against torch.optim.Adam's own step on a twin model: the
+    same schedule of batch_updates, parameters and Adam moments within 2 ulp-scale tolerances (the
+    per-element formula is torch's single-tensor Adam; torch's CUDA Adam is the multi-tensor form),
+    the step counts equal, and the optimizers' state_dict() keeps its structure."""
+    from redcliff_amd import generic
+    d, meta = load(name)
+    runs = []
+    for hip in (True, False):
+        m = build(meta)
+        oA = torch.optim.Adam(m.gen_model[0].parameters(), lr=meta["lrA"], betas=(0.9, 0.999), eps=1e-4,
+                              weight_decay=1e-4)
+        oB = torch.optim.Adam(m.gen_model[1].parameters(), lr=meta["lrB"], betas=(0.9, 0.999), eps=1e-4,
+                              weight_decay=1e-4)
+        if not hip:
+            monkeypatch.setattr(generic.GenericPath, "_step", lambda self, opt: opt.step())
+        for epoch in range(meta["pre"] + meta["acc"] + 2):
+            for bi, (Xb, Yb) in enumerate(batches(d, meta)):
+                m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+        torch.cuda.synchronize()
+        monkeypatch.undo()
+        runs.append((m, oA, oB))
+    (ma, aA, aB), (mb, bA, bB) = runs
+    if True:  # HipAdam was in charge of both groups
+        g = ma._generic()
+        assert all(h is not None and h.ok for h in g._adams.values()) and len(g._adams) == 2
+    sa, sb = ma.state_dict(), mb.state_dict()
+    for k in sb:
+        w = sb[k].detach().cpu().numpy().astype(np.float64)
+        scale = max(1.0, float(np.abs(w).max()))
+        assert_close("param " + k, sa[k].detach().cpu().numpy(), w, 1e-5, 1e-7 * scale)
+    for oa, ob in ((aA, bA), (aB, bB)):
+        da, db = oa.state_dict(), ob.state_dict()
+        assert da["param_groups"] == db["param_groups"] and da["state"].keys() == db["state"].keys()
+        for i in db["state"]:
+            assert float(da["state"][i]["step"]) == float(db["state"][i]["step"])
+            for k in ("exp_avg", "exp_avg_sq"):
+                w = db["state"][i][k].cpu().numpy().astype(np.float64)
+                assert_close("%s %s" % (i, k), da["state"][i][k].cpu().numpy(), w, 1e-4,
+                             1e-7 * max(1.0, float(np.abs(w).max())))
