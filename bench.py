@@ -521,7 +521,7 @@ def reference_grids(args, dev, rank, world, dist):
     validation on the GPU."""
     import redcliff_amd
     from redcliff_amd import PerReplica, ReplicaPack, fit_packs, shard_grid
-    share = rank % 8
+    share = rank % 8 if getattr(args, "ref_grid_share", -1) < 0 else args.ref_grid_share
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
     out = {"share": "%d of 8 (class-aware shard_grid)" % share, "epochs_per_fit": E, "train_windows": ntr * B,
            "val_windows": nva * B}
@@ -870,6 +870,8 @@ def main():
     ap.add_argument("--fit-train-batches", type=int, default=8)
     ap.add_argument("--ref-grid-epochs", type=int, default=30,
                     help="epochs per fit of the reference-grid fits/hour leg (0: skip)")
+    ap.add_argument("--ref-grid-share", type=int, default=-1,
+                    help="which 8-GPU share the reference-grid leg fits (default: the rank's)")
     ap.add_argument("--dp-batch", type=int, default=128, help="global batch of --mode dp")
     # 512 = the most windows one launch takes (Bmax), so one rank can run the same global batch
     ap.add_argument("--dp-leg-batch", type=int, default=512,

@@ -229,6 +229,8 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
   };
   if (SB == 1)
     fc1(std::integral_constant<int, 1>{});
+  else if (SB == 2)
+    fc1(std::integral_constant<int, 2>{});
   else
     fc1(std::integral_constant<int, 4>{});
   __syncthreads();

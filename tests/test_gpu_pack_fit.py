@@ -199,3 +199,63 @@ def test_fit_packs_interleaved_equals_pack_fits(monkeypatch):
         sa, sb = x.state_dict(), y.state_dict()
         for k in sa:
             np.testing.assert_array_equal(sb[k].cpu().numpy(), sa[k].cpu().numpy(), err_msg=k)
+
+
+@pytest.mark.parametrize("K,p", [(1, 3), (2, 3), (1, 12), (10, 6)])
+@pytest.mark.parametrize("kern", ["vector", "mfma-gemm"])
+def test_synthetic_grid_shape_classes_pack_fit(K, p, kern, monkeypatch):
+    """Shape classes of the reference's synthetic grid (num_factors = num_supervised_factors = numF in
+    1..10, numN in {3, 6, 12}, train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:97-100,
+    140-1131; model: h = 25, gen_lag 4, DGCNN 16 / 3 / 100) as PerReplica packs -- the extremes a GPU's
+    share can hold (a single factor, three channels) -- each replica bit-identical to its own fit().
+    kern "mfma-gemm": the packed grids' kernels (short-contraction factor kernels, GEMM-shaped embedder)."""
+    import redcliff_amd
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector" if kern == "vector" else "mfma")
+    if kern != "vector":
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
+    from redcliff_amd import PerReplica, ReplicaPack
+
+    def model(seed):
+        coeff = {"FORECAST_COEFF": 10.0, "FACTOR_SCORE_COEFF": 100.0,
+                 "FACTOR_COS_SIM_COEFF": 1.0 / (sum(range(1, K)) if K > 1 else 1.0), "FACTOR_WEIGHT_L1_COEFF": 1e-3,
+                 "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0, "ADJ_L1_REG_COEFF": 0.1 / K / np.sqrt(p * p - 1.0),
+                 "DAGNESS_REG_COEFF": 0.0, "DAGNESS_LAG_COEFF": 0.0, "DAGNESS_NODE_COEFF": 0.0}
+        eargs = [("num_features_per_node", 16), ("num_graph_conv_layers", 3), ("num_hidden_nodes", 100),
+                 ("sigmoid_eccentricity_coeff", 10.0)]
+        torch.manual_seed(seed)
+        return redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing(
+            p, 4, [25], 16, [0], 4, 1, K, K, coeff, False, "DGCNN", eargs, "conditional_factor_fixed_embedder",
+            "apply_factor_weights_after_sim_completion", num_sims=1,
+            training_mode="pretrain_embedder_then_acclimate_factors_then_combined", num_pretrain_epochs=2,
+            num_acclimation_epochs=1).cuda()
+
+    def dataset(seed, N):
+        rng = np.random.RandomState(seed)
+        X = rng.randn(N, 24, p).astype(np.float32)
+        Y = np.zeros((N, K, 24), np.float32)
+        Y[np.arange(N), rng.randint(0, K, N), :] = 1.0
+        X, Y = torch.from_numpy(X), torch.from_numpy(Y)
+        return [(X[i:i + 64], Y[i:i + 64]) for i in range(0, N, 64)]
+    R = 3
+    trains = [dataset(70 + r, 64 * 2 + 24) for r in range(R)]
+    vals = [dataset(80 + r, 96) for r in range(R)]
+    gcs = [true_graphs(K, p, 2, seed=90 + r) for r in range(R)]
+    kw = dict(lookback=1, check_every=1, deltaConEps=0.1, verbose=0, stopping_criteria_forecast_coeff=10.,
+              stopping_criteria_factor_coeff=100., stopping_criteria_cosSim_coeff=1.)
+    solo = []
+    for r in range(R):
+        m = model(100 + r)
+        oA, oB = opts(m, 5e-4, 5e-4)
+        m.fit(None, trains[r], oA, oB, 4, 1, 1, 7, vals[r], GC=gcs[r], **kw)
+        solo.append(m)
+    packed = [model(100 + r) for r in range(R)]
+    pack = ReplicaPack(packed, [opts(m, 5e-4, 5e-4) for m in packed])
+    pack.fit(None, PerReplica(trains), PerReplica(vals), 7, GC=PerReplica(gcs), **kw)
+    torch.cuda.synchronize()
+    for r, (a, b) in enumerate(zip(solo, packed)):
+        assert b.fit_history["best_it"] == a.fit_history["best_it"], r
+        for k in HKEYS:
+            assert same(b.fit_history[k], a.fit_history[k]), "replica %d %s" % (r, k)
+        sa, sb = a.state_dict(), b.state_dict()
+        for k in sa:
+            np.testing.assert_array_equal(sb[k].cpu().numpy(), sa[k].cpu().numpy(), err_msg="replica %d %s" % (r, k))
