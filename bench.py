@@ -523,6 +523,7 @@ def reference_grids(args, dev, rank, world, dist):
     from redcliff_amd import PerReplica, ReplicaPack, fit_packs, shard_grid
     share = rank % 8 if getattr(args, "ref_grid_share", -1) < 0 else args.ref_grid_share
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
+    prof = []
     out = {"share": "%d of 8 (class-aware shard_grid)" % share, "epochs_per_fit": E, "train_windows": ntr * B,
            "val_windows": nva * B}
 
@@ -544,7 +545,12 @@ def reference_grids(args, dev, rank, world, dist):
         def go():
             fit_packs([(pk, (None, tr, va), dict(max_iter=E, lookback=10 ** 6, check_every=10 ** 6, GC=gc))
                        for pk, tr, va, gc in built])
-        return timed(go, dist, dev)
+        el = timed(go, dist, dev)
+        if os.environ.get("REDCLIFF_PACK_PROFILE", "0") != "0":  # host ms per epoch of each pack (replicas.py)
+            prof.append([{"R": pk.R, "host_ms_per_epoch": [round(1e3 * float(v), 3) for v in
+                                                          np.mean(np.asarray(pk.last_profile), axis=0)]}
+                         for pk, _, _, _ in built if pk.last_profile])
+        return el
 
     # ---- TST grid share
     pts = tst_grid_points()
@@ -610,6 +616,9 @@ def reference_grids(args, dev, rank, world, dist):
     out["synthetic"] = {"fits": n, "packs": [{"K": k[0], "p": k[1], "replicas": len(v)} for k, v in by.items()],
                         "seconds": round(el_syn, 3), "fits_per_hour": round(n * 3600.0 / el_syn, 1),
                         "data": "PerReplica: one sVAR-shaped data set and one set of true graphs per fit"}
+    if prof:
+        out["host_profile"] = {"segments": "enqueue evaluation, enqueue next training epoch, wait for the device, "
+                                           "digest the epoch", "runs": prof}
     out["note"] = ("fixed 1/10-scaled schedules (%d epochs; TST pretrain {10, 5} / acclimation {2, 10}; synthetic "
                    "10 / 10), early stopping disabled, 8 x 128 training + 2 x 128 validation windows per fit; the "
                    "packs of a share (one per shape class) run concurrently, one stream each (fit_packs)" % E)
