@@ -524,7 +524,7 @@ def reference_grids(args, dev, rank, world, dist):
     share = rank % 8 if getattr(args, "ref_grid_share", -1) < 0 else args.ref_grid_share
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
     prof = []
-    out = {"share": "%d of 8 (class-aware shard_grid)" % share, "epochs_per_fit": E, "train_windows": ntr * B,
+    out = {"share": "%d of 8 (class-aware shard_grid, FLOP-weighted)" % share, "epochs_per_fit": E, "train_windows": ntr * B,
            "val_windows": nva * B}
 
     def run(packs, warm=True):
@@ -554,11 +554,15 @@ def reference_grids(args, dev, rank, world, dist):
 
     # ---- TST grid share
     pts = tst_grid_points()
-    mine = shard_grid(len(pts), 8, share, classes=[(q["lag"], q["layers"]) for q in pts])
+    base = CONFIGS["c4"]
+    # cost of a point: its shape class's algorithmic FLOPs per window (flops_per_window), so the shares
+    # hold equal work, not equal point counts (r05 shares cut by count ran 0.12 - 0.20 s,
+    # profiles/r05_refgrid_shares_h.jsonl)
+    tst_cost = [flops_per_window(dict(base, F=q["lag"], n=q["layers"], T=q["lag"] + 4))["total"] for q in pts]
+    mine = shard_grid(len(pts), 8, share, classes=[(q["lag"], q["layers"]) for q in pts], cost=tst_cost)
     classes = {}
     for i in mine:
         classes.setdefault((pts[i]["lag"], pts[i]["layers"]), []).append(i)
-    base = CONFIGS["c4"]
     sched = lambda q: (-(-q["pre"] // 10), -(-q["acc"] // 10))  # noqa: E731  (1/10 of the reference's epochs)
 
     def tst_packs(uniform):
@@ -593,13 +597,16 @@ def reference_grids(args, dev, rank, world, dist):
                   "mixed_over_uniform_time": round(el_mixed / el_uni, 3)}
     # ---- synthetic grid share
     kp = synthetic_grid_points()
-    mine = shard_grid(len(kp), 8, share, classes=kp, cost=[k * p * p for k, p in kp])
+    syn_cfg = lambda K, p: dict(base, p=p, K=K, nsup=K, F=16, n=3, T=100, label_T=100)  # noqa: E731
+    # cost per fit as above: the embedder's O(p) work dominates the small-K classes (a K * p^2 cost put
+    # 405 of the 990 fits on share 7, 1.07 s against 0.15 s on share 0)
+    mine = shard_grid(len(kp), 8, share, classes=kp, cost=[flops_per_window(syn_cfg(k, p))["total"] for k, p in kp])
     by = {}
     for i in mine:
         by.setdefault(kp[i], []).append(i)
     packs = []
     for (K, p), idx in by.items():
-        c = dict(base, p=p, K=K, nsup=K, F=16, n=3, T=100, label_T=100)
+        c = syn_cfg(K, p)
         trains, vals, gcs, ms, os_ = [], [], [], [], []
         for i in idx:
             X, Y = synth(c, (ntr + nva) * B, seed=9000 + i)

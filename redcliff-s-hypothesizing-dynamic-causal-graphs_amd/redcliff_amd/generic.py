@@ -208,6 +208,7 @@ class HipAdam:
         self.opt = opt
         grp = opt.param_groups[0]
         self.params = list(grp["params"])
+        self.released_for = None
         self.ok = (len(opt.param_groups) == 1 and not grp.get("amsgrad") and not grp.get("maximize")
                    and not grp.get("decoupled_weight_decay", False) and len(self.params) > 0
                    and all(p.is_cuda and p.dtype == torch.float32 for p in self.params))
@@ -268,6 +269,7 @@ class HipAdam:
 
     def step(self):
         if not self.bound() or any(p.grad is None for p in self.params):
+            self.released_for = "re-pointed parameters" if not self.bound() else "missing gradient"
             self.release()
             return self.opt.step()
         if int(float(self.step_t)) != self.t:  # stepped by torch in between (or its state edited)

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="2x3,1x12,1x3,10x6")
     ap.add_argument("--epochs", type=int, default=7)
+    ap.add_argument("--hist", action="store_true", help="the pack test's order and history comparison")
     ap.add_argument("--steps-only", action="store_true", help="plain batch_update epochs instead of fit()")
     args = ap.parse_args()
     os.environ.setdefault("REDCLIFF_FAC_PATH", "mfma")
@@ -87,6 +88,34 @@ def main():
                 pk.fit(None, PerReplica(trains), PerReplica(vals), args.epochs, GC=PerReplica(gcs), **kw)
             torch.cuda.synchronize()
             return [{k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()} for m in ms]
+
+        if args.hist:  # the test's order: solo fits r = 0, 1, 2, then the pack; histories entry by entry
+            HK = ("avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
+                  "avg_adj_penalty", "avg_combo_loss")
+            solo = []
+            for r in range(R):
+                m = model(100 + r)
+                oA, oB = opts(m)
+                m.fit(None, trains[r], oA, oB, 4, 1, 1, args.epochs, vals[r], GC=gcs[r], **kw)
+                torch.cuda.synchronize()
+                solo.append(m)
+            ms = [model(100 + r) for r in range(R)]
+            pk = ReplicaPack(ms, [opts(m) for m in ms])
+            pk.fit(None, PerReplica(trains), PerReplica(vals), args.epochs, GC=PerReplica(gcs), **kw)
+            torch.cuda.synchronize()
+            for r in range(R):
+                ha, hb = solo[r].fit_history, ms[r].fit_history
+                print("K=%d p=%d r=%d best_it solo %s pack %s stopped %s %s" % (K, p, r, ha["best_it"], hb["best_it"],
+                                                                       ha.get("stopped_at"), hb.get("stopped_at")))
+                for k in HK:
+                    a, b = list(ha[k]), list(hb[k])
+                    bad = [(i, float(x), float(y)) for i, (x, y) in enumerate(zip(a, b)) if not (x == y)]
+                    if bad or len(a) != len(b):
+                        print("   %s len %d/%d differ at %s" % (k, len(a), len(b), bad[:4]))
+                sa = {k: v.detach().cpu().numpy() for k, v in solo[r].state_dict().items()}
+                sb = {k: v.detach().cpu().numpy() for k, v in ms[r].state_dict().items()}
+                print("   state arrays differing:", [k for k in sa if not np.array_equal(sa[k], sb[k], equal_nan=True)][:6])
+            continue
 
         def ndiff(a, b):
             return [k for k in a if not np.array_equal(a[k], b[k], equal_nan=True)]

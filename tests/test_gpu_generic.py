@@ -181,13 +181,14 @@ def test_hip_adam_matches_torch_adam(name, monkeypatch):
         monkeypatch.undo()
         runs.append((m, oA, oB))
     (ma, aA, aB), (mb, bA, bB) = runs
-    # HipAdam was in charge of both groups, except one where some parameter has no gradient (the
-    # Vanilla embedders leave a layer out of the loss; torch skips it): that one went back to torch
+    # HipAdam was in charge of both groups, except one that met a step where some parameter had no
+    # gradient (a phase that leaves part of the Vanilla embedder out of the loss; torch skips those
+    # parameters, weight decay included): that one went back to torch for good
     g = ma._generic()
     assert len(g._adams) == 2 and all(h is not None for h in g._adams.values())
     assert any(h.ok for h in g._adams.values())
     for h in g._adams.values():
-        assert h.ok or any(p.grad is None for p in h.params)
+        assert h.ok or h.released_for == "missing gradient", h.released_for
     sa, sb = ma.state_dict(), mb.state_dict()
     for k in sb:
         w = sb[k].detach().cpu().numpy().astype(np.float64)
