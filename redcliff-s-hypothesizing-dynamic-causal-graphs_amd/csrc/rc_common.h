@@ -31,9 +31,10 @@ struct WsOff {
   int64_t w1;     // [K][p][h]         pre-update snapshot of the factor output weights
   int64_t gq;     // [nU][K][p][p*L]   squared layer-0 group norms, partial over hidden chunks
   int64_t ebp;    // [p*nch][nbw][pst] embedder-backward partials per (node, chunk, window block)
-  int64_t ecnt;   // [p*nch + 2]       arrival counters of those blocks (u32, self-resetting); the last
-                  //                   two slots count published factor-lead workgroups (k_bwd_merged) and
-                  //                   combine workgroups (k_emb_tail)
+  int64_t ecnt;   // [p*nch + 2 + Bmax] arrival counters of those blocks (u32, self-resetting); the
+                  //                   next two slots count published factor-lead workgroups (k_bwd_merged)
+                  //                   and combine workgroups (k_emb_tail), the last Bmax the channel-slice
+                  //                   workgroups of each window (k_forward, self-resetting)
   int64_t gfc1;   // [M1][p*H]         fc1 weight gradient (combined by the node blocks)
   int64_t dwp;    // [p][Bmax][K]      per-channel partial dL/dw
   int64_t dAadj;  // [K][p][p]         adjacency-L1 gradient wrt A, per factor
@@ -49,7 +50,7 @@ struct WsOff {
   int64_t xw;     // [Bmax][Qp]        factor input windows, q = c*L + t (MFMA path; Qp = Q rounded to 32)
   int64_t dyl;    // [K*p][Bmax]       dL/d(prediction of network kj) per window (MFMA path)
   int64_t dgs;    // [K*p][p*L]        adjacency-L1 gradient wrt the lagged group norms (MFMA path)
-  int64_t f1p;    // [64][Bmax][M1]    fc1 split-K partials (GEMM embedder)
+  int64_t f1p;    // [64][Bmax][M1]    fc1 split-K partials (GEMM embedder) / channel-slice partials (k_forward)
   int64_t edf1;   // [Bmax][M1]        dL/d fc1 pre-activation (GEMM embedder)
   int64_t edT;    // [Bmax][p][n][F]   dL/dT_i (GEMM embedder; T itself is [Bmax][p][n][F] there)
   int64_t edX;    // [Bmax][p][F]      dL/d x_bn (GEMM embedder)
@@ -183,7 +184,8 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.w1, K * p * d.h);
   put(o.gq, (int64_t)rc_nuchunk(d) * K * p * p * d.L);
   put(o.ebp, (int64_t)p * rc_nchunk(d) * rc_emb_nbw(d) * rc_emb_pstride(d));
-  put(o.ecnt, p * rc_nchunk(d) + 2);  // + the merged backward's factor-lead counter + k_emb_tail's
+  // + the merged backward's factor-lead counter + k_emb_tail's + one per window (split embedder forward)
+  put(o.ecnt, p * rc_nchunk(d) + 2 + B);
   put(o.gfc1, (int64_t)d.M1 * p * d.H);
   put(o.dwp, p * B * K);
   put(o.dAadj, K * p * p);

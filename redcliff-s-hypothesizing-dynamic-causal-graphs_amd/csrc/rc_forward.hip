@@ -27,17 +27,30 @@ __device__ inline int fq_tile(const RedcliffDims& d) { return d.p * d.L <= FQ_MA
 
 // ------------------------------------------------------------------------------------------
 // Embedder forward of windows [bx*SB, bx*SB + SB).
-__device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float* sm) {
+//
+// fc1 runs over channel slices of cs channels (columns [z*cs*H, min(p, (z+1)*cs)*H) of the p*H
+// contraction, Zs = ceil(p / cs) slices): every slice's 64 lane chains are reduced on their own and
+// f1 = ((part_0 + part_1) + ...) + fc1b, so the bits depend on cs only, never on how the slices are
+// spread over workgroups.  zs < 0: this workgroup runs every slice of its windows.  zs >= 0 (one
+// window per workgroup, the single fit): it runs slice zs only -- the Chebyshev rows, graph
+// convolution and fc1 columns of its channels -- stores its fc1 partials write-through and counts
+// itself in on the window's arrival counter; the workgroup that arrives last sums the partials in
+// slice order and runs fc2.  No workgroup waits for another.
+template <int NBT>
+__device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, int cs, int zs, float* sm) {
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.y);
   const int b0 = bx * SB;
   const int nb = min(SB, c.B - b0);
   if (nb <= 0) return;
+  const int Zs = (d.p + cs - 1) / cs;
+  const int zlo = zs < 0 ? 0 : zs, zhi = zs < 0 ? Zs : zs + 1;
+  const int ch0 = zlo * cs, ch1 = min(d.p, zhi * cs);  // channels whose T / R rows this workgroup forms
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 0);
   RC_PHASE(c.ws, c.wo.total, bx, 0);
   const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
   const int pF = p * F, pH = p * H, nFH = n * F * H;
-  const RcDiv dF(F), dp(p), dpF(pF), dnpF(n * pF), dpH(pH), dH(H);
+  const RcDiv dF(F), dp(p), dpF(pF), dH(H);
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -108,9 +121,12 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
   }
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, bx, 3);
-  // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x))
-  for (int e = tid; e < nb * n * pF; e += RC_BLOCK) {
-    const int s = dnpF.div(e), rem = e - s * n * pF, i = dpF.div(rem), q = rem - i * pF, ch = dF.div(q), f = q - ch * F;
+  // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x)), rows [ch0, ch1)
+  const int cF = (ch1 - ch0) * F, cH = (ch1 - ch0) * H;
+  const RcDiv dcF(cF), dncF(n * cF), dcH(cH);
+  for (int e = tid; e < nb * n * cF; e += RC_BLOCK) {
+    const int s = dncF.div(e), rs = e - s * n * cF, i = dcF.div(rs), qs = rs - i * cF;
+    const int q = ch0 * F + qs, rem = i * pF + q, ch = dF.div(q), f = q - ch * F;
     float v;
     if (i == 0) {
       v = xs[s * pF + q];
@@ -120,7 +136,7 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
       const float* xc = xs + s * pF + f;
       for (int cc = 0; cc < p; ++cc) v += Srow[cc] * xc[cc * F];
     }
-    Tl[e] = v;
+    Tl[s * n * pF + rem] = v;
     ws[c.wo.T + (int64_t)(b0 + s) * n * pF + rem] = v;
   }
   __syncthreads();
@@ -134,19 +150,21 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
   // later, with no register moves in between (a move of a loading register waits for the load).
   // Rows past M1 are wave-uniform zeros; a lane past p*H loads a clamped (valid) column that its
   // masked multiply never uses, so no load sits behind a lane-varying condition.
+  auto qend = [&](int z) { return min(p, (z + 1) * cs) * H; };  // fc1 columns of slice z: [z*cs*H, qend(z))
+  int qb = qend(zlo);
   auto ldw = [&](float (&w)[16], int qn) {
-    const int qc = qn < pH ? qn : pH - 1;
+    const int qc = qn < qb ? qn : qb - 1;
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = (j < RW && m0 + j < M1) ? W1[(int64_t)(m0 + j) * pH + qc] : 0.f;
   };
   float wb0[16], wb1[16], wb2[16];
-  ldw(wb0, lane);
-  ldw(wb1, lane + 64);
+  ldw(wb0, zlo * cs * H + lane);
+  ldw(wb1, zlo * cs * H + lane + 64);
   RC_PHASE(c.ws, c.wo.total, bx, 5);
   // Z = sum_i T_i W_i ; R = relu(Z)
   const float* Wsrc = w_lds ? Wl : gw;
-  for (int e = tid; e < nb * pH; e += RC_BLOCK) {
-    const int s = dpH.div(e), rem = e - s * pH, ch = dH.div(rem), hh = rem - ch * H;
+  for (int e = tid; e < nb * cH; e += RC_BLOCK) {
+    const int s = dcH.div(e), rem = ch0 * H + (e - s * cH), ch = dH.div(rem), hh = rem - ch * H;
     float a4[4] = {0.f, 0.f, 0.f, 0.f};  // four independent chains hide the LDS latency
     for (int i = 0; i < n; ++i) {
       const float* trow = Tl + (s * n + i) * pF + ch * F;
@@ -159,80 +177,113 @@ __device__ void emb_fwd_body(const StepCtx& c, int bx, int SB, int w_lds, float*
       for (; f < F; ++f) a4[0] += trow[f] * wc[f * H];
     }
     const float v = fmaxf((a4[0] + a4[1]) + (a4[2] + a4[3]), 0.f);
-    Rl[e] = v;
+    Rl[s * pH + rem] = v;
     ws[c.wo.R + (int64_t)(b0 + s) * pH + rem] = v;
   }
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, bx, 6);
-  // fc1: wave wv owns rows [wv*RW, wv*RW+RW) (RW <= 16); lanes split the p*H contraction.
+  // fc1: wave wv owns rows [wv*RW, wv*RW+RW) (RW <= 16); lanes split the slice's columns.
   // The next column step's weights are loaded while the current one is multiplied.
   // one window per workgroup (the single fit) multiplies only its own column: NB = 1 accumulators
+  const int jrow = (lane >> 2) & 15, mrow = m0 + jrow;
+  const bool wrow = (lane & 3) == 0 && jrow < RW && mrow < M1;  // the lane that holds row mrow's sum
   auto fc1 = [&](auto nbc) {
     constexpr int NB = decltype(nbc)::value;
-    float acc[16][NB];
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-#pragma unroll
-      for (int s = 0; s < NB; ++s) acc[j][s] = 0.f;
-    // column q of this lane (q ascending per lane: the same chains as one step per iteration)
-    auto mul = [&](const float (&w)[16], int q) {
-      if (q < pH) {
-        float rv[NB];
-#pragma unroll
-        for (int s = 0; s < NB; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-#pragma unroll
-          for (int s = 0; s < NB; ++s) acc[j][s] += w[j] * rv[s];
+    float tot[NB];  // row mrow of each window: the slice sums in slice order
+    for (int z = zlo; z < zhi; ++z) {
+      const int qa = z * cs * H;
+      qb = qend(z);
+      if (z > zlo) {  // the first slice's first two column steps were issued before the graph convolution
+        ldw(wb0, qa + lane);
+        ldw(wb1, qa + lane + 64);
       }
-    };
-    for (int q0 = 0; q0 < pH; q0 += 192) {  // wave-uniform steps of three column blocks
-      const int q = q0 + lane;
-      ldw(wb2, q + 128);
-      mul(wb0, q);
-      if (q0 + 64 >= pH) break;
-      ldw(wb0, q + 192);
-      mul(wb1, q + 64);
-      if (q0 + 128 >= pH) break;
-      ldw(wb1, q + 256);
-      mul(wb2, q + 128);
+      float acc[16][NB];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int s = 0; s < NB; ++s) acc[j][s] = 0.f;
+      // column q of this lane (q ascending per lane: the same chains as one step per iteration)
+      auto mul = [&](const float (&w)[16], int q) {
+        if (q < qb) {
+          float rv[NB];
+#pragma unroll
+          for (int s = 0; s < NB; ++s) rv[s] = s < nb ? Rl[s * pH + q] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+#pragma unroll
+            for (int s = 0; s < NB; ++s) acc[j][s] += w[j] * rv[s];
+        }
+      };
+      for (int q0 = qa; q0 < qb; q0 += 192) {  // wave-uniform steps of three column blocks
+        const int q = q0 + lane;
+        ldw(wb2, q + 128);
+        mul(wb0, q);
+        if (q0 + 64 >= qb) break;
+        ldw(wb0, q + 192);
+        mul(wb1, q + 64);
+        if (q0 + 128 >= qb) break;
+        ldw(wb1, q + 256);
+        mul(wb2, q + 128);
+      }
+      // reduce-scatter of the 16 row partials over the 64 lanes: 17 shuffles per window instead of
+      // 16 full reductions (96); afterwards lane l holds row (l >> 2) & 15 in every lane of its quad
+#pragma unroll
+      for (int s = 0; s < NB; ++s) {
+        if (s >= nb) break;
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = acc[j][s];
+#pragma unroll
+        for (int half = 8; half >= 1; half >>= 1) {
+          const int off = half * 4;  // lane bit that selects the kept half: 32, 16, 8, 4
+          const bool hi = lane & off;
+#pragma unroll
+          for (int i = 0; i < half; ++i) {
+            const float send = hi ? v[i] : v[i + half];
+            const float keep = hi ? v[i + half] : v[i];
+            v[i] = keep + __shfl_xor(send, off, 64);
+          }
+        }
+        float t = v[0];
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 1, 64);
+        tot[s] = z == zlo ? t : tot[s] + t;
+      }
     }
-    // reduce-scatter of the 16 row partials over the 64 lanes: 17 shuffles per window instead of
-    // 16 full reductions (96); afterwards lane l holds row (l >> 2) & 15 in every lane of its quad
+    if (zs < 0) {  // every slice here: f1 = slice sums + bias
 #pragma unroll
-    for (int s = 0; s < NB; ++s) {
-      if (s >= nb) break;
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = acc[j][s];
-#pragma unroll
-      for (int half = 8; half >= 1; half >>= 1) {
-        const int off = half * 4;  // lane bit that selects the kept half: 32, 16, 8, 4
-        const bool hi = lane & off;
-#pragma unroll
-        for (int i = 0; i < half; ++i) {
-          const float send = hi ? v[i] : v[i + half];
-          const float keep = hi ? v[i + half] : v[i];
-          v[i] = keep + __shfl_xor(send, off, 64);
+      for (int s = 0; s < NB; ++s) {
+        if (s >= nb) break;
+        if (wrow) {
+          const float val = tot[s] + fb1[mrow];
+          f1l[s * M1 + mrow] = val;
+          ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + mrow] = val;
         }
       }
-      float t = v[0];
-      t += __shfl_xor(t, 2, 64);
-      t += __shfl_xor(t, 1, 64);
-      const int j = (lane >> 2) & 15, m = m0 + j;
-      if ((lane & 3) == 0 && j < RW && m < M1) {
-        const float val = t + fb1[m];
-        f1l[s * M1 + m] = val;
-        ws[c.wo.f1 + (int64_t)(b0 + s) * M1 + m] = val;
-      }
+    } else if (wrow) {  // this slice's partial, written through for the window's last workgroup
+      rc_store_sc1(ws + c.wo.f1p + ((int64_t)zs * d.Bmax + b0) * M1 + mrow, tot[0]);
     }
   };
-  if (SB == 1)
-    fc1(std::integral_constant<int, 1>{});
-  else if (SB == 2)
-    fc1(std::integral_constant<int, 2>{});
-  else
-    fc1(std::integral_constant<int, 4>{});
+  fc1(std::integral_constant<int, NBT>{});  // NBT >= SB (k_forward's instantiation for this launch)
+  if (zs >= 0) {  // arrival: the last of the window's Zs workgroups sums the partials and runs fc2
+    __shared__ unsigned last;
+    unsigned* cnt = reinterpret_cast<unsigned*>(ws + c.wo.ecnt) + p * rc_nchunk(d) + 2 + b0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its partials
+    __syncthreads();
+    if (tid == 0) last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(Zs - 1);
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler barrier only: the partial loads are sc1
+    if (tid < M1) {
+      const float* part = ws + c.wo.f1p + (int64_t)b0 * M1 + tid;
+      float sum = rc_load_sc1(part);
+      for (int z = 1; z < Zs; ++z) sum = sum + rc_load_sc1(part + (int64_t)z * d.Bmax * M1);
+      const float val = sum + fb1[tid];
+      f1l[tid] = val;
+      ws[c.wo.f1 + (int64_t)b0 * M1 + tid] = val;
+    }
+  }
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, bx, 7);
   for (int e = tid; e < nb * K; e += RC_BLOCK) {
@@ -263,7 +314,7 @@ __device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, 
   return X[((c.row0 + b) * c.d.T + (c.Lmax - L + t)) * c.d.p + ch];
 }
 
-__device__ void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
+__device__ __attribute__((always_inline)) void fac_fwd_body(const StepCtx& c, int bx, float* sm) {
   const RedcliffDims& d = c.d;
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 0);
   const int nU = rc_nuchunk(d);
@@ -346,7 +397,11 @@ size_t fac_fwd_floats(const RedcliffDims& d) {
 }
 
 // grid (nemb + nfac, R): embedder blocks first, then factor blocks.
-__global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_lds, int nemb) {
+// split: one (window, channel slice) per embedder workgroup (SB = 1), window-major.  NBT: the fc1
+// accumulator columns (windows per workgroup, SB <= NBT): one instantiation per SB keeps the
+// single fit's kernel (NBT = 1) at its own register count, not the 4-window one's.
+template <int NBT>
+__global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_lds, int nemb, int cs, int split) {
   extern __shared__ float sm[];
   // every step with an embedder forward re-arms the merged backward's factor-lead counter (the
   // kernel boundary orders this store before k_bwd_merged's polls)
@@ -355,9 +410,14 @@ __global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_l
     lc[0] = 0u;  // merged backward: published factor leads
     lc[1] = 0u;  // k_emb_tail: published combine workgroups
   }
-  if ((int)blockIdx.x < nemb)
-    emb_fwd_body(c, blockIdx.x, SB, w_lds, sm);
-  else
+  if ((int)blockIdx.x < nemb) {
+    if (split) {
+      const int Zs = (c.d.p + cs - 1) / cs, b = blockIdx.x / Zs;
+      emb_fwd_body<NBT>(c, b, 1, w_lds, cs, blockIdx.x - b * Zs, sm);
+    } else {
+      emb_fwd_body<NBT>(c, blockIdx.x, SB, w_lds, cs, -1, sm);
+    }
+  } else
     fac_fwd_body(c, blockIdx.x - nemb, sm);
 }
 
@@ -371,10 +431,30 @@ static int lds_optin(Kern k, size_t bytes, const char* what) {
                                       (int)bytes), what);
 }
 
+// Channels per fc1 slice of the embedder forward (emb_fwd_body): slices of about RC_EMB_FWD_COLS
+// columns of the p*H contraction (REDCLIFF_EMB_FWD_COLS overrides; 0 = one slice).  A function of
+// the model's dimensions only -- never of R or the windows per workgroup -- so a packed fit and an
+// independent one sum fc1 in the same slices (bit for bit).
+#ifndef RC_EMB_FWD_COLS
+#define RC_EMB_FWD_COLS 0
+#endif
+int rc_emb_fwd_slice_channels(const RedcliffDims& d) {
+  static const int cols = [] {
+    const char* v = getenv("REDCLIFF_EMB_FWD_COLS");
+    return v ? atoi(v) : RC_EMB_FWD_COLS;
+  }();
+  if (cols <= 0) return d.p;
+  int cs = cols / d.H > 1 ? cols / d.H : 1;
+  const int cmin = (d.p + 63) / 64;  // at most 64 slices (the partial region's slots)
+  if (cs < cmin) cs = cmin;
+  return cs < d.p ? cs : d.p;
+}
+
 // One launch of the embedder forward (with_emb) and / or the vector-path factor forward (with_fac).
 int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac) {
   const RedcliffDims& d = c.d;
-  int SB = 1, w_lds = 1, nemb = 0;
+  int SB = 1, w_lds = 1, nemb = 0, split = 0;
+  const int cs = rc_emb_fwd_slice_channels(d);
   size_t lds = 0;
   if (with_emb) {
     static const int sb_env = [] {
@@ -394,6 +474,10 @@ int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_
     if (emb_fwd_floats(d, SB, w_lds) > limit) { rc_set_error("embedder forward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
     lds = emb_fwd_floats(d, SB, w_lds);
     nemb = (c.B + SB - 1) / SB;
+    if (SB == 1 && cs < d.p) {  // one window per workgroup: its slices on workgroups of their own
+      split = 1;
+      nemb = c.B * ((d.p + cs - 1) / cs);
+    }
   }
   int nfac = 0;
   if (with_fac) {
@@ -404,10 +488,15 @@ int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_
   }
   if (nemb + nfac == 0) return 0;
   lds *= sizeof(float);
-  int e = lds_optin(k_forward, lds, "k_forward LDS");
-  if (e) return e;
-  hipLaunchKernelGGL(k_forward, dim3(nemb + nfac, c.nrep), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb);
-  return rc_check(hipGetLastError(), "k_forward");
+  auto launch = [&](auto kern) {
+    int e = lds_optin(kern, lds, "k_forward LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(kern, dim3(nemb + nfac, c.nrep), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb, cs, split);
+    return rc_check(hipGetLastError(), "k_forward");
+  };
+  if (SB == 1) return launch(k_forward<1>);
+  if (SB == 2) return launch(k_forward<2>);
+  return launch(k_forward<4>);
 }
 
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s) { return rc_launch_forward(c, s, false, true); }

@@ -86,7 +86,9 @@ struct RcGemmZ {
   int zb;
 };
 __device__ inline RcGemmZ rc_gemm_z(const RcGemm& g, int z) {
-  if (g.nrep == 1) return RcGemmZ{0, z};
+  // one replica in the launch: replica 0, or the active list's only entry (a packed fit whose other
+  // replicas have stopped)
+  if (g.nrep == 1) return RcGemmZ{g.rident ? 0 : (int)g.rmap[0], z};
   const int i = z / g.batch, zb = z - i * g.batch;
   return RcGemmZ{g.rident ? i : (int)g.rmap[i], zb};
 }

@@ -125,6 +125,44 @@ def test_packed_replicas_match_independent_fits(path, grid, emb, monkeypatch):
     np.testing.assert_array_equal(g2[3][2].cpu().numpy(), g1[3][2].cpu().numpy())
 
 
+@pytest.mark.parametrize("path,emb", [("vector", None), ("mfma", None), ("vector", "gemm"), ("mfma", "gemm")])
+def test_single_active_replica_bitwise(path, emb, monkeypatch):
+    """A pack whose active list has ONE entry that is not replica 0 (every other replica has stopped
+    early): each launch then has one replica in its grid, and every kernel -- the GEMM core's
+    replica axis included -- must still address that replica's parameters and workspace.  Replica 2
+    trains alone for epochs 2 and 3 and ends bit-identical to its independent fit; the stopped
+    replicas are left untouched."""
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    if emb:
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", emb)
+    from redcliff_amd import ReplicaPack
+    train = data(64 * 2 + 24, seed=13)
+    val = data(80, seed=14)
+    solo = make(*GRID[2][:3])
+    oA, oB = opts(solo, GRID[2][3], GRID[2][4])
+    packed = [make(s, fc, adj) for s, fc, adj, _, _ in GRID]
+    pack = ReplicaPack(packed, [opts(m, lrB, lrA) for m, (_, _, _, lrB, lrA) in zip(packed, GRID)])
+    ds = pack.cache_dataset(train)
+    vds = pack.cache_dataset(val)
+    for epoch in (0, 1, 2, 3):
+        if epoch == 2:
+            torch.cuda.synchronize()
+            frozen = [{k: t.detach().cpu().numpy().copy() for k, t in m.state_dict().items()} for m in packed[:2]]
+        pack.run_epoch(epoch, ds, active=None if epoch < 2 else [2])
+        for bi, (Xb, Yb) in enumerate(train):
+            solo.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
+    torch.cuda.synchronize()
+    losses, _ = pack.validate(vds, active=[2])
+    a, b = solo.state_dict(), packed[2].state_dict()
+    for k in a:
+        np.testing.assert_array_equal(b[k].cpu().numpy(), a[k].cpu().numpy(), err_msg="replica 2 %s" % k)
+    for r in (0, 1):
+        for k, v in packed[r].state_dict().items():
+            np.testing.assert_array_equal(v.cpu().numpy(), frozen[r][k], err_msg="stopped replica %d %s" % (r, k))
+    v = solo.validate_training(val, 1, CFG["p"], *[[] for _ in range(5)])
+    np.testing.assert_allclose(losses[2], [v[0], v[1], v[2], v[3], v[4], v[5], v[9]], rtol=1e-6, atol=1e-9)
+
+
 def test_pack_mixes_phases_and_rejects_mixed_shapes():
     """Replicas in different phases of their schedules run as one launch chain per phase group,
     each bit-identical to its own batch_update sequence; differing shapes are refused."""
