@@ -887,7 +887,7 @@ def grid_packs(models_and_opts, max_replicas=256, key=None):
     return out
 
 
-def shard_grid(n_points, world, rank, classes=None, cost=None):
+def shard_grid(n_points, world, rank, classes=None, cost=None, min_piece=0):
     """Grid-point indices of rank `rank` of `world` GPUs.
 
     classes=None: round-robin over the grid order, as SLURM array tasks map onto nodes
@@ -897,7 +897,11 @@ def shard_grid(n_points, world, rank, classes=None, cost=None):
     (embed_lag, graph-conv layers) of the TST grid): the points ordered by class (classes in order
     of first appearance, grid order within a class) and cut into `world` contiguous runs of equal
     total cost (cost[i], default 1 per point), so every GPU holds whole classes or long runs of one
-    -- few, large packs per GPU instead of ~world-fold thinner packs of every class."""
+    -- few, large packs per GPU instead of ~world-fold thinner packs of every class.
+
+    min_piece: a GPU's piece of a class smaller than min(min_piece, half the class) joins the class's
+    largest piece on another GPU (a handful of points would be a pack of its own, whose per-epoch
+    launch chains cost about as much as a full one), at the price of a less even cost split."""
     if classes is None:
         return list(range(rank, n_points, world))
     if len(classes) != n_points:
@@ -912,4 +916,15 @@ def shard_grid(n_points, world, rank, classes=None, cost=None):
     # run g holds the points whose cumulative cost midpoint falls in [g, g+1) * total / world
     mid = cum - 0.5 * w[order]
     owner = np.minimum((mid * world / max(total, 1e-300)).astype(np.int64), world - 1)
+    if min_piece > 0:
+        pos = {}
+        for j in range(n_points):
+            pos.setdefault(classes[order[j]], []).append(j)
+        for js in pos.values():
+            counts = np.bincount(owner[js], minlength=world)
+            big = int(np.argmax(counts))
+            small = [g for g in range(world) if 0 < counts[g] < min(min_piece, len(js) / 2.0) and g != big]
+            for j in js:
+                if owner[j] in small:
+                    owner[j] = big
     return sorted(int(order[j]) for j in range(n_points) if owner[j] == rank)

@@ -80,6 +80,33 @@ def test_synthetic_grid_class_aware_shards_balance_cost():
         assert len(runs) == len(set(runs))
 
 
+@pytest.mark.parametrize("grid", ["tst", "synthetic"])
+def test_min_piece_merges_class_fragments(grid):
+    """min_piece: no GPU keeps a sliver of a class (a pack of a few fits) -- every class piece is at
+    least min(32, half the class) -- and the shares still partition the grid in class runs."""
+    if grid == "tst":
+        pts = tst_grid()
+        classes = [(p["lag"], p["layers"]) for p in pts]
+        cost = [{16: 1.3, 32: 1.55, 64: 2.03}[c[0]] + (0.2 if c[1] == 3 else 0.0) for c in classes]
+    else:
+        classes = synthetic_grid()
+        cost = [100 * k * p * p + 11200 * p for k, p in classes]
+    n, world = len(classes), 8
+    plain = [shard_grid(n, world, r, classes=classes, cost=cost) for r in range(world)]
+    shards = [shard_grid(n, world, r, classes=classes, cost=cost, min_piece=32) for r in range(world)]
+    assert sorted(sum(shards, [])) == list(range(n))
+    size = {c: classes.count(c) for c in set(classes)}
+    for s in shards:
+        for c in set(classes[i] for i in s):
+            assert sum(1 for i in s if classes[i] == c) >= min(32, size[c] / 2.0)
+        cls = [classes[i] for i in s]
+        runs = [c for j, c in enumerate(cls) if j == 0 or c != cls[j - 1]]
+        assert len(runs) == len(set(runs))
+    # fewer packs overall than the plain cost cut, which leaves slivers on this grid
+    npk = lambda sh: sum(len(set(classes[i] for i in s)) for s in sh)  # noqa: E731
+    assert npk(shards) < npk(plain)
+
+
 def _model(p=10, K=4, lag=20, layers=2, pre=1, acc=1):
     coeff = {"FORECAST_COEFF": 10., "FACTOR_SCORE_COEFF": 100.0, "FACTOR_COS_SIM_COEFF": 1.0,
              "FACTOR_WEIGHT_L1_COEFF": 1e-3, "FACTOR_WEIGHT_SMOOTHING_PENALTY_COEFF": 0.0, "ADJ_L1_REG_COEFF": 0.1,
