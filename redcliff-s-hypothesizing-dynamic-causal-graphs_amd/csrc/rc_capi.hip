@@ -63,7 +63,13 @@ int aux_stream(AuxStream** out) {
       const int prio = !strcmp(pv, "high") ? greatest : least;
       if (!e) e = rc_check(hipStreamCreateWithPriority(&a.s, hipStreamNonBlocking, prio), "hipStreamCreateWithPriority");
     }
-    for (int i = 0; i < 3 && !e; ++i) e = rc_check(hipEventCreateWithFlags(&a.ev[i], hipEventDisableTiming), "hipEventCreate");
+    // fork / join events order work between two streams of ONE device, so a device-scope release
+    // is all their record needs; REDCLIFF_EVENT_SCOPE=device | nofence | system (tuning knob)
+    const char* ev = getenv("REDCLIFF_EVENT_SCOPE");
+    unsigned ef = hipEventDisableTiming;
+    if (ev && !strcmp(ev, "device")) ef |= hipEventReleaseToDevice;
+    if (ev && !strcmp(ev, "nofence")) ef |= hipEventDisableSystemFence;
+    for (int i = 0; i < 3 && !e; ++i) e = rc_check(hipEventCreateWithFlags(&a.ev[i], ef), "hipEventCreate");
     if (e) return e;
   }
   *out = &a;

@@ -77,11 +77,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
 }
 
 // f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (ceil(B / 4), R): one window
-// per wave, lane m sums the partials in 4 interleaved chains, combined in fixed order; lane k forms
-// w[k] from the wave's relu(f1) read lane by lane (v_readlane: no LDS, no barrier).  Every load of a
-// round is issued before the first add: slots past nsplit (and lanes past M1 / K) read a valid
-// address and are not added -- a runtime-guarded load would wait for itself before the next one
-// is issued (one L2 round trip per partial slot and per fc2 weight).
+// per wave, lane m sums the partials in 4 interleaved chains (all loads in flight), combined in
+// fixed order; lane k forms w[k] from the wave's relu(f1) by shuffles (no LDS, no barrier).
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
@@ -90,32 +87,25 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   const int M1 = d.M1, K = d.K;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
-  const bool mlane = lane < M1;
-  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + (mlane ? lane : 0);
-  const int64_t qs = (int64_t)d.Bmax * M1;
+  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + lane;
   float t4[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int q0 = 0; q0 < nsplit; q0 += 8) {  // nsplit <= 64
-    float pv[8];
+  if (lane < M1) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) pv[u] = part[(int64_t)(q0 + u < nsplit ? q0 + u : 0) * qs];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) t4[u & 3] = (q0 + u < nsplit) ? t4[u & 3] + pv[u] : t4[u & 3];
+    for (int q = 0; q < 64; ++q)  // nsplit <= 64
+      if (q < nsplit) t4[q & 3] += part[(int64_t)q * d.Bmax * M1];
   }
   float v = 0.f;
-  if (mlane) {
+  if (lane < M1) {
     v = ((t4[0] + t4[1]) + (t4[2] + t4[3])) + E[c.eo.fc1b + lane];
     ws[c.wo.f1 + (int64_t)b * M1 + lane] = v;
   }
   const float rv = fmaxf(v, 0.f);
-  // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]), m ascending; the lane's fc2 row in registers first
-  const float* w2 = E + c.eo.fc2W + (lane < K ? lane : 0) * M1;
-  float w2r[64];
-#pragma unroll
-  for (int mm = 0; mm < 64; ++mm) w2r[mm] = w2[mm < M1 ? mm : 0];  // M1 <= 64
+  // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]), m ascending
   float a = 0.f;
-#pragma unroll
-  for (int mm = 0; mm < 64; ++mm) {
-    if (mm < M1) a = fmaf(w2r[mm], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), mm)), a);
+  const float* w2 = E + c.eo.fc2W + (lane < K ? lane : 0) * M1;
+  for (int mm = 0; mm < M1; ++mm) {
+    const float fm = __shfl(rv, mm, 64);
+    if (lane < K) a = fmaf(w2[mm], fm, a);
   }
   if (lane < K) ws[c.wo.w + (int64_t)b * K + lane] = a + E[c.eo.fc2b + lane];
 }
@@ -138,16 +128,13 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
   float t = 0.f;
-  if (ok && fac_grad) {  // all 16 loads in flight (slots past p read channel g and are not added)
+  if (ok && fac_grad) {
     const float* dw = ws + c.wo.dwp + (int64_t)b * K + k;
-    float dv[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {  // p <= 64
       const int j = g + 4 * u;
-      dv[u] = dw[(int64_t)(j < p ? j : g) * d.Bmax * K];
+      if (j < p) t += dw[(int64_t)j * d.Bmax * K];
     }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) t = (g + 4 * u < p) ? t + dv[u] : t;
   }
   t += __shfl_xor(t, 1);
   t += __shfl_xor(t, 2);
@@ -330,11 +317,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
   float v[16];
 #pragma unroll
   for (int u = 0; u < 16; ++u) {  // window w's F rows of X are contiguous ([t][c])
-    // every load issued before the first is used: elements past tot re-read element tot - 1 (a
-    // guarded load would wait for itself before the next one is issued)
-    const int e = min(u * RC_BLOCK + tid, tot - 1);
-    const int w = dpf.div(e);
-    v[u] = X[(int64_t)w * d.T * p + (e - w * pF)];
+    const int e = u * RC_BLOCK + tid;
+    v[u] = 0.f;
+    if (e < tot) {
+      const int w = dpf.div(e);
+      v[u] = X[(int64_t)w * d.T * p + (e - w * pF)];
+    }
   }
   for (int e = tid; e < (n - 1) * pp2; e += RC_BLOCK) S[e] = ws[c.wo.S + pp2 + e];
   if (tid < F) {
@@ -374,8 +362,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
     const float* Si = S + i1 * pp2 + ch * p;
     const float* xw = xb + w * pF + f;
     float t = 0.f;
-#pragma unroll 8
-    for (int cp = 0; cp < p; ++cp) t = fmaf(Si[cp], xw[cp * F], t);  // (unrolled: LDS reads in flight, same order)
+    for (int cp = 0; cp < p; ++cp) t = fmaf(Si[cp], xw[cp * F], t);
     T[w * pnF + ch * nF + (i1 + 1) * F + f] = t;
   }
 }
@@ -435,9 +422,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
       const int w = row / p, ch = row - w * p;
       const float* dtw = dT + w * pnF + f;
       float dx = 0.f;
-#pragma unroll 4
       for (int cp = 0; cp < p; ++cp)
-#pragma unroll 4
         for (int i = 0; i < n; ++i) dx = fmaf(S[i * pp2 + cp * p + ch], dtw[cp * nF + i * F], dx);
       const float x = xr[w * pF + f * p + ch];
       ag += dx * ((x - mean) * inv);
@@ -453,7 +438,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
     for (int w = 0; w < nw; ++w) {
       const float* a = dT + w * pnF + ch * nF + i * F;
       const float* bq = x0 + w * pF + cp * F;
-#pragma unroll 8
       for (int ff = 0; ff < F; ++ff) t = fmaf(a[ff], bq[ff], t);
     }
     dS[i * pp2 + rem] = t;

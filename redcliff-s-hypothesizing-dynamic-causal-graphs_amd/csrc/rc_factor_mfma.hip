@@ -950,8 +950,18 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
 //              adjacency-L1 term through the group norms, Adam (or the gradient).
 // A block costs one memory round trip: its W0 run, Adam moments, adjacency rows and output-layer
 // state are requested together at its start; dL/dy comes from the workgroup's LDS copy.
+// RC_S16_BWD_WAVES (experiment builds): the minimum waves per SIMD the register allocation must
+// allow (default: the compiler's choice, 176 VGPRs + 28 AGPRs = 2 waves).
+#ifndef RC_S16_BWD_WAVES
+#define RC_S16_BWD_WAVES 0
+#endif
+#if RC_S16_BWD_WAVES > 0
+#define RC_S16_BWD_BOUNDS __launch_bounds__(RC_BLOCK, RC_S16_BWD_WAVES)
+#else
+#define RC_S16_BWD_BOUNDS __launch_bounds__(RC_BLOCK)
+#endif
 template <int NK4>
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
+__global__ RC_S16_BWD_BOUNDS void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
   constexpr int S = ((NK4 + 3) / 4) * 16 + 4, NQT = (NK4 + 3) / 4;
   const RedcliffDims& d = c.d;
   int bx = blockIdx.x, bz = blockIdx.z;  // xcd: the replica's workgroups (its window tile) on one XCD
