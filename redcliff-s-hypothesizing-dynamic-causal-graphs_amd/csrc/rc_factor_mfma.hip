@@ -950,10 +950,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
 //              adjacency-L1 term through the group norms, Adam (or the gradient).
 // A block costs one memory round trip: its W0 run, Adam moments, adjacency rows and output-layer
 // state are requested together at its start; dL/dy comes from the workgroup's LDS copy.
-// RC_S16_BWD_WAVES (experiment builds): the minimum waves per SIMD the register allocation must
-// allow (default: the compiler's choice, 176 VGPRs + 28 AGPRs = 2 waves).
+// RC_S16_BWD_WAVES: the minimum waves per SIMD the register allocation must allow.  3 (168
+// registers, 16 of them spilled to scratch) instead of the compiler's 2 (176 VGPRs + 28 AGPRs): the
+// R = 128 grid's k_fac_bwd_s16 200.7-204.5 -> 193.7-196.1 us, whole packed fits bit-identical
+// (0 / 27931 arrays, gpurun_out r5m).  0: the compiler's choice.
 #ifndef RC_S16_BWD_WAVES
-#define RC_S16_BWD_WAVES 0
+#define RC_S16_BWD_WAVES 3
 #endif
 #if RC_S16_BWD_WAVES > 0
 #define RC_S16_BWD_BOUNDS __launch_bounds__(RC_BLOCK, RC_S16_BWD_WAVES)
