@@ -915,8 +915,15 @@ void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
 // other factor workgroups]; node and reduce workgroups wait on the leads' published count
 // (rc_wait_count), everything else runs free.  Same arithmetic in the same order as the two
 // launches, so the results are bit-identical (tests/test_gpu_replicas.py).
+// RC_MERGED_WAVES (experiment builds): a floor of waves per SIMD for the single-sub-block merged
+// kernel (0: the compiler's choice, 217 VGPRs + 24 AGPRs = 2 waves; 3 caps it at 168 registers with
+// 116 bytes of scratch per lane, and 3 workgroups per CU make C1(K=4)'s 681-workgroup grid resident)
+#ifndef RC_MERGED_WAVES
+#define RC_MERGED_WAVES 0
+#endif
 template <bool MULTI>
-__global__ __launch_bounds__(RC_BLOCK) void k_bwd_merged(StepCtx c, int nUl, int nQ, int nnode, int head, int nred,
+__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(MULTI || RC_MERGED_WAVES == 0 ? 1 : RC_MERGED_WAVES)))
+void k_bwd_merged(StepCtx c, int nUl, int nQ, int nnode, int head, int nred,
                                                          int BC, int WPB) {
   extern __shared__ float sm[];
   const int r = rc_rep(c, blockIdx.y);

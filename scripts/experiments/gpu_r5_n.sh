@@ -14,3 +14,13 @@ f=$(ls gpurun_out/n/kt0/*kernel_trace.csv 2>/dev/null | head -1)
 [ -n "$f" ] && step n_timeline0 60 python scripts/step_timeline.py "$f" --steps 4
 rm -rf gpurun_out/n/kt gpurun_out/n/kt0
 step n_bench 600 python bench.py
+# the merged backward at 3 waves per SIMD (scripts/bin/lib_mw3.so, -DRC_MERGED_WAVES=3): resident at C1(K=4)
+M=scripts/bin/lib_mw3.so
+B="python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-north-star --replicas 1 --fit-replicas 0 --dp-leg-batch 0 --ref-grid-epochs 0 --no-kernel-times"
+for rep in 1 2; do
+  for cfg in c1k4 c4 d4ic; do
+    step n_${cfg}_base_$rep 200 $B --config $cfg
+    REDCLIFF_HIP_LIB=$M step n_${cfg}_mw3_$rep 200 $B --config $cfg
+  done
+done
+REDCLIFF_HIP_LIB=$M step n_mw3_tests 600 python -u -m pytest tests/test_gpu_forked.py tests/test_gpu_parity.py -v --timeout 300 --timeout-method thread -rA
