@@ -351,23 +351,6 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     sf = aux->s;
     if ((e = stream_wait(sf, s, aux->ev[0]))) return e;
   }
-  // forward: the fused launch runs the embedder and (vector path, no fork) the factor networks
-  if (egemm) {
-    if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd_gemm(c, s); }))) return e;
-  } else if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_forward(c, s, true, fac && !mfma && !fork); }))) {
-    return e;
-  }
-  if (mfma) {
-    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_fac_fwd_mfma(c, sf); }))) return e;
-  } else if (fork) {
-    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_forward(c, sf, false, true); }))) return e;
-  }
-  if (mfma) {
-    if ((e = stream_wait(s, sf, aux->ev[1]))) return e;  // the mixing needs the factor forward
-    if ((e = timed(KT_FAC_MIX, s, [&] { return rc_launch_fac_mix(c, s); }))) return e;
-    if ((e = stream_wait(sf, s, aux->ev[0]))) return e;  // dW0 needs the mixing's dL/dy
-    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf); }))) return e;
-  }
   // Merged backward (vector factor path + fused embedder, one stream, training without loss
   // values): factor and embedder backward in one launch, the embedder workgroups waiting only
   // for the factor-lead workgroups' dL/dw / dL/dA records (k_bwd_merged), when its grid fits the
@@ -394,11 +377,43 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   const bool split_ok = !mfma && fac && !merged && !fork && emb_grad && (fl & RC_STEP_B) && !(fl & RC_GRAD_ONLY);
   const bool split = split_ok && (slv ? strcmp(slv, "0") != 0
                                       : c.d.R == 1 && 2 * rc_fac_bwd_grid(c) <= rc_cu_count());
+  // REDCLIFF_EXT_EVENT=1 (tuning knob): in a split-lead step the forward and the factor update
+  // complete the fork / join events themselves (hipExtLaunchKernel stop events) instead of an
+  // event-record packet on the stream after them
+  static const bool ext_ev = [] {
+    const char* v = getenv("REDCLIFF_EXT_EVENT");
+    return v && strcmp(v, "0") != 0;
+  }();
+  if (split && ext_ev && (e = aux_stream(&aux))) return e;
+  // forward: the fused launch runs the embedder and (vector path, no fork) the factor networks
+  if (egemm) {
+    if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd_gemm(c, s); }))) return e;
+  } else if ((e = timed(KT_EMB_FWD, s, [&] {
+               return rc_launch_forward(c, s, true, fac && !mfma && !fork, split && ext_ev ? aux->ev[1] : nullptr);
+             }))) {
+    return e;
+  }
+  if (mfma) {
+    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_fac_fwd_mfma(c, sf); }))) return e;
+  } else if (fork) {
+    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_forward(c, sf, false, true); }))) return e;
+  }
+  if (mfma) {
+    if ((e = stream_wait(s, sf, aux->ev[1]))) return e;  // the mixing needs the factor forward
+    if ((e = timed(KT_FAC_MIX, s, [&] { return rc_launch_fac_mix(c, s); }))) return e;
+    if ((e = stream_wait(sf, s, aux->ev[0]))) return e;  // dW0 needs the mixing's dL/dy
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf); }))) return e;
+  }
   if (split) {
     if ((e = aux_stream(&aux))) return e;
     sf = aux->s;
-    if ((e = stream_wait(sf, s, aux->ev[1]))) return e;  // the update needs the forward
-    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf, RC_FB_UPDATE); }))) return e;
+    if (ext_ev) {  // the forward completed ev[1] itself
+      if ((e = rc_check(hipStreamWaitEvent(sf, aux->ev[1], 0), "hipStreamWaitEvent"))) return e;
+    } else if ((e = stream_wait(sf, s, aux->ev[1]))) {  // the update needs the forward
+      return e;
+    }
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf, RC_FB_UPDATE, ext_ev ? aux->ev[0] : nullptr); })))
+      return e;
     if ((e = timed(KT_FAC_LEAD, s, [&] { return rc_launch_fac_bwd(c, s, RC_FB_RECORDS); }))) return e;
   } else if (!mfma && fac && !merged) {
     if (fork && (e = stream_wait(sf, s, aux->ev[1]))) return e;  // the mixing needs the embedder output w
@@ -445,7 +460,13 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }
-  if (split && (e = stream_wait(s, sf, aux->ev[0]))) return e;  // join before A changes
+  if (split) {  // join before A changes
+    if (ext_ev)
+      e = rc_check(hipStreamWaitEvent(s, aux->ev[0], 0), "hipStreamWaitEvent");
+    else
+      e = stream_wait(s, sf, aux->ev[0]);
+    if (e) return e;
+  }
   if (emb_grad || c.nbn > 0) {
     if ((e = timed(KT_EMB_FINAL, s, [&] { return tail ? rc_launch_emb_tail(c, s) : rc_launch_emb_final(c, s); }))) return e;
   }

@@ -1,6 +1,7 @@
 // rc_common.h -- shared layout / context definitions for the REDCLIFF-S gfx950 kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include "redcliff_hip.h"
 
@@ -596,11 +597,13 @@ inline int rc_lds_optin(Kern k, size_t bytes, const char* what) {
 
 // Launchers implemented in the kernel translation units.
 // embedder forward and / or vector-path factor forward in one launch (rc_forward.hip)
-int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac);
+// stop (optional): an event the launch itself completes (hipExtLaunchKernel), so a second stream can
+// wait for this kernel without an event-record packet between it and the next kernel of `s`
+int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac, hipEvent_t stop = nullptr);
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s);
 // factor backward roles (rc_fac_bwd.h fac_bwd_wg): one launch, or the split-lead pair
 enum { RC_FB_ALL = 0, RC_FB_RECORDS = 1, RC_FB_UPDATE = 2 };
-int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role);
+int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role, hipEvent_t stop = nullptr);
 int rc_fac_bwd_grid(const StepCtx& c);  // workgroups per replica of the update launch
 
 // compute units of the current device (cached per host thread)

@@ -60,7 +60,7 @@ int rc_fac_bwd_grid(const StepCtx& c) {
 // role: RC_FB_ALL (one launch), or the split-lead pair RC_FB_RECORDS (K*p lead workgroups: dL/dw,
 // dL/dA, group norms, x_sim, loss values) + RC_FB_UPDATE (every workgroup's dW0 / bias / Adam part),
 // which depend only on the forward and so run concurrently (rc_capi.hip redcliff_train_step)
-int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role) {
+int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role, hipEvent_t stop) {
   const RedcliffDims& d = c.d;
   const int Q = d.p * d.L;
   const bool upd = (c.flags & RC_STEP_B) && role != RC_FB_RECORDS;
@@ -79,7 +79,11 @@ int rc_launch_fac_bwd(const StepCtx& c, hipStream_t s, int role) {
   }
   // without a factor update only the lead workgroup of each network has work
   const int nUl = upd ? rc_nuchunk(d) : 1;
-  hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, role);
+  if (stop)
+    hipExtLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, nullptr, stop, 0, c, nUl,
+                          nQ, role);
+  else
+    hipLaunchKernelGGL(k_fac_bwd, dim3(d.K * d.p * nUl * nQ, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, role);
   return rc_check(hipGetLastError(), "k_fac_bwd");
 }
 

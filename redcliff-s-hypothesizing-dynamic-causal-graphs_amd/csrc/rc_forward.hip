@@ -451,7 +451,7 @@ int rc_emb_fwd_slice_channels(const RedcliffDims& d) {
 }
 
 // One launch of the embedder forward (with_emb) and / or the vector-path factor forward (with_fac).
-int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac) {
+int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac, hipEvent_t stop) {
   const RedcliffDims& d = c.d;
   int SB = 1, w_lds = 1, nemb = 0, split = 0;
   const int cs = rc_emb_fwd_slice_channels(d);
@@ -491,7 +491,11 @@ int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_
   auto launch = [&](auto kern) {
     int e = lds_optin(kern, lds, "k_forward LDS");
     if (e) return e;
-    hipLaunchKernelGGL(kern, dim3(nemb + nfac, c.nrep), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb, cs, split);
+    if (stop)
+      hipExtLaunchKernelGGL(kern, dim3(nemb + nfac, c.nrep), dim3(RC_BLOCK), lds, s, nullptr, stop, 0, c, SB, w_lds, nemb,
+                            cs, split);
+    else
+      hipLaunchKernelGGL(kern, dim3(nemb + nfac, c.nrep), dim3(RC_BLOCK), lds, s, c, SB, w_lds, nemb, cs, split);
     return rc_check(hipGetLastError(), "k_forward");
   };
   if (SB == 1) return launch(k_forward<1>);
