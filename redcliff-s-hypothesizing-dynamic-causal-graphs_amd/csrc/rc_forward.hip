@@ -436,7 +436,7 @@ static int lds_optin(Kern k, size_t bytes, const char* what) {
 // the model's dimensions only -- never of R or the windows per workgroup -- so a packed fit and an
 // independent one sum fc1 in the same slices (bit for bit).
 #ifndef RC_EMB_FWD_COLS
-#define RC_EMB_FWD_COLS 300
+#define RC_EMB_FWD_COLS 200
 #endif
 int rc_emb_fwd_slice_channels(const RedcliffDims& d) {
   static const int cols = [] {
