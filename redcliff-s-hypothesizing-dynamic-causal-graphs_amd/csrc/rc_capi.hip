@@ -424,7 +424,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   // adjacency chain starts with the combine instead of after it, and one kernel boundary goes.
   // REDCLIFF_TAIL=0 keeps the two launches.
   const char* tlv = getenv("REDCLIFF_TAIL");
-  bool tail = false, adj_early = false;
+  bool tail = false;
   auto tail_ok = [&]() {
     return !egemm && emb_grad && c.defer == 1 && !(fl & RC_VALUES) && !(tlv && strcmp(tlv, "0") == 0) &&
            rc_emb_tail_grid(c) > 0;
@@ -455,24 +455,11 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if (c.defer < 0 || c.defer > 2) c.defer = 1;
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
     tail = tail_ok();
-    // REDCLIFF_ADJ_EARLY=1 (tuning knob): k_emb_final's adjacency workgroup runs in the combine
-    // launch (k_emb_combine_adj), beside the combine instead of after it
-    const char* aev = getenv("REDCLIFF_ADJ_EARLY");  // read per step: tests switch it in-process
-    const bool adj_env = aev && strcmp(aev, "0") != 0;
-    adj_early = adj_env && c.defer == 1 && !tail && c.d.p * c.d.p <= 4 * RC_BLOCK;
-    if (adj_early) {
-      if (split) {  // the adjacency workgroup rewrites A, an operand of the factor update
-        e = ext_ev ? rc_check(hipStreamWaitEvent(s, aux->ev[0], 0), "hipStreamWaitEvent") : stream_wait(s, sf, aux->ev[0]);
-        if (e) return e;
-      }
-      if ((e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine_adj(c, s); }))) return e;
-    } else if (c.defer == 1 && !tail && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) {
-      return e;
-    }
+    if (c.defer == 1 && !tail && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }
-  if (split && !adj_early) {  // join before A changes
+  if (split) {  // join before A changes
     if (ext_ev)
       e = rc_check(hipStreamWaitEvent(s, aux->ev[0], 0), "hipStreamWaitEvent");
     else
@@ -480,8 +467,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if (e) return e;
   }
   if (emb_grad || c.nbn > 0) {
-    if ((e = timed(KT_EMB_FINAL, s, [&] { return tail ? rc_launch_emb_tail(c, s) : rc_launch_emb_final(c, s, !adj_early); })))
-      return e;
+    if ((e = timed(KT_EMB_FINAL, s, [&] { return tail ? rc_launch_emb_tail(c, s) : rc_launch_emb_final(c, s); }))) return e;
   }
   if (fork && (e = stream_wait(s, sf, aux->ev[2]))) return e;  // join: the caller's stream sees both chains
   return 0;

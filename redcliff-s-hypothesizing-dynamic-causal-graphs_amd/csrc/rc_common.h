@@ -633,9 +633,7 @@ void rc_emb_partial_layout(StepCtx& c, bool gemm);
 int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
-// adj = false: the adjacency workgroups ran in rc_launch_emb_combine_adj (parameter workgroups only)
-int rc_launch_emb_final(const StepCtx& c, hipStream_t s, bool adj = true);
-int rc_launch_emb_combine_adj(const StepCtx& c, hipStream_t s);
+int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
 int rc_emb_tail_grid(const StepCtx& c);
 int rc_launch_emb_tail(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);

@@ -1514,37 +1514,19 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
 }
 
 template <int NR>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int ept, int adj) {
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int ept) {
   rc_critical_priority();
   // the adjacency workgroups (the longest) are dispatched first for ALL replicas: linear
   // workgroup i < nrep is replica i's adjacency workgroup, the rest run the parameter updates
   // (R = 128 D4IC grid: the last replicas' adjacency workgroups no longer start behind ~10K
-  // parameter workgroups).  adj = 0: the adjacency workgroups ran in k_emb_combine_adj.
+  // parameter workgroups)
   const int lin = blockIdx.x + blockIdx.y * gridDim.x;
-  const int na = adj ? c.nrep : 0;
-  if (lin < na) {
+  if (lin < c.nrep) {
     emb_final_wg<NR>(c, 0, lin, ept, false, false);
   } else {
-    const int wy = (lin - na) / nw;
-    emb_final_wg<NR>(c, 1 + (lin - na) - wy * nw, wy, ept, false, false);
+    const int wy = (lin - c.nrep) / nw;
+    emb_final_wg<NR>(c, 1 + (lin - c.nrep) - wy * nw, wy, ept, false, false);
   }
-}
-
-// k_emb_combine with the adjacency workgroup of k_emb_final as workgroup 0 of each replica
-// (REDCLIFF_ADJ_EARLY): it sums its dS partials in place (the sums the combine forms, in the same
-// order, as in k_emb_tail), so the adjacency chain -- the longest workgroup of k_emb_final --
-// runs beside the combine instead of after it; k_emb_final then has parameter workgroups only.
-// Same arithmetic, same bits.  grid (1 + ncomb, R).
-template <int NR>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_combine_adj(StepCtx c, int ncx) {
-  rc_critical_priority();
-  const int b = blockIdx.x, r = rc_rep(c, blockIdx.y);
-  if (b == 0) {
-    emb_final_wg<NR>(c, 0, blockIdx.y, 1, false, true);
-    return;
-  }
-  const int q = b - 1, grp = q / ncx, x = q - grp * ncx;
-  emb_combine_elem(c, r, grp, x * RC_BLOCK + threadIdx.x, false);
 }
 
 // k_emb_combine + k_emb_final as one launch (single fits with the fused embedder; round 3):
@@ -1784,18 +1766,7 @@ int rc_launch_emb_tail(const StepCtx& c, hipStream_t s) {
   return rc_check(hipGetLastError(), "k_emb_tail");
 }
 
-int rc_launch_emb_combine_adj(const StepCtx& c, hipStream_t s) {
-  const RedcliffDims& d = c.d;
-  if (d.p * d.p > 4 * RC_BLOCK || c.defer != 1) { rc_set_error("early adjacency: p*p <= 1024 and defer == 1 required"); return REDCLIFF_EINVAL; }
-  const int ncx = (rc_emb_pstride(d) + RC_BLOCK - 1) / RC_BLOCK;
-  const size_t lds = rc_emb_final_lds(d);
-  int e = rc_lds_optin(k_emb_combine_adj<4>, lds, "k_emb_combine_adj LDS");
-  if (e) return e;
-  hipLaunchKernelGGL(k_emb_combine_adj<4>, dim3(1 + ncx * d.p * rc_nchunk(d), c.nrep), dim3(RC_BLOCK), lds, s, c, ncx);
-  return rc_check(hipGetLastError(), "k_emb_combine_adj");
-}
-
-int rc_launch_emb_final(const StepCtx& c, hipStream_t s, bool adj) {
+int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int total = d.n * d.F * d.H + d.K * d.M1 + d.K + d.M1 + 2 * d.F + d.M1 * d.p * d.H;
   // parameter elements per thread: 4 from 8 replicas, 8 from 96 (R = 128 D4IC with the forked step:
@@ -1808,13 +1779,11 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s, bool adj) {
   if (d.p * d.p <= 4 * RC_BLOCK) {
     int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");
     if (e) return e;
-    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + (adj ? 1 : 0), c.nrep), dim3(RC_BLOCK), adj ? lds : 0, s, c, nw, ept,
-                       adj ? 1 : 0);
+    hipLaunchKernelGGL(k_emb_final<4>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw, ept);
   } else {
     int e = rc_lds_optin(k_emb_final<16>, lds, "k_emb_final LDS");
     if (e) return e;
-    if (!adj) { rc_set_error("early adjacency: p*p <= 1024 required"); return REDCLIFF_EINVAL; }
-    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw, ept, 1);
+    hipLaunchKernelGGL(k_emb_final<16>, dim3(nw + 1, c.nrep), dim3(RC_BLOCK), lds, s, c, nw, ept);
   }
   return rc_check(hipGetLastError(), "k_emb_final");
 }

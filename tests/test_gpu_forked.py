@@ -114,12 +114,11 @@ def test_forked_pack_bitwise_equals_single_stream_pack(monkeypatch, guard_bands)
             np.testing.assert_array_equal(states["1"][r][k], want, err_msg="replica %d %s" % (r, k))
 
 
-def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", adj="0", ext="0"):
+def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", ext="1"):
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
     monkeypatch.setenv("REDCLIFF_MERGE", merge)
     monkeypatch.setenv("REDCLIFF_SPLIT_LEAD", split)
     monkeypatch.setenv("REDCLIFF_TAIL", tail)
-    monkeypatch.setenv("REDCLIFF_ADJ_EARLY", adj)
     monkeypatch.setenv("REDCLIFF_EXT_EVENT", ext)
     m = make(seed, 10.0, 0.1)
     oA, oB = opts(m, 5e-4, 2e-4)
@@ -131,7 +130,7 @@ def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", 
             m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
     torch.cuda.synchronize()
     if guarded:
-        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s tail=%s adj=%s ext=%s" % (merge, split, tail, adj, ext))
+        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s tail=%s ext=%s" % (merge, split, tail, ext))
     return {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
 
 
@@ -164,17 +163,15 @@ def test_split_lead_bitwise_equals_one_launch(monkeypatch, guard_bands):
         np.testing.assert_array_equal(again[k], want, err_msg=k)
 
 
-@pytest.mark.parametrize("split,ext", [("0", "0"), ("1", "0"), ("1", "1")])
-def test_early_adjacency_and_kernel_events_bitwise(split, ext, monkeypatch, guard_bands):
-    """k_emb_combine_adj (k_emb_final's adjacency workgroup in the combine launch, summing its dS
-    partials in place; REDCLIFF_ADJ_EARLY) with a parameter-only k_emb_final, and the split-lead
-    step's fork / join events completed by the forward and update kernels themselves
-    (REDCLIFF_EXT_EVENT), against the default launches: bit for bit through pretrain -> acclimate ->
-    combined, guard bands intact, a second run repeating the first."""
+def test_kernel_completed_events_bitwise(monkeypatch, guard_bands):
+    """The split-lead step's fork / join events completed by the forward and factor-update kernels
+    themselves (hipExtLaunchKernel stop events, the default) against event-record packets on the
+    streams (REDCLIFF_EXT_EVENT=0): bit for bit through pretrain -> acclimate -> combined, guard
+    bands intact, a second run repeating the first."""
     train = data(64 * 2 + 24, seed=17)
-    want = run_vector(monkeypatch, "0", train, True, split=split)
-    got = run_vector(monkeypatch, "0", train, True, split=split, adj="1", ext=ext)
-    again = run_vector(monkeypatch, "0", train, False, split=split, adj="1", ext=ext)
+    want = run_vector(monkeypatch, "0", train, True, split="1", ext="0")
+    got = run_vector(monkeypatch, "0", train, True, split="1", ext="1")
+    again = run_vector(monkeypatch, "0", train, False, split="1", ext="1")
     for k, w in want.items():
         np.testing.assert_array_equal(got[k], w, err_msg=k)
         np.testing.assert_array_equal(again[k], w, err_msg=k)
