@@ -392,16 +392,22 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
              }))) {
     return e;
   }
+  // forked matrix-core chain: the factor forward, the mixing and dW0 complete their hand-off events
+  // themselves (as the split-lead step's; REDCLIFF_EXT_EVENT=0: event-record packets)
+  const bool mext = mfma && sf != s && ext_ev, dw0_ev = mext && (fl & RC_STEP_B);
+  auto wait_ev = [&](hipStream_t to, hipStream_t from, hipEvent_t ev, bool completed) {
+    return completed ? rc_check(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent") : stream_wait(to, from, ev);
+  };
   if (mfma) {
-    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_fac_fwd_mfma(c, sf); }))) return e;
+    if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_fac_fwd_mfma(c, sf, mext ? aux->ev[1] : nullptr); }))) return e;
   } else if (fork) {
     if ((e = timed(KT_FAC_FWD, sf, [&] { return rc_launch_forward(c, sf, false, true); }))) return e;
   }
   if (mfma) {
-    if ((e = stream_wait(s, sf, aux->ev[1]))) return e;  // the mixing needs the factor forward
-    if ((e = timed(KT_FAC_MIX, s, [&] { return rc_launch_fac_mix(c, s); }))) return e;
-    if ((e = stream_wait(sf, s, aux->ev[0]))) return e;  // dW0 needs the mixing's dL/dy
-    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf); }))) return e;
+    if ((e = wait_ev(s, sf, aux->ev[1], mext))) return e;  // the mixing needs the factor forward
+    if ((e = timed(KT_FAC_MIX, s, [&] { return rc_launch_fac_mix(c, s, mext ? aux->ev[0] : nullptr); }))) return e;
+    if ((e = wait_ev(sf, s, aux->ev[0], mext))) return e;  // dW0 needs the mixing's dL/dy
+    if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf, dw0_ev ? aux->ev[2] : nullptr); }))) return e;
   }
   if (split) {
     if ((e = aux_stream(&aux))) return e;
@@ -469,7 +475,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   if (emb_grad || c.nbn > 0) {
     if ((e = timed(KT_EMB_FINAL, s, [&] { return tail ? rc_launch_emb_tail(c, s) : rc_launch_emb_final(c, s); }))) return e;
   }
-  if (fork && (e = stream_wait(s, sf, aux->ev[2]))) return e;  // join: the caller's stream sees both chains
+  if (fork && (e = wait_ev(s, sf, aux->ev[2], dw0_ev))) return e;  // join: the caller's stream sees both chains
   return 0;
 }
 

@@ -622,10 +622,10 @@ inline int rc_cu_count() {
 // MFMA path of the factor networks (large p*L): window transpose, GEMM forward, per-network
 // mixing / penalties / small-parameter updates, GEMM dW0 + Adam.
 bool rc_fac_use_mfma(const RedcliffDims& d);
-int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s);
-int rc_launch_fac_mix(const StepCtx& c, hipStream_t s);
+int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s, hipEvent_t stop = nullptr);
+int rc_launch_fac_mix(const StepCtx& c, hipStream_t s, hipEvent_t stop = nullptr);
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s);  // per-window cos-sim penalty values (rc_embed.hip)   // mixing, loss terms, output layer (MFMA path)
-int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
+int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s, hipEvent_t stop = nullptr);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);
 int rc_fac_slots(const RedcliffDims& d);  // rc_factor_mfma.hip
