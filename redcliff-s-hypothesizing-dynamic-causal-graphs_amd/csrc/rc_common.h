@@ -622,10 +622,10 @@ inline int rc_cu_count() {
 // MFMA path of the factor networks (large p*L): window transpose, GEMM forward, per-network
 // mixing / penalties / small-parameter updates, GEMM dW0 + Adam.
 bool rc_fac_use_mfma(const RedcliffDims& d);
-int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s, hipEvent_t stop = nullptr);
-int rc_launch_fac_mix(const StepCtx& c, hipStream_t s, hipEvent_t stop = nullptr);
+int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s);
+int rc_launch_fac_mix(const StepCtx& c, hipStream_t s);
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s);  // per-window cos-sim penalty values (rc_embed.hip)   // mixing, loss terms, output layer (MFMA path)
-int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s, hipEvent_t stop = nullptr);   // dW0 on the matrix cores + Adam (MFMA path)
+int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s);   // dW0 on the matrix cores + Adam (MFMA path)
 // GEMM-shaped embedder for large p*F (rc_embed_gemm.hip)
 bool rc_emb_use_gemm(const RedcliffDims& d);
 int rc_fac_slots(const RedcliffDims& d);  // rc_factor_mfma.hip
@@ -634,6 +634,8 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
+// the embedder backward and the factor update (RC_FB_UPDATE) in one launch (split-lead step on one stream)
+int rc_launch_emb_bwd_upd(const StepCtx& c, hipStream_t s);
 int rc_emb_tail_grid(const StepCtx& c);
 int rc_launch_emb_tail(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);

@@ -1216,7 +1216,7 @@ static int ms_occupancy(MsKern k, size_t lds) {
   return nb;
 }
 
-static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s, hipEvent_t stop) {
+static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
   static MsKern tf[16], tb[16];
   static const bool init = (MsTab<16>::fill(tf, tb), true);
   (void)init;
@@ -1259,62 +1259,42 @@ static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s, hipEvent_t stop)
     if (e) return e;
   }
   const char* xe = getenv("REDCLIFF_S16_XCD");  // read per launch (A/B); default on
-  const dim3 grid((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep);
-  if (stop)
-    hipExtLaunchKernelGGL(k, grid, dim3(RC_BLOCK), lds, s, nullptr, stop, 0, c, bpw, (int)!(xe && xe[0] == '0'));
-  else
-    hipLaunchKernelGGL(k, grid, dim3(RC_BLOCK), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
+  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), what);
 }
 
-int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s, hipEvent_t stop) {
+int rc_launch_fac_fwd_mfma(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (c.fslots != rc_fac_slots(d)) { rc_set_error("factor forward: slot layout changed within a step"); return REDCLIFF_EINVAL; }
-  if (rc_fac_short(d)) return ms_launch(false, c, s, stop);
+  if (rc_fac_short(d)) return ms_launch(false, c, s);
   const int KP = d.K * d.p;
   const int nxw = (c.B * rc_qpad(d) + XW_PER * RC_BLOCK - 1) / (XW_PER * RC_BLOCK);
   hipLaunchKernelGGL(k_xwin, dim3(nxw, c.nrep), dim3(RC_BLOCK), 0, s, c);
   int e = rc_check(hipGetLastError(), "k_xwin");
   if (e) return e;
   const int NB = KP * ((d.h + 31) / 32);
-  const dim3 grid((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, c.nrep);
-  if (stop)
-    hipExtLaunchKernelGGL(k_fac_fwd_mfma, grid, dim3(RC_BLOCK), 0, s, nullptr, stop, 0, c);
-  else
-    hipLaunchKernelGGL(k_fac_fwd_mfma, grid, dim3(RC_BLOCK), 0, s, c);
+  hipLaunchKernelGGL(k_fac_fwd_mfma, dim3((NB + 1) / 2, (c.B + MF_BT - 1) / MF_BT, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_fwd_mfma");
 }
 
-int rc_launch_fac_mix(const StepCtx& c, hipStream_t s, hipEvent_t stop) {
+int rc_launch_fac_mix(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   const int KP = d.K * d.p;
   const size_t lds = fac_mix_lds(d, c.Ls);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor mixing: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   const char* xe = getenv("REDCLIFF_MIX_XCD");  // read per launch (A/B); default on
-  if (stop)
-    hipExtLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, nullptr, stop, 0, c, (int)!(xe && xe[0] == '0'));
-  else
-    hipLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c, (int)!(xe && xe[0] == '0'));
+  hipLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), "k_fac_mix");
 }
 
-int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s, hipEvent_t stop) {
+int rc_launch_fac_dw0(const StepCtx& c, hipStream_t s) {
   const RedcliffDims& d = c.d;
   if (!(c.flags & RC_STEP_B)) return 0;
   const int NB = d.K * d.p * ((d.h + 31) / 32), Q = d.p * d.L;
-  if (rc_fac_short(d)) return ms_launch(true, c, s, stop);
-  if (Q <= 64) {  // short contraction rows: four column blocks share one 64-column X tile
-    const dim3 grid((NB + 3) / 4, 1, c.nrep);
-    if (stop)
-      hipExtLaunchKernelGGL(k_fac_bwd_mfma<4>, grid, dim3(RC_BLOCK), 0, s, nullptr, stop, 0, c);
-    else
-      hipLaunchKernelGGL(k_fac_bwd_mfma<4>, grid, dim3(RC_BLOCK), 0, s, c);
-  } else {
-    const dim3 grid((NB + 1) / 2, (Q + 127) / 128, c.nrep);
-    if (stop)
-      hipExtLaunchKernelGGL(k_fac_bwd_mfma<2>, grid, dim3(RC_BLOCK), 0, s, nullptr, stop, 0, c);
-    else
-      hipLaunchKernelGGL(k_fac_bwd_mfma<2>, grid, dim3(RC_BLOCK), 0, s, c);
-  }
+  if (rc_fac_short(d)) return ms_launch(true, c, s);
+  if (Q <= 64)  // short contraction rows: four column blocks share one 64-column X tile
+    hipLaunchKernelGGL(k_fac_bwd_mfma<4>, dim3((NB + 3) / 4, 1, c.nrep), dim3(RC_BLOCK), 0, s, c);
+  else
+    hipLaunchKernelGGL(k_fac_bwd_mfma<2>, dim3((NB + 1) / 2, (Q + 127) / 128, c.nrep), dim3(RC_BLOCK), 0, s, c);
   return rc_check(hipGetLastError(), "k_fac_bwd_mfma");
 }
