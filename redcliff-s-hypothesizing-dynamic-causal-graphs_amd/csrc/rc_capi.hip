@@ -383,16 +383,12 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   // (tests/test_gpu_forked.py).  REDCLIFF_EXT_EVENT=0 records the events as packets (read per step).
   const char* xev = getenv("REDCLIFF_EXT_EVENT");
   const bool ext_ev = !xev || strcmp(xev, "0") != 0;
-  // REDCLIFF_SPLIT_ONE=1 (tuning knob, read per step): the split-lead step on ONE stream -- the lead
-  // launch, then the embedder backward and the factor update in one launch (k_emb_bwd_upd)
-  const char* sov = getenv("REDCLIFF_SPLIT_ONE");
-  const bool split_one = split && sov && strcmp(sov, "0") != 0 && rc_emb_wpb(c.d) <= rc_emb_bc(c.d);
-  if (split && !split_one && ext_ev && (e = aux_stream(&aux))) return e;
+  if (split && ext_ev && (e = aux_stream(&aux))) return e;
   // forward: the fused launch runs the embedder and (vector path, no fork) the factor networks
   if (egemm) {
     if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd_gemm(c, s); }))) return e;
   } else if ((e = timed(KT_EMB_FWD, s, [&] {
-               return rc_launch_forward(c, s, true, fac && !mfma && !fork, split && !split_one && ext_ev ? aux->ev[1] : nullptr);
+               return rc_launch_forward(c, s, true, fac && !mfma && !fork, split && ext_ev ? aux->ev[1] : nullptr);
              }))) {
     return e;
   }
@@ -407,9 +403,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     if ((e = stream_wait(sf, s, aux->ev[0]))) return e;  // dW0 needs the mixing's dL/dy
     if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_dw0(c, sf); }))) return e;
   }
-  if (split_one) {
-    if ((e = timed(KT_FAC_LEAD, s, [&] { return rc_launch_fac_bwd(c, s, RC_FB_RECORDS); }))) return e;
-  } else if (split) {
+  if (split) {
     if ((e = aux_stream(&aux))) return e;
     sf = aux->s;
     if (ext_ev) {  // the forward completed ev[1] itself
@@ -459,14 +453,13 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     const char* dv = getenv("REDCLIFF_DEFER");
     c.defer = dv ? atoi(dv) : 1;
     if (c.defer < 0 || c.defer > 2) c.defer = 1;
-    if ((e = timed(KT_EMB_BWD, s, [&] { return split_one ? rc_launch_emb_bwd_upd(c, s) : rc_launch_emb_bwd(c, s, true); })))
-      return e;
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
     tail = tail_ok();
     if (c.defer == 1 && !tail && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {
     if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, false); }))) return e;
   }
-  if (split && !split_one) {  // join before A changes
+  if (split) {  // join before A changes
     if (ext_ev)
       e = rc_check(hipStreamWaitEvent(s, aux->ev[0], 0), "hipStreamWaitEvent");
     else

@@ -634,8 +634,6 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs);
 int rc_launch_emb_final(const StepCtx& c, hipStream_t s);
-// the embedder backward and the factor update (RC_FB_UPDATE) in one launch (split-lead step on one stream)
-int rc_launch_emb_bwd_upd(const StepCtx& c, hipStream_t s);
 int rc_emb_tail_grid(const StepCtx& c);
 int rc_launch_emb_tail(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);

@@ -906,44 +906,6 @@ void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   }
 }
 
-// Split-lead step on ONE stream (REDCLIFF_SPLIT_ONE): after the lead launch (the K*p networks'
-// dL/dw / dL/dA records), the embedder backward's workgroups (exactly k_emb_bwd<false>'s) and the
-// factor update's (every (network, chunk, column tile) workgroup in role RC_FB_UPDATE, exactly
-// k_fac_bwd's) share one grid, so the update runs beside the embedder backward without a second
-// stream and its fork / join hand-offs.  Embedder workgroups first (the critical chain).  Same
-// workgroup arithmetic as the two launches: the same bits.  RC_EMB_UPD_WAVES: the waves per SIMD
-// the registers must allow (the update's body alone takes 216 VGPRs, the embedder's 137).
-#ifndef RC_EMB_UPD_WAVES
-#define RC_EMB_UPD_WAVES 3
-#endif
-__global__ __launch_bounds__(RC_BLOCK) __attribute__((amdgpu_waves_per_eu(RC_EMB_UPD_WAVES)))
-void k_emb_bwd_upd(StepCtx c, int nnode, int head, int nred, int BC, int WPB, int nUl, int nQ) {
-  extern __shared__ float sm[];
-  const int r = rc_rep(c, blockIdx.y);
-  const int nemb = nnode + head + nred;
-  const int bx = blockIdx.x;
-  if (bx < nemb) {
-    const int nch = rc_nchunk(c.d);
-    const int nbw = (c.B + WPB - 1) / WPB;
-    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
-    RC_PHASE(c.ws, c.wo.total, bx, 32);
-    if (bx >= nnode + head) {
-      emb_bwd_dadj(c, r, bx - nnode - head);
-    } else if (bx == nnode) {
-      emb_bwd_head(c, r, sm);
-      RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
-    } else {
-      const int grp = bx / nbw, wb = bx - grp * nbw;
-      emb_bwd_node<false, true>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
-    }
-    return;
-  }
-  const int f = bx - nemb, per = nUl * nQ;
-  const int kj = f / per, rem = f - kj * per;
-  const int uc = rem / nQ, qc = rem - uc * nQ;
-  fac_bwd_wg(c, nUl, nQ, kj, uc, qc, r, sm, nullptr, RC_FB_UPDATE);
-}
-
 // Merged backward launch (vector factor path + fused embedder, training steps without loss
 // values): the factor backward and the embedder backward in ONE grid instead of two dependent
 // launches.  The embedder backward needs only the factor-side dL/dw partials and the
@@ -1746,25 +1708,6 @@ int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_bwd_merged<false>, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, nnode, head, nred, BC, WPB);
   }
   return rc_check(hipGetLastError(), "k_bwd_merged");
-}
-
-int rc_launch_emb_bwd_upd(const StepCtx& c, hipStream_t s) {
-  const RedcliffDims& d = c.d;
-  const int BC = rc_emb_bc(d), WPB = rc_emb_wpb(d);
-  if (WPB > BC || !(c.flags & RC_STEP_B)) { rc_set_error("embedder backward + factor update: single-sub-block embedder and a factor step required"); return REDCLIFF_EINVAL; }
-  const size_t le = rc_emb_bwd_lds(d, true), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
-  const size_t lds = le > lf ? le : lf;
-  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder backward + factor update: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  const int nnode = d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB);
-  const int head = (c.flags & (RC_VALUES | RC_CONFUSION)) ? 1 : 0;
-  const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
-  const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
-  const int Q = d.p * d.L, nQ = (Q + FB_QT - 1) / FB_QT, nUl = rc_nuchunk(d);
-  const int grid = nnode + head + nred + d.K * d.p * nUl * nQ;
-  int e = rc_lds_optin(k_emb_bwd_upd, lds, "k_emb_bwd_upd LDS");
-  if (e) return e;
-  hipLaunchKernelGGL(k_emb_bwd_upd, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, nnode, head, nred, BC, WPB, nUl, nQ);
-  return rc_check(hipGetLastError(), "k_emb_bwd_upd");
 }
 
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {

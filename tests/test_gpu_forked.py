@@ -114,13 +114,12 @@ def test_forked_pack_bitwise_equals_single_stream_pack(monkeypatch, guard_bands)
             np.testing.assert_array_equal(states["1"][r][k], want, err_msg="replica %d %s" % (r, k))
 
 
-def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", ext="1", one="0"):
+def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", ext="1"):
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
     monkeypatch.setenv("REDCLIFF_MERGE", merge)
     monkeypatch.setenv("REDCLIFF_SPLIT_LEAD", split)
     monkeypatch.setenv("REDCLIFF_TAIL", tail)
     monkeypatch.setenv("REDCLIFF_EXT_EVENT", ext)
-    monkeypatch.setenv("REDCLIFF_SPLIT_ONE", one)
     m = make(seed, 10.0, 0.1)
     oA, oB = opts(m, 5e-4, 2e-4)
     eng = m.engine()
@@ -131,7 +130,7 @@ def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", 
             m.batch_update(epoch, bi, Xb, Yb, oA, oB, 1)
     torch.cuda.synchronize()
     if guarded:
-        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s tail=%s ext=%s one=%s" % (merge, split, tail, ext, one))
+        check_bands(eng.ws, armed[0], armed[1], 1, "merge=%s split=%s tail=%s ext=%s" % (merge, split, tail, ext))
     return {k: t.detach().cpu().numpy() for k, t in m.state_dict().items()}
 
 
@@ -173,20 +172,6 @@ def test_kernel_completed_events_bitwise(monkeypatch, guard_bands):
     want = run_vector(monkeypatch, "0", train, True, split="1", ext="0")
     got = run_vector(monkeypatch, "0", train, True, split="1", ext="1")
     again = run_vector(monkeypatch, "0", train, False, split="1", ext="1")
-    for k, w in want.items():
-        np.testing.assert_array_equal(got[k], w, err_msg=k)
-        np.testing.assert_array_equal(again[k], w, err_msg=k)
-
-
-def test_split_lead_on_one_stream_bitwise(monkeypatch, guard_bands):
-    """The split-lead step on one stream (REDCLIFF_SPLIT_ONE: the lead launch, then k_emb_bwd_upd --
-    the embedder backward's and the factor update's workgroups in one grid) against the two-stream
-    split-lead step: bit for bit through pretrain -> acclimate -> combined, ragged last batch, guard
-    bands intact, a second run repeating the first."""
-    train = data(64 * 2 + 24, seed=19)
-    want = run_vector(monkeypatch, "0", train, True, split="1")
-    got = run_vector(monkeypatch, "0", train, True, split="1", one="1")
-    again = run_vector(monkeypatch, "0", train, False, split="1", one="1")
     for k, w in want.items():
         np.testing.assert_array_equal(got[k], w, err_msg=k)
         np.testing.assert_array_equal(again[k], w, err_msg=k)
