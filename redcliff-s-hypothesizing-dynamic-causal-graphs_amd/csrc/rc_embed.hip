@@ -1537,8 +1537,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
 // dispatch order and the whole grid is resident (rc_emb_tail_grid), as in k_bwd_merged; a wait
 // that runs out of polls counts into the status word.  Same sums, same order: the same bits as
 // the two launches (tests/test_gpu_forked.py).  grid (1 + ncomb + nw, R).
+#ifndef TAIL_CE
 #define TAIL_CE 1   // combine elements per thread in k_emb_tail (4: the grid fits C1(K=4) / TST but is slower)
+#endif
+#ifndef TAIL_EPT
 #define TAIL_EPT 1  // parameter elements per thread in k_emb_tail (2: slower, r03_emb_tail_variants.jsonl)
+#endif
 template <int NR>
 __global__ __launch_bounds__(RC_BLOCK) void k_emb_tail(StepCtx c, int ncx, int nw) {
   rc_critical_priority();
