@@ -728,6 +728,7 @@ def mode_fit(args, dev, rank, world, dist, holder):
                "updates": dsteps, "windows_per_s": round(dsteps * args.dp_leg_batch / del_, 1),
                "ms_per_update": round(1e3 * del_ / dsteps, 4), "scaling": "strong",
                "allreduce_floats_per_update": int(dpo.PA + dpo.PB),
+               "resident_windows_per_rank": getattr(dpo, "resident_windows", None),
                "workload": CONFIGS["c4"]["workload"].replace("B=128", "global B=%d" % args.dp_leg_batch)}
 
     if rank != 0:
@@ -763,9 +764,10 @@ def dp_throughput(B, steps, warmup, dev, dist, group=None):
     model = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).to(dev)
     oA, oB = adam_pair(model, c)
     nbatch = 16
-    X, Y = synth(c, nbatch * B, seed=100)  # every rank holds the whole (identical) data set
+    X, Y = synth(c, nbatch * B, seed=100)  # every rank generates the same host data set
     dp = DataParallelFit(model, oA, oB, group=group)
-    ds = dp.cache_dataset([(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)])
+    ds = dp.cache_dataset([(X[i:i + B], Y[i:i + B]) for i in range(0, X.shape[0], B)])  # the rank's shards only
+    dp.resident_windows = int(ds["X"].shape[0])
 
     def run(n, start):
         return lambda: dp.run_steps("combined", ds, [(start + i) % nbatch for i in range(n)])

@@ -3,16 +3,17 @@
 The reference fits one model per process (no torch.distributed anywhere).  For the LFP
 recordings (TST, many windows per subject) one fit is spread over the GPUs of a node:
 
-  * every rank holds the whole (device-resident) training set and the same model
-    (parameters broadcast from rank 0 at construction);
+  * every rank holds the same model (parameters broadcast from rank 0 at construction) and, in
+    device memory, only the windows of its own shards of the training set (cache_dataset streams
+    each global batch through once: its BatchNorm statistics, then the rank's rows);
   * each global batch of B windows is split into world_size contiguous shards; rank g runs
     the fused step on its shard in gradient-only mode (RC_GRAD_ONLY) with B_global = B, so
     batch-mean terms (forecast MSE :629, factor MSE :638-661) are scaled by 1/B and batch
     sums (fw-L1 :666, adj-L1 :696-715) are not: the shard gradients sum to the full-batch
     gradient.  The cos-sim penalty carries no gradient (metrics.py:380);
-  * BatchNorm uses the statistics of the GLOBAL batch (precomputed from the data, which
-    every rank has), so no SyncBN collective is needed and the running statistics advance
-    identically on every rank;
+  * BatchNorm uses the statistics of the GLOBAL batch (computed once per batch from the whole
+    batch, which every rank's loader yields, by the same kernel as the single fit's), so no SyncBN
+    collective is needed and the running statistics advance identically on every rank;
   * one all-reduce (sum) of one flat fp32 gradient buffer per update (embedder + factor
     groups, 0.4-0.9 MB at the published configs) over RCCL / xGMI, then the replicated Adam
     update of both groups in one launch (redcliff_dp_update, which also refreshes the DGCNN
@@ -29,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from . import _native as nat
-from .engine import _stream, flags_for, phase_of_epoch
+from .engine import _stream, flags_for, phase_of_epoch, select_labels
 from .kernels import ptr
 
 
@@ -74,8 +75,44 @@ class DataParallelFit:
             fused_update = os.environ.get("REDCLIFF_DP_FUSED", "1") != "0"
         self.fused_update = bool(fused_update)
 
-    def cache_dataset(self, loader):
-        return self.eng.cache_dataset(loader)
+    def cache_dataset(self, loader, sharded=None):
+        """The training set on the device.  sharded (default; REDCLIFF_DP_SHARDED=0 or
+        sharded=False keeps the whole set on every rank, the round-4 layout): each global batch of
+        the loader is uploaded once, its BatchNorm batch statistics are taken from the whole batch
+        (k_bn_stats, one workgroup per feature in a fixed order: the bits of the whole-set cache)
+        and only this rank's shard of it (shard_of) stays resident -- 1 / world of the windows."""
+        if sharded is None:
+            sharded = os.environ.get("REDCLIFF_DP_SHARDED", "1") != "0"
+        if not sharded:
+            return self.eng.cache_dataset(loader)
+        cache = self.__dict__.setdefault("_shard_cache", {})
+        if id(loader) in cache:
+            return cache[id(loader)]
+        eng = self.eng
+        xs, ls, sizes, local, stats = [], [], [], [], []
+        T = None
+        for bi, (X, Y) in enumerate(loader):
+            B = int(X.shape[0])
+            off, Bl = shard_of(B, self.world, self.rank)
+            if Bl < 1:
+                raise ValueError("batch %d has %d windows for %d ranks: every rank needs at least one window"
+                                 % (bi, B, self.world))
+            Xd = X.to(eng.device, torch.float32).contiguous()
+            T = int(Xd.shape[1])
+            stats.append(eng.bn_stats(eng.dims(1, T), Xd, B, B))
+            xs.append(Xd[off:off + Bl].clone())
+            lab = select_labels(Y, eng.K, eng.Lmax) if Y is not None else torch.zeros(B, eng.K)
+            ls.append(lab[off:off + Bl].to(eng.device, torch.float32))
+            sizes.append(B)
+            local.append(Bl)
+            del Xd
+        rows = np.cumsum([0] + local[:-1]).astype(np.int64)  # the rank's rows of each batch in its X
+        ds = {"X": torch.cat(xs, 0).contiguous(), "lab": torch.cat(ls, 0).contiguous(), "rows": rows,
+              "sizes": np.asarray(sizes, dtype=np.int32), "local_sizes": np.asarray(local, dtype=np.int32),
+              "stats": torch.cat(stats, 0).contiguous(), "T": T, "Bmax": max(sizes), "len": len(sizes),
+              "loader": loader, "sharded": True}
+        cache[id(loader)] = ds
+        return ds
 
     def _step(self, kind, ds, bi):
         eng = self.eng
@@ -89,7 +126,8 @@ class DataParallelFit:
         d = eng.workspace(-(-int(ds["Bmax"]) // self.world), ds["T"])  # the largest shard
         stats = ds["stats"][bi:bi + 1] if flags & nat.BN_TRAIN else None
         a = eng._args(d, flags | nat.GRAD_ONLY, nbn, ds["X"], ds["lab"], stats)
-        a.row0 = int(ds["rows"][bi]) + off
+        # the rank's rows: in its own shard cache, or at `off` inside the batch of a whole-set cache
+        a.row0 = int(ds["rows"][bi]) + (0 if ds.get("sharded") else off)
         a.B = Bl
         a.B_global = B
         a.grad_emb, a.grad_fac = ptr(self.gE), ptr(self.gF)

@@ -62,7 +62,7 @@ def _loader():
     return [(X[i:i + c["B"]], Y[i:i + c["B"]]) for i in range(0, c["N"], c["B"])]
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, sharded=True):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, PKG)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -73,7 +73,9 @@ def _worker(rank, world, port, outdir):
     from redcliff_amd import DataParallelFit
     m, oA, oB = _model()
     dp = DataParallelFit(m, oA, oB)
-    ds = dp.cache_dataset(_loader())
+    ds = dp.cache_dataset(_loader(), sharded=sharded)
+    if sharded:  # only this rank's windows are resident
+        assert ds["X"].shape[0] == int(ds["local_sizes"].sum()) < CFG["N"]
     for epoch in EPOCHS:
         dp.run_epoch(epoch, ds)
     conf = dp.train_confusion()
@@ -114,6 +116,24 @@ def test_two_rank_data_parallel_matches_full_batch(tmp_path):
         bad = np.abs(got - w) > tol
         assert not bad.any(), "%s: %d/%d off, max err %.3e" % (k, int(bad.sum()), w.size, np.abs(got - w).max())
     np.testing.assert_array_equal(r0["conf"].numpy(), conf)
+
+
+def test_sharded_cache_bitwise_equals_whole_set(tmp_path):
+    """DataParallelFit.cache_dataset keeps only the rank's shard windows resident (their rows
+    renumbered, the global batches' BatchNorm statistics taken from the whole batch by the same
+    kernel): both ranks end bit-identical to the run with the whole set on every rank."""
+    world = 2
+    for sharded in (True, False):
+        out = tmp_path / ("s%d" % int(sharded))
+        out.mkdir()
+        mp.start_processes(_worker, args=(world, _free_port(), str(out), sharded), nprocs=world,
+                           start_method="spawn", join=True)
+    for r in range(world):
+        a = torch.load(str(tmp_path / "s1" / ("rank%d.pt" % r)), weights_only=True)
+        b = torch.load(str(tmp_path / "s0" / ("rank%d.pt" % r)), weights_only=True)
+        for k in b["state"]:
+            np.testing.assert_array_equal(a["state"][k].numpy(), b["state"][k].numpy(), err_msg="rank %d %s" % (r, k))
+        np.testing.assert_array_equal(a["conf"].numpy(), b["conf"].numpy())
 
 
 def test_large_shard_takes_the_matrix_core_factor_path(monkeypatch):
