@@ -405,6 +405,40 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       t += __shfl_xor(t, 2);
       if (dg == 0 && i0 + ditem < nitem) dwl[i0 + ditem] = t;
     };
+    // the rounds after the first (nitem > 64: K > 4 at 16-window sub-blocks).  With p <= 16 four
+    // channel slots per lane cover every channel, so all the remaining rounds' loads are in flight
+    // together (one memory latency instead of one per round); same terms, same order, same sums
+    auto dw_rest = [&]() {
+      if (nitem <= RC_BLOCK / 4) return;
+      if (p <= 16 && nitem <= RC_BLOCK) {
+        float dr4[3][4];
+#pragma unroll
+        for (int rd = 0; rd < 3; ++rd) {
+          const int it2 = (rd + 1) * (RC_BLOCK / 4) + ditem, sw = dK.div(it2), kk = it2 - sw * K;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int j = dg + 4 * u;
+            const float* q = dwp + ((int64_t)j * d.Bmax + bw0 + sw) * K + kk;
+            dr4[rd][u] = (fac_grad && it2 < nitem && j < p) ? (wait_cnt ? rc_load_sc1(q) : *q) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int rd = 0; rd < 3; ++rd) {
+          const int it2 = (rd + 1) * (RC_BLOCK / 4) + ditem;
+          float t = 0.f;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) t += dr4[rd][u];
+          t += __shfl_xor(t, 1);
+          t += __shfl_xor(t, 2);
+          if (dg == 0 && it2 < nitem) dwl[it2] = t;
+        }
+      } else {
+        for (int i0 = RC_BLOCK / 4; i0 < nitem; i0 += RC_BLOCK / 4) {
+          dw_load(i0);
+          dw_store(i0);
+        }
+      }
+    };
     // merged launch: the factor-side partials come from the same launch's factor-lead workgroups;
     // stage everything else first, then wait for them
     const bool wait_now = wait_cnt != nullptr && it == 0;
@@ -432,10 +466,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
         dw_load(0);
       }
       dw_store(0);
-      for (int i0 = RC_BLOCK / 4; i0 < nitem; i0 += RC_BLOCK / 4) {
-        dw_load(i0);
-        dw_store(i0);
-      }
+      dw_rest();
       __syncthreads();
       if (tid < n) {
         float t = 0.f;
@@ -445,10 +476,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     } else {
       rc_stage_all(sR, sT, sX, sF1, sW, sL);
       dw_store(0);
-      for (int i0 = RC_BLOCK / 4; i0 < nitem; i0 += RC_BLOCK / 4) {
-        dw_load(i0);
-        dw_store(i0);
-      }
+      dw_rest();
       __syncthreads();
     }
   RC_PHASE(c.ws, c.wo.total, pbx, 34);

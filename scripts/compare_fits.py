@@ -37,7 +37,8 @@ def dump(path):
     import bench
     import redcliff_amd
     out = {}
-    for cfg in ("d4ic", "c1k4"):
+    # COMPARE_FITS_CFGS=d4ic,c1k4,c4: the configurations (c4: K = 9, p = 12)
+    for cfg in os.environ.get("COMPARE_FITS_CFGS", "d4ic,c1k4").split(","):
         c = dict(bench.CONFIGS[cfg])
         # COMPARE_FITS_R=8 or more: the packed (short-contraction matrix-core) factor kernels
         R, E = int(os.environ.get("COMPARE_FITS_R", "4")), 9
