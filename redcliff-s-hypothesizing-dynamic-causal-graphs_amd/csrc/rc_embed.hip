@@ -1024,23 +1024,42 @@ __device__ inline void lds_rowsum(int p, Fn f, Out out) {
 }
 
 // p x p product op(X) op(Y) on the matrix cores: wave w owns the 32x32 output tile
-// (w >> 1, w & 1); entries at or beyond p are zero padding.  out(a, b, v) receives each
-// in-range result (one writer per entry).
-template <bool TX, bool TY, class Out>
-__device__ inline void lds_mm(const float* X, const float* Y, int p, int P, Out out) {
+// (w >> 1, w & 1); entries at or beyond p are zero padding.  Returns false for a wave with no
+// tile; lane entry reg is row a0 + mf_row(reg, lane), column b0 + (lane & 31).
+template <bool TX, bool TY>
+__device__ inline bool lds_mm_tile(const float* X, const float* Y, int p, int P, f32x16& acc, int& a0, int& bj) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int a0 = 32 * (wv >> 1), b0 = 32 * (wv & 1);
-  if (a0 >= p || b0 >= p) return;
-  const int l31 = lane & 31, kh = lane >> 5, ai = a0 + l31, bj = b0 + l31;
-  f32x16 acc;
+  a0 = 32 * (wv >> 1);
+  const int b0 = 32 * (wv & 1);
+  if (a0 >= p || b0 >= p) return false;
+  const int l31 = lane & 31, kh = lane >> 5, ai = a0 + l31;
+  bj = b0 + l31;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  for (int k0 = 0; k0 < p; k0 += 2) {
-    const int k = k0 + kh;
-    const float x = (k < p && ai < p) ? (TX ? X[k * P + ai] : X[ai * P + k]) : 0.f;
-    const float y = (k < p && bj < p) ? (TY ? Y[bj * P + k] : Y[k * P + bj]) : 0.f;
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(x, y, acc, 0, 0, 0);
+  // four k steps' operands read before their products (one LDS round trip per four steps);
+  // the steps themselves are the k0 < p ones, in order
+  for (int k00 = 0; k00 < p; k00 += 8) {
+    float xs[4], ys[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k00 + 2 * u + kh;
+      xs[u] = (k < p && ai < p) ? (TX ? X[k * P + ai] : X[ai * P + k]) : 0.f;
+      ys[u] = (k < p && bj < p) ? (TY ? Y[bj * P + k] : Y[k * P + bj]) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (k00 + 2 * u < p) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[u], ys[u], acc, 0, 0, 0);
   }
+  return true;
+}
+
+// out(a, b, v) receives each in-range result (one writer per entry).
+template <bool TX, bool TY, class Out>
+__device__ inline void lds_mm(const float* X, const float* Y, int p, int P, Out out) {
+  f32x16 acc;
+  int a0, bj;
+  if (!lds_mm_tile<TX, TY>(X, Y, p, P, acc, a0, bj)) return;
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) {
     const int a = a0 + mf_row(reg, lane);
@@ -1048,10 +1067,35 @@ __device__ inline void lds_mm(const float* X, const float* Y, int p, int P, Out 
   }
 }
 
+// D[a][b] += (op(X) op(Y))[a][b] (D disjoint from X and Y, rows padded to P = p + 1): every old value is read before
+// any sum is written back, so the 16 read-modify-writes of a lane are not one LDS round trip
+// each; the sums are the per-entry ones (old + product)
+template <bool TX, bool TY>
+__device__ inline void lds_mm_acc(const float* X, const float* Y, int p, int P, float* D) {
+  f32x16 acc;
+  int a0, bj;
+  if (!lds_mm_tile<TX, TY>(X, Y, p, P, acc, a0, bj)) return;
+  // An entry outside p x p reads and writes its row's padding slot (column p, never read as an
+  // operand) instead of branching around the access: no exec-mask branch per entry, so the
+  // writes do not each wait for the previous one.
+  const int lane = threadIdx.x & 63;
+  const bool cin = bj < p;
+  int ad[16];
+  float old[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int a = a0 + mf_row(reg, lane);
+    ad[reg] = (cin && a < p) ? a * P + bj : min(a, p - 1) * P + p;
+    old[reg] = D[ad[reg]];
+  }
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) D[ad[reg]] = old[reg] + acc[reg];
+}
+
 // Supports of normalize_A(A) (S_0 = I, S_1 = L, S_l = S_{l-1} L): A padded in LDS, L and its
 // powers built in LDS slots 1..n-1 of Sl and written densely to S[n][p][p].  Used by the
 // optimizer's adjacency workgroup and by k_supports, so both produce the same bits.
-__device__ void supports_lds(const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
+__device__ __forceinline__ void supports_lds(const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
   const int P = p + 1, PP = p * P, pp2 = p * p;
   const RcDiv dpv(p);
   lds_rowsum(p, [&](int i, int j) { return fmaxf(Al[i * P + j], 0.f); },
@@ -1456,7 +1500,17 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
           if (fused || adj_inplace) {
             t = EmbWbSum(c, ws).nodes(cc * nch, 1, nch, ofs_s + (i - 1) * p + cp);
           } else {
-            for (int chk = 0; chk < c.dsN; ++chk) t += ws[c.wo.dS + cc * c.dsCC + chk * c.dsS + i * c.dsI + cp];
+            // eight records' loads in flight per round (a runtime-count loop waited for each load
+            // in turn: one memory latency per column chunk), added in record order
+            const float* q = ws + c.wo.dS + cc * c.dsCC + i * c.dsI + cp;
+            for (int c0 = 0; c0 < c.dsN; c0 += 8) {
+              float v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) v[u] = c0 + u < c.dsN ? q[(int64_t)(c0 + u) * c.dsS] : 0.f;
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                if (c0 + u < c.dsN) t += v[u];
+            }
           }
           return t;
         }, [&](int e, float v) { dSw[at(e)] = v; }),
@@ -1482,8 +1536,8 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
       float* dSprev = dSw + (l - 2) * PP;
       const float* Sprev = Sl + (l - 1) * PP;
       const float* Lm = Sl + PP;
-      lds_mm<false, true>(dSl, Lm, p, P, [&](int a, int b, float v) { dSprev[a * P + b] += v; });  // dS_l L^T
-      lds_mm<true, false>(Sprev, dSl, p, P, [&](int a, int b, float v) { dL[a * P + b] += v; });   // S_{l-1}^T dS_l
+      lds_mm_acc<false, true>(dSl, Lm, p, P, dSprev);  // dS_l L^T
+      lds_mm_acc<true, false>(Sprev, dSl, p, P, dL);   // S_{l-1}^T dS_l
       __syncthreads();
     }
     if (n >= 2) {
