@@ -26,26 +26,41 @@ namespace {
 
 // BatchNorm scale/shift exactly as torch's CPU kernel forms them
 // (batch_norm_cpu_collect_linear_and_constant_terms): y = x*alpha + beta.
-__device__ void bn_affine(const StepCtx& c, int r, const float* E, float* alpha, float* beta, float* mean_out,
-                          float* inv_out) {
+// BatchNorm affine of feature f (F <= 64 < RC_BLOCK: thread f): bn_affine_load requests the
+// operands, bn_affine_store forms alpha / beta (and the mean / invstd the backward needs) once
+// they are in -- split so that the node workgroup's staging loads go out in between.
+struct BnOperands {
+  double m, v;
+  float g, b;
+};
+__device__ inline void bn_affine_load(const StepCtx& c, int r, const float* E, int f, BnOperands& q) {
   const RedcliffDims& d = c.d;
-  const bool train = c.flags & RC_BN_TRAIN;
-  for (int f = threadIdx.x; f < d.F; f += blockDim.x) {
-    float mean, inv;
-    if (train) {
-      const double* st = c.bns + r * c.bnsr;
-      mean = (float)st[f];
-      inv = (float)(1.0 / sqrt(st[d.F + f] + c.hyp[r].bn_eps));
-    } else {
-      mean = c.rm[r * d.F + f];
-      inv = 1.0f / sqrtf(c.rv[r * d.F + f] + (float)c.hyp[r].bn_eps);
-    }
-    const float a = inv * E[c.eo.bnw + f];
-    alpha[f] = a;
-    beta[f] = E[c.eo.bnb + f] - mean * a;
-    if (mean_out) mean_out[f] = mean;
-    if (inv_out) inv_out[f] = inv;
+  if (c.flags & RC_BN_TRAIN) {
+    const double* st = c.bns + r * c.bnsr;
+    q.m = st[f];
+    q.v = st[d.F + f];
+  } else {
+    q.m = c.rm[r * d.F + f];
+    q.v = c.rv[r * d.F + f];
   }
+  q.g = E[c.eo.bnw + f];
+  q.b = E[c.eo.bnb + f];
+}
+__device__ inline void bn_affine_store(const StepCtx& c, int r, int f, const BnOperands& q, float* alpha, float* beta,
+                                       float* mean_out, float* inv_out) {
+  float mean, inv;
+  if (c.flags & RC_BN_TRAIN) {
+    mean = (float)q.m;
+    inv = (float)(1.0 / sqrt(q.v + c.hyp[r].bn_eps));
+  } else {
+    mean = (float)q.m;
+    inv = 1.0f / sqrtf((float)q.v + (float)c.hyp[r].bn_eps);
+  }
+  const float a = inv * q.g;
+  alpha[f] = a;
+  beta[f] = q.b - mean * a;
+  if (mean_out) mean_out[f] = mean;
+  if (inv_out) inv_out[f] = inv;
 }
 
 // dL/d(raw embedder output) of one window / factor: the factor-side gradient gw (sum of
@@ -324,7 +339,8 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const int pbx = wait_cnt ? (int)blockIdx.x - d.K * d.p : (int)blockIdx.x;
   (void)pbx;
   RC_PHASE(c.ws, c.wo.total, pbx, 33);
-  bn_affine(c, r, E, alpha, beta, mean, inv);
+  BnOperands bnq{0.0, 0.0, 0.f, 0.f};
+  if (tid < F) bn_affine_load(c, r, E, tid, bnq);  // stored after the first staging pass
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
   const float* f1 = ws + c.wo.f1;
@@ -460,6 +476,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
             return S[((int64_t)i * p + node) * p + cc];
           }, [&](int e, float v) { Srow[e] = v; }),
           sR, sT, sX, sF1, sW, sL);
+      if (tid < F) bn_affine_store(c, r, tid, bnq, alpha, beta, mean, inv);
       if (wait_now) {
         rc_wait_leads(c, c.ws + r * c.wss, wait_cnt, wait_target);
         RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_WAIT, 0);
@@ -1500,15 +1517,17 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
           if (fused || adj_inplace) {
             t = EmbWbSum(c, ws).nodes(cc * nch, 1, nch, ofs_s + (i - 1) * p + cp);
           } else {
-            // eight records' loads in flight per round (a runtime-count loop waited for each load
-            // in turn: one memory latency per column chunk), added in record order
+            // DSB records' loads in flight per round and staged element (a runtime-count loop
+            // waited for each load in turn: one memory latency per column chunk), added in record
+            // order; 32 / NR keeps the NR elements' loads within 32 registers
+            constexpr int DSB = NR <= 4 ? 8 : (32 / NR > 1 ? 32 / NR : 1);
             const float* q = ws + c.wo.dS + cc * c.dsCC + i * c.dsI + cp;
-            for (int c0 = 0; c0 < c.dsN; c0 += 8) {
-              float v[8];
+            for (int c0 = 0; c0 < c.dsN; c0 += DSB) {
+              float v[DSB];
 #pragma unroll
-              for (int u = 0; u < 8; ++u) v[u] = c0 + u < c.dsN ? q[(int64_t)(c0 + u) * c.dsS] : 0.f;
+              for (int u = 0; u < DSB; ++u) v[u] = c0 + u < c.dsN ? q[(int64_t)(c0 + u) * c.dsS] : 0.f;
 #pragma unroll
-              for (int u = 0; u < 8; ++u)
+              for (int u = 0; u < DSB; ++u)
                 if (c0 + u < c.dsN) t += v[u];
             }
           }

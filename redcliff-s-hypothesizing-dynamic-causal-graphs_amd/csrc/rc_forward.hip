@@ -276,9 +276,18 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
     if (tid == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler barrier only: the partial loads are sc1
     if (tid < M1) {
+      // the slice partials' loads in flight together, eight per round (a runtime-count loop waited
+      // for each load in turn), summed in slice order
       const float* part = ws + c.wo.f1p + (int64_t)b0 * M1 + tid;
-      float sum = rc_load_sc1(part);
-      for (int z = 1; z < Zs; ++z) sum = sum + rc_load_sc1(part + (int64_t)z * d.Bmax * M1);
+      float sum = 0.f;
+      for (int z0 = 0; z0 < Zs; z0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = z0 + u < Zs ? rc_load_sc1(part + (int64_t)(z0 + u) * d.Bmax * M1) : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < Zs) sum = z0 + u == 0 ? v[0] : sum + v[u];
+      }
       const float val = sum + fb1[tid];
       f1l[tid] = val;
       ws[c.wo.f1 + (int64_t)b0 * M1 + tid] = val;
