@@ -462,7 +462,8 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     __syncthreads();  // the previous sub-block is done with the LDS tiles
     if (it == 0) {
       rc_stage_all(
-          rc_seg<1>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
+          // (K M1 <= 1,024: one round; with one load per thread TST's 576 took three)
+          rc_seg<4>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
           rc_seg<4>(M1 * HC, [&](int e) {
             const int m = e / HC, hh = e - m * HC;
             return hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;

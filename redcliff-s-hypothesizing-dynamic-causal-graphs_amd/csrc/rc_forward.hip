@@ -90,9 +90,12 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
   }
   const float* S = ws + c.wo.S;
   const float* gw = E + c.eo.gcW;
+  // Loads per thread per segment sized so that the common shapes stage in ONE round (a second
+  // round is another memory latency on every workgroup's path): n p^2 <= 512 (C1(K=4) 300, TST 432),
+  // n F H <= 5,120 (4,800), K M1 <= 1,024 (TST 576)
   rc_stage_all(
-      rc_seg<1>(n * p * p, [&](int e) { return S[e]; }, [&](int e, float v) { Sl[e] = v; }),
-      rc_seg<8>(w_lds ? nFH : 0, [&](int e) { return gw[e]; }, [&](int e, float v) { Wl[e] = v; }),
+      rc_seg<2>(n * p * p, [&](int e) { return S[e]; }, [&](int e, float v) { Sl[e] = v; }),
+      rc_seg<20>(w_lds ? nFH : 0, [&](int e) { return gw[e]; }, [&](int e, float v) { Wl[e] = v; }),
       // window rows are contiguous in the channel index: read (s, f, ch), store [s][ch][f]
       rc_seg<4>(nb * pF, [&](int e) {
         const int s = dpF.div(e), rem = e - s * pF;
@@ -101,7 +104,7 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
         const int s = dpF.div(e), rem = e - s * pF, f = dp.div(rem), ch = rem - f * p;
         xs[s * pF + ch * F + f] = v;
       }),
-      rc_seg<2>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
+      rc_seg<4>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
       rc_seg<1>(M1 + K, [&](int e) { return e < M1 ? E[c.eo.fc1b + e] : E[c.eo.fc2b + e - M1]; },
                 [&](int e, float v) { fb1[e] = v; }));  // fb2 follows fb1
   RC_PHASE(c.ws, c.wo.total, bx, 2);
