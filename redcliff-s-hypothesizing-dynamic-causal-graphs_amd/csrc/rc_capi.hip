@@ -304,6 +304,7 @@ static int make_ctx(const RedcliffStepArgs* a, StepCtx& c) {
   c.wo = wo;
   rc_emb_partial_layout(c, rc_emb_use_gemm(d));
   c.fslots = rc_fac_slots(d);
+  rc_ctx_magics(c);
   return 0;
 }
 

@@ -235,6 +235,13 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
 #define ACC_BATCHES 7
 
 // Everything a step kernel needs, passed by value.
+// StepCtx::mg slots: F, p, p F, n F, K, M1, H, L, B, n p F, p H, and per fc1 slice width of the
+// embedder forward (cw channels: the regular width cs and the last slice's): cw F, n cw F, cw H
+enum {
+  RC_MG_F, RC_MG_P, RC_MG_PF, RC_MG_NF, RC_MG_K, RC_MG_M1, RC_MG_H, RC_MG_L, RC_MG_B, RC_MG_NPF, RC_MG_PH,
+  RC_MG_CS, RC_MG_CSF, RC_MG_NCSF, RC_MG_CSH, RC_MG_LS, RC_MG_LSF, RC_MG_NLSF, RC_MG_LSH, RC_MG_N
+};
+
 struct StepCtx {
   RedcliffDims d;
   int B, Lmax, Ls, flags, nbn;
@@ -272,6 +279,8 @@ struct StepCtx {
   // producer than exists, with a short poll bound -- forces the timeout path (tests)
   int wait_dbg;
   uint8_t rmap[RC_MAX_ACTIVE];
+  // RcDiv multipliers of the dimensions the hot kernels divide by (rc_ctx_magics; RC_MG_*)
+  unsigned long long mg[RC_MG_N];
 };
 
 __host__ __device__ inline int rc_rep(const StepCtx& c, int i) { return c.rident ? i : (int)c.rmap[i]; }
@@ -404,10 +413,19 @@ __device__ inline void rc_xcd_order(int nx, int nz, int& x, int& z) {
   z = (L & 7) + 8 * q;
 }
 
+// ceil(2^40 / d) for d > 1 (0 for d <= 1): RcDiv's multiplier
+__host__ __device__ inline unsigned long long rc_magic40(long long d) {
+  return d > 1 ? ((1ull << 40) + (unsigned long long)d - 1) / (unsigned long long)d : 0ull;
+}
+
 struct RcDiv {
   unsigned long long m;
   int d;
-  __device__ inline explicit RcDiv(int dd) : m(dd > 1 ? ((1ull << 40) + (unsigned long long)dd - 1) / (unsigned)dd : 0ull), d(dd) {}
+  // On the device the 64-bit integer division expands to ~150 dependent scalar instructions:
+  // with six divisors that is ~2 us of a kernel prologue (k_emb_bwd's node workgroups, phase trace).
+  // The hot kernels take the multipliers the host computed (StepCtx::mg, RcDiv(d, m)).
+  __device__ inline explicit RcDiv(int dd) : m(rc_magic40(dd)), d(dd) {}
+  __device__ inline RcDiv(int dd, unsigned long long mm) : m(mm), d(dd) {}
   __device__ inline int div(int n) const {
     return d == 1 ? n : (int)(((unsigned long long)(unsigned)n * m) >> 40);
   }
@@ -600,6 +618,8 @@ inline int rc_lds_optin(Kern k, size_t bytes, const char* what) {
 // stop (optional): an event the launch itself completes (hipExtLaunchKernel), so a second stream can
 // wait for this kernel without an event-record packet between it and the next kernel of `s`
 int rc_launch_forward(const StepCtx& c, hipStream_t s, bool with_emb, bool with_fac, hipEvent_t stop = nullptr);
+// fills StepCtx::mg from c.d and c.B (every StepCtx builder calls it last)
+void rc_ctx_magics(StepCtx& c);
 int rc_launch_fac_fwd(const StepCtx& c, hipStream_t s);
 // factor backward roles (rc_fac_bwd.h fac_bwd_wg): one launch, or the split-lead pair
 enum { RC_FB_ALL = 0, RC_FB_RECORDS = 1, RC_FB_UPDATE = 2 };

@@ -334,7 +334,8 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const bool late_x = LATE && rc_emb_late_x(d);
   float* xc = late_x ? f1r : dTc + BC * nF;  // [BC][p][F] raw window (late: over f1r .. Tc)
 
-  const RcDiv dF(F), dp(p), dpF(pF), dnF(nF), dK(K), dM1(M1);
+  const RcDiv dF(F, c.mg[RC_MG_F]), dp(p, c.mg[RC_MG_P]), dpF(pF, c.mg[RC_MG_PF]), dnF(nF, c.mg[RC_MG_NF]),
+      dK(K, c.mg[RC_MG_K]), dM1(M1, c.mg[RC_MG_M1]);
   // trace builds: the node workgroup's own index (inside the merged launch the factor leads come first)
   const int pbx = wait_cnt ? (int)blockIdx.x - d.K * d.p : (int)blockIdx.x;
   (void)pbx;
@@ -1472,7 +1473,7 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
   const int tid = threadIdx.x;
   extern __shared__ float sm[];
   const int pp2 = p * p, P = p + 1, PP = p * P;
-  const RcDiv dpv(p);
+  const RcDiv dpv(p, c.mg[RC_MG_P]);
   float* Al = sm;                  // A (pre-update, then the updated A)
   float* Ar = Al + PP;             // relu(A)
   float* dL = Ar + PP;             // dL/dL (the normalised Laplacian)

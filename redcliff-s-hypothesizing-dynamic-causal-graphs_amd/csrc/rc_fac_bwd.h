@@ -76,7 +76,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const int tid = threadIdx.x;
   const int B = c.B;
-  const RcDiv dL(d.L), dB(B);
+  const RcDiv dL(d.L, c.mg[RC_MG_L]), dB(B, c.mg[RC_MG_B]);
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const bool fgrad = (c.flags & RC_STEP_B) || (c.flags & RC_STEP_A);
@@ -179,11 +179,11 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   // and are not added): a guarded load is a branch, and a sum between branches waits for its
   // loads before the next element's are issued -- one memory round per element otherwise.
   rc_stage_all(
-      rc_seg<4>(B * K, [&](int e) { return ws[c.wo.w + e]; }, [&](int e, float v) { wrl[e] = v; }),
+      rc_seg<8>(B * K, [&](int e) { return ws[c.wo.w + e]; }, [&](int e, float v) { wrl[e] = v; }),
       rc_seg<1>(tgt ? B : 0, [&](int b) { return X[((c.row0 + b) * d.T + c.Lmax) * p + j]; },
                 [&](int b, float v) { xt[b] = v; }),
       rc_seg<1>(p, [&](int cc) { return E[c.eo.A + cc * p + j]; }, [&](int cc, float v) { Acol[cc] = v; }),
-      rc_seg<4>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order); e = kk * B + b
+      rc_seg<8>(B * K, [&](int e) {  // sum of the nU hidden-chunk partials (fixed order); e = kk * B + b
         const int kk = dB.div(e), b = e - kk * B;
         const float* yp = ws + c.wo.y + rc_y_idx(d, 0, kk * p + j, b);
         float v[8];

@@ -139,6 +139,7 @@ extern "C" int redcliff_factor_forward(const RedcliffDims* d, int32_t B, const f
   c.wo.G0 = c.wo.G + kp * d->p * d->L;
   c.wo.w1 = c.wo.G0 + kp * d->p;
   c.wo.gq = c.wo.w1 + kp * d->h;
+  rc_ctx_magics(c);
   int rc = rc_launch_fac_fwd(c, (hipStream_t)stream);
   if (rc) return rc;
   const int64_t n = kp * B;

@@ -50,7 +50,7 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
   RC_PHASE(c.ws, c.wo.total, bx, 0);
   const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
   const int pF = p * F, pH = p * H, nFH = n * F * H;
-  const RcDiv dF(F), dp(p), dpF(pF), dH(H);
+  const RcDiv dF(F, c.mg[RC_MG_F]), dp(p, c.mg[RC_MG_P]), dpF(pF, c.mg[RC_MG_PF]), dH(H, c.mg[RC_MG_H]);
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -126,7 +126,12 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
   RC_PHASE(c.ws, c.wo.total, bx, 3);
   // Chebyshev filtering T_i = S_i x_bn (T_0 = x_bn exactly, as matmul(eye, x)), rows [ch0, ch1)
   const int cF = (ch1 - ch0) * F, cH = (ch1 - ch0) * H;
-  const RcDiv dcF(cF), dncF(n * cF), dcH(cH);
+  // the slice width's multipliers (host-computed for the regular, the last and the whole width)
+  const int cw = ch1 - ch0;
+  const int mb = cw == (int)c.mg[RC_MG_CS] ? RC_MG_CSF : (cw == (int)c.mg[RC_MG_LS] ? RC_MG_LSF : -1);
+  const RcDiv dcF = mb >= 0 ? RcDiv(cF, c.mg[mb]) : (cw == p ? RcDiv(cF, c.mg[RC_MG_PF]) : RcDiv(cF));
+  const RcDiv dncF = mb >= 0 ? RcDiv(n * cF, c.mg[mb + 1]) : (cw == p ? RcDiv(n * cF, c.mg[RC_MG_NPF]) : RcDiv(n * cF));
+  const RcDiv dcH = mb >= 0 ? RcDiv(cH, c.mg[mb + 2]) : (cw == p ? RcDiv(cH, c.mg[RC_MG_PH]) : RcDiv(cH));
   for (int e = tid; e < nb * n * cF; e += RC_BLOCK) {
     const int s = dncF.div(e), rs = e - s * n * cF, i = dcF.div(rs), qs = rs - i * cF;
     const int q = ch0 * F + qs, rem = i * pF + q, ch = dF.div(q), f = q - ch * F;
@@ -460,6 +465,18 @@ int rc_emb_fwd_slice_channels(const RedcliffDims& d) {
   const int cmin = (d.p + 63) / 64;  // at most 64 slices (the partial region's slots)
   if (cs < cmin) cs = cmin;
   return cs < d.p ? cs : d.p;
+}
+
+void rc_ctx_magics(StepCtx& c) {
+  const RedcliffDims& d = c.d;
+  const int cs = rc_emb_fwd_slice_channels(d), Zs = (d.p + cs - 1) / cs, ls = d.p - (Zs - 1) * cs;
+  const long long v[RC_MG_N] = {d.F, d.p, (long long)d.p * d.F, (long long)d.n * d.F, d.K, d.M1, d.H, d.L, c.B,
+                                (long long)d.n * d.p * d.F, (long long)d.p * d.H,
+                                0, (long long)cs * d.F, (long long)d.n * cs * d.F, (long long)cs * d.H,
+                                0, (long long)ls * d.F, (long long)d.n * ls * d.F, (long long)ls * d.H};
+  for (int i = 0; i < RC_MG_N; ++i) c.mg[i] = rc_magic40(v[i]);
+  c.mg[RC_MG_CS] = (unsigned long long)cs;  // the widths themselves (the slice's width picks its slots)
+  c.mg[RC_MG_LS] = (unsigned long long)ls;
 }
 
 // One launch of the embedder forward (with_emb) and / or the vector-path factor forward (with_fac).
