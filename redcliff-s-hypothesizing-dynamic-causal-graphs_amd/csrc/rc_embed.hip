@@ -1551,6 +1551,12 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
                [&](int i, float s) { dinv[i] = 1.f / sqrtf(s + 1e-10f); });
     __syncthreads();
     RC_PHASE(c.ws, c.wo.total, wx, 51);
+#ifdef RC_ADJ_TWICE
+    // timing experiment (trace builds, wrong results): the products below run twice, marks 55 / 56
+    // after each pass -- a second pass much faster than the first means instruction fetch, not the
+    // arithmetic, sets the phase's length
+    for (int rep = 0; rep < 2; ++rep) {
+#endif
     // back through S_l = S_{l-1} L, l = n-1 .. 2
     for (int l = n - 1; l >= 2; --l) {
       const float* dSl = dSw + (l - 1) * PP;
@@ -1568,6 +1574,10 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
       }
       __syncthreads();
     }
+#ifdef RC_ADJ_TWICE
+    RC_PHASE(c.ws, c.wo.total, wx, 55 + rep);
+    }
+#endif
     RC_PHASE(c.ws, c.wo.total, wx, 52);
     // normalize_A backward: L[i][j] = dinv_i relu(A)[i][j] dinv_j, dinv_i = (sum_j relu(A)[i][j] + 1e-10)^-1/2,
     // d(dinv)/d(sum) = -1/2 (sum + 1e-10)^-3/2
@@ -1597,6 +1607,11 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
     // supports of the updated A for the next step (after a gradient-only shard step A changes
     // later, in redcliff_adam_apply, and the host refreshes them)
     if (adam) supports_lds(Al, Sl, ws + c.wo.S, dinv, p, n);
+#ifdef RC_ADJ_TWICE
+    RC_PHASE(c.ws, c.wo.total, wx, 57);
+    if (adam) supports_lds(Al, Sl, ws + c.wo.S, dinv, p, n);  // (same values again)
+    RC_PHASE(c.ws, c.wo.total, wx, 58);
+#endif
   }
   RC_PHASE(c.ws, c.wo.total, wx, 54);
   // BatchNorm running statistics (torch: double math, momentum*stat + (1-momentum)*running)

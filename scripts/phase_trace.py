@@ -24,7 +24,8 @@ def main():
     from redcliff_amd import build as b
     from redcliff_amd import _native
     assert _native._LIB is None
-    _native.LIB_PATH = b.build(trace=True)
+    # REDCLIFF_TRACE_LIB: a prebuilt trace variant (scripts/build_tree.sh <name> -DRC_TRACE ...)
+    _native.LIB_PATH = os.environ.get("REDCLIFF_TRACE_LIB") or b.build(trace=True)
     import numpy as np
     import torch
     import bench
@@ -56,6 +57,9 @@ def main():
         idx = [i for i in range(hi - lo) if t[i] > 0]
         if len(idx) > 1:
             print(label + ": " + "  ".join("%d->%d %.2f" % (lo + a, lo + b, (t[b] - t[a]) / 100.0) for a, b in zip(idx, idx[1:])))
+    if ph[48] > 0:  # the adjacency workgroup's marks in slot order, us after mark 48
+        print("emb_final adjacency WG marks (us after 48): " +
+              "  ".join("%d %.2f" % (i, (ph[i] - ph[48]) / 100.0) for i in range(48, 64) if ph[i] > 0))
     upd = [(i, (ph[i] - t_first) / 100.0) for i in range(19, 24) if ph[i] > 0]
     if upd:  # the (network 0, chunk 1) factor workgroup's update part (rc_fac_bwd.h, trace builds)
         print("factor update WG (network 0, chunk 1) phases at: " + "  ".join("%d %.2f us" % x for x in upd))
