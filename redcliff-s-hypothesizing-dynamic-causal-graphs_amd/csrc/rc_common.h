@@ -239,7 +239,8 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
 // embedder forward (cw channels: the regular width cs and the last slice's): cw F, n cw F, cw H
 enum {
   RC_MG_F, RC_MG_P, RC_MG_PF, RC_MG_NF, RC_MG_K, RC_MG_M1, RC_MG_H, RC_MG_L, RC_MG_B, RC_MG_NPF, RC_MG_PH,
-  RC_MG_CS, RC_MG_CSF, RC_MG_NCSF, RC_MG_CSH, RC_MG_LS, RC_MG_LSF, RC_MG_NLSF, RC_MG_LSH, RC_MG_N
+  RC_MG_CS, RC_MG_CSF, RC_MG_NCSF, RC_MG_CSH, RC_MG_LS, RC_MG_LSF, RC_MG_NLSF, RC_MG_LSH, RC_MG_NCH, RC_MG_ENBW,
+  RC_MG_ZS, RC_MG_N
 };
 
 struct StepCtx {
@@ -281,6 +282,10 @@ struct StepCtx {
   uint8_t rmap[RC_MAX_ACTIVE];
   // RcDiv multipliers of the dimensions the hot kernels divide by (rc_ctx_magics; RC_MG_*)
   unsigned long long mg[RC_MG_N];
+  // the embedder backward's window blocking, host-computed (each is several integer divisions on
+  // the device): rc_emb_wpb(d), rc_emb_nbw(d) and the blocks of this step's B windows
+  int ewpb, enbwm, enbw;
+  int fzs;  // the embedder forward's fc1 slices per window (slice width mg[RC_MG_CS])
 };
 
 __host__ __device__ inline int rc_rep(const StepCtx& c, int i) { return c.rident ? i : (int)c.rmap[i]; }

@@ -301,7 +301,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC, HP = EMB_HC + 1;
   const int h0 = ch * HC, hc = min(HC, H - h0);
   const int nch = rc_nchunk(d);
-  const int nbw = (B + WPB - 1) / WPB, nbw_max = rc_emb_nbw(d);
+  const int nbw = WPB == c.ewpb ? c.enbw : (B + WPB - 1) / WPB, nbw_max = c.enbwm;
   const int wend = min(B, (wb + 1) * WPB);
   const int grp = node * nch + ch;
   const bool head_grads = (grp == 0);  // fc2 / fc1-bias partials ride on group 0
@@ -863,7 +863,7 @@ __device__ __forceinline__ bool emb_combine_in(const StepCtx& c, int grp, int e)
 __device__ __forceinline__ float emb_combine_sum(const StepCtx& c, int r, int grp, int e) {
   const RedcliffDims& d = c.d;
   if (!emb_combine_in(c, grp, e)) return 0.f;
-  const int pst = rc_emb_pstride(d), nbwm = rc_emb_nbw(d), wpb = rc_emb_wpb(d), nbw = (c.B + wpb - 1) / wpb;
+  const int pst = rc_emb_pstride(d), nbwm = c.enbwm, nbw = c.enbw;
   const float* base = c.ws + r * c.wss + c.wo.ebp + (int64_t)grp * nbwm * pst + e;
   float t = 0.f;
   for (int w0 = 0; w0 < nbw; w0 += 8) {
@@ -880,7 +880,7 @@ __device__ __forceinline__ void emb_combine_store(const StepCtx& c, int r, int g
   const RedcliffDims& d = c.d;
   if (!emb_combine_in(c, grp, e)) return;
   const int p = d.p, n = d.n, F = d.F, H = d.H, M1 = d.M1, HC = EMB_HC;
-  const int nch = rc_nchunk(d), node = grp / nch, ch = grp - node * nch;
+  const int nch = rc_nchunk(d), node = RcDiv(nch, c.mg[RC_MG_NCH]).div(grp), ch = grp - node * nch;
   const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
   float* ws = c.ws + r * c.wss;
   const int h0 = ch * HC, hc = min(HC, H - h0);
@@ -939,7 +939,9 @@ void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   extern __shared__ float sm[];
   const int r = rc_rep(c, blockIdx.y);
   const int nch = rc_nchunk(c.d);
-  const int nbw = (c.B + WPB - 1) / WPB;
+  // the host's window blocking and multipliers when WPB is the default one (always, in the step)
+  const bool hb = WPB == c.ewpb;
+  const RcDiv dnbw = hb ? RcDiv(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv((c.B + WPB - 1) / WPB), dnch(nch, c.mg[RC_MG_NCH]);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 32);
   if ((int)blockIdx.x >= nnode + head) {
@@ -948,8 +950,8 @@ void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
     emb_bwd_head(c, r, sm);
     RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
   } else {
-    const int grp = blockIdx.x / nbw, wb = blockIdx.x - grp * nbw;
-    emb_bwd_node<MULTI, !MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm);
+    const int grp = dnbw.div(blockIdx.x), wb = blockIdx.x - grp * dnbw.d, node = dnch.div(grp);
+    emb_bwd_node<MULTI, !MULTI>(c, r, node, grp - node * nch, wb, BC, WPB, sm);
   }
 }
 
@@ -987,9 +989,10 @@ void k_bwd_merged(StepCtx c, int nUl, int nQ, int nnode, int head, int nred,
     } else if (e == nnode) {
       emb_bwd_head(c, r, sm);
     } else {
-      const int nch = rc_nchunk(c.d), nbw = (c.B + WPB - 1) / WPB;
-      const int grp = e / nbw, wb = e - grp * nbw;
-      emb_bwd_node<MULTI>(c, r, grp / nch, grp % nch, wb, BC, WPB, sm, cnt, (unsigned)KP);
+      const int nch = rc_nchunk(c.d);
+      const RcDiv dnbw = WPB == c.ewpb ? RcDiv(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv((c.B + WPB - 1) / WPB);
+      const int grp = dnbw.div(e), wb = e - grp * dnbw.d, node = RcDiv(nch, c.mg[RC_MG_NCH]).div(grp);
+      emb_bwd_node<MULTI>(c, r, node, grp - node * nch, wb, BC, WPB, sm, cnt, (unsigned)KP);
     }
     return;
   }
@@ -1225,10 +1228,7 @@ struct EmbWbSum {
   const float* base;
   int pst, nbw, nbwm;
   __device__ EmbWbSum(const StepCtx& c, const float* ws)
-      : base(ws + c.wo.ebp), pst(rc_emb_pstride(c.d)), nbwm(rc_emb_nbw(c.d)) {
-    const int wpb = rc_emb_wpb(c.d);
-    nbw = (c.B + wpb - 1) / wpb;
-  }
+      : base(ws + c.wo.ebp), pst(rc_emb_pstride(c.d)), nbw(c.enbw), nbwm(c.enbwm) {}
   __device__ float operator()(int grp, int off) const { return nodes(grp, 1, 1, off); }
   // Sum over u < nn, in order, of the window-block sums of group grp0 + u * gs: the combined
   // records added one after another, as k_emb_final adds them.  Four groups x eight window

@@ -21,9 +21,11 @@ namespace {
 __global__ __launch_bounds__(RC_BLOCK) void k_fac_bwd(StepCtx c, int nUl, int nQ, int role) {
   // nUl x nQ workgroups per network (1 x 1 when there is no factor update or only the records)
   extern __shared__ float sm[];
-  const int kj = blockIdx.x / (nUl * nQ);
-  const int rem0 = blockIdx.x - kj * nUl * nQ;
-  const int uc = rem0 / nQ, qc = rem0 - uc * nQ;
+  // (one workgroup per network -- the split-lead step's records launch -- needs no division)
+  const int per = nUl * nQ;
+  const int kj = per == 1 ? (int)blockIdx.x : (int)blockIdx.x / per;
+  const int rem0 = blockIdx.x - kj * per;
+  const int uc = nQ == 1 ? rem0 : rem0 / nQ, qc = rem0 - uc * nQ;
   fac_bwd_wg(c, nUl, nQ, kj, uc, qc, rc_rep(c, blockIdx.y), sm, nullptr, role);
 }
 

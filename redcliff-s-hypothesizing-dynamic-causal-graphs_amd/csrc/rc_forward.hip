@@ -43,7 +43,7 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
   const int b0 = bx * SB;
   const int nb = min(SB, c.B - b0);
   if (nb <= 0) return;
-  const int Zs = (d.p + cs - 1) / cs;
+  const int Zs = cs == (int)c.mg[RC_MG_CS] ? c.fzs : (d.p + cs - 1) / cs;
   const int zlo = zs < 0 ? 0 : zs, zhi = zs < 0 ? Zs : zs + 1;
   const int ch0 = zlo * cs, ch1 = min(d.p, zhi * cs);  // channels whose T / R rows this workgroup forms
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 0);
@@ -429,7 +429,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_l
   }
   if ((int)blockIdx.x < nemb) {
     if (split) {
-      const int Zs = (c.d.p + cs - 1) / cs, b = blockIdx.x / Zs;
+      const RcDiv dZs = cs == (int)c.mg[RC_MG_CS] ? RcDiv(c.fzs, c.mg[RC_MG_ZS]) : RcDiv((c.d.p + cs - 1) / cs);
+      const int Zs = dZs.d, b = dZs.div(blockIdx.x);
       emb_fwd_body<NBT>(c, b, 1, w_lds, cs, blockIdx.x - b * Zs, sm);
     } else {
       emb_fwd_body<NBT>(c, blockIdx.x, SB, w_lds, cs, -1, sm);
@@ -470,11 +471,18 @@ int rc_emb_fwd_slice_channels(const RedcliffDims& d) {
 void rc_ctx_magics(StepCtx& c) {
   const RedcliffDims& d = c.d;
   const int cs = rc_emb_fwd_slice_channels(d), Zs = (d.p + cs - 1) / cs, ls = d.p - (Zs - 1) * cs;
-  const long long v[RC_MG_N] = {d.F, d.p, (long long)d.p * d.F, (long long)d.n * d.F, d.K, d.M1, d.H, d.L, c.B,
+  const long long v[RC_MG_NCH] = {d.F, d.p, (long long)d.p * d.F, (long long)d.n * d.F, d.K, d.M1, d.H, d.L, c.B,
                                 (long long)d.n * d.p * d.F, (long long)d.p * d.H,
                                 0, (long long)cs * d.F, (long long)d.n * cs * d.F, (long long)cs * d.H,
                                 0, (long long)ls * d.F, (long long)d.n * ls * d.F, (long long)ls * d.H};
-  for (int i = 0; i < RC_MG_N; ++i) c.mg[i] = rc_magic40(v[i]);
+  c.ewpb = rc_emb_wpb(d);
+  c.enbwm = rc_emb_nbw(d);
+  c.enbw = (c.B + c.ewpb - 1) / c.ewpb;
+  for (int i = 0; i < RC_MG_NCH; ++i) c.mg[i] = rc_magic40(v[i]);
+  c.mg[RC_MG_NCH] = rc_magic40(rc_nchunk(d));
+  c.mg[RC_MG_ENBW] = rc_magic40(c.enbw);
+  c.fzs = Zs;
+  c.mg[RC_MG_ZS] = rc_magic40(Zs);
   c.mg[RC_MG_CS] = (unsigned long long)cs;  // the widths themselves (the slice's width picks its slots)
   c.mg[RC_MG_LS] = (unsigned long long)ls;
 }
