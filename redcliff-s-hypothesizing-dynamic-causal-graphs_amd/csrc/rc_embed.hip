@@ -1082,10 +1082,18 @@ __device__ inline void lds_mm(const float* X, const float* Y, int p, int P, Out 
   int a0, bj;
   if (!lds_mm_tile<TX, TY>(X, Y, p, P, acc, a0, bj)) return;
   const int lane = threadIdx.x & 63;
+  if (p <= 16) {  // rows 16..31 of the tile (registers 8..15) are padding: half the epilogue
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int a = a0 + mf_row(reg, lane);
-    if (a < p && bj < p) out(a, bj, acc[reg]);
+    for (int reg = 0; reg < 8; ++reg) {
+      const int a = a0 + mf_row(reg, lane);
+      if (a < p && bj < p) out(a, bj, acc[reg]);
+    }
+  } else {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int a = a0 + mf_row(reg, lane);
+      if (a < p && bj < p) out(a, bj, acc[reg]);
+    }
   }
 }
 
@@ -1102,24 +1110,30 @@ __device__ inline void lds_mm_acc(const float* X, const float* Y, int p, int P, 
   // writes do not each wait for the previous one.
   const int lane = threadIdx.x & 63;
   const bool cin = bj < p;
-  int ad[16];
-  float old[16];
+  auto rmw = [&](auto nreg) {  // (p <= 16: rows 16..31, registers 8..15, are padding)
+    constexpr int NR = decltype(nreg)::value;
+    int ad[NR];
+    float old[NR];
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int a = a0 + mf_row(reg, lane);
-    ad[reg] = (cin && a < p) ? a * P + bj : min(a, p - 1) * P + p;
-    old[reg] = D[ad[reg]];
-  }
+    for (int reg = 0; reg < NR; ++reg) {
+      const int a = a0 + mf_row(reg, lane);
+      ad[reg] = (cin && a < p) ? a * P + bj : min(a, p - 1) * P + p;
+      old[reg] = D[ad[reg]];
+    }
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) D[ad[reg]] = old[reg] + acc[reg];
+    for (int reg = 0; reg < NR; ++reg) D[ad[reg]] = old[reg] + acc[reg];
+  };
+  if (p <= 16)
+    rmw(std::integral_constant<int, 8>{});
+  else
+    rmw(std::integral_constant<int, 16>{});
 }
 
 // Supports of normalize_A(A) (S_0 = I, S_1 = L, S_l = S_{l-1} L): A padded in LDS, L and its
 // powers built in LDS slots 1..n-1 of Sl and written densely to S[n][p][p].  Used by the
 // optimizer's adjacency workgroup and by k_supports, so both produce the same bits.
-__device__ __forceinline__ void supports_lds(const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
+__device__ __forceinline__ void supports_lds(const RcDiv& dpv, const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
   const int P = p + 1, PP = p * P, pp2 = p * p;
-  const RcDiv dpv(p);
   lds_rowsum(p, [&](int i, int j) { return fmaxf(Al[i * P + j], 0.f); },
              [&](int i, float s) { dinv[i] = 1.f / sqrtf(s + 1e-10f); });
   __syncthreads();
@@ -1136,11 +1150,14 @@ __device__ __forceinline__ void supports_lds(const float* Al, float* Sl, float* 
   for (int l = 2; l < n; ++l) {
     float* out = Sl + l * PP;
     float* og = S + (int64_t)l * pp2;
-    lds_mm<false, false>(Sl + (l - 1) * PP, Sl + PP, p, P, [&](int a, int b, float v) {
-      out[a * P + b] = v;
-      og[a * p + b] = v;
-    });
+    lds_mm<false, false>(Sl + (l - 1) * PP, Sl + PP, p, P, [&](int a, int b, float v) { out[a * P + b] = v; });
     __syncthreads();
+    // the dense copy out by every thread (one element each for p <= 16) instead of 16 scattered
+    // stores with their address arithmetic on the product's one wave
+    for (int e = threadIdx.x; e < pp2; e += RC_BLOCK) {
+      const int i = dpv.div(e);
+      og[e] = out[i * P + (e - i * p)];
+    }
   }
 }
 
@@ -1156,7 +1173,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_supports(RedcliffDims d, const flo
     sm[i * P + (e - i * p)] = A[e];
   }
   __syncthreads();
-  supports_lds(sm, sm + p * P, ws + r * wss + wo.S, sm + (d.n + 1) * p * P, p, d.n);
+  supports_lds(RcDiv(p), sm, sm + p * P, ws + r * wss + wo.S, sm + (d.n + 1) * p * P, p, d.n);
 }
 
 // Data-parallel update after the all-reduce (DataParallelFit): Adam of both parameter groups from
@@ -1190,7 +1207,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_dp_update(StepCtx c, int64_t nE, i
       sm[a * P1 + (e - a * p)] = pv;
     }
     __syncthreads();
-    supports_lds(sm, sm + p * P1, c.ws + r * c.wss + c.wo.S, sm + (c.d.n + 1) * p * P1, p, c.d.n);
+    supports_lds(RcDiv(p, c.mg[RC_MG_P]), sm, sm + p * P1, c.ws + r * c.wss + c.wo.S, sm + (c.d.n + 1) * p * P1, p, c.d.n);
     return;
   }
   const bool emb = bx <= nbE;
@@ -1606,10 +1623,10 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
     RC_PHASE(c.ws, c.wo.total, wx, 53);
     // supports of the updated A for the next step (after a gradient-only shard step A changes
     // later, in redcliff_adam_apply, and the host refreshes them)
-    if (adam) supports_lds(Al, Sl, ws + c.wo.S, dinv, p, n);
+    if (adam) supports_lds(dpv, Al, Sl, ws + c.wo.S, dinv, p, n);
 #ifdef RC_ADJ_TWICE
     RC_PHASE(c.ws, c.wo.total, wx, 57);
-    if (adam) supports_lds(Al, Sl, ws + c.wo.S, dinv, p, n);  // (same values again)
+    if (adam) supports_lds(dpv, Al, Sl, ws + c.wo.S, dinv, p, n);  // (same values again)
     RC_PHASE(c.ws, c.wo.total, wx, 58);
 #endif
   }
