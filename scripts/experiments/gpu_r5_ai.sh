@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 5: the adjacency workgroup's p x p products (one wave, instruction-issue bound): half the
+# Round 5 (against the r5af build: includes r5ah's host window blocking): the adjacency workgroup's p x p products (one wave, instruction-issue bound): half the
 # epilogue for p <= 16 (rows 16..31 of the 32x32 tile are padding), the supports' dense copy out by
 # every thread, the supports' divider from the host.  Bitwise whole fits (R = 1 and 4), single-fit
 # steps, phase traces, the instruction-fetch experiment, the whole GPU suite.
 source "$(dirname "$0")/../gpu_steps.sh"
-P=scripts/bin/lib_prev_r5i.so
+P=scripts/bin/lib_prev_r5h.so
 COMPARE_FITS_CFGS=c4,c1k4,d4ic,c5 COMPARE_FITS_R=1 REDCLIFF_HIP_LIB=$P step ai_dump_prev 300 python scripts/compare_fits.py dump gpurun_out/fprev_1.npz
 COMPARE_FITS_CFGS=c4,c1k4,d4ic,c5 COMPARE_FITS_R=1 step ai_dump_cur 300 python scripts/compare_fits.py dump gpurun_out/fcur_1.npz
 step ai_cmp 60 python scripts/compare_fits.py compare gpurun_out/fprev_1.npz gpurun_out/fcur_1.npz
