@@ -478,6 +478,12 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
             return S[((int64_t)i * p + node) * p + cc];
           }, [&](int e, float v) { Srow[e] = v; }),
           sR, sT, sX, sF1, sW, sL);
+  RC_PHASE(c.ws, c.wo.total, pbx, 44);  // (trace builds: the staging pass's loads are in)
+#ifdef RC_STAGE_TWICE
+      // timing experiment (trace builds): the window operands staged again -- warm caches and TLB
+      rc_stage_all(sR, sT, sX, sF1, sW, sL);
+  RC_PHASE(c.ws, c.wo.total, pbx, 47);
+#endif
       if (tid < F) bn_affine_store(c, r, tid, bnq, alpha, beta, mean, inv);
       if (wait_now) {
         rc_wait_leads(c, c.ws + r * c.wss, wait_cnt, wait_target);
@@ -485,7 +491,9 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
         dw_load(0);
       }
       dw_store(0);
+  RC_PHASE(c.ws, c.wo.total, pbx, 45);  // the first dL/dw round is in
       dw_rest();
+  RC_PHASE(c.ws, c.wo.total, pbx, 46);
       __syncthreads();
       if (tid < n) {
         float t = 0.f;

@@ -57,6 +57,9 @@ def main():
         idx = [i for i in range(hi - lo) if t[i] > 0]
         if len(idx) > 1:
             print(label + ": " + "  ".join("%d->%d %.2f" % (lo + a, lo + b, (t[b] - t[a]) / 100.0) for a, b in zip(idx, idx[1:])))
+    if ph[32] > 0:  # the embedder backward's node workgroup 0 marks in slot order, us after mark 32
+        print("emb_bwd WG0 marks (us after 32): " +
+              "  ".join("%d %.2f" % (i, (ph[i] - ph[32]) / 100.0) for i in range(32, 48) if ph[i] > 0))
     if ph[48] > 0:  # the adjacency workgroup's marks in slot order, us after mark 48
         print("emb_final adjacency WG marks (us after 48): " +
               "  ".join("%d %.2f" % (i, (ph[i] - ph[48]) / 100.0) for i in range(48, 64) if ph[i] > 0))
