@@ -280,8 +280,8 @@ struct StepCtx {
   // producer than exists, with a short poll bound -- forces the timeout path (tests)
   int wait_dbg;
   uint8_t rmap[RC_MAX_ACTIVE];
-  // RcDiv multipliers of the dimensions the hot kernels divide by (rc_ctx_magics; RC_MG_*)
-  unsigned long long mg[RC_MG_N];
+  // RcDiv32 multipliers of the dimensions the hot kernels divide by (rc_ctx_magics; RC_MG_*)
+  unsigned mg[RC_MG_N];
   // the embedder backward's window blocking, host-computed (each is several integer divisions on
   // the device): rc_emb_wpb(d), rc_emb_nbw(d) and the blocks of this step's B windows
   int ewpb, enbwm, enbw;
@@ -430,10 +430,26 @@ struct RcDiv {
   // with six divisors that is ~2 us of a kernel prologue (k_emb_bwd's node workgroups, phase trace).
   // The hot kernels take the multipliers the host computed (StepCtx::mg, RcDiv(d, m)).
   __device__ inline explicit RcDiv(int dd) : m(rc_magic40(dd)), d(dd) {}
-  __device__ inline RcDiv(int dd, unsigned long long mm) : m(mm), d(dd) {}
   __device__ inline int div(int n) const {
     return d == 1 ? n : (int)(((unsigned long long)(unsigned)n * m) >> 40);
   }
+  __device__ inline int mod(int n) const { return n - div(n) * d; }
+};
+
+// ceil(2^32 / d) for d > 1 (0 for d <= 1): RcDiv32's multiplier
+__host__ __device__ inline unsigned rc_magic32(long long d) {
+  return d > 1 ? (unsigned)(((1ull << 32) + (unsigned long long)d - 1) / (unsigned long long)d) : 0u;
+}
+// n / d as one v_mul_hi_u32 with the multiplier the host computed (StepCtx::mg): exact for
+// 0 <= n, n * d < 2^32 (every use: indices < 2^20, divisors < 2^14).  One 32-bit register for the
+// multiplier where RcDiv's 64-bit one took two: the hot kernels run short of scalar registers
+// (k_emb_bwd spilled ~1,600 of them to vector lanes), and the 64-bit product was ~5 instructions.
+struct RcDiv32 {
+  unsigned m;
+  int d;
+  __device__ inline RcDiv32(int dd, unsigned mm) : m(mm), d(dd) {}
+  __device__ inline explicit RcDiv32(int dd) : m(rc_magic32(dd)), d(dd) {}  // (fallback: a device division)
+  __device__ inline int div(int n) const { return d == 1 ? n : (int)__umulhi((unsigned)n, m); }
   __device__ inline int mod(int n) const { return n - div(n) * d; }
 };
 

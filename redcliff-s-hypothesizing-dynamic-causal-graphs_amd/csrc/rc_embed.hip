@@ -334,7 +334,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const bool late_x = LATE && rc_emb_late_x(d);
   float* xc = late_x ? f1r : dTc + BC * nF;  // [BC][p][F] raw window (late: over f1r .. Tc)
 
-  const RcDiv dF(F, c.mg[RC_MG_F]), dp(p, c.mg[RC_MG_P]), dpF(pF, c.mg[RC_MG_PF]), dnF(nF, c.mg[RC_MG_NF]),
+  const RcDiv32 dF(F, c.mg[RC_MG_F]), dp(p, c.mg[RC_MG_P]), dpF(pF, c.mg[RC_MG_PF]), dnF(nF, c.mg[RC_MG_NF]),
       dK(K, c.mg[RC_MG_K]), dM1(M1, c.mg[RC_MG_M1]);
   // trace builds: the node workgroup's own index (inside the merged launch the factor leads come first)
   const int pbx = wait_cnt ? (int)blockIdx.x - d.K * d.p : (int)blockIdx.x;
@@ -888,7 +888,7 @@ __device__ __forceinline__ void emb_combine_store(const StepCtx& c, int r, int g
   const RedcliffDims& d = c.d;
   if (!emb_combine_in(c, grp, e)) return;
   const int p = d.p, n = d.n, F = d.F, H = d.H, M1 = d.M1, HC = EMB_HC;
-  const int nch = rc_nchunk(d), node = RcDiv(nch, c.mg[RC_MG_NCH]).div(grp), ch = grp - node * nch;
+  const int nch = rc_nchunk(d), node = RcDiv32(nch, c.mg[RC_MG_NCH]).div(grp), ch = grp - node * nch;
   const int ofs_w = M1 * HC, ofs_s = ofs_w + n * F * HC, ofs_g = ofs_s + (n - 1) * p, ofs_h = ofs_g + 2 * F;
   float* ws = c.ws + r * c.wss;
   const int h0 = ch * HC, hc = min(HC, H - h0);
@@ -949,7 +949,7 @@ void k_emb_bwd(StepCtx c, int nnode, int head, int BC, int WPB) {
   const int nch = rc_nchunk(c.d);
   // the host's window blocking and multipliers when WPB is the default one (always, in the step)
   const bool hb = WPB == c.ewpb;
-  const RcDiv dnbw = hb ? RcDiv(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv((c.B + WPB - 1) / WPB), dnch(nch, c.mg[RC_MG_NCH]);
+  const RcDiv32 dnbw = hb ? RcDiv32(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv32((c.B + WPB - 1) / WPB), dnch(nch, c.mg[RC_MG_NCH]);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 32);
   if ((int)blockIdx.x >= nnode + head) {
@@ -998,8 +998,8 @@ void k_bwd_merged(StepCtx c, int nUl, int nQ, int nnode, int head, int nred,
       emb_bwd_head(c, r, sm);
     } else {
       const int nch = rc_nchunk(c.d);
-      const RcDiv dnbw = WPB == c.ewpb ? RcDiv(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv((c.B + WPB - 1) / WPB);
-      const int grp = dnbw.div(e), wb = e - grp * dnbw.d, node = RcDiv(nch, c.mg[RC_MG_NCH]).div(grp);
+      const RcDiv32 dnbw = WPB == c.ewpb ? RcDiv32(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv32((c.B + WPB - 1) / WPB);
+      const int grp = dnbw.div(e), wb = e - grp * dnbw.d, node = RcDiv32(nch, c.mg[RC_MG_NCH]).div(grp);
       emb_bwd_node<MULTI>(c, r, node, grp - node * nch, wb, BC, WPB, sm, cnt, (unsigned)KP);
     }
     return;
@@ -1140,7 +1140,8 @@ __device__ inline void lds_mm_acc(const float* X, const float* Y, int p, int P, 
 // Supports of normalize_A(A) (S_0 = I, S_1 = L, S_l = S_{l-1} L): A padded in LDS, L and its
 // powers built in LDS slots 1..n-1 of Sl and written densely to S[n][p][p].  Used by the
 // optimizer's adjacency workgroup and by k_supports, so both produce the same bits.
-__device__ __forceinline__ void supports_lds(const RcDiv& dpv, const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
+template <class Div>
+__device__ __forceinline__ void supports_lds(const Div& dpv, const float* Al, float* Sl, float* S, float* dinv, int p, int n) {
   const int P = p + 1, PP = p * P, pp2 = p * p;
   lds_rowsum(p, [&](int i, int j) { return fmaxf(Al[i * P + j], 0.f); },
              [&](int i, float s) { dinv[i] = 1.f / sqrtf(s + 1e-10f); });
@@ -1215,7 +1216,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_dp_update(StepCtx c, int64_t nE, i
       sm[a * P1 + (e - a * p)] = pv;
     }
     __syncthreads();
-    supports_lds(RcDiv(p, c.mg[RC_MG_P]), sm, sm + p * P1, c.ws + r * c.wss + c.wo.S, sm + (c.d.n + 1) * p * P1, p, c.d.n);
+    supports_lds(RcDiv32(p, c.mg[RC_MG_P]), sm, sm + p * P1, c.ws + r * c.wss + c.wo.S, sm + (c.d.n + 1) * p * P1, p, c.d.n);
     return;
   }
   const bool emb = bx <= nbE;
@@ -1498,7 +1499,7 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
   const int tid = threadIdx.x;
   extern __shared__ float sm[];
   const int pp2 = p * p, P = p + 1, PP = p * P;
-  const RcDiv dpv(p, c.mg[RC_MG_P]);
+  const RcDiv32 dpv(p, c.mg[RC_MG_P]);
   float* Al = sm;                  // A (pre-update, then the updated A)
   float* Ar = Al + PP;             // relu(A)
   float* dL = Ar + PP;             // dL/dL (the normalised Laplacian)

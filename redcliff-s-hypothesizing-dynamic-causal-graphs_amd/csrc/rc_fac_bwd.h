@@ -17,7 +17,8 @@ namespace {
 #define RC_FB_MFMA 1  // activation recompute and dW0 tile on v_mfma_f32_16x16x4_f32 (same chains)
 #endif
 
-__device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
+template <class Div>
+__device__ inline float xwin(const StepCtx& c, const Div& dL, const float* X, int b, int q) {
   const int L = c.d.L;
   const int ch = dL.div(q), t = q - ch * L;
   return X[((c.row0 + b) * c.d.T + (c.Lmax - L + t)) * c.d.p + ch];
@@ -76,7 +77,7 @@ __device__ __forceinline__ void fac_bwd_wg(const StepCtx& c, int nUl, int nQ, in
   const RedcliffReplicaHyper& hy = c.hyp[r];
   const int tid = threadIdx.x;
   const int B = c.B;
-  const RcDiv dL(d.L, c.mg[RC_MG_L]), dB(B, c.mg[RC_MG_B]);
+  const RcDiv32 dL(d.L, c.mg[RC_MG_L]), dB(B, c.mg[RC_MG_B]);
   const bool sig = d.use_sigmoid;
   const float ecc = d.sigmoid_ecc;
   const bool fgrad = (c.flags & RC_STEP_B) || (c.flags & RC_STEP_A);

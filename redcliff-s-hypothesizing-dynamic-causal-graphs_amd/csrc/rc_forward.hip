@@ -50,7 +50,7 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
   RC_PHASE(c.ws, c.wo.total, bx, 0);
   const int p = d.p, F = d.F, H = d.H, n = d.n, M1 = d.M1, K = d.K;
   const int pF = p * F, pH = p * H, nFH = n * F * H;
-  const RcDiv dF(F, c.mg[RC_MG_F]), dp(p, c.mg[RC_MG_P]), dpF(pF, c.mg[RC_MG_PF]), dH(H, c.mg[RC_MG_H]);
+  const RcDiv32 dF(F, c.mg[RC_MG_F]), dp(p, c.mg[RC_MG_P]), dpF(pF, c.mg[RC_MG_PF]), dH(H, c.mg[RC_MG_H]);
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -129,9 +129,9 @@ __device__ __attribute__((always_inline)) void emb_fwd_body(const StepCtx& c, in
   // the slice width's multipliers (host-computed for the regular, the last and the whole width)
   const int cw = ch1 - ch0;
   const int mb = cw == (int)c.mg[RC_MG_CS] ? RC_MG_CSF : (cw == (int)c.mg[RC_MG_LS] ? RC_MG_LSF : -1);
-  const RcDiv dcF = mb >= 0 ? RcDiv(cF, c.mg[mb]) : (cw == p ? RcDiv(cF, c.mg[RC_MG_PF]) : RcDiv(cF));
-  const RcDiv dncF = mb >= 0 ? RcDiv(n * cF, c.mg[mb + 1]) : (cw == p ? RcDiv(n * cF, c.mg[RC_MG_NPF]) : RcDiv(n * cF));
-  const RcDiv dcH = mb >= 0 ? RcDiv(cH, c.mg[mb + 2]) : (cw == p ? RcDiv(cH, c.mg[RC_MG_PH]) : RcDiv(cH));
+  const RcDiv32 dcF = mb >= 0 ? RcDiv32(cF, c.mg[mb]) : (cw == p ? RcDiv32(cF, c.mg[RC_MG_PF]) : RcDiv32(cF));
+  const RcDiv32 dncF = mb >= 0 ? RcDiv32(n * cF, c.mg[mb + 1]) : (cw == p ? RcDiv32(n * cF, c.mg[RC_MG_NPF]) : RcDiv32(n * cF));
+  const RcDiv32 dcH = mb >= 0 ? RcDiv32(cH, c.mg[mb + 2]) : (cw == p ? RcDiv32(cH, c.mg[RC_MG_PH]) : RcDiv32(cH));
   for (int e = tid; e < nb * n * cF; e += RC_BLOCK) {
     const int s = dncF.div(e), rs = e - s * n * cF, i = dcF.div(rs), qs = rs - i * cF;
     const int q = ch0 * F + qs, rem = i * pF + q, ch = dF.div(q), f = q - ch * F;
@@ -325,7 +325,8 @@ size_t emb_fwd_floats(const RedcliffDims& d, int SB, int w_lds) {
 // a[kj][b][u], partial outputs y[uc][kj][b] = sum_{u in chunk} W1[u] a[b][u] (+ b1 in chunk
 // 0), the chunk's squared layer-0 group norms gq[uc][kj][q] and a snapshot of W1.
 // The whole window block and weight chunk are staged in one pass when p*L <= FQ_MAX.
-__device__ inline float xwin(const StepCtx& c, const RcDiv& dL, const float* X, int b, int q) {
+template <class Div>
+__device__ inline float xwin(const StepCtx& c, const Div& dL, const float* X, int b, int q) {
   const int L = c.d.L;
   const int ch = dL.div(q), t = q - ch * L;
   return X[((c.row0 + b) * c.d.T + (c.Lmax - L + t)) * c.d.p + ch];
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_forward(StepCtx c, int SB, int w_l
   }
   if ((int)blockIdx.x < nemb) {
     if (split) {
-      const RcDiv dZs = cs == (int)c.mg[RC_MG_CS] ? RcDiv(c.fzs, c.mg[RC_MG_ZS]) : RcDiv((c.d.p + cs - 1) / cs);
+      const RcDiv32 dZs = cs == (int)c.mg[RC_MG_CS] ? RcDiv32(c.fzs, c.mg[RC_MG_ZS]) : RcDiv32((c.d.p + cs - 1) / cs);
       const int Zs = dZs.d, b = dZs.div(blockIdx.x);
       emb_fwd_body<NBT>(c, b, 1, w_lds, cs, blockIdx.x - b * Zs, sm);
     } else {
@@ -478,13 +479,13 @@ void rc_ctx_magics(StepCtx& c) {
   c.ewpb = rc_emb_wpb(d);
   c.enbwm = rc_emb_nbw(d);
   c.enbw = (c.B + c.ewpb - 1) / c.ewpb;
-  for (int i = 0; i < RC_MG_NCH; ++i) c.mg[i] = rc_magic40(v[i]);
-  c.mg[RC_MG_NCH] = rc_magic40(rc_nchunk(d));
-  c.mg[RC_MG_ENBW] = rc_magic40(c.enbw);
+  for (int i = 0; i < RC_MG_NCH; ++i) c.mg[i] = rc_magic32(v[i]);
+  c.mg[RC_MG_NCH] = rc_magic32(rc_nchunk(d));
+  c.mg[RC_MG_ENBW] = rc_magic32(c.enbw);
   c.fzs = Zs;
-  c.mg[RC_MG_ZS] = rc_magic40(Zs);
-  c.mg[RC_MG_CS] = (unsigned long long)cs;  // the widths themselves (the slice's width picks its slots)
-  c.mg[RC_MG_LS] = (unsigned long long)ls;
+  c.mg[RC_MG_ZS] = rc_magic32(Zs);
+  c.mg[RC_MG_CS] = (unsigned)cs;  // the widths themselves (the slice's width picks its slots)
+  c.mg[RC_MG_LS] = (unsigned)ls;
 }
 
 // One launch of the embedder forward (with_emb) and / or the vector-path factor forward (with_fac).
