@@ -1,10 +1,17 @@
 #!/bin/bash
-# Round 5: kernel-completed fork / join events on the packed grid's forked matrix-core chain
-# (REDCLIFF_EXT_EVENT=0: event-record packets), R = 32 / 128 grid steps; forked-step bitwise tests
+# Round 5 final-tree evidence (after the latency work, r5ac-r5ak): the driver's bench command; the single-fit (D4IC) bench leg under
+# rocprofv3 --kernel-trace --stats and its FETCH / WRITE passes (the line's roofline kernel); the
+# R = 128 grid (one stream) kernel stats and passes; GPU suite + smoke
 source "$(dirname "$0")/../gpu_steps.sh"
-step u_tests 600 python -u -m pytest tests/test_gpu_forked.py tests/test_gpu_large_pack.py -v --timeout 300 --timeout-method thread -rA
-for R in 32 128; do
-  step u_sweep_$R 400 python scripts/grid_sweep.py --replicas $R --steps 50 --rounds 3 --settings '[{},{"REDCLIFF_EXT_EVENT":"0"}]'
-done
-step u_fits 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-north-star --replicas 1 --dp-leg-batch 0 --ref-grid-epochs 0 --no-kernel-times
-REDCLIFF_EXT_EVENT=0 step u_fits0 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-north-star --replicas 1 --dp-leg-batch 0 --ref-grid-epochs 0 --no-kernel-times
+step u_bench 600 python bench.py
+S="python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-north-star --replicas 1 --fit-replicas 0 --dp-leg-batch 0 --ref-grid-epochs 0"
+step u_stats 240 timeout -s KILL 220 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/u/stats -o run -- $S
+step u_fetch 240 timeout -s KILL 220 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/u/fetch -o run -- $S
+step u_write 240 timeout -s KILL 220 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/u/write -o run -- $S
+G="python scripts/grid_step.py --replicas 128 --steps 20"
+REDCLIFF_FORK=0 step u_gstats 240 timeout -s KILL 220 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/u/gstats -o run -- $G
+REDCLIFF_FORK=0 step u_gfetch 240 timeout -s KILL 220 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/u/gfetch -o run -- $G
+REDCLIFF_FORK=0 step u_gwrite 240 timeout -s KILL 220 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/u/gwrite -o run -- $G
+rm -f gpurun_out/u/*/run_kernel_trace.csv
+step u_suite 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA --durations=10
+step u_smoke 300 python -c "import __grafu_entry__ as g; g.smoke()"
