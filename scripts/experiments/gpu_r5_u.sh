@@ -14,4 +14,4 @@ REDCLIFF_FORK=0 step u_gfetch 240 timeout -s KILL 220 rocprofv3 --pmc FETCH_SIZE
 REDCLIFF_FORK=0 step u_gwrite 240 timeout -s KILL 220 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/u/gwrite -o run -- $G
 rm -f gpurun_out/u/*/run_kernel_trace.csv
 step u_suite 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA --durations=10
-step u_smoke 300 python -c "import __grafu_entry__ as g; g.smoke()"
+step u_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
