@@ -385,13 +385,6 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
   const char* xev = getenv("REDCLIFF_EXT_EVENT");
   const bool ext_ev = !xev || strcmp(xev, "0") != 0;
   if (split && ext_ev && (e = aux_stream(&aux))) return e;
-  // Split-lead records merged into the embedder backward's launch (k_bwd_lead_emb): the node
-  // workgroups stage their windows while the leads compute the records they wait for, and one
-  // launch boundary goes.  Needs the deferred combine (REDCLIFF_DEFER unset or 1), no loss values,
-  // one window sub-block per workgroup.  REDCLIFF_LEAD_EMB=0 keeps the records launch (same bits).
-  const char* lev = getenv("REDCLIFF_LEAD_EMB");
-  const bool lead_emb = split && !egemm && !(fl & RC_VALUES) && !(dv0 && strcmp(dv0, "1") != 0) &&
-                        rc_emb_wpb(c.d) <= rc_emb_bc(c.d) && !(lev && strcmp(lev, "0") == 0);
   // forward: the fused launch runs the embedder and (vector path, no fork) the factor networks
   if (egemm) {
     if ((e = timed(KT_EMB_FWD, s, [&] { return rc_launch_emb_fwd_gemm(c, s); }))) return e;
@@ -421,7 +414,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     }
     if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf, RC_FB_UPDATE, ext_ev ? aux->ev[0] : nullptr); })))
       return e;
-    if (!lead_emb && (e = timed(KT_FAC_LEAD, s, [&] { return rc_launch_fac_bwd(c, s, RC_FB_RECORDS); }))) return e;
+    if ((e = timed(KT_FAC_LEAD, s, [&] { return rc_launch_fac_bwd(c, s, RC_FB_RECORDS); }))) return e;
   } else if (!mfma && fac && !merged) {
     if (fork && (e = stream_wait(sf, s, aux->ev[1]))) return e;  // the mixing needs the embedder output w
     if ((e = timed(KT_FAC_BWD, sf, [&] { return rc_launch_fac_bwd(c, sf, RC_FB_ALL); }))) return e;
@@ -461,11 +454,7 @@ int redcliff_train_step(const RedcliffStepArgs* a, void* stream) {
     const char* dv = getenv("REDCLIFF_DEFER");
     c.defer = dv ? atoi(dv) : 1;
     if (c.defer < 0 || c.defer > 2) c.defer = 1;
-    if (lead_emb) {
-      if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_bwd_lead_emb(c, s); }))) return e;
-    } else if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) {
-      return e;
-    }
+    if ((e = timed(KT_EMB_BWD, s, [&] { return rc_launch_emb_bwd(c, s, true); }))) return e;
     tail = tail_ok();
     if (c.defer == 1 && !tail && (e = timed(KT_EMB_COMB, s, [&] { return rc_launch_emb_combine(c, s); }))) return e;
   } else if (fl & (RC_VALUES | RC_CONFUSION)) {

@@ -679,7 +679,6 @@ int rc_emb_tail_grid(const StepCtx& c);
 int rc_launch_emb_tail(const StepCtx& c, hipStream_t s);
 int rc_launch_emb_combine(const StepCtx& c, hipStream_t s);
 int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s);  // factor + embedder backward, one launch
-int rc_launch_bwd_lead_emb(const StepCtx& c, hipStream_t s);  // split-lead records + embedder backward
 int rc_bwd_merged_grid(const StepCtx& c);                    // its grid, 0 when not worth it  // window-block partials (c.defer)
 int rc_launch_dp_update(const StepCtx& c, int64_t nE, int64_t nF, hipStream_t s);
 int rc_launch_supports(const RedcliffDims& d, const float* emb, int64_t es, float* ws, int64_t wss, EmbOff eo,

@@ -1038,38 +1038,6 @@ void k_bwd_merged(StepCtx c, int nUl, int nQ, int nnode, int head, int nred,
   fac_bwd_wg(c, nUl, nQ, kj, uc, qc, r, sm, e < 0 ? cnt : nullptr, role);
 }
 
-// Split-lead step with the records merged into the embedder backward's launch (round 5):
-// [K*p factor-lead workgroups: records only, published][embedder node / head / dA-reduce
-// workgroups, waiting for the K*p published leads].  The factor update runs on the second stream
-// as in the split-lead step; the node workgroups stage their windows while the leads work instead
-// of after the leads' launch.  The update code is not compiled in (role is a constant), so the
-// kernel keeps the node workgroups' registers, not k_bwd_merged's.  Same arithmetic, same bits.
-template <bool MULTI>
-__global__ __launch_bounds__(RC_BLOCK) void k_bwd_lead_emb(StepCtx c, int nnode, int head, int nred, int BC, int WPB) {
-  extern __shared__ float sm[];
-  const int r = rc_rep(c, blockIdx.y);
-  unsigned* cnt = rc_fac_lead_cnt(c, c.ws + r * c.wss);
-  const int KP = c.d.K * c.d.p;
-  const int bx = blockIdx.x;
-  if (bx < KP) {
-    fac_bwd_wg(c, 1, 1, bx, 0, 0, r, sm, cnt, RC_FB_RECORDS);
-    return;
-  }
-  const int e = bx - KP;
-  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
-  if (e >= nnode + head) {
-    rc_wait_leads(c, c.ws + r * c.wss, cnt, KP);
-    emb_bwd_dadj(c, r, e - nnode - head, true);
-  } else if (e == nnode) {
-    emb_bwd_head(c, r, sm);
-  } else {
-    const int nch = rc_nchunk(c.d);
-    const RcDiv32 dnbw = WPB == c.ewpb ? RcDiv32(c.enbw, c.mg[RC_MG_ENBW]) : RcDiv32((c.B + WPB - 1) / WPB);
-    const int grp = dnbw.div(e), wb = e - grp * dnbw.d, node = RcDiv32(nch, c.mg[RC_MG_NCH]).div(grp);
-    emb_bwd_node<MULTI>(c, r, node, grp - node * nch, wb, BC, WPB, sm, cnt, (unsigned)KP);
-  }
-}
-
 // ---- adjacency algebra for p <= 64 in one workgroup, operands in LDS with row stride P = p + 1
 
 // Row sums over j < p of f(i, j), i < p: four lanes per row, each summing a strided quarter,
@@ -1888,29 +1856,6 @@ int rc_launch_bwd_merged(const StepCtx& c, hipStream_t s) {
     hipLaunchKernelGGL(k_bwd_merged<false>, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, nUl, nQ, nnode, head, nred, BC, WPB);
   }
   return rc_check(hipGetLastError(), "k_bwd_merged");
-}
-
-// The split-lead step's records + embedder backward launch (k_bwd_lead_emb); deferred combine,
-// no loss values (the head's loss sums read the factor leads' records), one window sub-block per
-// workgroup.  The leads come first in the grid and are dispatched before the workgroups that wait
-// for them.
-int rc_launch_bwd_lead_emb(const StepCtx& c, hipStream_t s) {
-  const RedcliffDims& d = c.d;
-  if (c.defer != 1 || (c.flags & RC_VALUES)) { rc_set_error("lead+embedder backward: needs defer == 1 and no values"); return REDCLIFF_EINVAL; }
-  const size_t le = rc_emb_bwd_lds(d, false), lf = sizeof(float) * (size_t)fac_bwd_lds_floats(d);
-  const size_t lds = le > lf ? le : lf;
-  if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("lead+embedder backward: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  const int BC = rc_emb_bc(d), WPB = rc_emb_wpb(d);
-  if (WPB > BC) { rc_set_error("lead+embedder backward: one sub-block per workgroup only"); return REDCLIFF_EINVAL; }
-  const int nnode = d.p * rc_nchunk(d) * ((c.B + WPB - 1) / WPB);
-  const int head = (c.flags & RC_CONFUSION) ? 1 : 0;
-  const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
-  const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
-  const int grid = d.K * d.p + nnode + head + nred;
-  int e = rc_lds_optin(k_bwd_lead_emb<false>, lds, "k_bwd_lead_emb LDS");
-  if (e) return e;
-  hipLaunchKernelGGL(k_bwd_lead_emb<false>, dim3(grid, c.nrep), dim3(RC_BLOCK), lds, s, c, nnode, head, nred, BC, WPB);
-  return rc_check(hipGetLastError(), "k_bwd_lead_emb");
 }
 
 int rc_launch_cos_values(const StepCtx& c, hipStream_t s) {

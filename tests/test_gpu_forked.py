@@ -114,13 +114,12 @@ def test_forked_pack_bitwise_equals_single_stream_pack(monkeypatch, guard_bands)
             np.testing.assert_array_equal(states["1"][r][k], want, err_msg="replica %d %s" % (r, k))
 
 
-def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", ext="1", lead_emb="1"):
+def run_vector(monkeypatch, merge, train, guarded, seed=0, split="0", tail="0", ext="1"):
     monkeypatch.setenv("REDCLIFF_FAC_PATH", "vector")
     monkeypatch.setenv("REDCLIFF_MERGE", merge)
     monkeypatch.setenv("REDCLIFF_SPLIT_LEAD", split)
     monkeypatch.setenv("REDCLIFF_TAIL", tail)
     monkeypatch.setenv("REDCLIFF_EXT_EVENT", ext)
-    monkeypatch.setenv("REDCLIFF_LEAD_EMB", lead_emb)
     m = make(seed, 10.0, 0.1)
     oA, oB = opts(m, 5e-4, 2e-4)
     eng = m.engine()
@@ -173,21 +172,6 @@ def test_kernel_completed_events_bitwise(monkeypatch, guard_bands):
     want = run_vector(monkeypatch, "0", train, True, split="1", ext="0")
     got = run_vector(monkeypatch, "0", train, True, split="1", ext="1")
     again = run_vector(monkeypatch, "0", train, False, split="1", ext="1")
-    for k, w in want.items():
-        np.testing.assert_array_equal(got[k], w, err_msg=k)
-        np.testing.assert_array_equal(again[k], w, err_msg=k)
-
-
-def test_lead_records_merged_into_embedder_backward_bitwise(monkeypatch, guard_bands):
-    """Split-lead step with the factor leads' records in the embedder backward's launch
-    (k_bwd_lead_emb: the node workgroups stage while the leads work, then wait for the K*p
-    published leads) against the records' own launch (REDCLIFF_LEAD_EMB=0): bit for bit through
-    pretrain -> acclimate -> combined, ragged last batch included, guard bands intact; a second
-    run repeats the first (the lead counter re-arms every step)."""
-    train = data(64 * 2 + 24, seed=21)
-    want = run_vector(monkeypatch, "0", train, True, split="1", lead_emb="0")
-    got = run_vector(monkeypatch, "0", train, True, split="1", lead_emb="1")
-    again = run_vector(monkeypatch, "0", train, False, split="1", lead_emb="1")
     for k, w in want.items():
         np.testing.assert_array_equal(got[k], w, err_msg=k)
         np.testing.assert_array_equal(again[k], w, err_msg=k)
