@@ -340,8 +340,14 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const int pbx = wait_cnt ? (int)blockIdx.x - d.K * d.p : (int)blockIdx.x;
   (void)pbx;
   RC_PHASE(c.ws, c.wo.total, pbx, 33);
+  // (single sub-block: the BatchNorm operands are requested here and stored after the staging
+  // pass; the multi-sub-block kernel, at 256 registers, stores them at once -- six more live
+  // registers there spilled into accumulation registers and cost it half its occupancy)
   BnOperands bnq{0.0, 0.0, 0.f, 0.f};
-  if (tid < F) bn_affine_load(c, r, E, tid, bnq);  // stored after the first staging pass
+  if (tid < F) {
+    bn_affine_load(c, r, E, tid, bnq);
+    if (MULTI) bn_affine_store(c, r, tid, bnq, alpha, beta, mean, inv);
+  }
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
   const float* f1 = ws + c.wo.f1;
@@ -427,7 +433,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     // together (one memory latency instead of one per round); same terms, same order, same sums
     auto dw_rest = [&]() {
       if (nitem <= RC_BLOCK / 4) return;
-      if (p <= 16 && nitem <= RC_BLOCK) {
+      if (!MULTI && p <= 16 && nitem <= RC_BLOCK) {  // (not at the multi-sub-block kernel's 256 registers)
         float dr4[3][4];
 #pragma unroll
         for (int rd = 0; rd < 3; ++rd) {
@@ -463,8 +469,9 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
     __syncthreads();  // the previous sub-block is done with the LDS tiles
     if (it == 0) {
       rc_stage_all(
-          // (K M1 <= 1,024: one round; with one load per thread TST's 576 took three)
-          rc_seg<4>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
+          // (K M1 <= 1,024: one round; with one load per thread TST's 576 took three.  The
+          // multi-sub-block kernel keeps one: its registers are at the limit)
+          rc_seg<MULTI ? 1 : 4>(K * M1, [&](int e) { return E[c.eo.fc2W + e]; }, [&](int e, float v) { fc2s[e] = v; }),
           rc_seg<4>(M1 * HC, [&](int e) {
             const int m = e / HC, hh = e - m * HC;
             return hh < hc ? E[c.eo.fc1W + (int64_t)m * pH + node * H + h0 + hh] : 0.f;
@@ -484,7 +491,7 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
       rc_stage_all(sR, sT, sX, sF1, sW, sL);
   RC_PHASE(c.ws, c.wo.total, pbx, 47);
 #endif
-      if (tid < F) bn_affine_store(c, r, tid, bnq, alpha, beta, mean, inv);
+      if (!MULTI && tid < F) bn_affine_store(c, r, tid, bnq, alpha, beta, mean, inv);
       if (wait_now) {
         rc_wait_leads(c, c.ws + r * c.wss, wait_cnt, wait_target);
         RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_WAIT, 0);
