@@ -301,7 +301,9 @@ __device__ __forceinline__ void emb_bwd_node(const StepCtx& c, int r, int node, 
   const int pH = p * H, pF = p * F, nF = n * F, HC = EMB_HC, HP = EMB_HC + 1;
   const int h0 = ch * HC, hc = min(HC, H - h0);
   const int nch = rc_nchunk(d);
-  const int nbw = WPB == c.ewpb ? c.enbw : (B + WPB - 1) / WPB, nbw_max = c.enbwm;
+  // (the host's window blocking in the single-sub-block kernels; the multi-sub-block merged kernel
+  // keeps the divisions -- the two more live scalars there cost it a wave per SIMD: 244 -> 256 VGPRs)
+  const int nbw = (!MULTI && WPB == c.ewpb) ? c.enbw : (B + WPB - 1) / WPB, nbw_max = MULTI ? rc_emb_nbw(d) : c.enbwm;
   const int wend = min(B, (wb + 1) * WPB);
   const int grp = node * nch + ch;
   const bool head_grads = (grp == 0);  // fc2 / fc1-bias partials ride on group 0
