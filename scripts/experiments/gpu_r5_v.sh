@@ -1,19 +1,17 @@
 #!/bin/bash
-# Round 5: the split-lead step on one stream (REDCLIFF_SPLIT_ONE=1: lead launch, then the embedder
-# backward and the factor update in one launch, k_emb_bwd_upd at 3 waves per SIMD) against the
-# two-stream split-lead step: bitwise test, C1(K=4) / TST A/B, per-step timeline
-source "$(dirname "$0")/../gpu_steps.sh"
-step v_tests 600 python -u -m pytest tests/test_gpu_forked.py -v --timeout 300 --timeout-method thread -rA
-B="python bench.py --steps 200 --warmup 10 --no-cpu-baseline --no-north-star --replicas 1 --fit-replicas 0 --dp-leg-batch 0 --ref-grid-epochs 0 --no-kernel-times"
-for rep in 1 2; do
-  for cfg in c1k4 c4; do
-    step v_${cfg}_base_$rep 200 $B --config $cfg
-    REDCLIFF_SPLIT_ONE=1 step v_${cfg}_one_$rep 200 $B --config $cfg
-    REDCLIFF_SPLIT_ONE=1 REDCLIFF_SPLIT_LEAD=1 step v_${cfg}_one_forced_$rep 200 $B --config $cfg
-  done
-done
-K="--steps 50 --warmup 10 --no-cpu-baseline --no-north-star --replicas 1 --fit-replicas 0 --dp-leg-batch 0 --ref-grid-epochs 0 --no-kernel-times --config c1k4 --preheat-s 0"
-REDCLIFF_SPLIT_ONE=1 step v_kt 240 timeout -s KILL 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/v/kt -o run -- python bench.py $K
-f=$(ls gpurun_out/v/kt/*kernel_trace.csv 2>/dev/null | head -1)
-[ -n "$f" ] && step v_timeline 60 python scripts/step_timeline.py "$f" --steps 4
-rm -rf gpurun_out/v/kt
+# Round 5 final-tree evidence (final: after the data-parallel register fix, r5ao): the driver's bench command; the single-fit (D4IC) bench leg under
+# rocprofv3 --kernel-trace --stats and its FETCH / WRITE passes (the line's roofline kernel); the
+# R = 128 grid (one stream) kernel stats and passes; GPU suite + smoke
+source "$(dirname "$0")/../gpv_steps.sh"
+step v_bench 600 python bench.py
+S="python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-north-star --replicas 1 --fit-replicas 0 --dp-leg-batch 0 --ref-grid-epochs 0"
+step v_stats 240 timeout -s KILL 220 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/v/stats -o run -- $S
+step v_fetch 240 timeout -s KILL 220 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/v/fetch -o run -- $S
+step v_write 240 timeout -s KILL 220 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/v/write -o run -- $S
+G="python scripts/grid_step.py --replicas 128 --steps 20"
+REDCLIFF_FORK=0 step v_gstats 240 timeout -s KILL 220 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/v/gstats -o run -- $G
+REDCLIFF_FORK=0 step v_gfetch 240 timeout -s KILL 220 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/v/gfetch -o run -- $G
+REDCLIFF_FORK=0 step v_gwrite 240 timeout -s KILL 220 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/v/gwrite -o run -- $G
+rm -f gpurun_out/v/*/run_kernel_trace.csv
+step v_suite 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -rA --durations=10
+step v_smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
