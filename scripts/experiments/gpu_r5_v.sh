@@ -2,7 +2,7 @@
 # Round 5 final-tree evidence (final: after the data-parallel register fix, r5ao): the driver's bench command; the single-fit (D4IC) bench leg under
 # rocprofv3 --kernel-trace --stats and its FETCH / WRITE passes (the line's roofline kernel); the
 # R = 128 grid (one stream) kernel stats and passes; GPU suite + smoke
-source "$(dirname "$0")/../gpv_steps.sh"
+source "$(dirname "$0")/../gpu_steps.sh"
 step v_bench 600 python bench.py
 S="python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-north-star --replicas 1 --fit-replicas 0 --dp-leg-batch 0 --ref-grid-epochs 0"
 step v_stats 240 timeout -s KILL 220 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/v/stats -o run -- $S
