@@ -37,6 +37,7 @@ struct RcGemm {
   int batch, nrep, rident;
   int xcd;  // 1: XCD-aware tile order (rc_gemm_tile)
   int64_t qA, qB, qC, qAux;
+  int extA, extB;  // wave core: elements of A / B one slice spans (set by rc_gemm_launch)
   uint8_t rmap[RC_MAX_ACTIVE];
 };
 
@@ -284,6 +285,96 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
   }
 }
 
+// Wave core: one 64-lane workgroup per 32x32 output tile, no workgroup-wide barriers, so every
+// wave runs on its own and a SIMD holds several to cover the loads' latency (the packed grid's
+// embedder products are 0.4 - 0.6 GFLOP over 128 replicas with K = 30 - 300: short chains of
+// dependent loads, not arithmetic).  v_mfma_f32_32x32x2f32 wants 32 rows of A / columns of B across
+// the lanes: an operand contiguous along m (A^T) or n (B) is loaded straight into the operand
+// registers (coalesced); one contiguous along k (LA: A, LB: B^T) is loaded 16 k x 4 rows per
+// instruction (coalesced) and transposed through the wave's own LDS tile.  16 k per chunk, the next
+// chunk's loads in flight while the current one multiplies.  The k order and the zero padding past K
+// are k_rc_gemm_mfma<64>'s, so an output has the same bits.
+template <bool LA, bool LB>
+__global__ __launch_bounds__(64) static void k_rc_gemm_wave(RcGemm g) {
+  rc_critical_priority();
+  const RcTile tl = rc_gemm_tile(g);
+  const RcGemmZ zz = rc_gemm_z(g, tl.z);
+  const int bz = zz.zb;
+  const float* A = g.A + bz * g.sA + zz.r * g.qA;
+  const float* B = g.B + bz * g.sB + zz.r * g.qB;
+  float* C = g.C + bz * g.sC + zz.r * g.qC;
+  const float* aux = g.aux ? g.aux + zz.r * g.qAux : nullptr;
+  const int lane = threadIdx.x, l31 = lane & 31, kh = lane >> 5, k16 = lane & 15, r4 = lane >> 4;
+  const int n0 = tl.x * 32, m0 = tl.y * 32;
+  // buffer loads with 32-bit offsets (the launcher checks every operand's extent fits); k >= K reads
+  // past the resource's end, which returns 0 -- the zero padding, without a branch.  Rows / columns
+  // past M / N are clamped into the matrix: they only feed outputs that are not stored.
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), (short)0, g.extA * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), (short)0, g.extB * 4, 0x00020000);
+  const int lda = (int)g.lda, ldb = (int)g.ldb;
+  const bool split = g.Kblk < g.K;
+  const RcDiv dkb(split ? g.Kblk : 1);
+  constexpr int OOB = 0x7ffffff0;
+  __shared__ float As[LA ? 16 : 1][33], Bs[LB ? 16 : 1][33];
+  auto load = [&](int k0, float* a_, float* b_) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ka = LA ? k0 + k16 : k0 + 2 * j + kh, kb_ = LB ? k0 + k16 : k0 + 2 * j + kh;
+      const int am = min(m0 + (LA ? r4 + 4 * j : l31), g.M - 1), bn = min(n0 + (LB ? r4 + 4 * j : l31), g.N - 1);
+      int qa = 0, ra_ = ka, qb = 0, rb_ = kb_;
+      if (split) {
+        qa = dkb.div(ka); ra_ = ka - qa * g.Kblk;
+        qb = dkb.div(kb_); rb_ = kb_ - qb * g.Kblk;
+      }
+      const int oa = ka < g.K ? 4 * (qa * (int)g.rA + (g.ta ? ra_ * lda + am : am * lda + ra_)) : OOB;
+      const int ob = kb_ < g.K ? 4 * (qb * (int)g.rB + (g.tb ? bn * ldb + rb_ : rb_ * ldb + bn)) : OOB;
+      a_[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, oa, 0, 0));
+      b_[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, ob, 0, 0));
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  auto mult = [&](const float* a_, const float* b_) {
+    if constexpr (LA || LB) {
+      __syncthreads();  // one wave: orders the previous chunk's operand reads before these writes
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if constexpr (LA) As[k16][r4 + 4 * j] = a_[j];
+        if constexpr (LB) Bs[k16][r4 + 4 * j] = b_[j];
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float av = LA ? As[LA ? 2 * j + kh : 0][l31] : a_[j];
+      const float bv = LB ? Bs[LB ? 2 * j + kh : 0][l31] : b_[j];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
+  };
+  float a0[8], b0[8], a1[8], b1[8];
+  if (g.K > 0) load(0, a0, b0);
+  for (int k0 = 0; k0 < g.K; k0 += 32) {
+    if (k0 + 16 < g.K) load(k0 + 16, a1, b1);
+    mult(a0, b0);
+    if (k0 + 16 >= g.K) break;
+    if (k0 + 32 < g.K) load(k0 + 32, a0, b0);
+    mult(a1, b1);
+  }
+  const int gn = n0 + l31;
+  if (gn >= g.N) return;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int gm = m0 + mf_row(reg, lane);
+    if (gm >= g.M) continue;
+    float* cp = C + (int64_t)gm * g.ldc + gn;
+    float v = g.beta == 0.f ? g.alpha * acc[reg] : g.alpha * acc[reg] + g.beta * *cp;
+    if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
+    else if (g.epi == RC_EPI_MASK) v = aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
+    *cp = v;
+  }
+}
+
 inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char* what) {
   if (g0.M <= 0 || g0.N <= 0 || batch <= 0 || g0.nrep <= 0) return 0;
   if (batch > 65535) { rc_set_error("%s: batch %d > 65535", what, batch); return REDCLIFF_ELIMIT; }
@@ -311,9 +402,32 @@ inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char
   }();
   const char* core = getenv("REDCLIFF_GEMM_CORE");  // read per launch: the tests switch it
   const bool valu = core != nullptr && core[0] == 'v';
+  // Core choice (same bits): REDCLIFF_GEMM_CORE=wave (wave core, k-contiguous operands through LDS),
+  // wd (wave core, every operand loaded straight into the lanes), mfma (LDS-tiled workgroups), valu.
+  // Default, measured by product on the R = 128 D4IC grid (profiles/r05_gemm_wave_ab.txt): the wave
+  // core where both operands load straight into the lanes (A^T, B: dW 33 -> 20 us, dfc1W 25 -> 20) or
+  // one column tile reads the rows (N <= 32: graph conv ~26 -> 22); the LDS-tiled workgroups where a
+  // k-contiguous operand is re-read by several column tiles (dZ 28 vs 36, dT 24 vs 27, fc1 even).
+  const bool wd = core != nullptr && core[0] == 'w' && core[1] == 'd';
+  const bool wave = core != nullptr ? core[0] == 'w' : ((g.ta == 1 && g.tb == 0) || g.N <= 32);
   const char* xe = getenv("REDCLIFF_GEMM_XCD");  // XCD-aware tile order: default on; 0 = dispatch order
   g.xcd = !(xe && xe[0] == '0');
   const int64_t t64 = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * batch;
+  // the wave core addresses its operands with 32-bit offsets: only slices whose extent fits
+  const int64_t nkb = (g.K + g.Kblk - 1) / g.Kblk;
+  const int64_t extA = g.K <= 0 ? 1 : (nkb - 1) * g.rA + (g.ta ? (int64_t)(g.Kblk - 1) * g.lda + g.M : (int64_t)(g.M - 1) * g.lda + g.Kblk);
+  const int64_t extB = g.K <= 0 ? 1 : (nkb - 1) * g.rB + (g.tb ? (int64_t)(g.N - 1) * g.ldb + g.Kblk : (int64_t)(g.Kblk - 1) * g.ldb + g.N);
+  if (wave && extA < (1 << 28) && extB < (1 << 28) && g.rA >= 0 && g.rB >= 0) {
+    g.extA = (int)extA;
+    g.extB = (int)extB;
+    dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, batch);
+    const bool la = !wd && !g.ta, lb = !wd && g.tb;
+    if (la && lb) hipLaunchKernelGGL((k_rc_gemm_wave<true, true>), grid, dim3(64), 0, s, g);
+    else if (la) hipLaunchKernelGGL((k_rc_gemm_wave<true, false>), grid, dim3(64), 0, s, g);
+    else if (lb) hipLaunchKernelGGL((k_rc_gemm_wave<false, true>), grid, dim3(64), 0, s, g);
+    else hipLaunchKernelGGL((k_rc_gemm_wave<false, false>), grid, dim3(64), 0, s, g);
+    return rc_check(hipGetLastError(), what);
+  }
   const bool small = tile_env == 32 || (tile_env != 64 && t64 < 512);
   if (small) {
     dim3 grid((g.N + 31) / 32, (g.M + 31) / 32, batch);

@@ -136,8 +136,10 @@ def test_hip_gemm_against_fp64():
 
 
 def test_gemm_cores_bitwise(monkeypatch):
-    """The matrix-core GEMM (k_rc_gemm_mfma: 32x32x2 / 16x16x4 fp32 MFMA) and the vector-ALU
-    one (k_rc_gemm, REDCLIFF_GEMM_CORE=valu) give the same bits: both are in-order fmaf chains
+    """The matrix-core GEMM (k_rc_gemm_mfma: 32x32x2 / 16x16x4 fp32 MFMA), the vector-ALU
+    one (k_rc_gemm, REDCLIFF_GEMM_CORE=valu) and the wave core (k_rc_gemm_wave, one wave per
+    32x32 tile, k-contiguous operands transposed through the wave's LDS tile: REDCLIFF_GEMM_CORE=wave;
+    every operand loaded straight into the lanes: wd) give the same bits: all are in-order fmaf chains
     over k.  Shapes cover both tile sizes (64x64 tiles when the launch has >= 512 of them),
     ragged edges and all transpose combinations."""
     from redcliff_amd.generic import _raw_bmm
@@ -151,9 +153,10 @@ def test_gemm_cores_bitwise(monkeypatch):
                 b = torch.randn((nb,) + ((N, K) if tb else (K, N)), generator=g).cuda()
                 monkeypatch.delenv("REDCLIFF_GEMM_CORE", raising=False)
                 got = _raw_bmm(a, b, ta, tb).cpu().numpy()
-                monkeypatch.setenv("REDCLIFF_GEMM_CORE", "valu")
-                want = _raw_bmm(a, b, ta, tb).cpu().numpy()
-                np.testing.assert_array_equal(got, want, err_msg="M=%d N=%d K=%d ta=%d tb=%d" % (M, N, K, ta, tb))
+                for core in ("valu", "wave", "wd", "mfma"):
+                    monkeypatch.setenv("REDCLIFF_GEMM_CORE", core)
+                    want = _raw_bmm(a, b, ta, tb).cpu().numpy()
+                    np.testing.assert_array_equal(got, want, err_msg="%s M=%d N=%d K=%d ta=%d tb=%d" % (core, M, N, K, ta, tb))
 
 
 @pytest.mark.parametrize("name", ["cemb", "vanilla"])
