@@ -77,8 +77,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
 }
 
 // f1 = sum of the split-K partials + bias; w = fc2(relu(f1)).  grid (ceil(B / 4), R): one window
-// per wave, lane m sums the partials in 4 interleaved chains (all loads in flight), combined in
-// fixed order; lane k forms w[k] from the wave's relu(f1) by shuffles (no LDS, no barrier).
+// per wave, lane m sums the partials in 4 interleaved chains, combined in fixed order; lane k forms
+// w[k] from the wave's relu(f1) (no LDS, no barrier).  Every load is issued before the first use:
+// the partials four at a time (clamped indices, no branch per load) and lane k's fc2 row into
+// registers 32 terms at a time; relu(f1[m]) is read with v_readlane.  (The previous form -- a branch per partial and a
+// global load per fc2 term inside the chain -- compiled to 68 serial load round trips per wave.)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
@@ -87,25 +90,40 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   const int M1 = d.M1, K = d.K;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
-  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + lane;
-  float t4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (lane < M1) {
+  const int ml = lane < M1 ? lane : M1 - 1;
+  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + ml;
+  const int64_t pst = (int64_t)d.Bmax * M1;
+  // lane k's fc2 row (lanes >= K read row 0 and do not store), 32 terms per round of loads
+  const float* w2 = E + c.eo.fc2W + (lane < K ? lane : 0) * M1;
+  float w2r[32];
 #pragma unroll
-    for (int q = 0; q < 64; ++q)  // nsplit <= 64
-      if (q < nsplit) t4[q & 3] += part[(int64_t)q * d.Bmax * M1];
+  for (int u = 0; u < 32; ++u) w2r[u] = w2[min(u, M1 - 1)];
+  const float fb1 = E[c.eo.fc1b + ml];
+  float t4[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < nsplit; q0 += 4) {  // nsplit <= 64; t4[q & 3] += partial q, q ascending
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = part[(int64_t)min(q0 + u, nsplit - 1) * pst];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (q0 + u < nsplit) t4[u] += v[u];
   }
   float v = 0.f;
   if (lane < M1) {
-    v = ((t4[0] + t4[1]) + (t4[2] + t4[3])) + E[c.eo.fc1b + lane];
+    v = ((t4[0] + t4[1]) + (t4[2] + t4[3])) + fb1;
     ws[c.wo.f1 + (int64_t)b * M1 + lane] = v;
   }
   const float rv = fmaxf(v, 0.f);
   // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]), m ascending
   float a = 0.f;
-  const float* w2 = E + c.eo.fc2W + (lane < K ? lane : 0) * M1;
-  for (int mm = 0; mm < M1; ++mm) {
-    const float fm = __shfl(rv, mm, 64);
-    if (lane < K) a = fmaf(w2[mm], fm, a);
+  for (int m0 = 0; m0 < M1; m0 += 32) {  // M1 <= 64
+    if (m0 > 0) {
+#pragma unroll
+      for (int u = 0; u < 32; ++u) w2r[u] = w2[min(m0 + u, M1 - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (m0 + u < M1) a = fmaf(w2r[u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), m0 + u)), a);
   }
   if (lane < K) ws[c.wo.w + (int64_t)b * K + lane] = a + E[c.eo.fc2b + lane];
 }
@@ -129,11 +147,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
   float t = 0.f;
   if (ok && fac_grad) {
+    // four loads in flight at a time (clamped channel indices, no branch per load), added in j order
     const float* dw = ws + c.wo.dwp + (int64_t)b * K + k;
+    const int nu = (p + 3) >> 2;  // p <= 64
+    for (int u0 = 0; u0 < nu; u0 += 4) {
+      float v[4];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {  // p <= 64
-      const int j = g + 4 * u;
-      if (j < p) t += dw[(int64_t)j * d.Bmax * K];
+      for (int u = 0; u < 4; ++u) v[u] = dw[(int64_t)min(g + 4 * (u0 + u), p - 1) * d.Bmax * K];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (g + 4 * (u0 + u) < p) t += v[u];
     }
   }
   t += __shfl_xor(t, 1);
@@ -150,9 +173,15 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   for (int e = tid; e < WPW * M1; e += RC_BLOCK) {
     const int sw = e / M1, m = e - sw * M1, bb = b0 + sw;
     if (bb >= B) continue;
+    float w2[16];  // K <= 16: fc2W[.][m] requested together, not once per term of the chain
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) w2[kk] = E[c.eo.fc2W + min(kk, K - 1) * M1 + m];
     float gg = 0.f;
-    if (f1[(int64_t)bb * M1 + m] > 0.f)
-      for (int kk = 0; kk < K; ++kk) gg += drs[sw * K + kk] * E[c.eo.fc2W + kk * M1 + m];
+    if (f1[(int64_t)bb * M1 + m] > 0.f) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk)
+        if (kk < K) gg += drs[sw * K + kk] * w2[kk];
+    }
     df1[(int64_t)bb * M1 + m] = gg;
   }
 }
@@ -362,6 +391,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
     const float* Si = S + i1 * pp2 + ch * p;
     const float* xw = xb + w * pF + f;
     float t = 0.f;
+#pragma unroll 4
     for (int cp = 0; cp < p; ++cp) t = fmaf(Si[cp], xw[cp * F], t);
     T[w * pnF + ch * nF + (i1 + 1) * F + f] = t;
   }
@@ -422,6 +452,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
       const int w = row / p, ch = row - w * p;
       const float* dtw = dT + w * pnF + f;
       float dx = 0.f;
+#pragma unroll 4
       for (int cp = 0; cp < p; ++cp)
         for (int i = 0; i < n; ++i) dx = fmaf(S[i * pp2 + cp * p + ch], dtw[cp * nF + i * F], dx);
       const float x = xr[w * pF + f * p + ch];
@@ -438,6 +469,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
     for (int w = 0; w < nw; ++w) {
       const float* a = dT + w * pnF + ch * nF + i * F;
       const float* bq = x0 + w * pF + cp * F;
+#pragma unroll 4
       for (int ff = 0; ff < F; ++ff) t = fmaf(a[ff], bq[ff], t);
     }
     dS[i * pp2 + rem] = t;

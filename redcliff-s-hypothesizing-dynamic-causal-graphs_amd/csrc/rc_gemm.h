@@ -188,6 +188,37 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm(RcGemm g) {
   }
 }
 
+// Epilogue of the matrix-core kernels: this lane's NR outputs of column gn (rows row(reg)),
+// C = alpha acc + beta C, then ReLU or the (aux > 0) mask.  The C / aux operands of all NR rows are
+// requested together (rows past M clamped, not stored) -- one branch per row around each load made
+// the compiler wait for every load in turn (16 round trips per wave for dZ's mask).
+template <int NR, typename RowF>
+__device__ inline void rc_gemm_store(const RcGemm& g, float* C, const float* aux, int bz, int gn, const float (&av)[NR],
+                                     RowF row) {
+  // one operand array: the mask's aux rows, else C's rows when beta != 0 (both at once -- no caller
+  // does that -- reads C per row)
+  const bool mask = g.epi == RC_EPI_MASK, bc = g.beta != 0.f;
+  float xv[NR];
+#pragma unroll
+  for (int reg = 0; reg < NR; ++reg) xv[reg] = 0.f;
+  if (mask || bc) {
+    const float* src = mask ? aux + bz * g.sAux : C;
+    const int64_t ld = mask ? g.ldaux : g.ldc;
+#pragma unroll
+    for (int reg = 0; reg < NR; ++reg) xv[reg] = src[(int64_t)min(row(reg), g.M - 1) * ld + gn];
+  }
+#pragma unroll
+  for (int reg = 0; reg < NR; ++reg) {
+    const int gm = row(reg);
+    if (gm >= g.M) continue;
+    const float cv = !bc ? 0.f : mask ? C[(int64_t)gm * g.ldc + gn] : xv[reg];
+    float v = !bc ? g.alpha * av[reg] : g.alpha * av[reg] + g.beta * cv;
+    if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
+    else if (mask) v = xv[reg] > 0.f ? v : 0.f;
+    C[(int64_t)gm * g.ldc + gn] = v;
+  }
+}
+
 // Matrix-core variant: the same tiles, staging and workgroup shape as k_rc_gemm, the
 // products on the fp32 matrix cores.  TT = 64: each of the 4 waves owns a 32x32 quarter
 // (v_mfma_f32_32x32x2f32); TT = 32: a 16x16 quarter (v_mfma_f32_16x16x4f32).  The fp32 MFMA
@@ -272,17 +303,10 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
   constexpr int NR = TT == 64 ? 16 : 4;
   const int gn = n0 + wn + (TT == 64 ? (lane & 31) : (lane & 15));
   if (gn >= g.N) return;
+  float accv[NR];
 #pragma unroll
-  for (int reg = 0; reg < NR; ++reg) {
-    const int gm = m0 + wm + (TT == 64 ? mf_row(reg, lane) : 4 * (lane >> 4) + reg);
-    if (gm >= g.M) continue;
-    float* cp = C + (int64_t)gm * g.ldc + gn;
-    const float a = TT == 64 ? acc32[reg] : acc16[reg];
-    float v = g.beta == 0.f ? g.alpha * a : g.alpha * a + g.beta * *cp;
-    if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
-    else if (g.epi == RC_EPI_MASK) v = aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
-    *cp = v;
-  }
+  for (int reg = 0; reg < NR; ++reg) accv[reg] = TT == 64 ? acc32[reg] : acc16[reg];
+  rc_gemm_store<NR>(g, C, aux, bz, gn, accv, [&](int reg) { return m0 + wm + (TT == 64 ? mf_row(reg, lane) : 4 * (lane >> 4) + reg); });
 }
 
 // Wave core: one 64-lane workgroup per 32x32 output tile, no workgroup-wide barriers, so every
@@ -295,7 +319,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
 // chunk's loads in flight while the current one multiplies.  The k order and the zero padding past K
 // are k_rc_gemm_mfma<64>'s, so an output has the same bits.
 template <bool LA, bool LB>
-__global__ __launch_bounds__(64) static void k_rc_gemm_wave(RcGemm g) {
+__global__ __launch_bounds__(64, 5) static void k_rc_gemm_wave(RcGemm g) {
   rc_critical_priority();
   const RcTile tl = rc_gemm_tile(g);
   const RcGemmZ zz = rc_gemm_z(g, tl.z);
@@ -363,16 +387,10 @@ __global__ __launch_bounds__(64) static void k_rc_gemm_wave(RcGemm g) {
   }
   const int gn = n0 + l31;
   if (gn >= g.N) return;
+  float accv[16];
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int gm = m0 + mf_row(reg, lane);
-    if (gm >= g.M) continue;
-    float* cp = C + (int64_t)gm * g.ldc + gn;
-    float v = g.beta == 0.f ? g.alpha * acc[reg] : g.alpha * acc[reg] + g.beta * *cp;
-    if (g.epi == RC_EPI_RELU) v = fmaxf(v, 0.f);
-    else if (g.epi == RC_EPI_MASK) v = aux[bz * g.sAux + (int64_t)gm * g.ldaux + gn] > 0.f ? v : 0.f;
-    *cp = v;
-  }
+  for (int reg = 0; reg < 16; ++reg) accv[reg] = acc[reg];
+  rc_gemm_store<16>(g, C, aux, bz, gn, accv, [&](int reg) { return m0 + mf_row(reg, lane); });
 }
 
 inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char* what) {

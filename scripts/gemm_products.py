@@ -23,7 +23,7 @@ def main():
         for r in csv.DictReader(f):
             if args.match not in r["Kernel_Name"]:
                 continue
-            key = (r["Kernel_Name"].split("(")[0].replace("void ", ""),
+            key = (r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0],
                    int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
             if key not in by:
                 order.append(key)
