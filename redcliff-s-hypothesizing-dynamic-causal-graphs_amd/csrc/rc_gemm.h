@@ -422,12 +422,11 @@ inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char
   const bool valu = core != nullptr && core[0] == 'v';
   // Core choice (same bits): REDCLIFF_GEMM_CORE=wave (wave core, k-contiguous operands through LDS),
   // wd (wave core, every operand loaded straight into the lanes), mfma (LDS-tiled workgroups), valu.
-  // Default, measured by product on the R = 128 D4IC grid (profiles/r05_gemm_wave_ab.txt): the wave
-  // core where both operands load straight into the lanes (A^T, B: dW 33 -> 20 us, dfc1W 25 -> 20) or
-  // one column tile reads the rows (N <= 32: graph conv ~26 -> 22); the LDS-tiled workgroups where a
-  // k-contiguous operand is re-read by several column tiles (dZ 28 vs 36, dT 24 vs 27, fc1 even).
+  // Default: the wave core for every product.  Measured by product on the R = 128 D4IC grid, one stream
+  // (profiles/r05_gemm_wave_ab.txt, r5aw): dW 33 -> 19.4 us, dfc1W 25 -> 20.2, graph conv ~26 -> 18.1,
+  // dZ 25.0 -> 22.9, fc1 22.8 -> 21.6, dT 25.5 -> 25.7 against the LDS-tiled workgroups.
   const bool wd = core != nullptr && core[0] == 'w' && core[1] == 'd';
-  const bool wave = core != nullptr ? core[0] == 'w' : ((g.ta == 1 && g.tb == 0) || g.N <= 32);
+  const bool wave = core == nullptr || core[0] == 'w';
   const char* xe = getenv("REDCLIFF_GEMM_XCD");  // XCD-aware tile order: default on; 0 = dispatch order
   g.xcd = !(xe && xe[0] == '0');
   const int64_t t64 = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * batch;
