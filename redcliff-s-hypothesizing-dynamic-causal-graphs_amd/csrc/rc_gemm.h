@@ -424,9 +424,12 @@ inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char
   // wd (wave core, every operand loaded straight into the lanes), mfma (LDS-tiled workgroups), valu.
   // Default: the wave core for every product.  Measured by product on the R = 128 D4IC grid, one stream
   // (profiles/r05_gemm_wave_ab.txt, r5aw): dW 33 -> 19.4 us, dfc1W 25 -> 20.2, graph conv ~26 -> 18.1,
-  // dZ 25.0 -> 22.9, fc1 22.8 -> 21.6, dT 25.5 -> 25.7 against the LDS-tiled workgroups.
+  // dZ 25.0 -> 22.9, fc1 22.8 -> 21.6, dT 25.5 -> 25.7 against the LDS-tiled workgroups.  A single
+  // fit's products (one replica: C5, p = 64, B = 128) keep the LDS-tiled workgroups, whose k-contiguous
+  // tiles are shared by the workgroup's four column quarters: C5 with the wave core 0.4351 -> 0.4558 ms
+  // per step (profiles/r05_c5_gemm_core_ab_ax.jsonl).
   const bool wd = core != nullptr && core[0] == 'w' && core[1] == 'd';
-  const bool wave = core == nullptr || core[0] == 'w';
+  const bool wave = core == nullptr ? g0.nrep > 1 : core[0] == 'w';
   const char* xe = getenv("REDCLIFF_GEMM_XCD");  // XCD-aware tile order: default on; 0 = dispatch order
   g.xcd = !(xe && xe[0] == '0');
   const int64_t t64 = (int64_t)((g.N + 63) / 64) * ((g.M + 63) / 64) * batch;
