@@ -503,30 +503,74 @@ def synthetic_grid_points():
     return [kp for kp in order for _ in range(counts[kp])]
 
 
+SYN_GRID_NOTE = (
+    "models the synthetic grid as its data sets define it: K = nsup = the numF of the data set's name, and for "
+    "K = 1 FACTOR_COS_SIM_COEFF is left undivided (no cosine pairs exist, the term is 0).  The reference driver "
+    "as written does not train 255 of these 990 tasks: it reads K as int(data_set_name[4]) "
+    "(train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:99-100), so 'numF10' gives K = 1, and "
+    "for K = 1 it divides FACTOR_COS_SIM_COEFF by sum([]) = 0 (:101-102), a ZeroDivisionError before the fit "
+    "starts (the 225 numF1 tasks and the 30 numF10 tasks)")
+
+
+def ref_grid_shares():
+    """Both reference grids dealt to an 8-GPU node by class-aware, FLOP-weighted sharding
+    (redcliff_amd.shard_grid, min_piece 32): {grid: (points, class of each point, cost of each point,
+    [point indices of share s for s in 0..7], [summed cost of share s])}."""
+    from redcliff_amd import shard_grid
+    out = {}
+    pts = tst_grid_points()
+    base = CONFIGS["c4"]
+    # cost of a point: its shape class's algorithmic FLOPs per window (flops_per_window), so the shares
+    # hold equal work, not equal point counts (r05 shares cut by count ran 0.12 - 0.20 s,
+    # profiles/r05_refgrid_shares_h.jsonl)
+    cls = [(q["lag"], q["layers"]) for q in pts]
+    cost = [flops_per_window(dict(base, F=q["lag"], n=q["layers"], T=q["lag"] + 4))["total"] for q in pts]
+    shares = [shard_grid(len(pts), 8, s, classes=cls, cost=cost, min_piece=32) for s in range(8)]
+    out["tst"] = (pts, cls, cost, shares, [float(sum(cost[i] for i in sh)) for sh in shares])
+    kp = synthetic_grid_points()
+    # cost per fit as above: the embedder's O(p) work dominates the small-K classes (a K * p^2 cost put
+    # 405 of the 990 fits on share 7, 1.07 s against 0.15 s on share 0)
+    cost = [flops_per_window(_syn_cfg(k, p))["total"] for k, p in kp]
+    shares = [shard_grid(len(kp), 8, s, classes=kp, cost=cost, min_piece=32) for s in range(8)]
+    out["synthetic"] = (kp, kp, cost, shares, [float(sum(cost[i] for i in sh)) for sh in shares])
+    return out
+
+
+def _syn_cfg(K, p):
+    """The synthetic grid's model at (K, p) (cached args: gen_lag 4, h 25, DGCNN 16 / 3 / 100)."""
+    return dict(CONFIGS["c4"], p=p, K=K, nsup=K, F=16, n=3, T=100, label_T=100)
+
+
 def reference_grids(args, dev, rank, world, dist):
-    """fits/hour on one GPU's share of the reference's own grids, dealt to an 8-GPU node by class-aware
-    sharding (redcliff_amd.shard_grid; rank r of an N <= 8 GPU run fits share r):
+    """fits/hour on the reference's own grids, dealt to an 8-GPU node by class-aware sharding
+    (ref_grid_shares):
 
     * TST grid, 1536 points: one TST-shaped data set (p = 12, K = 9, nsup = 3, h = 25, gen_lag 4) for
       every point; the share's shape classes (embed_lag x graph-conv layers) are packs whose replicas
-      mix the four pretrain / acclimation schedules.  Timed against a control: the same packs with
-      every replica on replica 0's schedule (the uniform-pack figure).
+      mix the four pretrain / acclimation schedules.  Share `share` is also timed against a control:
+      the same packs with every replica on replica 0's schedule (the uniform-pack figure).
     * synthetic grid, 990 data sets: one model config (h = 25, gen_lag 4, DGCNN 16 / 3 / 100, K =
       nsup = numF) per data set; each (K, p) class of the share is a pack with PerReplica data and
-      true graphs (sVAR-shaped windows, one seeded set per replica).
+      true graphs (sVAR-shaped windows, one seeded set per replica).  See SYN_GRID_NOTE for which grid.
+
+    Rank r of an N-GPU run fits share r (mod 8); the timed regions are max-over-ranks, so with 8 ranks the
+    per-grid seconds ARE the node's.  A one-GPU run fits share 0 and then, one after the other on the same
+    GPU, the grid's COSTLIEST share (the largest summed cost), and derives the node's figure from the
+    slowest share timed: node_fits_per_hour = grid fits x 3600 / max(share seconds) -- a 1-GPU per-share
+    timing, no collective (the shares share nothing).
 
     Every fit runs a fixed schedule scaled 1/10 from the reference's (max_iter 300 -> 30 epochs,
     pretrain / acclimation epochs / 10, rounded up) over 8 training and 2 validation batches of 128
     windows, early stopping disabled so every fit does the same work, per-epoch GC tracking and
     validation on the GPU."""
     import redcliff_amd
-    from redcliff_amd import PerReplica, ReplicaPack, fit_packs, shard_grid
+    from redcliff_amd import PerReplica, ReplicaPack, fit_packs
     share = rank % 8 if getattr(args, "ref_grid_share", -1) < 0 else args.ref_grid_share
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
     prof = []
+    grids = ref_grid_shares()
     out = {"share": "%d of 8 (class-aware shard_grid, FLOP-weighted, min_piece 32)" % share, "epochs_per_fit": E,
-           "train_windows": ntr * B,
-           "val_windows": nva * B}
+           "train_windows": ntr * B, "val_windows": nva * B}
 
     def run(packs, warm=True):
         """[(models, opts, train, val, gc)] -> seconds for all packs, fitted concurrently (fit_packs: one
@@ -553,22 +597,21 @@ def reference_grids(args, dev, rank, world, dist):
             prof.append([{"R": pk.R, "host_ms_per_epoch": [round(1e3 * float(v), 3) for v in
                                                           np.mean(np.asarray(pk.last_profile), axis=0)]}
                          for pk, _, _, _ in built if pk.last_profile])
+        del built
         return el
 
-    # ---- TST grid share
-    pts = tst_grid_points()
+    # ---- TST grid
+    pts, _, _, tshares, tcost = grids["tst"]
     base = CONFIGS["c4"]
-    # cost of a point: its shape class's algorithmic FLOPs per window (flops_per_window), so the shares
-    # hold equal work, not equal point counts (r05 shares cut by count ran 0.12 - 0.20 s,
-    # profiles/r05_refgrid_shares_h.jsonl)
-    tst_cost = [flops_per_window(dict(base, F=q["lag"], n=q["layers"], T=q["lag"] + 4))["total"] for q in pts]
-    mine = shard_grid(len(pts), 8, share, classes=[(q["lag"], q["layers"]) for q in pts], cost=tst_cost, min_piece=32)
-    classes = {}
-    for i in mine:
-        classes.setdefault((pts[i]["lag"], pts[i]["layers"]), []).append(i)
     sched = lambda q: (-(-q["pre"] // 10), -(-q["acc"] // 10))  # noqa: E731  (1/10 of the reference's epochs)
 
-    def tst_packs(uniform):
+    def tst_classes(s):
+        classes = {}
+        for i in tshares[s]:
+            classes.setdefault((pts[i]["lag"], pts[i]["layers"]), []).append(i)
+        return classes
+
+    def tst_packs(classes, uniform):
         packs = []
         for (lag, layers), idx in classes.items():
             c = dict(base, F=lag, n=layers, T=lag + 4)
@@ -588,45 +631,73 @@ def reference_grids(args, dev, rank, world, dist):
             packs.append((ms, os_, train, val, gc))
         return packs
 
-    el_mixed = run(tst_packs(False))
-    el_uni = run(tst_packs(True), warm=False)  # the same shapes: warm
-    n = len(mine)
-    out["tst"] = {"fits": n, "packs": [{"embed_lag": k[0], "graph_conv_layers": k[1], "replicas": len(v),
-                                        "schedules": sorted(set(sched(pts[i]) for i in v))}
-                                       for k, v in classes.items()],
-                  "seconds": round(el_mixed, 3), "fits_per_hour": round(n * 3600.0 / el_mixed, 1),
-                  "uniform_schedule_seconds": round(el_uni, 3),
-                  "uniform_schedule_fits_per_hour": round(n * 3600.0 / el_uni, 1),
-                  "mixed_over_uniform_time": round(el_mixed / el_uni, 3)}
-    # ---- synthetic grid share
-    kp = synthetic_grid_points()
-    syn_cfg = lambda K, p: dict(base, p=p, K=K, nsup=K, F=16, n=3, T=100, label_T=100)  # noqa: E731
-    # cost per fit as above: the embedder's O(p) work dominates the small-K classes (a K * p^2 cost put
-    # 405 of the 990 fits on share 7, 1.07 s against 0.15 s on share 0)
-    mine = shard_grid(len(kp), 8, share, classes=kp, cost=[flops_per_window(syn_cfg(k, p))["total"] for k, p in kp],
-                      min_piece=32)
-    by = {}
-    for i in mine:
-        by.setdefault(kp[i], []).append(i)
-    packs = []
-    for (K, p), idx in by.items():
-        c = syn_cfg(K, p)
-        trains, vals, gcs, ms, os_ = [], [], [], [], []
-        for i in idx:
-            X, Y = synth(c, (ntr + nva) * B, seed=9000 + i)
-            trains.append([(X[j:j + B], Y[j:j + B]) for j in range(0, ntr * B, B)])
-            vals.append([(X[j:j + B], Y[j:j + B]) for j in range(ntr * B, (ntr + nva) * B, B)])
-            rng = np.random.RandomState(i)
-            gcs.append([(rng.rand(p, p, 2) < 0.3).astype(np.float64) for _ in range(K)])
-            m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=11000 + i, pre=10, acc=10).to(dev)
-            ms.append(m)
-            os_.append(adam_pair(m, c))
-        packs.append((ms, os_, PerReplica(trains), PerReplica(vals), PerReplica(gcs)))
-    el_syn = run(packs)
-    n = len(mine)
-    out["synthetic"] = {"fits": n, "packs": [{"K": k[0], "p": k[1], "replicas": len(v)} for k, v in by.items()],
-                        "seconds": round(el_syn, 3), "fits_per_hour": round(n * 3600.0 / el_syn, 1),
-                        "data": "PerReplica: one sVAR-shaped data set and one set of true graphs per fit"}
+    def tst_share(s, control):
+        classes = tst_classes(s)
+        el = run(tst_packs(classes, False))
+        n = len(tshares[s])
+        r = {"share": s, "fits": n, "cost": tcost[s],
+             "packs": [{"embed_lag": k[0], "graph_conv_layers": k[1], "replicas": len(v),
+                        "schedules": sorted(set(sched(pts[i]) for i in v))} for k, v in classes.items()],
+             "seconds": round(el, 3), "fits_per_hour": round(n * 3600.0 / el, 1)}
+        if control:
+            el_uni = run(tst_packs(classes, True), warm=False)  # the same shapes: warm
+            r.update(uniform_schedule_seconds=round(el_uni, 3),
+                     uniform_schedule_fits_per_hour=round(n * 3600.0 / el_uni, 1),
+                     mixed_over_uniform_time=round(el / el_uni, 3))
+        return r
+
+    # ---- synthetic grid
+    kp, _, _, sshares, scost = grids["synthetic"]
+
+    def syn_share(s):
+        by = {}
+        for i in sshares[s]:
+            by.setdefault(kp[i], []).append(i)
+        packs = []
+        for (K, p), idx in by.items():
+            c = _syn_cfg(K, p)
+            trains, vals, gcs, ms, os_ = [], [], [], [], []
+            for i in idx:
+                X, Y = synth(c, (ntr + nva) * B, seed=9000 + i)
+                trains.append([(X[j:j + B], Y[j:j + B]) for j in range(0, ntr * B, B)])
+                vals.append([(X[j:j + B], Y[j:j + B]) for j in range(ntr * B, (ntr + nva) * B, B)])
+                rng = np.random.RandomState(i)
+                gcs.append([(rng.rand(p, p, 2) < 0.3).astype(np.float64) for _ in range(K)])
+                m = build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=11000 + i, pre=10,
+                                acc=10).to(dev)
+                ms.append(m)
+                os_.append(adam_pair(m, c))
+            packs.append((ms, os_, PerReplica(trains), PerReplica(vals), PerReplica(gcs)))
+        el = run(packs)
+        n = len(sshares[s])
+        return {"share": s, "fits": n, "cost": scost[s],
+                "packs": [{"K": k[0], "p": k[1], "replicas": len(v)} for k, v in by.items()],
+                "seconds": round(el, 3), "fits_per_hour": round(n * 3600.0 / el, 1)}
+
+    for name, timer, gcost, n_all in (("tst", lambda s, first: tst_share(s, first), tcost, len(pts)),
+                                      ("synthetic", lambda s, first: syn_share(s), scost, len(kp))):
+        costliest = int(np.argmax(gcost))
+        todo = [share] + ([costliest] if world == 1 and costliest != share else [])
+        if world == 1 and getattr(args, "ref_grid_all_shares", False):
+            todo = [share] + [s for s in range(8) if s != share]
+        runs = []
+        for j, s_ in enumerate(todo):
+            runs.append(timer(s_, j == 0))
+            # progress on stderr (a long all-shares run must not look hung to the GPU harness)
+            print("reference_grids: %s share %d: %d fits, %.3f s" % (name, s_, runs[-1]["fits"], runs[-1]["seconds"]),
+                  file=sys.stderr, flush=True)
+        g = dict(runs[0])
+        g["shares_timed"] = runs
+        g["costliest_share"] = costliest
+        g["share_costs"] = [round(x / max(gcost), 4) for x in gcost]
+        slowest = max(r_["seconds"] for r_ in runs)
+        g["node_fits_per_hour"] = round(n_all * 3600.0 / slowest, 1)
+        g["node_fits_per_hour_basis"] = (
+            "%d-GPU run: every rank fits its own share, seconds are max over ranks" % world if world > 1 else
+            "1-GPU per-share timing, no collective: %d grid fits x 3600 / the slowest of the timed shares %s "
+            "(%.3f s)" % (n_all, [r_["share"] for r_ in runs], slowest))
+        out[name] = g
+    out["synthetic"]["grid"] = SYN_GRID_NOTE
     if prof:
         out["host_profile"] = {"segments": "enqueue evaluation, enqueue next training epoch, wait for the device, "
                                            "digest the epoch", "runs": prof}
@@ -705,6 +776,10 @@ def mode_fit(args, dev, rank, world, dist, holder):
         ns = {"workload": cn["workload"], "windows_per_s": round(nsteps * cn["B"] / nel, 1),
               "ms_per_step": round(1e3 * nel / nsteps, 4), "steps": nsteps, "target_gpu_over_cpu": 50.0}
 
+    c5 = None
+    if world == 1 and args.c5_steps > 0:
+        c5 = stress_leg(args, dev, rank)
+
     dpl = None
     dpg = None
     if args.dp_leg_batch > 0 and dist is None and world == 1:
@@ -751,7 +826,45 @@ def mode_fit(args, dev, rank, world, dist, holder):
             ns["cpu_baseline"] = cpu_baseline(CONFIGS["c1k4"], args.cpu_seconds * 2.0 / 3.0)
             ns["gpu_over_cpu"] = round(ns["windows_per_s"] / ns["cpu_baseline"]["value"], 1)
     out["north_star_config"] = ns
+    out["stress_config"] = c5
     return out
+
+
+def stress_leg(args, dev, rank):
+    """BASELINE configs[4] (p = 64, L = 20, K = 8, h = 25, DGCNN F = 64 / 3 / 100, B = 128): the
+    single fit's combined-phase steps (the factor networks on the matrix cores, the GEMM-shaped
+    embedder, the two chains on two streams), timed like the headline leg, with the roofline of its
+    dominant kernel from HIP events taken with the factor chain on the caller's stream
+    (REDCLIFF_FORK=0, the same bits; on two streams concurrent kernels' event buckets overlap) and
+    the embedder chains' throughput beside it (chains of launches, not one kernel)."""
+    c = CONFIGS["c5"]
+    B = c["B"]
+    _, plan = single_fit(c, args, dev, rank, nbatch=8)
+    plan(5, 0).run()
+    extra = preheat(plan, 5, args.preheat_s)
+    el = timed(plan(args.c5_steps, 5 + extra).run, None, dev)
+    fork_env = os.environ.get("REDCLIFF_FORK")
+    os.environ["REDCLIFF_FORK"] = "0"
+    try:
+        kt = kernel_times_of(plan(min(args.c5_steps, 20), 3).run)
+    finally:
+        if fork_env is None:
+            del os.environ["REDCLIFF_FORK"]
+        else:
+            os.environ["REDCLIFF_FORK"] = fork_env
+    fl = flops_per_window(c)
+    roof = roofline_of(kt, fl, B, "c5", False, chains=("emb_fwd", "emb_bwd"))
+    roof["timing"] = "HIP events per kernel with the factor chain on one stream (REDCLIFF_FORK=0)"
+    chains = {}
+    for k in ("emb_fwd", "emb_bwd"):
+        if kt.get(k, (0, 0))[0] > 0:
+            tf = fl[k] * B / (kt[k][0] * 1e-3) / 1e12
+            chains[k] = {"avg_us": round(kt[k][0] * 1e3, 2), "algorithmic_flops": fl[k] * B, "tflops": round(tf, 3),
+                         "frac": round(tf / FP32_PEAK_TFLOPS, 6)}
+    return {"workload": c["workload"], "windows_per_s": round(args.c5_steps * B / el, 1),
+            "ms_per_step": round(1e3 * el / args.c5_steps, 4), "steps": args.c5_steps,
+            "flops_per_window": fl["total"], "step_tflops": round(fl["total"] * B * args.c5_steps / el / 1e12, 3),
+            "roofline": roof, "embedder_chains": chains}
 
 
 def dp_throughput(B, steps, warmup, dev, dist, group=None):
@@ -894,6 +1007,10 @@ def main():
                     help="epochs per fit of the reference-grid fits/hour leg (0: skip)")
     ap.add_argument("--ref-grid-share", type=int, default=-1,
                     help="which 8-GPU share the reference-grid leg fits (default: the rank's)")
+    ap.add_argument("--ref-grid-all-shares", action="store_true",
+                    help="one GPU: time all 8 shares of each reference grid (default: the share and the costliest)")
+    ap.add_argument("--c5-steps", type=int, default=20,
+                    help="combined-phase steps of the configs[4] stress leg at N = 1 (0: skip)")
     ap.add_argument("--dp-batch", type=int, default=128, help="global batch of --mode dp")
     # 512 = the most windows one launch takes (Bmax), so one rank can run the same global batch
     ap.add_argument("--dp-leg-batch", type=int, default=512,

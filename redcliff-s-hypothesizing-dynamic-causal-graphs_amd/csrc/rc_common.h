@@ -190,7 +190,8 @@ inline WsOff rc_ws_off(const RedcliffDims& d, int64_t* ext = nullptr, int* next 
   put(o.gfc1, (int64_t)d.M1 * p * d.H);
   put(o.dwp, p * B * K);
   put(o.dAadj, K * p * p);
-  // per-node slices (node-chunk / GEMM paths) or per-16-window-tile records (rc_embed_batched.hip)
+  // per-node slices (node-chunk / GEMM paths); the bound by 16-window tiles is kept from the removed
+  // replica-batched embedder (round 5) and only over-allocates when ceil(B / 16) > p
   put(o.dWi, (p > (B + 15) / 16 ? p : (B + 15) / 16) * d.n * d.F * d.H);
   put(o.dS, (rc_nchunk(d) > 64 ? rc_nchunk(d) : 64) * d.n * p * p);
   put(o.dgb, (p * rc_nchunk(d) > 64 ? p * rc_nchunk(d) : 64) * 2 * d.F);
@@ -261,7 +262,7 @@ struct StepCtx {
   float *gE, *gF;  // RC_GRAD_ONLY gradient outputs (emb / fac layouts)
   // layout of the embedder-backward partials the final kernel reduces (node-chunk kernel vs GEMM path):
   // dS_i[cc][c'] = sum_s ws.dS[cc*dsCC + s*dsS + i*dsI + c'], s < dsN;  BN affine: ws.dgb[s][2][F], s < dgN;
-  // graph-conv weights: dW_i = sum_s ws.dWi[s][n][F][H], s < dwN (p node slices, or 1: rc_embed_batched.hip)
+  // graph-conv weights: dW_i = sum_s ws.dWi[s][n][F][H], s < dwN (p node slices)
   int dsN, dgN, dwN;
   int64_t dsCC, dsS, dsI;
   // matrix-core factor path: y / group-norm partial slots the forward writes (rc_fac_slots)

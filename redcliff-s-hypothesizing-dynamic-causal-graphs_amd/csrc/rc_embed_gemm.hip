@@ -505,7 +505,9 @@ int ds_splits(int B) {
 
 // GEMM-shaped embedder: large p (C5), or a packed grid search of >= RC_EMB_GEMM_R replicas, whose
 // products batched over the replicas keep the matrix cores busy where the fused node-chunk
-// kernels' per-workgroup latency chains set the time.  REDCLIFF_EMB_PATH=gemm|fused overrides.
+// kernels' per-workgroup latency chains set the time.  REDCLIFF_EMB_PATH=gemm|fused overrides; the
+// round-4 value "batched" (the replica-batched embedder, removed in round 5) is no longer accepted
+// and, like any other value, leaves the default choice.
 #ifndef RC_EMB_GEMM_R
 #define RC_EMB_GEMM_R 16
 #endif
@@ -573,11 +575,16 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
   float* ws = c.ws;  // replica 0's slice; the replica axis adds r * c.wss
   const float* E = c.emb;
   float* T = ws + c.wo.T;
-  // T_i[b] = S_i x_bn[b]  (p x p x F per window)
-  for (int i = 1; i < n && !e && !wb; ++i) {
-    RcGemm g = rc_gemm_args(0, 0, p, F, p, ws + c.wo.S + (int64_t)i * p * p, p, 0, T, nF, pnF, T + i * F, nF, pnF);
-    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
-    e = rc_gemm_launch(g, B, s, "emb T_i");
+  // T_i[b] = S_i x_bn[b]  (p x p x F per window), the n - 1 products independent: up to three per launch
+  for (int i0 = 1; i0 < n && !e && !wb; i0 += RC_GEMM_SET_MAX) {
+    RcGemm gs[RC_GEMM_SET_MAX];
+    int bs[RC_GEMM_SET_MAX], ng = 0;
+    for (int i = i0; i < n && ng < RC_GEMM_SET_MAX; ++i, ++ng) {
+      gs[ng] = rc_gemm_args(0, 0, p, F, p, ws + c.wo.S + (int64_t)i * p * p, p, 0, T, nF, pnF, T + i * F, nF, pnF);
+      rc_gemm_reps(gs[ng], c, c.wss, c.wss, c.wss);
+      bs[ng] = B;
+    }
+    e = rc_gemm_launch_set(gs, bs, ng, s, "emb T_i");
   }
   if (!e) {  // R = relu(T gcW): (B*p) x (n*F) x H
     RcGemm g = rc_gemm_args(0, 0, B * p, H, (int)nF, T, nF, 0, E + c.eo.gcW, H, 0, ws + c.wo.R, H, 0);
@@ -617,50 +624,64 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
   const float* E = c.emb;
   const float* T = ws + c.wo.T;
   const float* df1 = ws + c.wo.edf1;
-  if (!e) {  // dfc1W = df1^T R   (M1 x B x p*H), applied by the final kernel's Adam
-    RcGemm g = rc_gemm_args(1, 0, M1, (int)pH, B, df1, M1, 0, ws + c.wo.R, pH, 0, ws + c.wo.gfc1, pH, 0);
-    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
-    e = rc_gemm_launch(g, 1, s, "emb dfc1W");
+  // (pairs of products that do not depend on each other share a launch where the LDS-tiled core runs
+  // them, rc_gemm_launch_set: dfc1W and dZ both read df1; dW and dT both read dZ)
+  if (!e) {
+    RcGemm gs[2];
+    const int bs[2] = {1, 1};
+    // dfc1W = df1^T R   (M1 x B x p*H), applied by the final kernel's Adam
+    gs[0] = rc_gemm_args(1, 0, M1, (int)pH, B, df1, M1, 0, ws + c.wo.R, pH, 0, ws + c.wo.gfc1, pH, 0);
+    rc_gemm_reps(gs[0], c, c.wss, c.wss, c.wss);
+    // dZ = [R > 0] (df1 fc1W)   (B x M1 x p*H)
+    gs[1] = rc_gemm_args(0, 0, B, (int)pH, M1, df1, M1, 0, E + c.eo.fc1W, pH, 0, ws + c.wo.dZ, pH, 0);
+    gs[1].epi = RC_EPI_MASK;
+    gs[1].aux = ws + c.wo.R;
+    gs[1].ldaux = pH;
+    rc_gemm_reps(gs[1], c, c.wss, c.es, c.wss, c.wss);
+    e = rc_gemm_launch_set(gs, bs, 2, s, "emb dfc1W + dZ");
   }
-  if (!e) {  // dZ = [R > 0] (df1 fc1W)   (B x M1 x p*H)
-    RcGemm g = rc_gemm_args(0, 0, B, (int)pH, M1, df1, M1, 0, E + c.eo.fc1W, pH, 0, ws + c.wo.dZ, pH, 0);
-    g.epi = RC_EPI_MASK;
-    g.aux = ws + c.wo.R;
-    g.ldaux = pH;
-    rc_gemm_reps(g, c, c.wss, c.es, c.wss, c.wss);
-    e = rc_gemm_launch(g, 1, s, "emb dZ");
-  }
-  if (!e) {  // dW slices: dWi[s] = T[rows s]^T dZ[rows s], p slices of B rows of the (b, c) axis
-    RcGemm g = rc_gemm_args(1, 0, (int)nF, H, B, T, nF, (int64_t)B * nF, ws + c.wo.dZ, H, (int64_t)B * H, ws + c.wo.dWi,
-                            H, nF * H);
-    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
-    e = rc_gemm_launch(g, p, s, "emb dW");
-  }
-  if (!e) {  // dT = dZ gcW^T   ((B*p) x H x n*F)
-    RcGemm g = rc_gemm_args(0, 1, B * p, (int)nF, H, ws + c.wo.dZ, H, 0, E + c.eo.gcW, H, 0, ws + c.wo.edT, nF, 0);
-    rc_gemm_reps(g, c, c.wss, c.es, c.wss);
-    e = rc_gemm_launch(g, 1, s, "emb dT");
+  if (!e) {
+    RcGemm gs[2];
+    const int bs[2] = {p, 1};
+    // dW slices: dWi[s] = T[rows s]^T dZ[rows s], p slices of B rows of the (b, c) axis
+    gs[0] = rc_gemm_args(1, 0, (int)nF, H, B, T, nF, (int64_t)B * nF, ws + c.wo.dZ, H, (int64_t)B * H, ws + c.wo.dWi,
+                         H, nF * H);
+    rc_gemm_reps(gs[0], c, c.wss, c.wss, c.wss);
+    // dT = dZ gcW^T   ((B*p) x H x n*F)
+    gs[1] = rc_gemm_args(0, 1, B * p, (int)nF, H, ws + c.wo.dZ, H, 0, E + c.eo.gcW, H, 0, ws + c.wo.edT, nF, 0);
+    rc_gemm_reps(gs[1], c, c.wss, c.es, c.wss);
+    e = rc_gemm_launch_set(gs, bs, 2, s, "emb dW + dT");
   }
   if (wb) {  // dx_bn, its BatchNorm partials and the dS_i partials, wb windows per workgroup
     if (e) return e;
     hipLaunchKernelGGL(k_lemb_win_bwd, dim3(c.dsN, c.nrep), dim3(RC_BLOCK), lemb_win_lds_bwd(d, wb), s, c, wb);
     return rc_check(hipGetLastError(), "k_lemb_win_bwd");
   }
-  if (!e) {  // dx_bn[b] = Af dT[b]   (p x p*n x F per window)
-    RcGemm g = rc_gemm_args(0, 0, p, F, p * n, ws + c.wo.eAf, (int64_t)p * n, 0, ws + c.wo.edT, F, pnF, ws + c.wo.edX,
-                            F, (int64_t)p * F);
-    rc_gemm_reps(g, c, c.wss, c.wss, c.wss);
-    e = rc_gemm_launch(g, B, s, "emb dx_bn");
-  }
-  // dS_i slices: sum over the windows of group z of dT_i[b] x_bn[b]^T   (p x wps*F x p)
-  for (int i = 1; i < n && !e; ++i) {
-    RcGemm q = rc_gemm_args(0, 1, p, p, wps * F, ws + c.wo.edT + i * F, nF, (int64_t)wps * pnF, T, nF, (int64_t)wps * pnF,
-                            ws + c.wo.dS + (int64_t)i * p * p, p, c.dsS);
-    q.Kblk = F;
-    q.rA = pnF;
-    q.rB = pnF;
-    rc_gemm_reps(q, c, c.wss, c.wss, c.wss);
-    e = rc_gemm_launch(q, nds, s, "emb dS");
+  // dx_bn[b] = Af dT[b] (p x p*n x F per window) and the dS_i slices (sum over the windows of group z of
+  // dT_i[b] x_bn[b]^T, p x wps*F x p): independent products, up to three per launch
+  {
+    RcGemm gs[RC_GEMM_SET_MAX];
+    int bs[RC_GEMM_SET_MAX], ng = 0;
+    gs[0] = rc_gemm_args(0, 0, p, F, p * n, ws + c.wo.eAf, (int64_t)p * n, 0, ws + c.wo.edT, F, pnF, ws + c.wo.edX,
+                         F, (int64_t)p * F);
+    rc_gemm_reps(gs[0], c, c.wss, c.wss, c.wss);
+    bs[0] = B;
+    ng = 1;
+    for (int i = 1; i < n && !e; ++i) {
+      RcGemm q = rc_gemm_args(0, 1, p, p, wps * F, ws + c.wo.edT + i * F, nF, (int64_t)wps * pnF, T, nF,
+                              (int64_t)wps * pnF, ws + c.wo.dS + (int64_t)i * p * p, p, c.dsS);
+      q.Kblk = F;
+      q.rA = pnF;
+      q.rB = pnF;
+      rc_gemm_reps(q, c, c.wss, c.wss, c.wss);
+      if (ng == RC_GEMM_SET_MAX) {
+        e = rc_gemm_launch_set(gs, bs, ng, s, "emb dx_bn + dS");
+        ng = 0;
+      }
+      gs[ng] = q;
+      bs[ng++] = nds;
+    }
+    if (!e && ng) e = rc_gemm_launch_set(gs, bs, ng, s, "emb dx_bn + dS");
   }
   if (e) return e;
   const int ndr = (int)(((int64_t)(n - 1) * p * p + RC_BLOCK - 1) / RC_BLOCK);

@@ -72,13 +72,21 @@ inline void rc_gemm_reps(RcGemm& g, const StepCtx& c, int64_t qA, int64_t qB, in
 struct RcTile {
   int x, y, z;
 };
+// rc_gemm_tile_in: the same for the workgroup at linear index L of an nx x ny x nz grid (x fastest,
+// as the hardware linearises dispatch), when several products share one launch (rc_gemm_launch_set).
+__device__ inline RcTile rc_gemm_tile_in(const RcGemm& g, int L, int nx, int ny, int nz) {
+  const int T = nx * ny;
+  if (!g.xcd || (nz & 7) != 0) {
+    const int z = L / T, t = L - z * T, y = t / nx;
+    return RcTile{t - y * nx, y, z};
+  }
+  const int slot = L >> 3, zq = slot / T, t = slot - zq * T, ty = t / nx;
+  return RcTile{t - ty * nx, ty, (L & 7) + 8 * zq};
+}
 __device__ inline RcTile rc_gemm_tile(const RcGemm& g) {
   const int nx = gridDim.x, ny = gridDim.y, nz = gridDim.z;
   if (!g.xcd || (nz & 7) != 0) return RcTile{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-  const int T = nx * ny;
-  const int L = (int)blockIdx.x + nx * ((int)blockIdx.y + ny * (int)blockIdx.z);
-  const int slot = L >> 3, zq = slot / T, t = slot - zq * T, ty = t / nx;
-  return RcTile{t - ty * nx, ty, (L & 7) + 8 * zq};
+  return rc_gemm_tile_in(g, (int)blockIdx.x + nx * ((int)blockIdx.y + ny * (int)blockIdx.z), nx, ny, nz);
 }
 
 // The replica of grid slice z and the slice inside it: (replica, zb).
@@ -226,11 +234,9 @@ __device__ inline void rc_gemm_store(const RcGemm& g, float* C, const float* aux
 // output has the same bits as k_rc_gemm's in-order fmaf chain, whatever the tile or core
 // (tests/test_gpu_generic.py::test_gemm_cores_bitwise).
 template <int TT>
-__global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
+__device__ __forceinline__ void rc_gemm_mfma_body(const RcGemm& g, const RcTile tl) {
   constexpr int NL = RC_GEMM_K * TT / RC_BLOCK;  // operand elements per thread per K step
   constexpr int QT = TT / 2;                      // quarter tile per wave
-  rc_critical_priority();
-  const RcTile tl = rc_gemm_tile(g);
   const RcGemmZ zz = rc_gemm_z(g, tl.z);
   const int bz = zz.zb;
   const float* A = g.A + bz * g.sA + zz.r * g.qA;
@@ -307,6 +313,45 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
 #pragma unroll
   for (int reg = 0; reg < NR; ++reg) accv[reg] = TT == 64 ? acc32[reg] : acc16[reg];
   rc_gemm_store<NR>(g, C, aux, bz, gn, accv, [&](int reg) { return m0 + wm + (TT == 64 ? mf_row(reg, lane) : 4 * (lane >> 4) + reg); });
+}
+
+template <int TT>
+__global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma(RcGemm g) {
+  rc_critical_priority();
+  rc_gemm_mfma_body<TT>(g, rc_gemm_tile(g));
+}
+
+// Up to three INDEPENDENT products in one launch (the same LDS-tiled matrix-core body, TT x TT tiles):
+// product i owns the linear workgroups [start[i], start[i + 1]), its grid nx x ny x nz laid out from
+// start[i] (a multiple of 8, so a workgroup's XCD is its product-local index mod 8 and the XCD-aware
+// tile order holds per product; the padding workgroups exit).  Every output is computed by the same
+// body with the same k order as in its own launch: the same bits.  A chain of short single-replica
+// products (the GEMM-shaped embedder's backward at C5: dfc1W with dZ, dW with dT) is bound by one
+// workgroup's chain of operand round trips per launch, not by the chip; products that do not depend
+// on each other then share that latency instead of paying it one after the other.
+#define RC_GEMM_SET_MAX 3
+struct RcGemmSet {
+  RcGemm g[RC_GEMM_SET_MAX];
+  int nx[RC_GEMM_SET_MAX], ny[RC_GEMM_SET_MAX], nz[RC_GEMM_SET_MAX];
+  int start[RC_GEMM_SET_MAX + 1];
+  int n;
+};
+template <int TT>
+__global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma_set(RcGemmSet s) {
+  rc_critical_priority();
+  const int bx = blockIdx.x;
+  // (no dynamic index into the kernel-argument struct: each product's branch reads its own fields)
+#define RC_SET_CASE(i)                                                                                 \
+  if (i < s.n && bx >= s.start[i] && bx < s.start[i + 1]) {                                            \
+    const int L = bx - s.start[i];                                                                     \
+    if (L >= s.nx[i] * s.ny[i] * s.nz[i]) return;                                                      \
+    rc_gemm_mfma_body<TT>(s.g[i], rc_gemm_tile_in(s.g[i], L, s.nx[i], s.ny[i], s.nz[i]));              \
+    return;                                                                                            \
+  }
+  RC_SET_CASE(0)
+  RC_SET_CASE(1)
+  RC_SET_CASE(2)
+#undef RC_SET_CASE
 }
 
 // Wave core: one 64-lane workgroup per 32x32 output tile, no workgroup-wide barriers, so every
@@ -391,6 +436,68 @@ __global__ __launch_bounds__(64, 5) static void k_rc_gemm_wave(RcGemm g) {
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) accv[reg] = acc[reg];
   rc_gemm_store<16>(g, C, aux, bz, gn, accv, [&](int reg) { return m0 + mf_row(reg, lane); });
+}
+
+// Whether rc_gemm_launch runs a product on the LDS-tiled matrix-core workgroups (k_rc_gemm_mfma) --
+// the products rc_gemm_launch_set can group -- rather than the wave or vector-ALU cores.
+inline bool rc_gemm_lds_core(const RcGemm& g0) {
+  const char* core = getenv("REDCLIFF_GEMM_CORE");
+  if (core != nullptr) return core[0] == 'm';
+  return g0.nrep <= 1;
+}
+
+inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char* what);
+
+// Independent products gs[0 .. n) (each with its batch count) in ONE launch of k_rc_gemm_mfma_set
+// when all of them run on the LDS-tiled matrix-core workgroups (single-replica steps); otherwise, or
+// with REDCLIFF_GEMM_SET=0, one rc_gemm_launch each, in order.  The same bits either way.
+inline int rc_gemm_launch_set(const RcGemm* gs, const int* batches, int n, hipStream_t s, const char* what) {
+  const char* sv = getenv("REDCLIFF_GEMM_SET");  // read per call: the tests switch it in-process
+  const bool on = !(sv && sv[0] == '0');
+  bool ok = on && n > 1 && n <= RC_GEMM_SET_MAX;
+  for (int i = 0; ok && i < n; ++i)
+    ok = rc_gemm_lds_core(gs[i]) && gs[i].M > 0 && gs[i].N > 0 && batches[i] > 0 &&
+         (int64_t)batches[i] * gs[i].nrep <= 65535;
+  const char* core = getenv("REDCLIFF_GEMM_CORE");
+  if (ok && core != nullptr && core[0] == 'v') ok = false;
+  if (!ok) {
+    for (int i = 0; i < n; ++i) {
+      const int e = rc_gemm_launch(gs[i], batches[i], s, what);
+      if (e) return e;
+    }
+    return 0;
+  }
+  static const int tile_env = [] {
+    const char* v = getenv("REDCLIFF_GEMM_TILE");
+    return v ? atoi(v) : 0;
+  }();
+  const char* xe = getenv("REDCLIFF_GEMM_XCD");
+  // one tile size for the launch (the bits do not depend on it): 32 x 32 unless the products hold at
+  // least two 64 x 64 tiles per CU between them
+  RcGemmSet set;
+  set.n = n;
+  int64_t t64 = 0;
+  for (int i = 0; i < n; ++i) {
+    const int z = batches[i] * gs[i].nrep;
+    t64 += (int64_t)((gs[i].N + 63) / 64) * ((gs[i].M + 63) / 64) * z;
+  }
+  const bool small = tile_env == 32 || (tile_env != 64 && t64 < 512);
+  const int TT = small ? 32 : 64;
+  set.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    set.g[i] = gs[i];
+    set.g[i].batch = batches[i];
+    set.g[i].xcd = !(xe && xe[0] == '0');
+    set.nx[i] = (gs[i].N + TT - 1) / TT;
+    set.ny[i] = (gs[i].M + TT - 1) / TT;
+    set.nz[i] = batches[i] * gs[i].nrep;
+    const int64_t nb = (int64_t)set.nx[i] * set.ny[i] * set.nz[i];
+    set.start[i + 1] = set.start[i] + (int)((nb + 7) / 8 * 8);
+  }
+  for (int i = n; i < RC_GEMM_SET_MAX; ++i) set.start[i + 1] = set.start[n];
+  if (small) hipLaunchKernelGGL(k_rc_gemm_mfma_set<32>, dim3(set.start[n]), dim3(RC_BLOCK), 0, s, set);
+  else hipLaunchKernelGGL(k_rc_gemm_mfma_set<RC_GEMM_T>, dim3(set.start[n]), dim3(RC_BLOCK), 0, s, set);
+  return rc_check(hipGetLastError(), what);
 }
 
 inline int rc_gemm_launch(const RcGemm& g0, int batch, hipStream_t s, const char* what) {

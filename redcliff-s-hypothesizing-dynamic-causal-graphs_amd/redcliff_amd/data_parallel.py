@@ -4,16 +4,17 @@ The reference fits one model per process (no torch.distributed anywhere).  For t
 recordings (TST, many windows per subject) one fit is spread over the GPUs of a node:
 
   * every rank holds the same model (parameters broadcast from rank 0 at construction) and, in
-    device memory, only the windows of its own shards of the training set (cache_dataset streams
-    each global batch through once: its BatchNorm statistics, then the rank's rows);
+    device memory, only the windows of its own shards of the training set (cache_dataset: a global
+    batch is uploaded whole by one owner rank, which takes its BatchNorm statistics; the others
+    upload their shards and receive the statistics in one all-reduce of the [nbatch][2][F] table);
   * each global batch of B windows is split into world_size contiguous shards; rank g runs
     the fused step on its shard in gradient-only mode (RC_GRAD_ONLY) with B_global = B, so
     batch-mean terms (forecast MSE :629, factor MSE :638-661) are scaled by 1/B and batch
     sums (fw-L1 :666, adj-L1 :696-715) are not: the shard gradients sum to the full-batch
     gradient.  The cos-sim penalty carries no gradient (metrics.py:380);
-  * BatchNorm uses the statistics of the GLOBAL batch (computed once per batch from the whole
-    batch, which every rank's loader yields, by the same kernel as the single fit's), so no SyncBN
-    collective is needed and the running statistics advance identically on every rank;
+  * BatchNorm uses the statistics of the GLOBAL batch (computed once per batch, at caching time,
+    from the whole batch by its owner rank with the same kernel as the single fit's), so no SyncBN
+    collective runs per step and the running statistics advance identically on every rank;
   * one all-reduce (sum) of one flat fp32 gradient buffer per update (embedder + factor
     groups, 0.4-0.9 MB at the published configs) over RCCL / xGMI, then the replicated Adam
     update of both groups in one launch (redcliff_dp_update, which also refreshes the DGCNN
@@ -78,9 +79,13 @@ class DataParallelFit:
     def cache_dataset(self, loader, sharded=None):
         """The training set on the device.  sharded (default; REDCLIFF_DP_SHARDED=0 or
         sharded=False keeps the whole set on every rank, the round-4 layout): each global batch of
-        the loader is uploaded once, its BatchNorm batch statistics are taken from the whole batch
-        (k_bn_stats, one workgroup per feature in a fixed order: the bits of the whole-set cache)
-        and only this rank's shard of it (shard_of) stays resident -- 1 / world of the windows."""
+        the loader goes to the device ONCE over the whole group: global batch bi is uploaded whole
+        only by its owner rank (bi mod world), which takes its BatchNorm batch statistics from the
+        whole batch (k_bn_stats, one workgroup per feature in a fixed order: the bits of the
+        whole-set cache); every other rank uploads only its own shard of it (shard_of).  The 2 F
+        doubles per batch reach the other ranks in ONE all-reduce over the [nbatch][2][F] table
+        (each row is non-zero on its owner only, so the sum is exact), and only this rank's shards
+        stay resident -- 1 / world of the windows."""
         if sharded is None:
             sharded = os.environ.get("REDCLIFF_DP_SHARDED", "1") != "0"
         if not sharded:
@@ -97,19 +102,29 @@ class DataParallelFit:
             if Bl < 1:
                 raise ValueError("batch %d has %d windows for %d ranks: every rank needs at least one window"
                                  % (bi, B, self.world))
-            Xd = X.to(eng.device, torch.float32).contiguous()
-            T = int(Xd.shape[1])
-            stats.append(eng.bn_stats(eng.dims(1, T), Xd, B, B))
-            xs.append(Xd[off:off + Bl].clone())
+            T = int(X.shape[1])
+            if bi % self.world == self.rank:  # the batch's owner: the whole batch, for its statistics
+                Xd = X.to(eng.device, torch.float32).contiguous()
+                stats.append(eng.bn_stats(eng.dims(1, T), Xd, B, B))
+                xs.append(Xd[off:off + Bl].clone())
+            else:
+                Xd = None
+                stats.append(torch.zeros(1, 2, eng.F, device=eng.device, dtype=torch.float64))
+                xs.append(X[off:off + Bl].to(eng.device, torch.float32).contiguous())
             lab = select_labels(Y, eng.K, eng.Lmax) if Y is not None else torch.zeros(B, eng.K)
             ls.append(lab[off:off + Bl].to(eng.device, torch.float32))
             sizes.append(B)
             local.append(Bl)
             del Xd
         rows = np.cumsum([0] + local[:-1]).astype(np.int64)  # the rank's rows of each batch in its X
+        stats = torch.cat(stats, 0).contiguous()
+        if self.world > 1:
+            dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=self.group)
+        self.uploaded_windows = int(sum(s_ if bi % self.world == self.rank else l_
+                                        for bi, (s_, l_) in enumerate(zip(sizes, local))))
         ds = {"X": torch.cat(xs, 0).contiguous(), "lab": torch.cat(ls, 0).contiguous(), "rows": rows,
               "sizes": np.asarray(sizes, dtype=np.int32), "local_sizes": np.asarray(local, dtype=np.int32),
-              "stats": torch.cat(stats, 0).contiguous(), "T": T, "Bmax": max(sizes), "len": len(sizes),
+              "stats": stats, "T": T, "Bmax": max(sizes), "len": len(sizes),
               "loader": loader, "sharded": True}
         cache[id(loader)] = ds
         return ds
@@ -223,7 +238,8 @@ class DataParallelFit:
         return run_fit(m, save_dir, X_train, self.oA, self.oB, output_length, max_iter, X_val, lookback, check_every,
                        verbose, GC, deltaConEps, in_degree_coeff, out_degree_coeff, (None, "CosineSimilarity", 0, 10),
                        stopping_criteria_forecast_coeff, stopping_criteria_factor_coeff,
-                       stopping_criteria_cosSim_coeff, save_plots, runner=runner, writer=self.rank == 0)
+                       stopping_criteria_cosSim_coeff, save_plots, runner=runner, writer=self.rank == 0,
+                       train_ds=ds)
 
     def train_confusion(self):
         """Factor-score confusion matrix of the last epoch summed over ranks (:786-803)."""

@@ -775,9 +775,11 @@ def _freeze_by_batch(model, fused, X_train, oA, oB, output_length, it):
 
 def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, lookback, check_every, verbose, GC,
              deltaConEps, in_degree_coeff, out_degree_coeff, prior, sc_forecast, sc_factor, sc_cos,
-             save_plots, runner=None, writer=True):
+             save_plots, runner=None, writer=True, train_ds=None):
     """runner(it), when given, trains epoch `it` in place of the fused single-fit epoch (the
-    data-parallel fit: redcliff_amd.data_parallel); writer=False: no files (ranks > 0)."""
+    data-parallel fit: redcliff_amd.data_parallel); writer=False: no files (ranks > 0);
+    train_ds: the runner's own device copy of the training set (the data-parallel fit's shard
+    cache), used in place of caching X_train whole -- a rank then holds only its shards."""
     if output_length != 1:
         raise NotImplementedError("output_length must be 1")
     fused = model.fused_supported()
@@ -801,7 +803,9 @@ def _run_fit(model, save_dir, X_train, oA, oB, output_length, max_iter, X_val, l
         del model.chkpt_optimizer_state
 
     if fused:
-        train = eng.cache_dataset(X_train)
+        if train_ds is not None and runner is None:
+            raise ValueError("train_ds is the runner's training set: pass both or neither")
+        train = train_ds if train_ds is not None else eng.cache_dataset(X_train)
         val = eng.cache_dataset(X_val)
         # (a data-parallel runner sizes the workspace for its shards; validation is unsharded)
         d_train = eng.workspace(max(train["Bmax"] if runner is None else 1, val["Bmax"]), train["T"])

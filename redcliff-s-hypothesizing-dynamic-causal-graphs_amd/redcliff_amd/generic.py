@@ -214,6 +214,14 @@ class HipAdam:
                    and all(p.is_cuda and p.dtype == torch.float32 for p in self.params))
         if not self.ok:
             return
+        # one step count for the whole group: torch advances each parameter's own and skips those
+        # without a gradient, so a torch-stepped optimizer whose parameters disagree stays with torch
+        steps = set(int(float(st["step"])) if "step" in st else 0
+                    for st in (opt.state.get(p) or {} for p in self.params))
+        if len(steps) > 1:
+            self.ok = False
+            self.released_for = "unequal step counts %s" % sorted(steps)
+            return
         dev = self.params[0].device
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, device=dev, dtype=torch.float32)
@@ -247,6 +255,17 @@ class HipAdam:
 
     def bound(self):
         return self.ok and all(p.data_ptr() == self.flat.data_ptr() + 4 * o for p, (o, _) in zip(self.params, self.views))
+
+    def state_is_ours(self):
+        """The optimizer's state still is this object's flat moments and shared step tensor
+        (optimizer.load_state_dict() swaps in new tensors: then the loaded state must be taken)."""
+        for p, (o, _) in zip(self.params, self.views):
+            st = self.opt.state.get(p)
+            if (not st or st.get("step") is not self.step_t
+                    or st["exp_avg"].data_ptr() != self.m.data_ptr() + 4 * o
+                    or st["exp_avg_sq"].data_ptr() != self.v.data_ptr() + 4 * o):
+                return False
+        return True
 
     def _hyper(self):
         g = self.opt.param_groups[0]
@@ -295,9 +314,12 @@ class GenericPath:
     def _step(self, opt):
         """opt.step() through HipAdam (one per optimizer object, built on its first step)."""
         h = self._adams.get(id(opt))
-        if h is None or h.opt is not opt or (h.ok and not h.bound()):
-            if h is not None and h.opt is opt:
+        reloaded = h is not None and h.opt is opt and h.ok and h.bound() and not h.state_is_ours()
+        if h is None or h.opt is not opt or (h.ok and not h.bound()) or reloaded:
+            if h is not None and h.opt is opt and not reloaded:
                 h.release()  # its parameters were re-pointed: rebuild on the current ones
+            # (after optimizer.load_state_dict() the rebuilt object continues from the loaded moments
+            # and step count, which HipAdam.__init__ copies into its flat buffers)
             h = self._adams[id(opt)] = HipAdam(opt) if isinstance(opt, torch.optim.Adam) else None
         if h is None or not h.ok:  # released optimizers stay with torch (per-parameter step counts)
             return opt.step()

@@ -242,6 +242,15 @@ def _device_truth(GC, G, p, eps, dev):
     return truth, eps_pow
 
 
+def _used_here(truth, eps_pow, dev):
+    """A cached truth table may be read on another stream than the one it was allocated on (packs
+    fitted concurrently by fit_packs, one stream each, sharing one true-graph list): tell the
+    caching allocator, so evicting the entry never frees memory a pending launch still reads."""
+    s = torch.cuda.current_stream(dev)
+    truth.record_stream(s)
+    eps_pow.record_stream(s)
+
+
 def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1., host=True):
     """est: float32 CUDA tensor (S, nE, p, p, Lt) of GC estimates; GC: true graphs (p, p, lags).
     Returns float64 (S, G, 6 + p), G = min(nE, len(GC)): f1, roc_auc, f1 / roc_auc without
@@ -255,6 +264,7 @@ def gc_progress_values(GC, est, eps=0.1, in_degree_coeff=1., out_degree_coeff=1.
     dev = est.device
     est = est.to(torch.float32).contiguous()
     truth, eps_pow = _device_truth(GC, G, p, eps, dev)
+    _used_here(truth, eps_pow, dev)
     out = torch.empty(S, G, 6 + p, dtype=torch.float64, device=dev)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     nat.check(nat.lib().redcliff_gc_progress(S, nE, G, p, Lt, est.data_ptr(), truth.data_ptr(), eps_pow.data_ptr(),
@@ -289,6 +299,7 @@ def gc_progress_values_grouped(GCs, est, spt, eps=0.1, in_degree_coeff=1., out_d
         _TRUTH_CACHE.insert(0, hit)
         del _TRUTH_CACHE[16:]
     truth, eps_pow = hit[6], hit[7]
+    _used_here(truth, eps_pow, dev)
     out = torch.empty(S, G, 6 + p, dtype=torch.float64, device=dev)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     nat.check(nat.lib().redcliff_gc_progress_grouped(S, spt, nE, G, p, Lt, est.data_ptr(), truth.data_ptr(),

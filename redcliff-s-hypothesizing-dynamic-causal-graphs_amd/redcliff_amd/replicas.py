@@ -734,7 +734,14 @@ def fit_packs(jobs):
     classes hold 15 to 105 data sets (train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:
     140-1131) -- where one small pack's latency-bound epoch leaves most of the chip idle.  Every pack's
     arithmetic is unchanged (the same launches, on another stream), so each replica ends exactly as
-    in its pack's own fit.  Returns the packs' fit results in job order."""
+    in its pack's own fit.  Returns the packs' fit results in job order.
+
+    Concurrency is per pack stream, with one limit: a pack of 32 or more replicas forks its factor
+    chain onto the library's auxiliary stream, and there is ONE of those per host thread and device
+    (rc_capi.hip g_aux, with its fork / join events), so the forked factor chains of several large
+    packs run one after another on it while their embedder chains overlap on the packs' own
+    streams.  A share of the reference grids holds at most two packs that large (the TST grid's
+    256-point classes, shard_grid); the synthetic grid's classes stay below the fork threshold."""
     gc_was = gc.isenabled()
     gc.disable()
     cur = torch.cuda.current_stream()

@@ -198,6 +198,10 @@ def merge(name, J):
 
 if __name__ == "__main__":
     torch.set_num_threads(1)
+    if sys.argv[1] == "run" and int(sys.argv[3]) > 0 and os.environ.get("ENVELOPE_THREADS"):
+        # realizations j > 0 differ from the fixture by their batch permutations already; their thread
+        # count is one more rounding-order choice (realization 0 stays at one thread, see run())
+        torch.set_num_threads(int(os.environ["ENVELOPE_THREADS"]))
     if sys.argv[1] == "run":
         run(sys.argv[2], int(sys.argv[3]))
     else:

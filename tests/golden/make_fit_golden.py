@@ -86,6 +86,12 @@ SCENARIOS = {
     "fit_tst": dict(seed=2, p=12, L=4, K=9, nsup=3, S=3, h=25, F=16, n=3, H=100, B=128, N=256, Nv=128, T=20,
                     label="onehot", pre=2, acc=2, max_iter=200, lookback=1, check_every=2, lrA=5e-4, lrB=5e-4,
                     data_seed=777, smooth=25.0, resume_at=None),
+    # the TST grid's costliest shape class (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:302-303:
+    # embed_lag 64, 3 graph-conv layers): the same TST model otherwise, so Lmax = 64 windows of
+    # T_rec = 70 steps; the embedder sees n*F = 192 features per node
+    "fit_tst_lag64": dict(seed=3, p=12, L=4, K=9, nsup=3, S=3, h=25, F=64, n=3, H=100, B=128, N=256, Nv=128, T=70,
+                          label="onehot", pre=2, acc=2, max_iter=200, lookback=1, check_every=2, lrA=5e-4,
+                          lrB=5e-4, data_seed=778, smooth=25.0, resume_at=None),
 }
 
 

@@ -361,6 +361,11 @@ SCENARIOS = {
     # count), DGCNN over p * 4 nodes and the cEmbedder with its ranking mask
     "dgcnn_wavelet": dict(BASE, wl=3, p=2, data_seed=11, seed=10),
     "cemb_wavelet": dict(BASE, emb="cEmbedder", wl=3, p=2, F=4, eh=5, nsup=2, data_seed=12, seed=11),
+    # the synthetic grid's extreme classes (train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:
+    # numF1_numN3 and numF10_numN6; K = nsup = numF): one factor (no cosine-similarity pairs, the
+    # penalty's sum over an empty set) on a 3-channel system, and ten factors on six channels
+    "dgcnn_k1p3": dict(BASE, p=3, K=1, nsup=1, data_seed=13, seed=12),
+    "dgcnn_k10p6": dict(BASE, K=10, nsup=10, data_seed=14, seed=13),
 }
 
 if __name__ == "__main__":

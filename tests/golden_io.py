@@ -7,7 +7,7 @@ import torch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 SCENARIOS = ["dgcnn_c1", "dgcnn_d4ic", "dgcnn_partial_sigmoid", "dgcnn_unsup", "dgcnn_base", "dgcnn_sims2",
-             "dgcnn_eachstep", "dgcnn_feql", "cemb", "vanilla"]
+             "dgcnn_eachstep", "dgcnn_feql", "cemb", "vanilla", "dgcnn_k1p3", "dgcnn_k10p6"]
 
 
 def load(name):

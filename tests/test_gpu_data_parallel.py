@@ -74,8 +74,9 @@ def _worker(rank, world, port, outdir, sharded=True):
     m, oA, oB = _model()
     dp = DataParallelFit(m, oA, oB)
     ds = dp.cache_dataset(_loader(), sharded=sharded)
-    if sharded:  # only this rank's windows are resident
+    if sharded:  # only this rank's windows are resident; the whole batches it uploaded are its own
         assert ds["X"].shape[0] == int(ds["local_sizes"].sum()) < CFG["N"]
+        assert dp.uploaded_windows < CFG["N"]
     for epoch in EPOCHS:
         dp.run_epoch(epoch, ds)
     conf = dp.train_confusion()
@@ -192,8 +193,14 @@ def _fit_worker(rank, world, port, outdir):
     m, oA, oB = _model()
     dp = DataParallelFit(m, oA, oB)
     save = os.path.join(outdir, "ckpt%d" % rank)
-    ret = dp.fit(save, _loader(), 1, FIT_EPOCHS, _val_loader(), GC=_true_gc(), **FIT_KW)
+    train = _loader()
+    ret = dp.fit(save, train, 1, FIT_EPOCHS, _val_loader(), GC=_true_gc(), **FIT_KW)
     torch.cuda.synchronize()
+    # the fit trained from the rank's shard cache: the engine never cached the whole training set
+    eng = m.engine()
+    assert id(train) not in eng.dataset_cache
+    assert all(int(ds_["X"].shape[0]) < CFG["N"] for ds_ in eng.dataset_cache.values())
+    assert dp.uploaded_windows < CFG["N"]
     h = m.fit_history
     sd = dict((k, v.detach().cpu()) for k, v in m.state_dict().items())
     hist = dict((k, torch.tensor(np.asarray(h[k], np.float64))) for k in

@@ -206,3 +206,87 @@ def test_hip_adam_matches_torch_adam(name, monkeypatch):
                 w = db["state"][i][k].cpu().numpy().astype(np.float64)
                 assert_close("%s %s" % (i, k), da["state"][i][k].cpu().numpy(), w, 1e-4,
                              1e-7 * max(1.0, float(np.abs(w).max())))
+
+
+def test_hip_adam_reloaded_state_and_unequal_steps():
+    """generic.HipAdam and torch.optim.Adam's own state handling:
+      * optimizer.load_state_dict() on an optimizer HipAdam already steps swaps new moment / step
+        tensors into its state; the next step continues from the LOADED moments and step count
+        (GenericPath._step rebuilds on them), as torch's Adam does;
+      * an optimizer torch stepped with a parameter left out (no gradient: torch skips it) has
+        per-parameter step counts that differ, which one flat launch cannot reproduce: it stays
+        with torch."""
+    from redcliff_amd import generic
+    gp = generic.GenericPath(None)
+    g = torch.Generator().manual_seed(5)
+    init = [torch.randn(7, 5, generator=g), torch.randn(11, generator=g)]
+    grads = [[torch.randn(t.shape, generator=g) for t in init] for _ in range(6)]
+
+    def make():
+        ps = [torch.nn.Parameter(t.clone().cuda()) for t in init]
+        return ps, torch.optim.Adam(ps, lr=1e-2, betas=(0.9, 0.999), eps=1e-4, weight_decay=1e-4)
+
+    (pa, oa), (pb, ob) = make(), make()
+    saved = None
+    for i, gr in enumerate(grads):
+        if i == 4:  # both optimizers reload the twin's state of step 2
+            oa.load_state_dict(saved)
+            ob.load_state_dict(saved)
+            with torch.no_grad():
+                for x, y in zip(pa, pb):
+                    x.copy_(y)
+        for ps in (pa, pb):
+            for p, t in zip(ps, gr):
+                p.grad = t.cuda()
+        gp._step(oa)
+        ob.step()
+        if i == 1:
+            import copy
+            saved = copy.deepcopy(ob.state_dict())
+    torch.cuda.synchronize()
+    h = gp._adams[id(oa)]
+    assert h.ok and h.state_is_ours() and h.t == 4
+    for x, y in zip(pa, pb):
+        np.testing.assert_allclose(x.detach().cpu().numpy(), y.detach().cpu().numpy(), rtol=1e-6, atol=1e-7)
+    for i in ob.state_dict()["state"]:
+        sa, sb = oa.state_dict()["state"][i], ob.state_dict()["state"][i]
+        assert float(sa["step"]) == float(sb["step"]) == 4.0
+        for k in ("exp_avg", "exp_avg_sq"):
+            np.testing.assert_allclose(sa[k].cpu().numpy(), sb[k].cpu().numpy(), rtol=1e-6, atol=1e-9)
+    # unequal per-parameter step counts stay with torch
+    ps, oc = make()
+    for i in range(3):
+        ps[0].grad = grads[i][0].cuda()
+        ps[1].grad = grads[i][1].cuda() if i != 1 else None
+        oc.step()
+    assert float(oc.state[ps[0]]["step"]) == 3.0 and float(oc.state[ps[1]]["step"]) == 2.0
+    h = generic.HipAdam(oc)
+    assert not h.ok and h.released_for.startswith("unequal step counts")
+
+
+@pytest.mark.parametrize("shape", ["c5", "d4ic-products"])
+def test_gemm_product_sets_bitwise(shape, monkeypatch):
+    """rc_gemm_launch_set: the GEMM-shaped embedder's independent products in one launch (forward: the
+    T_i = S_i x_bn products; backward: dfc1W with dZ, dW with dT, dx_bn with the dS_i slices) against
+    one launch per product (REDCLIFF_GEMM_SET=0) -- the same body and k order per output, so three
+    combined-phase steps end bit-identical.  "c5": configs[4] (p = 64, the single fit's default GEMM
+    embedder); "d4ic-products": the D4IC shape with the GEMM products forced (REDCLIFF_EMB_PATH=gemm,
+    REDCLIFF_EMB_WIN=0)."""
+    import bench
+    import redcliff_amd
+    c = dict(bench.CONFIGS["c5" if shape == "c5" else "d4ic"])
+    if shape != "c5":
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
+        monkeypatch.setenv("REDCLIFF_EMB_WIN", "0")
+    X, Y = bench.synth(c, 2 * c["B"], seed=3)
+    out = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("REDCLIFF_GEMM_SET", on)
+        m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).cuda()
+        oA, oB = bench.adam_pair(m, c)
+        for ep, bi in ((0, 0), (1, 1), (2, 0)):  # pretrain, acclimate, combined
+            m.batch_update(ep, bi, X[bi * c["B"]:(bi + 1) * c["B"]], Y[bi * c["B"]:(bi + 1) * c["B"]], oA, oB, 1)
+        torch.cuda.synchronize()
+        out.append(dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items()))
+    for k in out[0]:
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)

@@ -6,7 +6,9 @@ each held to independent fits or to the path it replaces, bit for bit:
   second stream from 32 replicas, rc_capi.hip; the GEMM-shaped embedder from 16) through all three
   phases, three sampled replicas against independent single fits on the same factor / embedder path;
 * `REDCLIFF_EMB_FINAL_EPT=8` forced on an 8-replica pack against the default (4 elements per thread);
-* the forked packed step (factor chain on the second stream) against the single-stream step at R = 32.
+* the forked packed step (factor chain on the second stream) against the single-stream step at R = 32;
+* the 256-replica TST-grid pack with mixed phase schedules (the bench's reference-grid pack size)
+  against sampled independent fits.
 """
 import numpy as np
 import pytest
@@ -101,3 +103,64 @@ def test_forked_pack_step_bitwise_equals_single_stream(monkeypatch):
         out[fork] = states(run_pack(points, train)[1])
     for r, (a, b) in enumerate(zip(out["1"], out["0"])):
         assert_same(a, b, "replica %d" % r)
+
+
+def test_tst_pack_of_256_mixed_schedules_matches_sampled_independent_fits(monkeypatch):
+    """The pack the bench's reference-grid leg times: 256 points of one TST-grid shape class
+    (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:278-309: p = 12 region averages, K = 9
+    factors of which 3 supervised, h = 25, gen_lag 4, DGCNN embed_lag 16 / 2 graph-conv layers / 100
+    hidden), each point with its own learning rates, FORECAST / ADJ_L1 coefficients and its own phase
+    schedule (the grid's pretrain x acclimation axes, scaled down: four schedules mixed in one pack,
+    Adam step numbers per replica through t_offset) -- ReplicaPack.fit over whole fits with per-epoch
+    GC tracking and validation; three sampled replicas (first, middle, last) bit-identical to their
+    own independent fit(): histories, stopping epoch, parameters, buffers, Adam moments and steps."""
+    import bench
+    import redcliff_amd
+    from redcliff_amd import ReplicaPack
+    from test_gpu_pack_fit import HKEYS, same
+    monkeypatch.setenv("REDCLIFF_FAC_PATH", "mfma")
+    monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
+    for k in ("REDCLIFF_FORK", "REDCLIFF_EMB_FINAL_EPT"):
+        monkeypatch.delenv(k, raising=False)
+    c = dict(bench.CONFIGS["c4"], F=16, n=2, T=20)
+    pts = [q for q in bench.tst_grid_points() if (q["lag"], q["layers"]) == (16, 2)]
+    assert len(pts) == 256
+    sched = {(100, 15): (2, 1), (100, 100): (2, 2), (50, 15): (1, 1), (50, 100): (1, 2)}
+    B = 128
+    X, Y = bench.synth(c, 3 * B, seed=401)
+    train = [(X[i:i + B], Y[i:i + B]) for i in range(0, 2 * B, B)]
+    val = [(X[2 * B:], Y[2 * B:])]
+    rng = np.random.RandomState(8)
+    gc = [(rng.rand(c["p"], c["p"], c["L"]) < 0.2).astype(np.float64) for _ in range(c["nsup"])]
+    kw = dict(lookback=10 ** 6, check_every=10 ** 6, GC=gc, deltaConEps=0.1, verbose=0)
+    max_iter = 5
+
+    def model(i):
+        q = pts[i]
+        pre, acc = sched[(q["pre"], q["acc"])]
+        m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=7000 + i, pre=pre, acc=acc,
+                              forecast=q["forecast"], adj=q["adj"]).cuda()
+        return m, bench.adam_pair(m, dict(c, lrA=q["embed_lr"], lrB=q["gen_lr"]))
+
+    made = [model(i) for i in range(256)]
+    packed = [m for m, _ in made]
+    pack_opts = [o for _, o in made]
+    pack = ReplicaPack(packed, pack_opts)
+    assert len(pack.phase_groups(1)) > 1  # the schedules really are mixed
+    pack.fit(None, train, val, max_iter, **kw)
+    torch.cuda.synchronize()
+    for r in (0, 131, 255):
+        m, (oA, oB) = model(r)
+        m.fit(None, train, oA, oB, c["L"], 1, 1, max_iter, val, **kw)
+        torch.cuda.synchronize()
+        ha, hb = m.fit_history, packed[r].fit_history
+        assert hb["best_it"] == ha["best_it"] and hb["stopped_at"] == ha["stopped_at"], r
+        for k in HKEYS + ("f1score_histories", "roc_auc_histories", "deltacon0_histories"):
+            assert same(hb[k], ha[k]), "replica %d %s" % (r, k)
+        assert_same(states([packed[r]])[0], states([m])[0], "replica %d" % r)
+        for oa, ob in zip((oA, oB), pack_opts[r]):
+            stA, stB = oa.state_dict()["state"], ob.state_dict()["state"]
+            for i in stA:
+                for k in ("exp_avg", "exp_avg_sq", "step"):
+                    np.testing.assert_array_equal(stB[i][k].cpu().numpy(), stA[i][k].cpu().numpy(),
+                                                  err_msg="replica %d optimizer state %s %s" % (r, i, k))

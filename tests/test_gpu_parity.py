@@ -18,7 +18,8 @@ from golden_io import assert_close, batches, ctor_args, load, state
 
 pytestmark = pytest.mark.gpu
 
-FUSED_SCENARIOS = ["dgcnn_c1", "dgcnn_d4ic", "dgcnn_partial_sigmoid", "dgcnn_unsup", "dgcnn_base", "dgcnn_feql"]
+FUSED_SCENARIOS = ["dgcnn_c1", "dgcnn_d4ic", "dgcnn_partial_sigmoid", "dgcnn_unsup", "dgcnn_base", "dgcnn_feql",
+                   "dgcnn_k1p3", "dgcnn_k10p6"]
 RTOL, ATOL = 1e-4, 2e-6
 
 
@@ -167,6 +168,18 @@ CONFIGS = {
     # C4 TST-shaped: p=12, L=4, K=9 (3 supervised), h=25, F=16, 3 layers, 100 hidden, T=150
     "C4": dict(p=12, L=4, K=9, nsup=3, h=25, F=16, n=3, H=100, B=128, T=150, label_T=150),
 }
+# The reference's grid-search shape classes beyond the published single configs.
+# TST grid (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:302-303): embed_lag {16, 32, 64} x
+# graph-conv layers {2, 3} at the TST model (C4 is (16, 3)); Lmax = embed_lag, so the windows hold
+# embed_lag + 1 steps of the 150-step recordings.
+GRID_TST = dict(("TST_l%d_n%d" % (F, n), dict(CONFIGS["C4"], F=F, n=n)) for F, n in ((16, 2), (32, 2), (32, 3), (64, 2),
+                                                                                    (64, 3)))
+# synthetic grid (train/REDCLIFF_S_CMLP_synSysInnovGauss1030_BSCgsSmooth3Parsim.py:140-1131, cached args: gen_lag 4,
+# h 25, DGCNN 16 / 3 / 100; K = nsup = numF, p = numN): its extreme classes -- K = 1 (no cosine pairs),
+# p = 3 (ADJ_L1 / sqrt(8)), K = 10 on 6 channels, K = 1 on 12
+GRID_SYN = dict(("SYN_K%d_p%d" % (K, p), dict(p=p, L=4, K=K, nsup=K, h=25, F=16, n=3, H=100, B=128, T=100, label_T=100))
+                for K, p in ((1, 3), (2, 3), (10, 6), (1, 12)))
+GRID_CLASSES = dict(GRID_TST, **GRID_SYN)
 # C5 stress: p=64, L=20, K=8, h=25, F=64, 3 layers, 100 hidden
 C5 = dict(p=64, L=20, K=8, nsup=8, h=25, F=64, n=3, H=100, B=128, T=128, label_T=128)
 
@@ -207,6 +220,20 @@ def synth(cfg, N, seed):
                                                                         ("C2", "mfma"), ("C1K4", "embgemm"),
                                                                         ("C2", "embgemm"), ("C2", "embgemm-products")])
 def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
+    _three_phases_vs_oracle(CONFIGS[cname], cname, path, monkeypatch)
+
+
+@pytest.mark.parametrize("cname,path", [(c, pth) for c in GRID_CLASSES for pth in ("auto", "packed")])
+def test_grid_shape_classes_three_phases_vs_oracle(cname, path, monkeypatch):
+    """Every TST-grid shape class and the synthetic grid's extreme classes, on the single-fit default
+    path ("auto": the fused vector kernels, the merged / split-lead backward) and on the kernels a
+    packed grid runs ("packed": the matrix-core factor chain k_fac_*_s16 and the GEMM-shaped
+    embedder with its windowed kernels, REDCLIFF_FAC_PATH=mfma + REDCLIFF_EMB_PATH=gemm) -- the same
+    three-phase schedule against the oracle as the published configs."""
+    _three_phases_vs_oracle(GRID_CLASSES[cname], cname, path, monkeypatch)
+
+
+def _three_phases_vs_oracle(cfg, cname, path, monkeypatch):
     """path "mfma" forces the matrix-core factor kernels (rc_factor_mfma.hip, normally chosen
     for p*L >= 256; C2's h=100 runs as four 32-unit hidden blocks per network), "embgemm" the
     GEMM-shaped embedder (rc_embed_gemm.hip, normally chosen for p >= 32 or a packed grid of
@@ -215,11 +242,13 @@ def test_published_configs_three_phases_vs_oracle(cname, path, monkeypatch):
     p >= 32 form) onto the published shapes."""
     if path == "mfma":
         monkeypatch.setenv("REDCLIFF_FAC_PATH", path)
+    elif path == "packed":
+        monkeypatch.setenv("REDCLIFF_FAC_PATH", "mfma")
+        monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
     elif path.startswith("embgemm"):
         monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
         if path == "embgemm-products":
             monkeypatch.setenv("REDCLIFF_EMB_WIN", "0")
-    cfg = CONFIGS[cname]
     o, m = oracle_and_hip(cfg)
     X, Y = synth(cfg, 2 * cfg["B"] + 40, seed=5)
     B = cfg["B"]
