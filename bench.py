@@ -292,42 +292,23 @@ def hbm_roofline(c, eng, ms_per_step, ktimes_roof):
 
 
 def pmc_traffic(kernel_name, cfg):
-    """HBM bytes per launch of ``kernel_name`` from committed rocprofv3 PMC summaries:
-    FETCH_SIZE x 2 (gfx950 under-count, MI355X_MICROARCH.md HBM) + WRITE_SIZE.  cfg "<config>"
-    reads profiles/*pmc_<config>_*counter_collection*.csv and keeps the launches with the
-    SMALLEST grid (the single fit); "<config>_r<R>" (a packed grid search) reads the same passes
-    and keeps the LARGEST grid (the R-replica launches)."""
-    import csv
-    import glob
-    import re
+    """HBM bytes per launch of ``kernel_name`` from the committed rocprofv3 PMC passes, condensed by
+    scripts/pmc_traffic.py into profiles/pmc_traffic.json: FETCH_SIZE x 2 (gfx950 under-count,
+    MI355X_MICROARCH.md HBM) + WRITE_SIZE.  cfg "<config>" takes the launches with the SMALLEST grid (the
+    single fit); "<config>_r<R>" (a packed grid search) the LARGEST grid (the R-replica launches); the
+    newest round that measured the kernel at that config first (kernels change between rounds)."""
     base, packed = (cfg.rsplit("_r", 1)[0], True) if "_r" in cfg else (cfg, False)
-    # the newest round's passes first (kernels change between rounds), then older ones
-    pats = [os.path.join(ROOT, "profiles", "r%02d_pmc_%s_*counter_collection*.csv" % (rnd, base)) for rnd in (5, 4, 3, 2)]
-    if base == "d4ic" and not packed:
-        pats.append(os.path.join(ROOT, "profiles", "r01_pmc_*counter_collection*.csv"))
-    for pat in pats:
-        # every pass of the pattern (single-fit and grid passes share it): the launches with the
-        # smallest / largest grid over ALL of them, so a single-fit pass never stands in for the grid
-        rows = []
-        for path in sorted(glob.glob(pat)):
-            with open(path) as f:
-                for row in csv.DictReader(f):
-                    if re.search(r"(^|::)%s(<|\(|$)" % re.escape(kernel_name), row.get("Kernel_Name", "")):
-                        rows.append(row)
-        if not rows:
-            continue
-        gsz = [int(r_.get("Grid_Size", 0) or 0) for r_ in rows]
-        vals = {}
-        for cname in ("FETCH_SIZE", "WRITE_SIZE"):
-            g_c = [g for row, g in zip(rows, gsz) if row["Counter_Name"] == cname]
-            if not g_c:
-                continue
-            keep = max(g_c) if packed else min(g_c)
-            vals[cname] = float(np.mean([float(row["Counter_Value"]) for row, g in zip(rows, gsz)
-                                         if row["Counter_Name"] == cname and g == keep]))
-        if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
-            return (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0  # counters are in KiB
-    return None
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        recs = [r for r in json.load(f) if r["config"] == base and r["kernel"] == kernel_name]
+    if not recs:
+        return None
+    rnd = max(r["round"] for r in recs)
+    recs = [r for r in recs if r["round"] == rnd]
+    pick = (max if packed else min)(recs, key=lambda r: r["grid_size"])
+    return (2.0 * pick["fetch_kib"] + pick["write_kib"]) * 1024.0  # counters are in KiB
 
 
 # --------------------------------------------------------------------------- timing helpers

@@ -230,10 +230,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_gfc(StepCtx c, int ngfc) {
 
 // BatchNorm affine partials: slot s of c.dgN sums rows (b, c) [s*rows, (s+1)*rows) of
 //   dgamma[f] = sum dx_bn[b][c][f] * xhat[b][c][f],  dbeta[f] = sum dx_bn[b][c][f].  grid (dgN, R)
-__global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
-  rc_critical_priority();
+__device__ __forceinline__ void lemb_bn_body(const StepCtx& c, int s) {
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.y), s = blockIdx.x;
+  const int r = rc_rep(c, blockIdx.y);
   const int p = d.p, F = d.F;
   float* ws = c.ws + r * c.wss;
   const float* X = c.X + r * c.xr;
@@ -277,13 +276,12 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_bn(StepCtx c) {
 }
 
 // dS_i slices -> slot 0 (fixed order), so the final kernel's adjacency workgroup reads one record.
-// grid (ceil((n-1) p^2 / 256), R)
-__global__ __launch_bounds__(RC_BLOCK) void k_lemb_dsred(StepCtx c, int nds) {
-  rc_critical_priority();
+// block bx of ceil((n-1) p^2 / 256)
+__device__ __forceinline__ void lemb_dsred_body(const StepCtx& c, int nds, int bx) {
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.y), p = d.p, n = d.n;
   const int64_t pp2 = (int64_t)p * p;
-  const int e = blockIdx.x * RC_BLOCK + threadIdx.x;
+  const int e = bx * RC_BLOCK + threadIdx.x;
   if (e >= (n - 1) * pp2) return;
   float* dS = c.ws + r * c.wss + c.wo.dS + pp2 + e;  // rows i >= 1 of slot 0
   const int64_t ss = (int64_t)n * pp2;
@@ -294,6 +292,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dsred(StepCtx c, int nds) {
     for (int u = 0; u < 4; ++u) t4[u] += dS[(s + u) * ss];
   for (; s < nds; ++s) t4[0] += dS[s * ss];
   dS[0] = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+}
+
+// The two independent ends of the GEMM-embedder backward in one launch: workgroups [0, ndr) reduce
+// the dS_i slices (lemb_dsred_body), workgroups [ndr, ndr + dgN) the BatchNorm affine partials
+// (lemb_bn_body).  grid (ndr + dgN, R)
+__global__ __launch_bounds__(RC_BLOCK) void k_lemb_bwd_ends(StepCtx c, int nds, int ndr) {
+  rc_critical_priority();
+  const int bx = blockIdx.x;
+  if (bx < ndr) lemb_dsred_body(c, nds, bx);
+  else lemb_bn_body(c, bx - ndr);
 }
 
 // ---- small-node windowed kernels (p < 32): the per-window products T_i = S_i x_bn (forward) and
@@ -684,11 +692,7 @@ int rc_launch_emb_bwd_gemm(const StepCtx& c, hipStream_t s) {
     if (!e && ng) e = rc_gemm_launch_set(gs, bs, ng, s, "emb dx_bn + dS");
   }
   if (e) return e;
-  const int ndr = (int)(((int64_t)(n - 1) * p * p + RC_BLOCK - 1) / RC_BLOCK);
-  if (n > 1) {
-    hipLaunchKernelGGL(k_lemb_dsred, dim3(ndr, c.nrep), dim3(RC_BLOCK), 0, s, c, nds);
-    if ((e = rc_check(hipGetLastError(), "k_lemb_dsred"))) return e;
-  }
-  hipLaunchKernelGGL(k_lemb_bn, dim3(c.dgN, c.nrep), dim3(RC_BLOCK), 0, s, c);
-  return rc_check(hipGetLastError(), "k_lemb_bn");
+  const int ndr = n > 1 ? (int)(((int64_t)(n - 1) * p * p + RC_BLOCK - 1) / RC_BLOCK) : 0;
+  hipLaunchKernelGGL(k_lemb_bwd_ends, dim3(ndr + c.dgN, c.nrep), dim3(RC_BLOCK), 0, s, c, nds, ndr);
+  return rc_check(hipGetLastError(), "k_lemb_bwd_ends");
 }

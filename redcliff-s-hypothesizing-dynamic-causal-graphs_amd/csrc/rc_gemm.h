@@ -364,9 +364,7 @@ __global__ __launch_bounds__(RC_BLOCK) static void k_rc_gemm_mfma_set(RcGemmSet 
 // chunk's loads in flight while the current one multiplies.  The k order and the zero padding past K
 // are k_rc_gemm_mfma<64>'s, so an output has the same bits.
 template <bool LA, bool LB>
-__global__ __launch_bounds__(64, 5) static void k_rc_gemm_wave(RcGemm g) {
-  rc_critical_priority();
-  const RcTile tl = rc_gemm_tile(g);
+__device__ __forceinline__ void rc_gemm_wave_body(const RcGemm& g, const RcTile tl) {
   const RcGemmZ zz = rc_gemm_z(g, tl.z);
   const int bz = zz.zb;
   const float* A = g.A + bz * g.sA + zz.r * g.qA;
@@ -438,6 +436,41 @@ __global__ __launch_bounds__(64, 5) static void k_rc_gemm_wave(RcGemm g) {
   rc_gemm_store<16>(g, C, aux, bz, gn, accv, [&](int reg) { return m0 + mf_row(reg, lane); });
 }
 
+template <bool LA, bool LB>
+__global__ __launch_bounds__(64, 5) static void k_rc_gemm_wave(RcGemm g) {
+  rc_critical_priority();
+  rc_gemm_wave_body<LA, LB>(g, rc_gemm_tile(g));
+}
+
+// Two independent products on the wave core in one launch (packed grids: dfc1W with dZ, dW with dT):
+// the layout of k_rc_gemm_mfma_set (product i's 32 x 32 tiles from start[i], a multiple of 8), each
+// product with its own operand-staging form (LA / LB), the same body and bits as its own launch.
+template <bool LA0, bool LB0, bool LA1, bool LB1>
+__global__ __launch_bounds__(64, 5) static void k_rc_gemm_wave_pair(RcGemmSet s) {
+  rc_critical_priority();
+  const int bx = blockIdx.x;
+  if (bx < s.start[1]) {
+    if (bx >= s.nx[0] * s.ny[0] * s.nz[0]) return;
+    rc_gemm_wave_body<LA0, LB0>(s.g[0], rc_gemm_tile_in(s.g[0], bx, s.nx[0], s.ny[0], s.nz[0]));
+  } else {
+    const int L = bx - s.start[1];
+    if (L >= s.nx[1] * s.ny[1] * s.nz[1]) return;
+    rc_gemm_wave_body<LA1, LB1>(s.g[1], rc_gemm_tile_in(s.g[1], L, s.nx[1], s.ny[1], s.nz[1]));
+  }
+}
+typedef void (*RcWavePairKern)(RcGemmSet);
+template <int I>
+struct RcWavePairTab {
+  static void fill(RcWavePairKern* t) {
+    t[I] = k_rc_gemm_wave_pair<(I & 1) != 0, (I & 2) != 0, (I & 4) != 0, (I & 8) != 0>;
+    RcWavePairTab<I - 1>::fill(t);
+  }
+};
+template <>
+struct RcWavePairTab<-1> {
+  static void fill(RcWavePairKern*) {}
+};
+
 // Whether rc_gemm_launch runs a product on the LDS-tiled matrix-core workgroups (k_rc_gemm_mfma) --
 // the products rc_gemm_launch_set can group -- rather than the wave or vector-ALU cores.
 inline bool rc_gemm_lds_core(const RcGemm& g0) {
@@ -456,10 +489,51 @@ inline int rc_gemm_launch_set(const RcGemm* gs, const int* batches, int n, hipSt
   const bool on = !(sv && sv[0] == '0');
   bool ok = on && n > 1 && n <= RC_GEMM_SET_MAX;
   for (int i = 0; ok && i < n; ++i)
-    ok = rc_gemm_lds_core(gs[i]) && gs[i].M > 0 && gs[i].N > 0 && batches[i] > 0 &&
-         (int64_t)batches[i] * gs[i].nrep <= 65535;
+    ok = gs[i].M > 0 && gs[i].N > 0 && batches[i] > 0 && (int64_t)batches[i] * gs[i].nrep <= 65535;
   const char* core = getenv("REDCLIFF_GEMM_CORE");
   if (ok && core != nullptr && core[0] == 'v') ok = false;
+  // every product on the LDS-tiled core (single replica), or a PAIR on the wave core (packed grids)
+  bool lds = ok, wave = ok && n == 2;
+  for (int i = 0; ok && i < n; ++i) {
+    lds = lds && rc_gemm_lds_core(gs[i]);
+    wave = wave && !rc_gemm_lds_core(gs[i]);
+  }
+  if (wave) {
+    const bool wd = core != nullptr && core[0] == 'w' && core[1] == 'd';
+    RcGemmSet set;
+    set.n = 2;
+    set.start[0] = 0;
+    int idx = 0;
+    for (int i = 0; i < 2 && wave; ++i) {
+      RcGemm g = gs[i];
+      g.batch = batches[i];
+      const char* xe = getenv("REDCLIFF_GEMM_XCD");
+      g.xcd = !(xe && xe[0] == '0');
+      const int64_t nkb = (g.K + g.Kblk - 1) / g.Kblk;
+      const int64_t extA = g.K <= 0 ? 1 : (nkb - 1) * g.rA + (g.ta ? (int64_t)(g.Kblk - 1) * g.lda + g.M : (int64_t)(g.M - 1) * g.lda + g.Kblk);
+      const int64_t extB = g.K <= 0 ? 1 : (nkb - 1) * g.rB + (g.tb ? (int64_t)(g.N - 1) * g.ldb + g.Kblk : (int64_t)(g.Kblk - 1) * g.ldb + g.N);
+      wave = extA < (1 << 28) && extB < (1 << 28) && g.rA >= 0 && g.rB >= 0;
+      g.extA = (int)extA;
+      g.extB = (int)extB;
+      set.g[i] = g;
+      set.nx[i] = (g.N + 31) / 32;
+      set.ny[i] = (g.M + 31) / 32;
+      set.nz[i] = batches[i] * g.nrep;
+      const int64_t nb = (int64_t)set.nx[i] * set.ny[i] * set.nz[i];
+      set.start[i + 1] = set.start[i] + (int)((nb + 7) / 8 * 8);
+      const bool la = !wd && !g.ta, lb = !wd && g.tb;
+      idx |= (la ? 1 : 0) << (2 * i) | (lb ? 2 : 0) << (2 * i);
+    }
+    if (wave) {
+      static RcWavePairKern tab[16];
+      static const bool init = (RcWavePairTab<15>::fill(tab), true);
+      (void)init;
+      set.start[3] = set.start[2];
+      hipLaunchKernelGGL(tab[idx], dim3(set.start[2]), dim3(64), 0, s, set);
+      return rc_check(hipGetLastError(), what);
+    }
+  }
+  ok = lds;
   if (!ok) {
     for (int i = 0; i < n; ++i) {
       const int e = rc_gemm_launch(gs[i], batches[i], s, what);

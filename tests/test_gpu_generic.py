@@ -264,29 +264,40 @@ def test_hip_adam_reloaded_state_and_unequal_steps():
     assert not h.ok and h.released_for.startswith("unequal step counts")
 
 
-@pytest.mark.parametrize("shape", ["c5", "d4ic-products"])
+@pytest.mark.parametrize("shape", ["c5", "d4ic-products", "d4ic-pack"])
 def test_gemm_product_sets_bitwise(shape, monkeypatch):
     """rc_gemm_launch_set: the GEMM-shaped embedder's independent products in one launch (forward: the
     T_i = S_i x_bn products; backward: dfc1W with dZ, dW with dT, dx_bn with the dS_i slices) against
     one launch per product (REDCLIFF_GEMM_SET=0) -- the same body and k order per output, so three
     combined-phase steps end bit-identical.  "c5": configs[4] (p = 64, the single fit's default GEMM
     embedder); "d4ic-products": the D4IC shape with the GEMM products forced (REDCLIFF_EMB_PATH=gemm,
-    REDCLIFF_EMB_WIN=0)."""
+    REDCLIFF_EMB_WIN=0); "d4ic-pack": a 16-replica D4IC pack on the GEMM embedder, whose pairs run on
+    the wave core (k_rc_gemm_wave_pair)."""
     import bench
     import redcliff_amd
     c = dict(bench.CONFIGS["c5" if shape == "c5" else "d4ic"])
     if shape != "c5":
         monkeypatch.setenv("REDCLIFF_EMB_PATH", "gemm")
+    if shape == "d4ic-products":
         monkeypatch.setenv("REDCLIFF_EMB_WIN", "0")
     X, Y = bench.synth(c, 2 * c["B"], seed=3)
+    R = 16 if shape == "d4ic-pack" else 1
     out = []
     for on in ("1", "0"):
         monkeypatch.setenv("REDCLIFF_GEMM_SET", on)
-        m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=0).cuda()
-        oA, oB = bench.adam_pair(m, c)
-        for ep, bi in ((0, 0), (1, 1), (2, 0)):  # pretrain, acclimate, combined
-            m.batch_update(ep, bi, X[bi * c["B"]:(bi + 1) * c["B"]], Y[bi * c["B"]:(bi + 1) * c["B"]], oA, oB, 1)
+        ms = [bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=s_).cuda() for s_ in range(R)]
+        ops = [bench.adam_pair(m, c) for m in ms]
+        if R == 1:
+            m, (oA, oB) = ms[0], ops[0]
+            for ep, bi in ((0, 0), (1, 1), (2, 0)):  # pretrain, acclimate, combined
+                m.batch_update(ep, bi, X[bi * c["B"]:(bi + 1) * c["B"]], Y[bi * c["B"]:(bi + 1) * c["B"]], oA, oB, 1)
+        else:
+            pack = redcliff_amd.ReplicaPack(ms, ops)
+            ds = pack.cache_dataset([(X[i:i + c["B"]], Y[i:i + c["B"]]) for i in range(0, X.shape[0], c["B"])])
+            for ep in (0, 1, 2):
+                pack.run_epoch(ep, ds)
         torch.cuda.synchronize()
-        out.append(dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items()))
-    for k in out[0]:
-        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
+        out.append([dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items()) for m in ms])
+    for r in range(R):
+        for k in out[0][r]:
+            np.testing.assert_array_equal(out[0][r][k], out[1][r][k], err_msg="replica %d %s" % (r, k))
