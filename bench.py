@@ -493,27 +493,41 @@ SYN_GRID_NOTE = (
     "starts (the 225 numF1 tasks and the 30 numF10 tasks)")
 
 
-def ref_grid_shares():
-    """Both reference grids dealt to an 8-GPU node by class-aware, FLOP-weighted sharding
-    (redcliff_amd.shard_grid, min_piece 32): {grid: (points, class of each point, cost of each point,
-    [point indices of share s for s in 0..7], [summed cost of share s])}."""
+# Time model of one GPU's share of a reference grid (a packed fit per shape class, the share's packs run
+# concurrently by fit_packs): seconds ~ per_pack x packs + per_fit x fits + per_mflop x the fits' summed
+# algorithmic MFLOP per window (flops_per_window).  Least-squares fit over all 16 shares of both grids
+# timed one by one on one GPU with FLOP-weighted equal-cost shares (profiles/r06_refgrid_all_shares_c.json;
+# residuals within 0.04 s of 0.32 - 0.71 s).  Only the ratios matter to the sharding.
+REF_GRID_COST = dict(per_pack=0.0728, per_fit=0.00065, per_mflop=0.001202)
+
+
+def ref_grid_shares(model=REF_GRID_COST):
+    """Both reference grids dealt to an 8-GPU node by class-aware sharding (redcliff_amd.shard_grid):
+    each point costs per_fit + per_mflop x its class's MFLOP per window, each class a share touches
+    per_pack, and the class-ordered points are cut into the 8 contiguous runs that minimise the largest
+    share's cost (piece_cost).  model=None: the round-5 rule (FLOP cost, equal-cost cut, min_piece 32).
+    {grid: (points, class of each point, cost of each point, [point indices of share s for s in 0..7],
+    [modelled cost of share s])}."""
     from redcliff_amd import shard_grid
     out = {}
     pts = tst_grid_points()
     base = CONFIGS["c4"]
-    # cost of a point: its shape class's algorithmic FLOPs per window (flops_per_window), so the shares
-    # hold equal work, not equal point counts (r05 shares cut by count ran 0.12 - 0.20 s,
-    # profiles/r05_refgrid_shares_h.jsonl)
     cls = [(q["lag"], q["layers"]) for q in pts]
-    cost = [flops_per_window(dict(base, F=q["lag"], n=q["layers"], T=q["lag"] + 4))["total"] for q in pts]
-    shares = [shard_grid(len(pts), 8, s, classes=cls, cost=cost, min_piece=32) for s in range(8)]
-    out["tst"] = (pts, cls, cost, shares, [float(sum(cost[i] for i in sh)) for sh in shares])
+    fl = [flops_per_window(dict(base, F=q["lag"], n=q["layers"], T=q["lag"] + 4))["total"] for q in pts]
     kp = synthetic_grid_points()
-    # cost per fit as above: the embedder's O(p) work dominates the small-K classes (a K * p^2 cost put
-    # 405 of the 990 fits on share 7, 1.07 s against 0.15 s on share 0)
-    cost = [flops_per_window(_syn_cfg(k, p))["total"] for k, p in kp]
-    shares = [shard_grid(len(kp), 8, s, classes=kp, cost=cost, min_piece=32) for s in range(8)]
-    out["synthetic"] = (kp, kp, cost, shares, [float(sum(cost[i] for i in sh)) for sh in shares])
+    fl_syn = [flops_per_window(_syn_cfg(k, p))["total"] for k, p in kp]
+    for name, keys, f in (("tst", cls, fl), ("synthetic", kp, fl_syn)):
+        if model is None:
+            cost = list(f)
+            shares = [shard_grid(len(keys), 8, s, classes=keys, cost=cost, min_piece=32) for s in range(8)]
+            loads = [float(sum(cost[i] for i in sh)) for sh in shares]
+        else:
+            cost = [model["per_fit"] + model["per_mflop"] * x / 1e6 for x in f]
+            shares = [shard_grid(len(keys), 8, s, classes=keys, cost=cost, piece_cost=model["per_pack"])
+                      for s in range(8)]
+            loads = [float(sum(cost[i] for i in sh) + model["per_pack"] * len(set(keys[i] for i in sh)))
+                     for sh in shares]
+        out[name] = (pts if name == "tst" else kp, keys, cost, shares, loads)
     return out
 
 
@@ -550,7 +564,7 @@ def reference_grids(args, dev, rank, world, dist):
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
     prof = []
     grids = ref_grid_shares()
-    out = {"share": "%d of 8 (class-aware shard_grid, FLOP-weighted, min_piece 32)" % share, "epochs_per_fit": E,
+    out = {"share": "%d of 8 (class-aware shard_grid: min-max runs under REF_GRID_COST)" % share, "epochs_per_fit": E,
            "train_windows": ntr * B, "val_windows": nva * B}
 
     def run(packs, warm=True):
@@ -671,6 +685,7 @@ def reference_grids(args, dev, rank, world, dist):
         g["shares_timed"] = runs
         g["costliest_share"] = costliest
         g["share_costs"] = [round(x / max(gcost), 4) for x in gcost]
+        g["share_model_seconds"] = [round(x, 3) for x in gcost]
         slowest = max(r_["seconds"] for r_ in runs)
         g["node_fits_per_hour"] = round(n_all * 3600.0 / slowest, 1)
         g["node_fits_per_hour_basis"] = (

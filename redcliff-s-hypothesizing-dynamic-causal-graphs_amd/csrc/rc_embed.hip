@@ -941,6 +941,21 @@ __device__ __forceinline__ void emb_bwd_dadj(const StepCtx& c, int r, int blk, b
   dA[e] = t;
 }
 
+// The embedder backward's launch without node workgroups (the GEMM-shaped embedder computes those
+// products itself; validation steps compute none): the optional head workgroup and the adjacency-L1
+// reduce workgroups, as a light kernel of its own -- k_emb_bwd's node-sized LDS and registers (the
+// multi-sub-block instantiation: 256 VGPRs) made this launch take 32.5 us at C5 for 17 workgroups of
+// trivial work (profiles/r06_kernel_stats_c5_f.csv).  The same device functions, so the same bits.
+// grid (head + nred, R)
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_head_dadj(StepCtx c, int head) {
+  __shared__ __attribute__((aligned(16))) float sm[32 + 16 * 16];  // [8] floats, [8] doubles, hist[nsup][nsup] (nsup <= K <= 16)
+  const int r = rc_rep(c, blockIdx.y);
+  if ((int)blockIdx.x >= head)
+    emb_bwd_dadj(c, r, (int)blockIdx.x - head);
+  else
+    emb_bwd_head(c, r, sm);
+}
+
 // grid (p * nchunk * nbw [+ 1] [+ nred], R): workgroups [0, p*nchunk*nbw) are (node, column
 // chunk, window block) blocks; then the optional head (loss values / confusion), then the
 // adjacency-L1 reduce workgroups.
@@ -1778,6 +1793,10 @@ int rc_launch_emb_bwd(const StepCtx& c, hipStream_t s, bool node_wgs) {
   const bool dadj = (c.flags & RC_STEP_A) && (c.flags & RC_LOSS_ADJ);
   const int nred = dadj ? (d.p * d.p + RC_BLOCK - 1) / RC_BLOCK : 0;
   if (nnode + head + nred == 0) return 0;
+  if (nnode == 0) {
+    hipLaunchKernelGGL(k_emb_head_dadj, dim3(head + nred, c.nrep), dim3(RC_BLOCK), 0, s, c, head);
+    return rc_check(hipGetLastError(), "k_emb_head_dadj");
+  }
   if (WPB > BC) {
     int e = rc_lds_optin(k_emb_bwd<true>, lds, "k_emb_bwd LDS");
     if (e) return e;

@@ -894,7 +894,45 @@ def grid_packs(models_and_opts, max_replicas=256, key=None):
     return out
 
 
-def shard_grid(n_points, world, rank, classes=None, cost=None, min_piece=0):
+def _minmax_runs(w, cls, world, piece_cost):
+    """Cut the class-ordered points (costs w, class keys cls) into at most `world` contiguous runs
+    minimising the largest run cost, where a run costs the sum of its points' costs plus piece_cost
+    for every class it touches (each is a pack of its own, with a pack's fixed per-epoch latency).
+    Greedy filling is optimal for a given bound (a point only ever adds to the run it joins), so a
+    bisection on the bound finds the optimum to within a 1e-6 relative step.  Returns the run index
+    of every (ordered) point."""
+    n = len(w)
+
+    def fill(bound):
+        owner = np.zeros(n, np.int64)
+        g, load, last = 0, 0.0, None
+        for j in range(n):
+            add = w[j] + (piece_cost if cls[j] != last else 0.0)
+            if load > 0.0 and load + add > bound:
+                g += 1
+                if g >= world:
+                    return None
+                load, last = 0.0, None
+                add = w[j] + piece_cost
+            load += add
+            last = cls[j]
+            owner[j] = g
+        return owner
+
+    lo = max(float(np.max(w)) + piece_cost, 0.0) if n else 0.0
+    hi = float(np.sum(w)) + piece_cost * len(set(cls)) + 1.0
+    best = fill(hi)
+    while hi - lo > 1e-6 * hi:
+        mid = 0.5 * (lo + hi)
+        o = fill(mid)
+        if o is None:
+            lo = mid
+        else:
+            hi, best = mid, o
+    return best
+
+
+def shard_grid(n_points, world, rank, classes=None, cost=None, min_piece=0, piece_cost=None):
     """Grid-point indices of rank `rank` of `world` GPUs.
 
     classes=None: round-robin over the grid order, as SLURM array tasks map onto nodes
@@ -908,7 +946,13 @@ def shard_grid(n_points, world, rank, classes=None, cost=None, min_piece=0):
 
     min_piece: a GPU's piece of a class smaller than min(min_piece, half the class) joins the class's
     largest piece on another GPU (a handful of points would be a pack of its own, whose per-epoch
-    launch chains cost about as much as a full one), at the price of a less even cost split."""
+    launch chains cost about as much as a full one), at the price of a less even cost split.
+
+    piece_cost (round 6): instead of the equal-cost cut, the contiguous runs minimise the largest run
+    cost counting `piece_cost` for every class a run touches -- the fixed per-pack time measured for a
+    share (bench.py REF_GRID_COST: a share's time is close to 0.073 s per pack + 0.65 ms per fit + 1.2 ms
+    per algorithmic MFLOP of a window, fitted over all 16 shares of both reference grids); min_piece is
+    then not used."""
     if classes is None:
         return list(range(rank, n_points, world))
     if len(classes) != n_points:
@@ -918,6 +962,9 @@ def shard_grid(n_points, world, rank, classes=None, cost=None, min_piece=0):
         first.setdefault(c, len(first))
     order = sorted(range(n_points), key=lambda i: (first[classes[i]], i))
     w = np.ones(n_points) if cost is None else np.asarray(cost, dtype=np.float64)
+    if piece_cost is not None:
+        owner = _minmax_runs(w[order], [classes[i] for i in order], world, float(piece_cost))
+        return sorted(int(order[j]) for j in range(n_points) if owner[j] == rank)
     cum = np.cumsum(w[order])
     total = cum[-1] if n_points else 0.0
     # run g holds the points whose cumulative cost midpoint falls in [g, g+1) * total / world

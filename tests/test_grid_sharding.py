@@ -135,3 +135,53 @@ def test_grid_packs_one_pack_per_shape_class_with_mixed_schedules():
     assert len(grid_packs(models, key=lambda i: pts[i][2])) == 8
     with pytest.raises(ValueError):
         grid_packs(models, max_replicas=257)
+
+
+@pytest.mark.parametrize("grid", ["tst", "synthetic"])
+def test_minmax_runs_with_piece_cost(grid):
+    """shard_grid(piece_cost=...): the 8 shares are contiguous runs of the class-ordered points (a
+    partition; classes never interleaved inside a share) whose largest modelled cost -- points' costs
+    plus piece_cost per class a share touches -- is no larger than the equal-cost cut's, and a
+    bisection bound: no feasible cut has a max more than 1e-6 relative below it (checked by refilling
+    at 0.999 x the bound and failing)."""
+    from redcliff_amd.replicas import _minmax_runs
+    if grid == "tst":
+        pts = tst_grid()
+        keys = [(q["lag"], q["layers"]) for q in pts]
+        w = [1.0 + q["lag"] * q["layers"] / 16.0 for q in pts]
+    else:
+        keys = synthetic_grid()
+        w = [0.5 + k * p / 12.0 for k, p in keys]
+    pc = 40.0
+    world = 8
+    shards = [shard_grid(len(keys), world, r, classes=keys, cost=w, piece_cost=pc) for r in range(world)]
+    assert sorted(sum(shards, [])) == list(range(len(keys)))
+
+    def load(s):
+        return sum(w[i] for i in s) + pc * len(set(keys[i] for i in s))
+    new_max = max(load(s) for s in shards)
+    old = [shard_grid(len(keys), world, r, classes=keys, cost=w) for r in range(world)]
+    assert new_max <= max(load(s) for s in old) + 1e-9
+    # every share is one contiguous run of the class-ordered points
+    first = {}
+    for c in keys:
+        first.setdefault(c, len(first))
+    order = sorted(range(len(keys)), key=lambda i: (first[keys[i]], i))
+    pos = dict((i, j) for j, i in enumerate(order))
+    for s in shards:
+        js = sorted(pos[i] for i in s)
+        assert js == list(range(js[0], js[0] + len(js)))
+    # optimality of the bound: the class-ordered sequence cannot be cut into 8 runs under 0.999 x it
+    wo = np.asarray([w[i] for i in order])
+    ko = [keys[i] for i in order]
+    g, cur, last, ok = 0, 0.0, None, True
+    bound = 0.999 * new_max
+    for j in range(len(wo)):
+        add = wo[j] + (pc if ko[j] != last else 0.0)
+        if cur > 0 and cur + add > bound:
+            g, cur, last = g + 1, 0.0, None
+            add = wo[j] + pc
+        cur += add
+        last = ko[j]
+    assert g >= world, "a cut under 0.999 x the returned max exists"
+    assert _minmax_runs(wo, ko, 1, pc).max() == 0
