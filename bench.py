@@ -496,18 +496,22 @@ SYN_GRID_NOTE = (
 # Time model of one GPU's share of a reference grid (a packed fit per shape class, the share's packs run
 # concurrently by fit_packs): seconds ~ per_pack x packs + per_fit x fits + per_mflop x the fits' summed
 # algorithmic MFLOP per window (flops_per_window).  Least-squares fit over all 16 shares of both grids
-# timed one by one on one GPU with FLOP-weighted equal-cost shares (profiles/r06_refgrid_all_shares_c.json;
-# residuals within 0.04 s of 0.32 - 0.71 s).  Only the ratios matter to the sharding.
+# timed one by one on one GPU (profiles/r06_refgrid_all_shares_c.json; 0.32 - 0.71 s, residuals within
+# 0.04 s).  Used to pick the share a one-GPU run times beside share 0 (the slowest one by the model), and
+# by the opt-in min-max cut (--ref-grid-model 1).  That cut is NOT the default: back to back on one box
+# it helped the TST grid (slowest share 0.767 -> 0.733 s) and hurt the synthetic one (0.504 -> 0.563 s;
+# profiles/r06_refgrid_all_shares_h_{old,model}.json) -- the same share varies by up to 10 % from run to
+# run, about the model's own error, so the round-5 FLOP-weighted cut stays.
 REF_GRID_COST = dict(per_pack=0.0728, per_fit=0.00065, per_mflop=0.001202)
 
 
-def ref_grid_shares(model=REF_GRID_COST):
-    """Both reference grids dealt to an 8-GPU node by class-aware sharding (redcliff_amd.shard_grid):
-    each point costs per_fit + per_mflop x its class's MFLOP per window, each class a share touches
-    per_pack, and the class-ordered points are cut into the 8 contiguous runs that minimise the largest
-    share's cost (piece_cost).  model=None: the round-5 rule (FLOP cost, equal-cost cut, min_piece 32).
-    {grid: (points, class of each point, cost of each point, [point indices of share s for s in 0..7],
-    [modelled cost of share s])}."""
+def ref_grid_shares(cut="flop", model=REF_GRID_COST):
+    """Both reference grids dealt to an 8-GPU node by class-aware sharding (redcliff_amd.shard_grid).
+    cut "flop": the points cost their class's algorithmic FLOPs per window and are cut into equal-cost
+    runs (min_piece 32); cut "model": each point costs per_fit + per_mflop x its MFLOP per window, each
+    class a share touches per_pack, and the 8 contiguous runs minimise the largest share's modelled
+    time (piece_cost).  {grid: (points, class of each point, FLOPs of each point, [point indices of share
+    s for s in 0..7], [modelled seconds of share s])}."""
     from redcliff_amd import shard_grid
     out = {}
     pts = tst_grid_points()
@@ -517,17 +521,14 @@ def ref_grid_shares(model=REF_GRID_COST):
     kp = synthetic_grid_points()
     fl_syn = [flops_per_window(_syn_cfg(k, p))["total"] for k, p in kp]
     for name, keys, f in (("tst", cls, fl), ("synthetic", kp, fl_syn)):
-        if model is None:
-            cost = list(f)
-            shares = [shard_grid(len(keys), 8, s, classes=keys, cost=cost, min_piece=32) for s in range(8)]
-            loads = [float(sum(cost[i] for i in sh)) for sh in shares]
+        tcost = [model["per_fit"] + model["per_mflop"] * x / 1e6 for x in f]
+        if cut == "flop":
+            shares = [shard_grid(len(keys), 8, s, classes=keys, cost=list(f), min_piece=32) for s in range(8)]
         else:
-            cost = [model["per_fit"] + model["per_mflop"] * x / 1e6 for x in f]
-            shares = [shard_grid(len(keys), 8, s, classes=keys, cost=cost, piece_cost=model["per_pack"])
+            shares = [shard_grid(len(keys), 8, s, classes=keys, cost=tcost, piece_cost=model["per_pack"])
                       for s in range(8)]
-            loads = [float(sum(cost[i] for i in sh) + model["per_pack"] * len(set(keys[i] for i in sh)))
-                     for sh in shares]
-        out[name] = (pts if name == "tst" else kp, keys, cost, shares, loads)
+        loads = [float(sum(tcost[i] for i in sh) + model["per_pack"] * len(set(keys[i] for i in sh))) for sh in shares]
+        out[name] = (pts if name == "tst" else kp, keys, f, shares, loads)
     return out
 
 
@@ -563,8 +564,9 @@ def reference_grids(args, dev, rank, world, dist):
     share = rank % 8 if getattr(args, "ref_grid_share", -1) < 0 else args.ref_grid_share
     E, ntr, nva, B = args.ref_grid_epochs, 8, 2, 128
     prof = []
-    grids = ref_grid_shares()
-    out = {"share": "%d of 8 (class-aware shard_grid: min-max runs under REF_GRID_COST)" % share, "epochs_per_fit": E,
+    grids = ref_grid_shares("model" if getattr(args, "ref_grid_model", 0) else "flop")
+    out = {"share": "%d of 8 (class-aware shard_grid: %s)" % (share, "min-max runs under REF_GRID_COST" if getattr(
+        args, "ref_grid_model", 0) else "FLOP-weighted equal-cost cut, min_piece 32"), "epochs_per_fit": E,
            "train_windows": ntr * B, "val_windows": nva * B}
 
     def run(packs, warm=True):
@@ -630,7 +632,7 @@ def reference_grids(args, dev, rank, world, dist):
         classes = tst_classes(s)
         el = run(tst_packs(classes, False))
         n = len(tshares[s])
-        r = {"share": s, "fits": n, "cost": tcost[s],
+        r = {"share": s, "fits": n, "model_seconds": round(tcost[s], 3),
              "packs": [{"embed_lag": k[0], "graph_conv_layers": k[1], "replicas": len(v),
                         "schedules": sorted(set(sched(pts[i]) for i in v))} for k, v in classes.items()],
              "seconds": round(el, 3), "fits_per_hour": round(n * 3600.0 / el, 1)}
@@ -665,7 +667,7 @@ def reference_grids(args, dev, rank, world, dist):
             packs.append((ms, os_, PerReplica(trains), PerReplica(vals), PerReplica(gcs)))
         el = run(packs)
         n = len(sshares[s])
-        return {"share": s, "fits": n, "cost": scost[s],
+        return {"share": s, "fits": n, "model_seconds": round(scost[s], 3),
                 "packs": [{"K": k[0], "p": k[1], "replicas": len(v)} for k, v in by.items()],
                 "seconds": round(el, 3), "fits_per_hour": round(n * 3600.0 / el, 1)}
 
@@ -683,8 +685,7 @@ def reference_grids(args, dev, rank, world, dist):
                   file=sys.stderr, flush=True)
         g = dict(runs[0])
         g["shares_timed"] = runs
-        g["costliest_share"] = costliest
-        g["share_costs"] = [round(x / max(gcost), 4) for x in gcost]
+        g["costliest_share"] = costliest  # the slowest by the REF_GRID_COST model
         g["share_model_seconds"] = [round(x, 3) for x in gcost]
         slowest = max(r_["seconds"] for r_ in runs)
         g["node_fits_per_hour"] = round(n_all * 3600.0 / slowest, 1)
@@ -1003,6 +1004,8 @@ def main():
                     help="epochs per fit of the reference-grid fits/hour leg (0: skip)")
     ap.add_argument("--ref-grid-share", type=int, default=-1,
                     help="which 8-GPU share the reference-grid leg fits (default: the rank's)")
+    ap.add_argument("--ref-grid-model", type=int, default=0,
+                    help="1: shares cut by the REF_GRID_COST min-max rule (A/B); 0: the FLOP-weighted equal-cost cut")
     ap.add_argument("--ref-grid-all-shares", action="store_true",
                     help="one GPU: time all 8 shares of each reference grid (default: the share and the costliest)")
     ap.add_argument("--c5-steps", type=int, default=20,

@@ -949,10 +949,11 @@ def shard_grid(n_points, world, rank, classes=None, cost=None, min_piece=0, piec
     launch chains cost about as much as a full one), at the price of a less even cost split.
 
     piece_cost (round 6): instead of the equal-cost cut, the contiguous runs minimise the largest run
-    cost counting `piece_cost` for every class a run touches -- the fixed per-pack time measured for a
-    share (bench.py REF_GRID_COST: a share's time is close to 0.073 s per pack + 0.65 ms per fit + 1.2 ms
-    per algorithmic MFLOP of a window, fitted over all 16 shares of both reference grids); min_piece is
-    then not used."""
+    cost counting `piece_cost` for every class a run touches -- the fixed per-pack time of a share
+    (bench.py REF_GRID_COST: a share's time is close to 0.073 s per pack + 0.65 ms per fit + 1.2 ms per
+    algorithmic MFLOP of a window, fitted over all 16 shares of both reference grids); min_piece is then
+    not used.  Measured against the equal-cost cut it was not better overall (bench.py REF_GRID_COST),
+    so it is an option, not the default."""
     if classes is None:
         return list(range(rank, n_points, world))
     if len(classes) != n_points:
