@@ -1697,22 +1697,6 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
   }
 }
 
-// k_emb_final as two launches when the adjacency workgroup's LDS is large (p >= 32: (2n + 2) p (p + 1)
-// floats, 133 KB at C5): one launch's dynamic LDS is reserved for EVERY workgroup of it, so the ~1,700
-// parameter workgroups of a C5 step -- which use no LDS -- ran one per CU in ~7 rounds.  The adjacency
-// workgroups (grid (R)) with the LDS, then the parameter workgroups (grid (nw, R)) without; the same
-// device function per workgroup, so the same bits.
-template <int NR>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_final_adj(StepCtx c) {
-  rc_critical_priority();
-  emb_final_wg<NR>(c, 0, blockIdx.x, 1, false, false);
-}
-template <int NR>
-__global__ __launch_bounds__(RC_BLOCK) void k_emb_final_params(StepCtx c, int ept) {
-  rc_critical_priority();
-  emb_final_wg<NR>(c, 1 + blockIdx.x, blockIdx.y, ept, false, false);
-}
-
 // k_emb_combine + k_emb_final as one launch (single fits with the fused embedder; round 3):
 // workgroup 0 is the adjacency workgroup, which sums its dS partials in place (the sums
 // k_emb_combine forms) and so starts at once; workgroups 1 .. ncomb are the combine's, which
@@ -1968,23 +1952,6 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const int nw = (total + ept * RC_BLOCK - 1) / (ept * RC_BLOCK);
   const size_t lds = rc_emb_final_lds(d);
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
-  const char* sv = getenv("REDCLIFF_EMB_FINAL_SPLIT");  // 0: one launch whatever the LDS (A/B)
-  if (lds > 32768 && !(sv && sv[0] == '0')) {
-    if (d.p * d.p <= 4 * RC_BLOCK) {
-      int e = rc_lds_optin(k_emb_final_adj<4>, lds, "k_emb_final LDS");
-      if (e) return e;
-      hipLaunchKernelGGL(k_emb_final_adj<4>, dim3(c.nrep), dim3(RC_BLOCK), lds, s, c);
-      if ((e = rc_check(hipGetLastError(), "k_emb_final_adj"))) return e;
-      hipLaunchKernelGGL(k_emb_final_params<4>, dim3(nw, c.nrep), dim3(RC_BLOCK), 0, s, c, ept);
-    } else {
-      int e = rc_lds_optin(k_emb_final_adj<16>, lds, "k_emb_final LDS");
-      if (e) return e;
-      hipLaunchKernelGGL(k_emb_final_adj<16>, dim3(c.nrep), dim3(RC_BLOCK), lds, s, c);
-      if ((e = rc_check(hipGetLastError(), "k_emb_final_adj"))) return e;
-      hipLaunchKernelGGL(k_emb_final_params<16>, dim3(nw, c.nrep), dim3(RC_BLOCK), 0, s, c, ept);
-    }
-    return rc_check(hipGetLastError(), "k_emb_final_params");
-  }
   if (d.p * d.p <= 4 * RC_BLOCK) {
     int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");
     if (e) return e;

@@ -88,10 +88,16 @@ SCENARIOS = {
                     data_seed=777, smooth=25.0, resume_at=None),
     # the TST grid's costliest shape class (train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:302-303:
     # embed_lag 64, 3 graph-conv layers): the same TST model otherwise, so Lmax = 64 windows of
-    # T_rec = 70 steps; the embedder sees n*F = 192 features per node
+    # T_rec = 70 steps; the embedder sees n*F = 192 features per node.  FIXED LENGTH (12 epochs, the
+    # stopping rule evaluated every epoch but never met): at this shape the reference's own early-stopping
+    # decisions are not stable under fp32 rounding order -- with max_iter 200 the fixture's fit stopped at
+    # epoch 28 and its resume at 43, while batch-permuted / one-thread realizations of the same fit stopped
+    # at 23 or 28 and resumed to 38 (make_fit_envelope.py runs), so exact decisions are no parity target
+    # there; the fixed-length fit's histories, GC progress and final state are (tests/test_gpu_fit_golden.py,
+    # within the reference's own spread, make_fit_envelope.py)
     "fit_tst_lag64": dict(seed=3, p=12, L=4, K=9, nsup=3, S=3, h=25, F=64, n=3, H=100, B=128, N=256, Nv=128, T=70,
-                          label="onehot", pre=2, acc=2, max_iter=200, lookback=1, check_every=2, lrA=5e-4,
-                          lrB=5e-4, data_seed=778, smooth=25.0, resume_at=None),
+                          label="onehot", pre=2, acc=2, max_iter=12, lookback=50, check_every=2, lrA=5e-4,
+                          lrB=5e-4, data_seed=778, smooth=25.0, resume_at=None, expect_stop=False),
 }
 
 
@@ -278,7 +284,8 @@ def run(name, cfg):
     last = loc["it"]
     print("%s: fit stopped at epoch %d (max_iter %d), best_it %d, %d checkpoints, %.1f s"
           % (name, last, cfg["max_iter"], loc["best_it"], len(cap.metas), time.time() - t0))
-    assert last < cfg["max_iter"] - 1, "early stopping never engaged"
+    if cfg.get("expect_stop", True):
+        assert last < cfg["max_iter"] - 1, "early stopping never engaged"
     _record_hist("hist", meta, out, cfg["nsup"])
     out["hist/n_epochs"] = np.asarray(len(meta["avg_combo_loss"]))
     _record_tracking("hist", meta, out, cfg["nsup"], cfg["p"])

@@ -302,23 +302,3 @@ def test_gemm_product_sets_bitwise(shape, monkeypatch):
         for k in out[0][r]:
             np.testing.assert_array_equal(out[0][r][k], out[1][r][k], err_msg="replica %d %s" % (r, k))
 
-
-def test_emb_final_split_launch_bitwise(monkeypatch):
-    """k_emb_final as an adjacency launch (with its LDS) plus a parameter launch (without) at C5, where
-    the adjacency workgroup's LDS is 133 KB, against the one launch (REDCLIFF_EMB_FINAL_SPLIT=0): the same
-    workgroup functions, so three combined-phase steps end bit-identical."""
-    import bench
-    import redcliff_amd
-    c = dict(bench.CONFIGS["c5"])
-    X, Y = bench.synth(c, 2 * c["B"], seed=4)
-    out = []
-    for sp in ("1", "0"):
-        monkeypatch.setenv("REDCLIFF_EMB_FINAL_SPLIT", sp)
-        m = bench.build_model(redcliff_amd.REDCLIFF_S_CMLP_withStateSmoothing, c, seed=1).cuda()
-        oA, oB = bench.adam_pair(m, c)
-        for ep, bi in ((0, 0), (1, 1), (2, 0)):
-            m.batch_update(ep, bi, X[bi * c["B"]:(bi + 1) * c["B"]], Y[bi * c["B"]:(bi + 1) * c["B"]], oA, oB, 1)
-        torch.cuda.synchronize()
-        out.append(dict((k, v.detach().cpu().numpy()) for k, v in m.state_dict().items()))
-    for k in out[0]:
-        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
