@@ -21,7 +21,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 HKEYS = ["avg_forecasting_loss", "avg_factor_loss", "avg_factor_cos_sim_penalty", "avg_fw_l1_penalty",
          "avg_fw_smoothing_penalty", "avg_adj_penalty", "avg_dagness_reg_loss", "avg_dagness_lag_loss",
          "avg_dagness_node_loss", "avg_combo_loss"]
-SCENARIOS = [n for n in ("fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst") if os.path.exists(os.path.join(GOLDEN, n + "_envelope.npz"))]
+SCENARIOS = [n for n in ("fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst", "fit_tst_lag64") if os.path.exists(os.path.join(GOLDEN, n + "_envelope.npz"))]
 
 
 def _load(name):

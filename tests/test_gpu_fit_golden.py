@@ -5,7 +5,11 @@ tests/golden/fit_d4ic.npz (configs[1] D4IC shape: p=10, L=4, K=4, h=100, DGCNN 2
 by tests/golden/make_fit_golden.py, which runs the reference's ``fit``
 (models/redcliff_s_cmlp_withStateSmoothing.py:1175-1647) with early stopping engaged, and then a
 reference-style resume (fresh optimizers, :209-251, redcliff_s_cmlp.py:245) from a mid-fit
-checkpoint.
+checkpoint.  tests/golden/fit_tst_lag64.npz is the TST grid's costliest shape class (p=12, L=4, K=9
+of which 3 supervised, h=25, DGCNN embed_lag 64 / 3 layers / 100 hidden,
+train/REDCLIFF_S_CMLP_tst100hzRerun1024AvgReg_gsSmooth1.py:302-303) as a fixed-length 12-epoch fit
+(no early stop: at this shape the reference's own stopping epoch moves between rounding-order
+realizations, make_fit_golden.py), with its resume and envelope.
 
 The HIP fit runs on the same seeded model and the same windows and must give (north_star):
   * the same stopping epoch and best_it, and the same number of history entries;
@@ -188,10 +192,10 @@ def true_gc(d, meta):
     return [d["true_gc%d" % k] for k in range(n)]
 
 
-ENV_FIT = ("fit_d4ic_pub", "fit_tst")  # long trajectories: the fit is held to the reference's own spread
+ENV_FIT = ("fit_d4ic_pub", "fit_tst", "fit_tst_lag64")  # long trajectories: the fit is held to the reference's own spread
 
 
-@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst"])
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst", "fit_tst_lag64"])
 def test_fit_matches_reference_fit(name):
     d, meta = load(name)
     env = load_envelope(name) if name in ENV_FIT else None
@@ -258,7 +262,7 @@ def check_fit(name, m, ret, d, meta, env, val):
     np.testing.assert_array_equal(f1, d["f1"])
 
 
-@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst"])
+@pytest.mark.parametrize("name", ["fit_c1", "fit_d4ic", "fit_d4ic_pub", "fit_tst", "fit_tst_lag64"])
 def test_resume_matches_reference_resume(name, tmp_path):
     """The reference's resume: the model saved at a mid-fit checkpoint (best_model) plus its
     metadata, resume_training_from_checkpoint, fit with FRESH Adam objects (the default here,
