@@ -457,18 +457,19 @@ struct RcDiv32 {
 // Global -> LDS staging with U independent loads in flight per thread: the loads of U
 // elements are issued before any of them is consumed, so a staging loop costs ~N/(U*256)
 // memory latencies instead of N/256.  ld(e) returns element e, st(e, v) consumes it.
-template <int U, class Ld, class St>
+// NT: the workgroup's threads (RC_BLOCK unless the kernel launches narrower workgroups).
+template <int U, int NT = RC_BLOCK, class Ld, class St>
 __device__ inline void rc_stage(int N, Ld ld, St st) {
-  for (int base = threadIdx.x; base < N; base += U * RC_BLOCK) {
+  for (int base = threadIdx.x; base < N; base += U * NT) {
     float v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = base + u * RC_BLOCK;
+      const int e = base + u * NT;
       v[u] = e < N ? ld(e) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = base + u * RC_BLOCK;
+      const int e = base + u * NT;
       if (e < N) st(e, v[u]);
     }
   }

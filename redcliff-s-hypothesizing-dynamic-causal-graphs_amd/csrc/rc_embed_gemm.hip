@@ -337,6 +337,7 @@ __host__ __device__ inline int lemb_win(const RedcliffDims& d, int B) {
 // x_bn and T_i (i >= 1) of windows [b0, b0 + wb) of replica r.  grid (ceil(B / wb), R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
   rc_critical_priority();
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 0);
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.y), b0 = blockIdx.x * wb;
   const int p = d.p, F = d.F, n = d.n, pF = p * F, pp2 = p * p;
@@ -389,7 +390,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
       T[w * pnF + ch * nF + f] = x;
     }
   }
-  if (n == 1) return;
+  if (n == 1) {
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 1);
+    return;
+  }
   __syncthreads();
   // T_i[w][ch][f] = sum_{c'} S_i[ch][c'] x_bn[w][c'][f]  (c' in order), items (i, w, ch, f)
   const RcDiv dF(F);
@@ -403,6 +407,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
     for (int cp = 0; cp < p; ++cp) t = fmaf(Si[cp], xw[cp * F], t);
     T[w * pnF + ch * nF + (i1 + 1) * F + f] = t;
   }
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 1);
 }
 
 // Backward of the per-window products for windows [g * wb, g * wb + wb) of replica r: dx_bn
@@ -411,6 +416,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
 // grid (ceil(B / wb), R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
   rc_critical_priority();
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.y), g = blockIdx.x, b0 = g * wb;
   const int p = d.p, F = d.F, n = d.n, pF = p * F, pp2 = p * p;
@@ -492,6 +498,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
     ws[c.wo.dgb + ((int64_t)g * 2) * F + tid] = ga;
     ws[c.wo.dgb + ((int64_t)g * 2 + 1) * F + tid] = gb;
   }
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
 }
 
 // splits of the fc1 contraction (p*H): largest divisor of p*H that is <= 64 with >= 64 terms each

@@ -207,7 +207,8 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
 //   terms, -> ws.dwp), group norms G / G0, adjacency-L1 value and its gradients wrt the
 //   lagged group norms (-> ws.dgs, used by the dW0 epilogue) and A (-> ws.dAadj), and the
 //   output-layer / hidden-bias gradients + Adam (b0, W1, b1).
-__global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
   const RedcliffDims& d = c.d;
   // xcd: every network of one replica on one XCD (rc_xcd_order): the K networks of a channel
   // read the same y rows, and the replica's w and window targets are shared by all of them
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   float* rB = rA + RC_BLOCK;      // [256]
   float* dwf = rB + RC_BLOCK;     // [Bmax]  forecast part of dL/dw_bk
 
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_MIX, 0);
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
@@ -253,7 +255,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   // the nUB (<= 8) slot partials of every prediction requested together, summed in slot order;
   // element e = kk * B + b (consecutive windows of one network: contiguous in y) -> ybuf[b][kk]
   const RcDiv dB(B);
-  rc_stage<2>(B * K, [&](int e) {
+  rc_stage<2, NT>(B * K, [&](int e) {
     const int kk = dB.div(e), b = e - kk * B;
     const float* yp = ws + c.wo.y + rc_y_idx(d, 0, kk * p + j, b);
     const int64_t ys_ = (int64_t)d.Bmax * K * p;
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   });
   __syncthreads();
   float fsum = 0.f;
-  for (int b = tid; b < B; b += RC_BLOCK) {
+  for (int b = tid; b < B; b += NT) {
     const float* wr = ws + c.wo.w + (int64_t)b * K;
     const bool tgt = c.flags & (RC_LOSS_FORECAST | RC_VALUES);
     const float xt = tgt ? X[((c.row0 + b) * d.T + c.Lmax) * p + j] : 0.f;
@@ -299,7 +301,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 17);
   // ---- group norms G[kj][c][t], G0[kj][c] (cmlp.py:147-167) from the forward's squared norms
-  for (int e = tid; e < Q; e += RC_BLOCK) {
+  for (int e = tid; e < Q; e += NT) {
     const float* gp = ws + c.wo.gq + (int64_t)kj * Q + e;
     const int64_t gs_ = (int64_t)K * p * Q;
     float v[8];
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
     ws[c.wo.G + (int64_t)kj * Q + e] = Gs[e];
   }
   __syncthreads();
-  for (int cc = tid; cc < p; cc += RC_BLOCK) {
+  for (int cc = tid; cc < p; cc += NT) {
     float sq = 0.f;
     for (int t = 0; t < L; ++t) sq += sqs[cc * L + t];
     ws[c.wo.G0 + (int64_t)kj * p + cc] = sqrtf(sq);
@@ -326,44 +328,63 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   // dL/dA[c][j] (-> ws.dAadj) from one sign evaluation
   const bool adj_on = adj_grad || values;
   if (adj_on) {
-    for (int cc = tid; cc < p; cc += RC_BLOCK) Acol[cc] = E[c.eo.A + cc * p + j];
-    for (int i = tid; i < Ls; i += RC_BLOCK) lwt[i] = logf((float)(i + 2));
+    for (int cc = tid; cc < p; cc += NT) Acol[cc] = E[c.eo.A + cc * p + j];
+    for (int i = tid; i < Ls; i += NT) lwt[i] = logf((float)(i + 2));
     __syncthreads();
     const int half = tid & 1, hp = (p + 1) / 2, c0 = half * hp, c1 = min(p, c0 + hp);
-    float vsum = 0.f;
+    // windows in the layout of a 256-thread workgroup (thread vt = vv * NT + tid: window
+    // b0 + vt / 2), so the loss value's block sum below keeps one summation order for every NT
+    constexpr int NV = RC_BLOCK / NT;
+    float vsum[NV];
+#pragma unroll
+    for (int vv = 0; vv < NV; ++vv) vsum[vv] = 0.f;
     for (int b0 = 0; b0 < B; b0 += RC_BLOCK / 2) {
-      const int b = b0 + (tid >> 1);
-      float t = 0.f, v = 0.f;
-      if (b < B) {
-        const float wb = wk[b];
-        for (int cc = c0; cc < c1; ++cc) {  // this lane's half of the channels
-          const float ac = Acol[cc];
-          const float* gr = Gs + cc * L + (L - Ls);
+#pragma unroll
+      for (int vv = 0; vv < NV; ++vv) {
+        const int b = b0 + ((vv * NT + tid) >> 1);
+        float t = 0.f, v = 0.f;
+        if (b < B) {
+          const float wb = wk[b];
+          for (int cc = c0; cc < c1; ++cc) {  // this lane's half of the channels
+            const float ac = Acol[cc];
+            const float* gr = Gs + cc * L + (L - Ls);
 #pragma unroll 4
-          for (int i = 0; i < Ls; ++i) {
-            const float g = gr[i];
-            const float val = wb * g + ac;
-            t += lwt[i] * rc_sign(val) * g;
-            v += lwt[i] * fabsf(val);
+            for (int i = 0; i < Ls; ++i) {
+              const float g = gr[i];
+              const float val = wb * g + ac;
+              t += lwt[i] * rc_sign(val) * g;
+              v += lwt[i] * fabsf(val);
+            }
           }
         }
-      }
-      // the two halves of window b are adjacent lanes: combined in fixed order (first + second)
-      const float t_hi = __shfl_xor(t, 1), v_hi = __shfl_xor(v, 1);
-      if (half == 0 && b < B) {
-        if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = dwf[b] + hy.c_adj * (t + t_hi);
-        vsum += v + v_hi;
+        // the two halves of window b are adjacent lanes: combined in fixed order (first + second)
+        const float t_hi = __shfl_xor(t, 1), v_hi = __shfl_xor(v, 1);
+        if (half == 0 && b < B) {
+          if (adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = dwf[b] + hy.c_adj * (t + t_hi);
+          vsum[vv] += v + v_hi;
+        }
       }
     }
-    if (values) {
-      const float vs = rc_block_sum(vsum, red);
-      if (tid == 0) ws[c.wo.lossp + p + kj] = hy.c_adj * vs;
+    if (values) {  // rc_block_sum's order over the 256-thread layout: wave sums, then the waves in order
+      __syncthreads();
+#pragma unroll
+      for (int vv = 0; vv < NV; ++vv) {
+        const float w = rc_wave_sum(vsum[vv]);
+        if ((tid & 63) == 0) red[vv * (NT / 64) + (tid >> 6)] = w;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        float vs = 0.f;
+        for (int i = 0; i < RC_BLOCK / 64; ++i) vs += red[i];
+        ws[c.wo.lossp + p + kj] = hy.c_adj * vs;
+      }
+      __syncthreads();
     }
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 19);
   if (adj_grad) {
     const bool wg = c.flags & RC_STEP_B, ag = c.flags & RC_STEP_A;
-    for (int e = tid; e < p * Ls; e += RC_BLOCK) {
+    for (int e = tid; e < p * Ls; e += NT) {
       const int cc = e / Ls, i = e - cc * Ls;
       const float g = Gs[cc * L + (L - Ls + i)], ac = Acol[cc];
       float sw = 0.f, s1 = 0.f;
@@ -379,7 +400,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 20);
   if (c.flags & RC_STEP_B) {  // dL/dG is zero outside the lag slice (and everywhere without the adj-L1 term)
-    for (int q = tid; q < Q; q += RC_BLOCK) {
+    for (int q = tid; q < Q; q += NT) {
       const int cc = q / L, tt = q - cc * L;
       if (!adj_grad || tt < L - Ls) ws[c.wo.dgs + (int64_t)kj * Q + q] = 0.f;
     }
@@ -387,13 +408,16 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 21);
   if (adj_grad && (c.flags & RC_STEP_A)) {
     __syncthreads();
-    for (int cc = tid; cc < p; cc += RC_BLOCK) {
+    for (int cc = tid; cc < p; cc += NT) {
       float s = 0.f;
       for (int i = 0; i < Ls; ++i) s += dAp[cc * Ls + i];
       ws[c.wo.dAadj + ((int64_t)k * p + cc) * p + j] = s;  // d/dA[c][j]
     }
   }
-  if (!(c.flags & RC_STEP_B)) return;
+  if (!(c.flags & RC_STEP_B)) {
+    RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_MIX, 1);
+    return;
+  }
   __syncthreads();
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 22);
   // ---- output layer / hidden bias gradients + Adam: 32 units x 8 batch slices per pass
@@ -401,7 +425,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
   const float* W1 = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by the forward
   float db1 = 0.f;
-  for (int b = tid; b < B; b += RC_BLOCK) db1 += dyl[b];
+  for (int b = tid; b < B; b += NT) db1 += dyl[b];
   db1 = rc_block_sum(db1, red);
   for (int u0 = 0; u0 < (mf_recompute(d) ? 0 : h); u0 += 32) {  // else: in k_fac_bwd_mfma<4>
     const int uu = tid & 31, part = tid >> 5, u = u0 + uu;
@@ -430,6 +454,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_mix(StepCtx c, int xcd) {
   }
   if (tid == 0) rc_update(c, P, PM, PV, GF, c.fo.b1 + kj, db1, as);
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 23);
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_MIX, 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -862,6 +887,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
   extern __shared__ float Xs[];
   const float* P = c.fac + r * c.fs;
   float* ws = c.ws + r * c.wss;
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 0);
   ms_stage_x(c, r, Xs);
   __syncthreads();
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
@@ -936,6 +962,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
     ms_st(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), w1_off, cur.w1A);
     cur = nxt;
   }
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_FWD, 1);
 }
 
 // Backward (RC_STEP_B): per 16-unit block,
@@ -956,6 +983,11 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
 // (0 / 27931 arrays, gpurun_out r5m).  0: the compiler's choice.
 #ifndef RC_S16_BWD_WAVES
 #define RC_S16_BWD_WAVES 3
+#endif
+// RC_S16_EXP (timing experiments only, wrong results): bit 0 replaces the epilogue's Adam by one
+// multiply-add (loads and stores unchanged), bit 1 skips the recompute / dW0 matrix-core passes.
+#ifndef RC_S16_EXP
+#define RC_S16_EXP 0
 #endif
 #if RC_S16_BWD_WAVES > 0
 #define RC_S16_BWD_BOUNDS __launch_bounds__(RC_BLOCK, RC_S16_BWD_WAVES)
@@ -987,6 +1019,7 @@ __global__ RC_S16_BWD_BOUNDS void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
   const int cb_lo = bx * 4 * bpw, cb_hi = min(NB, cb_lo + 4 * bpw) - 1;
   const int kjlo = cb_lo / nU, nnet = cb_hi / nU - kjlo + 1;
   float* Dys = Xs + rows * S;
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 0);
   {  // dL/dy of the workgroup's networks (zero past B), then the window tile
     const RcDiv drow(rows);
     const float* dyg = ws + c.wo.dyl;
@@ -1048,7 +1081,7 @@ __global__ RC_S16_BWD_BOUNDS void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
     const float* dyn = Dys + (kj - kjlo) * rows + 4 * g;
     // two 16-window tiles per pass (independent recompute chains); rows past B are zero windows
     // with zero dL/dy, which add exact zeros, and the tile pairs run to a multiple of 32 <= rows
-    for (int t0 = 0; t0 < B; t0 += 32) {
+    for (int t0 = 0; t0 < ((RC_S16_EXP & 2) ? 0 : B); t0 += 32) {
       f32x4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       const float* xr = Xs + (t0 + l15) * S + ms_sh(l15) + g;
 #pragma unroll
@@ -1133,7 +1166,10 @@ __global__ RC_S16_BWD_BOUNDS void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
         ms_st(rG, 4 * e, gr);
       } else {
         float pp = pw, mm = mt[k], vv = vt[k];
-        rc_adam(pp, mm, vv, gr, as);
+        if constexpr ((RC_S16_EXP & 1) != 0)
+          pp = fmaf(-1e-3f, gr, pp);
+        else
+          rc_adam(pp, mm, vv, gr, as);
         ms_st(rW, 4 * e, pp);
         ms_st(rM, 4 * e, mm);
         ms_st(rV, 4 * e, vv);
@@ -1143,6 +1179,17 @@ __global__ RC_S16_BWD_BOUNDS void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
     }
     cur = nxt;
   }
+  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 1);
+}
+
+// k_fac_mix's workgroup: 128 threads when B <= 128 (one window per thread, so the per-thread
+// window sums and the block sums of the loss value and the output-bias gradient see the same
+// operands in the same order as at 256 threads, whose upper waves held zeros) and the hidden-layer
+// gradients come from the dW0 kernel (mf_recompute: the 32-units-by-8-slices pass is not run).
+static int fac_mix_nt(const RedcliffDims& d, int B) {
+  const char* v = getenv("REDCLIFF_MIX_NT");
+  if (v && atoi(v) == 256) return RC_BLOCK;
+  return (B <= 128 && mf_recompute(d)) ? 128 : RC_BLOCK;
 }
 
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
@@ -1283,7 +1330,14 @@ int rc_launch_fac_mix(const StepCtx& c, hipStream_t s) {
   const size_t lds = fac_mix_lds(d, c.Ls);
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) { rc_set_error("factor mixing: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
   const char* xe = getenv("REDCLIFF_MIX_XCD");  // read per launch (A/B); default on
-  hipLaunchKernelGGL(k_fac_mix, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c, (int)!(xe && xe[0] == '0'));
+  // 128-thread workgroups where every window has its own thread and the output-layer sums run in
+  // the dW0 kernel: twice the resident workgroups for a kernel whose time is its workgroups'
+  // chains of dependent memory rounds, the same bits (every sum keeps its order: fac_mix_nt).
+  // REDCLIFF_MIX_NT=256 keeps the full workgroups (A/B).
+  if (fac_mix_nt(d, c.B) == 128)
+    hipLaunchKernelGGL(k_fac_mix<128>, dim3(KP, c.nrep), dim3(128), lds, s, c, (int)!(xe && xe[0] == '0'));
+  else
+    hipLaunchKernelGGL(k_fac_mix<RC_BLOCK>, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), "k_fac_mix");
 }
 

@@ -44,7 +44,8 @@ def main():
     pack = packs[-1]
     tot = pack.ws_off["total"]
     tr = pack.ws[tot - 32768:tot].cpu().numpy().view(np.uint64).astype(np.int64).reshape(8, 2048)
-    names = ["emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix"]
+    names = ["emb_fwd", "fac_fwd", "fac_bwd", "emb_bwd", "emb_final", "fac_mix"]  # RC_KID_* (packed grid: emb_fwd =
+    # k_lemb_prep_win, emb_bwd = k_lemb_win_bwd, fac_fwd / fac_bwd = the s16 kernels)
     starts = [tr[k][0::2][tr[k][0::2] > 0] for k in range(len(names))]
     t_first = min(int(s.min()) for s in starts if s.size)
     for k, name in enumerate(names):
