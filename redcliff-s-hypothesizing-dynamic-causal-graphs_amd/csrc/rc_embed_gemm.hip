@@ -338,6 +338,7 @@ __host__ __device__ inline int lemb_win(const RedcliffDims& d, int B) {
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
   rc_critical_priority();
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 0);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 8);
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.y), b0 = blockIdx.x * wb;
   const int p = d.p, F = d.F, n = d.n, pF = p * F, pp2 = p * p;
@@ -378,6 +379,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
     beta[tid] = E[c.eo.bnb + tid] - mean * a;
   }
   __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 9);
   const int64_t pnF = (int64_t)pF * n, nF = (int64_t)n * F;
   float* T = ws + c.wo.T + (int64_t)b0 * pnF;
 #pragma unroll
@@ -395,6 +397,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
     return;
   }
   __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 10);
   // T_i[w][ch][f] = sum_{c'} S_i[ch][c'] x_bn[w][c'][f]  (c' in order), items (i, w, ch, f)
   const RcDiv dF(F);
   for (int e = tid; e < (n - 1) * tot; e += RC_BLOCK) {
@@ -407,6 +410,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
     for (int cp = 0; cp < p; ++cp) t = fmaf(Si[cp], xw[cp * F], t);
     T[w * pnF + ch * nF + (i1 + 1) * F + f] = t;
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 11);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_FWD, 1);
 }
 
@@ -417,6 +421,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep_win(StepCtx c, int wb) {
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
   rc_critical_priority();
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 0);
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 0);
   const RedcliffDims& d = c.d;
   const int r = rc_rep(c, blockIdx.y), g = blockIdx.x, b0 = g * wb;
   const int p = d.p, F = d.F, n = d.n, pF = p * F, pp2 = p * p;
@@ -446,6 +451,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
                  return X[(int64_t)w * d.T * p + (e - w * pF)];
                }, [&](int e, float v) { xr[e] = v; }),
                rc_seg<2>(n * pp2, [&](int e) { return ws[c.wo.S + e]; }, [&](int e, float v) { S[e] = v; }));
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 1);
   const int f = tid % F, sl = tid / F, nsl = RC_BLOCK / F;
   float mean = 0.f, inv = 0.f;
   if (sl < nsl) {
@@ -458,21 +464,40 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
     }
   }
   __syncthreads();
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 2);
   // dx_bn[w][ch][f] = sum_{c'} sum_i S_i[c'][ch] dT[w][c'][i][f]  (k = c' n + i, the GEMM's order);
   // lanes (f, slot) over rows (w, ch): dgamma[f] += dx xhat, dbeta[f] += dx
+  // (a thread's rows sl, sl + nsl, ... run four at a time as interleaved chains; each row's chain and
+  // the row order of the dgamma / dbeta sums are unchanged)
   float ag = 0.f, ab = 0.f;
   if (sl < nsl)
-    for (int row = sl; row < nw * p; row += nsl) {
-      const int w = row / p, ch = row - w * p;
-      const float* dtw = dT + w * pnF + f;
-      float dx = 0.f;
-#pragma unroll 4
+    for (int r0 = sl; r0 < nw * p; r0 += 4 * nsl) {
+      int chj[4], dtj[4];  // the row's channel and the LDS offset of its window's dT column f
+      float dx[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = min(r0 + j * nsl, nw * p - 1);  // past the end: a repeat of the last row, not summed
+        const int w = row / p;
+        chj[j] = row - w * p;
+        dtj[j] = w * (int)pnF + f;
+        dx[j] = 0.f;
+      }
       for (int cp = 0; cp < p; ++cp)
-        for (int i = 0; i < n; ++i) dx = fmaf(S[i * pp2 + cp * p + ch], dtw[cp * nF + i * F], dx);
-      const float x = xr[w * pF + f * p + ch];
-      ag += dx * ((x - mean) * inv);
-      ab += dx;
+        for (int i = 0; i < n; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dx[j] = fmaf(S[i * pp2 + cp * p + chj[j]], dT[dtj[j] + cp * (int)nF + i * F], dx[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = r0 + j * nsl;
+        if (row < nw * p) {
+          const int w = row / p, ch = row - w * p;
+          const float x = xr[w * pF + f * p + ch];
+          ag += dx[j] * ((x - mean) * inv);
+          ab += dx[j];
+        }
+      }
     }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 3);
   red[tid] = ag;
   red[RC_BLOCK + tid] = ab;
   // dS_i[ch][c'] partial = sum_w sum_f dT[w][ch][i][f] x_bn[w][c'][f]   (w outer, f inner), i >= 1
@@ -488,6 +513,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
     }
     dS[i * pp2 + rem] = t;
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 4);
   __syncthreads();
   if (tid < F) {
     float ga = 0.f, gb = 0.f;
@@ -498,6 +524,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_win_bwd(StepCtx c, int wb) {
     ws[c.wo.dgb + ((int64_t)g * 2) * F + tid] = ga;
     ws[c.wo.dgb + ((int64_t)g * 2 + 1) * F + tid] = gb;
   }
+  RC_PHASE(c.ws, c.wo.total, blockIdx.x, 5);
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_EMB_BWD, 1);
 }
 

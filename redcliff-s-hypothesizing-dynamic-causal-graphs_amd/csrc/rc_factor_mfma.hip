@@ -986,14 +986,9 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_s16(StepCtx c, int bpw, in
 #define RC_S16_BWD_WAVES 3
 #endif
 // RC_S16_EXP (timing experiments only, wrong results): bit 0 replaces the epilogue's Adam by one
-// multiply-add (loads and stores unchanged), bit 1 skips the recompute / dW0 matrix-core passes;
-// in k_fac_bwd_s16r bit 2 idles the update waves, bit 3 the contract waves (barriers kept).
+// multiply-add (loads and stores unchanged), bit 1 skips the recompute / dW0 matrix-core passes.
 #ifndef RC_S16_EXP
 #define RC_S16_EXP 0
-#endif
-// the role-split backward (k_fac_bwd_s16r) by default
-#ifndef RC_S16_ROLES_DEFAULT
-#define RC_S16_ROLES_DEFAULT 0
 #endif
 #if RC_S16_BWD_WAVES > 0
 #define RC_S16_BWD_BOUNDS __launch_bounds__(RC_BLOCK, RC_S16_BWD_WAVES)
@@ -1198,258 +1193,6 @@ static int fac_mix_nt(const RedcliffDims& d, int B) {
   return (B <= 128 && mf_recompute(d)) ? 128 : RC_BLOCK;
 }
 
-// Backward in two wave roles (RC_S16_ROLES): 512-thread workgroups, waves 0-3 CONTRACT (the
-// recompute, dZ and the dW0 products of k_fac_bwd_s16, matrix cores only: no global memory) and
-// waves 4-7 UPDATE (every global load and store of a block: its W0 run, Adam moments, adjacency
-// rows, hidden bias / W1 snapshot / output-layer state; the adjacency term and Adam on the gradient
-// tile).  Wave w + 4 serves wave w through two LDS buffers; the workgroup moves in stages separated
-// by barriers.  In stage s contract wave w works on its block i = s - 1 (operands from buffer
-// i & 1, written there in stage s - 1; its gradient tile and output-layer sums back into the same
-// buffer), while update wave w runs the epilogue of block s - 2 from buffer s & 1 and then fills
-// that buffer with block s's operands: the matrix-core passes of one block overlap the memory
-// traffic and the Adam arithmetic of others by construction, where in k_fac_bwd_s16 every wave
-// alternates between the two (timing-only builds: memory alone 104 us, memory + contraction
-// without Adam 168 us of the kept kernel's 191 at R = 128, profiles/r06_s16_bwd_parts.jsonl).
-// Every value is computed by the same operations in the same order as in k_fac_bwd_s16: the same
-// bits.  The update wave issues a block's W0 run before the epilogue of the block two stages back,
-// and the moments of the next block to finish after it.
-__host__ __device__ inline int msr_buf(int nk4) { return 64 * nk4 + 160 + 64; }  // tile + bu, w1, g0, g1 rows
-inline size_t ms_lds_bwd_roles(const RedcliffDims& d, int B, int bpw) {
-  return sizeof(float) * ((size_t)ms_rows(B) * (ms_qp16(d) + 4) + (size_t)ms_rows(B) * ms_nnet(bpw, (d.h + 15) >> 4) +
-                          4 * 2 * (size_t)msr_buf(ms_nk4(d)) + 4 * 128);
-}
-template <int NK4>
-__global__ __launch_bounds__(2 * RC_BLOCK, 4) void k_fac_bwd_s16r(StepCtx c, int bpw, int xcd) {
-  static_assert(!kMsTilePad, "the role-split backward uses the linear weight / gradient tile");
-  constexpr int NT = 2 * RC_BLOCK;
-  constexpr int S = ((NK4 + 3) / 4) * 16 + 4, NQT = (NK4 + 3) / 4, TILE = 64 * NK4 + 160, BUF = TILE + 64;
-  const RedcliffDims& d = c.d;
-  int bx = blockIdx.x, bz = blockIdx.z;
-  if (xcd) rc_xcd_order(gridDim.x, gridDim.z, bx, bz);
-  const int r = rc_rep(c, bz);
-  const int p = d.p, h = d.h, K = d.K, Q = p * d.L, B = c.B, nU = (h + 15) >> 4, NB = K * p * nU;
-  const int rows = ms_rows(B);
-  extern __shared__ float Xs[];
-  float* P = c.fac + r * c.fs;
-  float* PM = c.facM + r * c.fs;
-  float* PV = c.facV + r * c.fs;
-  float* GF = c.gF + r * c.fs;
-  const float* ws = c.ws + r * c.wss;
-  const RedcliffReplicaHyper& hy = c.hyp[r];
-  const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
-  const bool adam = !(c.flags & RC_GRAD_ONLY);
-  const bool adj_grad = (c.flags & RC_LOSS_ADJ) && ((c.flags & RC_STEP_B) || (c.flags & RC_STEP_A));
-  float* PMr = adam ? PM : P;
-  float* PVr = adam ? PV : P;
-  const int cb_lo = bx * 4 * bpw, cb_hi = min(NB, cb_lo + 4 * bpw) - 1;
-  const int kjlo = cb_lo / nU, nnet = cb_hi / nU - kjlo + 1;
-  float* Dys = Xs + rows * S;
-  RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 0);
-  {
-    const RcDiv drow(rows);
-    const float* dyg = ws + c.wo.dyl;
-    rc_stage<4, NT>(nnet * rows, [&](int e) {
-      const int n_ = drow.div(e), b = e - n_ * rows;
-      return b < B ? dyg[(int64_t)(kjlo + n_) * d.Bmax + b] : 0.f;
-    }, [&](int e, float v) { Dys[e] = v; });
-  }
-  ms_stage_x<NT>(c, r, Xs);
-  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), pair = wv & 3;
-  float* Bf = Dys + ms_nnet(bpw, nU) * rows + pair * 2 * BUF;  // the pair's two buffers
-  float* Dg = Dys + ms_nnet(bpw, nU) * rows + 4 * 2 * BUF + pair * 128;  // update wave: dL/dG row, then G
-  float* Gn = Dg + 64;
-  const int u_off = g == 0 ? 4 * l15 : MS_OOB;
-  const int q0 = lane % Q, dq = 64 % Q;
-  // update wave's registers: the pre-update W0 runs (and hidden biases) of blocks s - 2 and s - 1
-  // (two sets by stage parity: the set of block s - 2 takes block s after its epilogue), and one
-  // set of Adam moments / adjacency rows / output-layer state, loaded one stage ahead of its epilogue
-  struct WSet {
-    float wt[NK4], b0;
-  };
-  struct MSet {
-    float mt[NK4], vt[NK4], sb[5], dgv, gnv;
-  };
-  WSet ws0, ws1;
-  MSet mv;
-  auto issue_w = [&](int cb, float (&w)[NK4], float& b0, float& w1s) {  // what the contract wave needs next stage
-    const int kj = cb / nU, u0 = (cb - kj * nU) * 16, nu = min(16, h - u0);
-    ms_load_tile<NK4>(ms_rsrc(P + c.fo.W0 + ((int64_t)kj * h + u0) * Q, nu * Q), lane, w);
-    b0 = ms_ld(ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu), 4 * l15);    // 0 past h
-    w1s = ms_ld(ms_rsrc(ws + c.wo.w1 + (int64_t)kj * h + u0, nu), 4 * l15);  // pre-update snapshot
-  };
-  auto issue_m = [&](int cb, MSet& o) {  // what the epilogue of block cb reads besides the W0 run
-    const int kj = cb / nU, u0 = (cb - kj * nU) * 16, nu = min(16, h - u0);
-    const int64_t wofs = c.fo.W0 + ((int64_t)kj * h + u0) * Q;
-    ms_load_tile<NK4>(ms_rsrc(PMr + wofs, nu * Q), lane, o.mt);
-    ms_load_tile<NK4>(ms_rsrc(PVr + wofs, nu * Q), lane, o.vt);
-    o.dgv = ms_ld(ms_rsrc(ws + c.wo.dgs + (int64_t)kj * Q, Q), 4 * lane);
-    o.gnv = ms_ld(ms_rsrc(ws + c.wo.G + (int64_t)kj * Q, Q), 4 * lane);
-    o.sb[0] = ms_ld(ms_rsrc(PMr + c.fo.b0 + (int64_t)kj * h + u0, nu), 4 * l15);
-    o.sb[1] = ms_ld(ms_rsrc(PVr + c.fo.b0 + (int64_t)kj * h + u0, nu), 4 * l15);
-    o.sb[2] = ms_ld(ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu), 4 * l15);
-    o.sb[3] = ms_ld(ms_rsrc(PMr + c.fo.W1 + (int64_t)kj * h + u0, nu), 4 * l15);
-    o.sb[4] = ms_ld(ms_rsrc(PVr + c.fo.W1 + (int64_t)kj * h + u0, nu), 4 * l15);
-  };
-  __syncthreads();
-  // The two roles run separate stage loops with the same barriers (bpw + 2 stages), so neither
-  // role's registers are live in the other's code.
-  if (wv < 4) {
-    for (int s = 0; s < bpw + 2; ++s) {
-      // ---------------- contract wave: block i = s - 1
-      const int i = s - 1, cb = cb_lo + 4 * i + pair;
-      if (!(RC_S16_EXP & 8) && i >= 0 && i < bpw && cb < NB) {
-        float* T = Bf + (i & 1) * BUF;
-        const int kj = cb / nU;
-        float wB[NK4];
-        {
-          const float* row = T + l15 * Q + g;
-#pragma unroll
-          for (int k = 0; k < NK4; ++k) {
-            const float v = row[4 * k];
-            wB[k] = (k + 1 < NK4 || 4 * k + g < Q) ? v : 0.f;
-          }
-        }
-        const float bu = T[TILE + l15], w1 = T[TILE + 16 + l15];  // 0 past h
-        f32x4 acc[NQT];
-#pragma unroll
-        for (int t = 0; t < NQT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        float pa = 0.f, pb = 0.f;
-        const float* dyn = Dys + (kj - kjlo) * rows + 4 * g;
-        for (int t0 = 0; t0 < B; t0 += 32) {
-          f32x4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-          const float* xr = Xs + (t0 + l15) * S + ms_sh(l15) + g;
-#pragma unroll
-          for (int k = 0; k < NK4; ++k) {
-            z[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[4 * k], wB[k], z[0], 0, 0, 0);
-            z[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[16 * S + 4 * k], wB[k], z[1], 0, 0, 0);
-          }
-          float dz[2][4];
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const f32x4 dy = *reinterpret_cast<const f32x4*>(dyn + t0 + 16 * tt);
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-#pragma clang fp contract(off)
-              const float a = fmaxf(z[tt][reg] + bu, 0.f);
-              dz[tt][reg] = a > 0.f ? dy[reg] * w1 : 0.f;
-              pa = pa + dy[reg] * a;
-              pb = pb + dz[tt][reg];
-            }
-          }
-#pragma unroll
-          for (int tt = 0; tt < 2; ++tt) {
-            const float* xq = Xs + (t0 + 16 * tt + 4 * g) * S + ms_sh(4 * g) + l15;
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg)
-#pragma unroll
-              for (int qt = 0; qt < NQT; ++qt)
-                acc[qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[tt][reg], xq[reg * S + 16 * qt], acc[qt], 0, 0, 0);
-          }
-        }
-        const float a1 = __shfl(pa, l15 + 16, 64), a2 = __shfl(pa, l15 + 32, 64), a3 = __shfl(pa, l15 + 48, 64);
-        const float b1 = __shfl(pb, l15 + 16, 64), b2 = __shfl(pb, l15 + 32, 64), b3 = __shfl(pb, l15 + 48, 64);
-        if (g == 0) {
-          T[TILE + 32 + l15] = ((pb + b1) + b2) + b3;  // dL/db0 of unit l15
-          T[TILE + 48 + l15] = ((pa + a1) + a2) + a3;  // dL/dW1
-        }
-#pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) {
-          const int q = 16 * qt + l15;
-          if (qt + 1 < NQT || q < Q)
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) T[(4 * g + reg) * Q + q] = acc[qt][reg];
-        }
-      }
-      __syncthreads();
-    }
-    RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 1);
-    return;
-  }
-  // stage s of the update wave; A = its W0 set of blocks s - 2 and s (the sets alternate by stage
-  // parity, and the loop below names them statically so they stay in registers)
-  auto ustage = [&](const int s, WSet& A) {
-    {
-      // ---------------- update wave: epilogue of block j = s - 2, moments of block m = s - 1,
-      // operands of block k = s
-      const int j = s - 2, cbj = cb_lo + 4 * j + pair, m = s - 1, cbm = cb_lo + 4 * m + pair, k = s,
-                cbk = cb_lo + 4 * k + pair;
-      const bool uon = !(RC_S16_EXP & 4);
-      const bool doj = uon && j >= 0 && j < bpw && cbj < NB, dom = uon && m >= 0 && m < bpw && cbm < NB,
-                 dok = uon && k < bpw && cbk < NB;
-      float wk[NK4], b0k = 0.f, w1k = 0.f;
-      if (dok) issue_w(cbk, wk, b0k, w1k);
-      if (doj) {
-        const float* T = Bf + (j & 1) * BUF;
-        const int kj = cbj / nU, u0 = (cbj - kj * nU) * 16, nu = min(16, h - u0);
-        const int64_t wofs = c.fo.W0 + ((int64_t)kj * h + u0) * Q;
-        {  // output layer / hidden bias of unit l15 (group 0 stores, rows past h dropped)
-          const float g0 = T[TILE + 32 + l15], g1 = T[TILE + 48 + l15];
-          const auto rB0 = ms_rsrc(P + c.fo.b0 + (int64_t)kj * h + u0, nu);
-          const auto rW1 = ms_rsrc(P + c.fo.W1 + (int64_t)kj * h + u0, nu);
-          if (!adam) {
-            ms_st(ms_rsrc(GF + c.fo.b0 + (int64_t)kj * h + u0, nu), u_off, g0);
-            ms_st(ms_rsrc(GF + c.fo.W1 + (int64_t)kj * h + u0, nu), u_off, g1);
-          } else {
-            const auto rMb = ms_rsrc(PMr + c.fo.b0 + (int64_t)kj * h + u0, nu), rVb = ms_rsrc(PVr + c.fo.b0 + (int64_t)kj * h + u0, nu);
-            const auto rMw = ms_rsrc(PMr + c.fo.W1 + (int64_t)kj * h + u0, nu), rVw = ms_rsrc(PVr + c.fo.W1 + (int64_t)kj * h + u0, nu);
-            float b0v = A.b0, mb = mv.sb[0], vb = mv.sb[1], w1v = mv.sb[2], mw = mv.sb[3], vw = mv.sb[4];
-            rc_adam(b0v, mb, vb, g0, as);
-            rc_adam(w1v, mw, vw, g1, as);
-            ms_st(rB0, u_off, b0v);
-            ms_st(rMb, u_off, mb);
-            ms_st(rVb, u_off, vb);
-            ms_st(rW1, u_off, w1v);
-            ms_st(rMw, u_off, mw);
-            ms_st(rVw, u_off, vw);
-          }
-        }
-        Dg[lane] = mv.dgv;
-        Gn[lane] = mv.gnv;
-        const auto rW = ms_rsrc(P + wofs, nu * Q), rM = ms_rsrc(PMr + wofs, nu * Q), rV = ms_rsrc(PVr + wofs, nu * Q),
-                   rG = ms_rsrc(GF + wofs, nu * Q);
-        int q = q0;
-#pragma unroll
-        for (int kk = 0; kk < NK4; ++kk) {
-          const int e = lane + 64 * kk;
-          float gr = T[e];
-          const float dg = Dg[q], gn = Gn[q], pw = A.wt[kk];
-          if (adj_grad && gn > 0.f) gr += dg * (pw / gn);
-          if (!adam) {
-            ms_st(rG, 4 * e, gr);
-          } else {
-            float pp = pw, mm = mv.mt[kk], vv = mv.vt[kk];
-            rc_adam(pp, mm, vv, gr, as);
-            ms_st(rW, 4 * e, pp);
-            ms_st(rM, 4 * e, mm);
-            ms_st(rV, 4 * e, vv);
-          }
-          q += dq;
-          q = q >= Q ? q - Q : q;
-        }
-      }
-      if (dom) issue_m(cbm, mv);
-      if (dok) {
-#pragma unroll
-        for (int q = 0; q < NK4; ++q) A.wt[q] = wk[q];
-        A.b0 = b0k;
-        float* T = Bf + (k & 1) * BUF;  // block j's gradient was read above: the buffer is free
-#pragma unroll
-        for (int q = 0; q < NK4; ++q) T[lane + 64 * q] = wk[q];
-        if (g == 0) {
-          T[TILE + l15] = b0k;
-          T[TILE + 16 + l15] = w1k;
-        }
-      }
-    }
-    __syncthreads();
-  };
-  for (int s = 0; s < bpw + 2; s += 2) {
-    ustage(s, ws0);
-    if (s + 1 < bpw + 2) ustage(s + 1, ws1);
-  }
-}
-
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
   const int Q = d.p * d.L;
   return sizeof(float) * (size_t)(2 * d.Bmax + 2 * Q + d.p + d.L + 16 + d.p * Ls + d.Bmax * d.K + 2 * RC_BLOCK + d.Bmax);
@@ -1488,23 +1231,16 @@ int rc_fac_slots(const RedcliffDims& d) { return rc_fac_short(d) ? (d.h + 15) / 
 typedef void (*MsKern)(StepCtx, int, int);
 template <int N>
 struct MsTab {
-  static void fill(MsKern* f, MsKern* b, MsKern* br) {
+  static void fill(MsKern* f, MsKern* b) {
     f[N - 1] = k_fac_fwd_s16<N>;
     b[N - 1] = k_fac_bwd_s16<N>;
-    br[N - 1] = k_fac_bwd_s16r<N>;
-    MsTab<N - 1>::fill(f, b, br);
+    MsTab<N - 1>::fill(f, b);
   }
 };
 template <>
 struct MsTab<0> {
-  static void fill(MsKern*, MsKern*, MsKern*) {}
+  static void fill(MsKern*, MsKern*) {}
 };
-
-// the role-split backward (k_fac_bwd_s16r); REDCLIFF_S16_ROLES=0|1 overrides (read per launch, A/B)
-static bool ms_roles() {
-  const char* v = getenv("REDCLIFF_S16_ROLES");
-  return v ? v[0] == '1' : RC_S16_ROLES_DEFAULT;
-}
 
 static int ms_cus() {
   static const int n = [] {
@@ -1516,69 +1252,62 @@ static int ms_cus() {
   return n;
 }
 
-static int ms_occupancy(MsKern k, size_t lds, int nt) {
+static int ms_occupancy(MsKern k, size_t lds) {
   struct Ent { MsKern k; size_t lds; int occ; };
   static thread_local Ent cache[32];
   static thread_local int n = 0;
   for (int i = 0; i < n; ++i)
     if (cache[i].k == k && cache[i].lds == lds) return cache[i].occ;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, nt, lds) != hipSuccess) nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, RC_BLOCK, lds) != hipSuccess) nb = 0;
   cache[n < 32 ? n++ : 31] = Ent{k, lds, nb};
   return nb;
 }
 
 static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
-  static MsKern tf[16], tb[16], tbr[16];
-  static const bool init = (MsTab<16>::fill(tf, tb, tbr), true);
+  static MsKern tf[16], tb[16];
+  static const bool init = (MsTab<16>::fill(tf, tb), true);
   (void)init;
   const RedcliffDims& d = c.d;
-  const bool roles = bwd && ms_roles();
-  const char* what = roles ? "k_fac_bwd_s16r" : (bwd ? "k_fac_bwd_s16" : "k_fac_fwd_s16");
+  const char* what = bwd ? "k_fac_bwd_s16" : "k_fac_fwd_s16";
   const int nk4 = ms_nk4(d);
   if (nk4 < 1 || nk4 > 16) { rc_set_error("%s: p*L = %d outside the short-contraction kernels", what, d.p * d.L); return REDCLIFF_ELIMIT; }
-  MsKern k = roles ? tbr[nk4 - 1] : (bwd ? tb[nk4 - 1] : tf[nk4 - 1]);
-  const int nt = roles ? 2 * RC_BLOCK : RC_BLOCK, kind = roles ? 2 : (int)bwd;
-  auto lds_of = [&](int bpw_) {
-    return roles ? ms_lds_bwd_roles(d, c.B, bpw_) : (bwd ? ms_lds_bwd(d, c.B, bpw_) : ms_lds_fwd(d, c.B));
-  };
+  MsKern k = bwd ? tb[nk4 - 1] : tf[nk4 - 1];
   const int NB = d.K * d.p * ((d.h + 15) / 16);
   const size_t cap = RC_LDS_MAX_FLOATS * sizeof(float);
-  size_t lds = lds_of(1);
+  size_t lds = bwd ? ms_lds_bwd(d, c.B, 1) : ms_lds_fwd(d, c.B);
   if (lds > cap) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
   int bpw = 1;
   const char* env = getenv("REDCLIFF_FAC_BPW");
   if (env && atoi(env) > 0) {
     bpw = atoi(env);
   } else {
-    static bool optin[3][16];
-    if (!optin[kind][nk4 - 1]) {  // the occupancy query of a launch past 64 KiB needs the opt-in
+    static bool optin[2][16];
+    if (!optin[bwd][nk4 - 1]) {  // the occupancy query of a launch past 64 KiB needs the opt-in
       const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap), what);
       if (e) return e;
-      optin[kind][nk4 - 1] = true;
+      optin[bwd][nk4 - 1] = true;
     }
-    const int64_t slots = (int64_t)ms_occupancy(k, lds, nt) * ms_cus();
+    const int64_t slots = (int64_t)ms_occupancy(k, lds) * ms_cus();
     if (slots > 0) {
       // the backward as one round of resident workgroups, the forward (short blocks, a staging
       // prologue per workgroup) as about two: R = 128 D4IC grid, bpw 4 / 8 / 16 -> forward 114 /
-      // 140 / 145 us, backward 228 / 236 / 266 us against 205 us at one round (12).  The role-split
-      // backward pipelines its blocks (two stages of fill / drain per workgroup), so it takes more
-      // blocks per wave than the 16 of the others.
-      const int64_t rounds = bwd ? 1 : 2, maxb = roles ? 64 : 16;
+      // 140 / 145 us, backward 228 / 236 / 266 us against 205 us at one round (12)
+      const int64_t rounds = bwd ? 1 : 2;
       const int64_t blocks = (int64_t)NB * c.nrep, want = (blocks + 4 * rounds * slots - 1) / (4 * rounds * slots);
-      bpw = (int)(want < 1 ? 1 : (want > maxb ? maxb : want));
+      bpw = (int)(want < 1 ? 1 : (want > 16 ? 16 : want));
     }
   }
   if (bwd)
-    while (bpw > 1 && lds_of(bpw) > cap) --bpw;
-  if (bwd) lds = lds_of(bpw);
+    while (bpw > 1 && ms_lds_bwd(d, c.B, bpw) > cap) --bpw;
+  if (bwd) lds = ms_lds_bwd(d, c.B, bpw);
   if (lds > cap) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
   if (lds > RC_LDS_LIMIT_FLOATS * sizeof(float)) {
     const int e = rc_check(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), what);
     if (e) return e;
   }
   const char* xe = getenv("REDCLIFF_S16_XCD");  // read per launch (A/B); default on
-  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(nt), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
+  hipLaunchKernelGGL(k, dim3((NB + 4 * bpw - 1) / (4 * bpw), 1, c.nrep), dim3(RC_BLOCK), lds, s, c, bpw, (int)!(xe && xe[0] == '0'));
   return rc_check(hipGetLastError(), what);
 }
 

@@ -57,13 +57,14 @@ def main():
         print("%-9s WGs %4d  start %8.2f us  span %7.2f us  WG dur min/med/max %6.2f %6.2f %6.2f  WG0 %6.2f"
               % (name, ok.sum(), (st[ok].min() - t_first) / 100.0, (en[ok].max() - st[ok].min()) / 100.0,
                  dur.min(), np.median(dur), dur.max(), (en[0] - st[0]) / 100.0 if ok[0] else -1), flush=True)
-    # phase marks of workgroup 0 of replica 0 (RC_PHASE slots 6 * 2048 + i): k_fac_mix 16..23
+    # phase marks of workgroup 0 of replica 0 (RC_PHASE slots 6 * 2048 + i), per kernel relative to
+    # its first mark: k_lemb_win_bwd 0..7, k_lemb_prep_win 8..15, k_fac_mix 16..23, k_emb_final 48..58
     ph = tr[6]
-    marks = [(i, int(ph[i])) for i in range(64) if ph[i] > 0]
-    if marks:
-        print("phase marks of workgroup 0 (us after the first mark): " +
-              " ".join("%d:%.2f" % (i, (t - marks[0][1]) / 100.0) for i, t in marks), flush=True)
-
+    for name, lo, hi in (("lemb_win_bwd", 0, 8), ("lemb_prep_win", 8, 16), ("fac_mix", 16, 24), ("emb_final", 48, 64)):
+        marks = [(i, int(ph[i])) for i in range(lo, hi) if ph[i] > 0]
+        if marks:
+            print("phase marks %-13s (us after its first mark): " % name +
+                  " ".join("%d:%.2f" % (i, (t - marks[0][1]) / 100.0) for i, t in marks), flush=True)
 
 if __name__ == "__main__":
     main()
