@@ -248,6 +248,22 @@ __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
   float* dwf = rB + RC_BLOCK;     // [Bmax]  forecast part of dL/dw_bk
 
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_MIX, 0);
+  // NT < 256 (B <= 128, fac_mix_nt): the block sums run over the windows in the layout of a
+  // 256-thread workgroup, window b = virtual thread vv * NT + tid, so every sum keeps its order
+  constexpr int NV = RC_BLOCK / NT;
+  auto vsum256 = [&](const float (&v)[NV]) {  // rc_block_sum over the virtual layout, every thread gets it
+    __syncthreads();
+#pragma unroll
+    for (int vv = 0; vv < NV; ++vv) {
+      const float w = rc_wave_sum(v[vv]);
+      if ((tid & 63) == 0) red[vv * (NT / 64) + (tid >> 6)] = w;
+    }
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < RC_BLOCK / 64; ++i) t += red[i];
+    __syncthreads();
+    return t;
+  };
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 16);
   // ---- mixture, forecast residual, dL/dy, forecast part of dL/dw
   const float gscale = (c.flags & RC_LOSS_FORECAST) ? hy.c_forecast * (2.f / (float)c.Bg) : 0.f;
@@ -272,8 +288,10 @@ __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
     ybuf[(e - kk * B) * K + kk] = v;
   });
   __syncthreads();
-  float fsum = 0.f;
-  for (int b = tid; b < B; b += NT) {
+  float fsum[NV];
+#pragma unroll
+  for (int vv = 0; vv < NV; ++vv) fsum[vv] = 0.f;
+  for (int b = tid, it = 0; b < B; b += NT, ++it) {
     const float* wr = ws + c.wo.w + (int64_t)b * K;
     const bool tgt = c.flags & (RC_LOSS_FORECAST | RC_VALUES);
     const float xt = tgt ? X[((c.row0 + b) * d.T + c.Lmax) * p + j] : 0.f;
@@ -291,12 +309,12 @@ __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
     dwf[b] = g * ybuf[b * K + k];
     if (fgrad && !adj_grad) ws[c.wo.dwp + ((int64_t)j * d.Bmax + b) * K + k] = dwf[b];
     if (k == 0) {
-      fsum += res * res;
+      fsum[min(it, NV - 1)] += res * res;  // (NT < 256: one window per virtual slot)
       ws[c.wo.xsim + (int64_t)b * p + j] = xs;
     }
   }
   if (values && k == 0) {
-    const float t = rc_block_sum(fsum, red);
+    const float t = vsum256(fsum);
     if (tid == 0) ws[c.wo.lossp + j] = t;
   }
   RC_PHASE(c.ws, c.wo.total, blockIdx.x, 17);
@@ -334,7 +352,6 @@ __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
     const int half = tid & 1, hp = (p + 1) / 2, c0 = half * hp, c1 = min(p, c0 + hp);
     // windows in the layout of a 256-thread workgroup (thread vt = vv * NT + tid: window
     // b0 + vt / 2), so the loss value's block sum below keeps one summation order for every NT
-    constexpr int NV = RC_BLOCK / NT;
     float vsum[NV];
 #pragma unroll
     for (int vv = 0; vv < NV; ++vv) vsum[vv] = 0.f;
@@ -424,10 +441,12 @@ __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
   const RcAdamScalars as = rc_adam_scalars(hy.B, c.tB);
   const float* aw = ws + c.wo.a + (int64_t)kj * d.Bmax * h;
   const float* W1 = ws + c.wo.w1 + (int64_t)kj * h;  // pre-update snapshot written by the forward
-  float db1 = 0.f;
-  for (int b = tid; b < B; b += NT) db1 += dyl[b];
-  db1 = rc_block_sum(db1, red);
-  for (int u0 = 0; u0 < (mf_recompute(d) ? 0 : h); u0 += 32) {  // else: in k_fac_bwd_mfma<4>
+  float db1v[NV];
+#pragma unroll
+  for (int vv = 0; vv < NV; ++vv) db1v[vv] = 0.f;
+  for (int b = tid, it = 0; b < B; b += NT, ++it) db1v[min(it, NV - 1)] += dyl[b];
+  const float db1 = vsum256(db1v);
+  for (int u0 = 0; u0 < ((mf_recompute(d) || NT != RC_BLOCK) ? 0 : h); u0 += 32) {  // else: in k_fac_bwd_mfma<4>
     const int uu = tid & 31, part = tid >> 5, u = u0 + uu;
     float dW1u = 0.f, db0u = 0.f;
     if (u < h) {
@@ -1183,14 +1202,19 @@ __global__ RC_S16_BWD_BOUNDS void k_fac_bwd_s16(StepCtx c, int bpw, int xcd) {
   RC_WG_MARK(c.ws, c.wo.total, RC_KID_FAC_BWD, 1);
 }
 
+// k_fac_mix's workgroup threads where it may be narrower than 256 (64 / 128)
+#ifndef RC_MIX_NT
+#define RC_MIX_NT 128
+#endif
 // k_fac_mix's workgroup: 128 threads when B <= 128 (one window per thread, so the per-thread
 // window sums and the block sums of the loss value and the output-bias gradient see the same
 // operands in the same order as at 256 threads, whose upper waves held zeros) and the hidden-layer
 // gradients come from the dW0 kernel (mf_recompute: the 32-units-by-8-slices pass is not run).
 static int fac_mix_nt(const RedcliffDims& d, int B) {
-  const char* v = getenv("REDCLIFF_MIX_NT");
-  if (v && atoi(v) == 256) return RC_BLOCK;
-  return (B <= 128 && mf_recompute(d)) ? 128 : RC_BLOCK;
+  const char* v = getenv("REDCLIFF_MIX_NT");  // read per launch (A/B)
+  const int want = v ? atoi(v) : RC_MIX_NT;
+  if (!(B <= 128 && mf_recompute(d))) return RC_BLOCK;
+  return want == 64 || want == 128 ? want : RC_BLOCK;
 }
 
 size_t fac_mix_lds(const RedcliffDims& d, int Ls) {
@@ -1227,7 +1251,8 @@ int rc_fac_slots(const RedcliffDims& d) { return rc_fac_short(d) ? (d.h + 15) / 
 
 // Launch of the short-contraction kernels: the k-step count picks the instantiation, and the
 // blocks per wave are chosen from the resident workgroups (the occupancy the runtime computes
-// from the kernel's registers and this launch's LDS, times the CUs).  REDCLIFF_FAC_BPW=n overrides.
+// from the kernel's registers and this launch's LDS, times the CUs).  REDCLIFF_FAC_BPW=n (backward) /
+// REDCLIFF_FAC_BPW_FWD=n (forward) override.
 typedef void (*MsKern)(StepCtx, int, int);
 template <int N>
 struct MsTab {
@@ -1278,7 +1303,7 @@ static int ms_launch(bool bwd, const StepCtx& c, hipStream_t s) {
   size_t lds = bwd ? ms_lds_bwd(d, c.B, 1) : ms_lds_fwd(d, c.B);
   if (lds > cap) { rc_set_error("%s: %d windows do not fit in LDS", what, c.B); return REDCLIFF_ELIMIT; }
   int bpw = 1;
-  const char* env = getenv("REDCLIFF_FAC_BPW");
+  const char* env = getenv(bwd ? "REDCLIFF_FAC_BPW" : "REDCLIFF_FAC_BPW_FWD");
   if (env && atoi(env) > 0) {
     bpw = atoi(env);
   } else {
@@ -1335,7 +1360,10 @@ int rc_launch_fac_mix(const StepCtx& c, hipStream_t s) {
   // the dW0 kernel: twice the resident workgroups for a kernel whose time is its workgroups'
   // chains of dependent memory rounds, the same bits (every sum keeps its order: fac_mix_nt).
   // REDCLIFF_MIX_NT=256 keeps the full workgroups (A/B).
-  if (fac_mix_nt(d, c.B) == 128)
+  const int nt = fac_mix_nt(d, c.B);
+  if (nt == 64)
+    hipLaunchKernelGGL(k_fac_mix<64>, dim3(KP, c.nrep), dim3(64), lds, s, c, (int)!(xe && xe[0] == '0'));
+  else if (nt == 128)
     hipLaunchKernelGGL(k_fac_mix<128>, dim3(KP, c.nrep), dim3(128), lds, s, c, (int)!(xe && xe[0] == '0'));
   else
     hipLaunchKernelGGL(k_fac_mix<RC_BLOCK>, dim3(KP, c.nrep), dim3(RC_BLOCK), lds, s, c, (int)!(xe && xe[0] == '0'));
