@@ -7,6 +7,9 @@ tests/test_gpu_fit_golden.py relies on when it bounds the GPU fit by that spread
   * every realization takes the fixture's decisions (stopping epoch, best_it): the spread is
     rounding, not a different trajectory;
   * realization 0 (the fixture's own window order) stays within 1e-3 of the fixture along the fit;
+  * fit_tst_lag64's envelope adds a float64 realization (ENVELOPE_DTYPE=float64, the fixture's window
+    order): its flat-start windows make the float32 computation ill-conditioned, so the float64 run
+    leaves the window-order spread by far (DESIGN.md §5) while taking the same decisions;
   * the resumed C1 fit's spread exceeds the 1e-4 loss tolerance (measured 2.2e-3 on the last fw-L1
     entry) and its states leave the 2e-4 state tolerance at dozens of entries -- the reason the
     resume test cannot hold the fixed tolerance for any implementation, the reference included.
