@@ -195,7 +195,7 @@ def true_gc(d, meta):
 ENV_FIT = ("fit_d4ic_pub", "fit_tst", "fit_tst_lag64")  # long trajectories: the fit is held to the reference's own spread
 # float32-ill-conditioned fixtures: the reference's fp32 GC trajectory is no reachable target
 # (its embedder weights move by 1e-3 between float32 and float64 in one step), so the fixed-tolerance
-# GC-progress / final-GC checks are made against the reference's own float64 fit instead
+# GC-progress / final-GC / final-state checks are made against the reference's own float64 fit instead
 # (test_lag64_fit_tracks_the_float64_reference_fit)
 ILL_CONDITIONED = ("fit_tst_lag64",)
 
@@ -228,8 +228,7 @@ def check_fit(name, m, ret, d, meta, env, val):
     assert len(h["avg_combo_loss"]) == n, (len(h["avg_combo_loss"]), n)
     check_stop(h, d, meta, "hist/epoch")
     compare_hist(name, h, d, "hist", env=env, part="fit")
-    if name in ILL_CONDITIONED:
-        compare_state_envelope("final", m, state(d, "final"), env, "fit")
+    if name in ILL_CONDITIONED:  # (its final state: against the float64 fit, in the test below)
         fr = float(d["fit_return"])
         within_envelope("fit return", np.asarray([ret]), np.asarray([fr]), np.asarray([1e-4 * abs(fr) + 1e-6]),
                         np.abs(env["fit/fit_return"] - fr)[:, None])
