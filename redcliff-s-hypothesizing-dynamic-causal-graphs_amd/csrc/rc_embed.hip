@@ -1697,6 +1697,23 @@ __global__ __launch_bounds__(RC_BLOCK) void k_emb_final(StepCtx c, int nw, int e
   }
 }
 
+// k_emb_final as two launches for packed grids at small node counts: the one launch's register
+// allocation is the adjacency workgroup's (k_emb_final<4>: 190 VGPRs + 16 AGPRs, 2 waves per SIMD), so
+// its ~11 parameter workgroups per replica (R = 128 D4IC: 1,408) ran in three rounds; the parameter
+// workgroups in a launch of their own take only the registers of the Adam pass.  The same device
+// function per workgroup, so the same bits.  (At C5 the adjacency workgroup alone outlasts the
+// combined launch -- measured, not used there.)
+template <int NR>
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_final_adj(StepCtx c) {
+  rc_critical_priority();
+  emb_final_wg<NR>(c, 0, blockIdx.x, 1, false, false);
+}
+template <int NR>
+__global__ __launch_bounds__(RC_BLOCK) void k_emb_final_params(StepCtx c, int ept) {
+  rc_critical_priority();
+  emb_final_wg<NR>(c, 1 + (int)(blockIdx.x & 0xffffff), blockIdx.y, ept, false, false);  // (wx > 0 provably: no adjacency code)
+}
+
 // k_emb_combine + k_emb_final as one launch (single fits with the fused embedder; round 3):
 // workgroup 0 is the adjacency workgroup, which sums its dS partials in place (the sums
 // k_emb_combine forms) and so starts at once; workgroups 1 .. ncomb are the combine's, which
@@ -1902,6 +1919,9 @@ int rc_launch_emb_combine(const StepCtx& c, hipStream_t s) {
   return rc_check(hipGetLastError(), "k_emb_combine");
 }
 
+#ifndef RC_EMB_FINAL_SPLIT_NW
+#define RC_EMB_FINAL_SPLIT_NW 32  // parameter workgroups per replica from which packed grids split k_emb_final
+#endif
 static size_t rc_emb_final_lds(const RedcliffDims& d) {
   return sizeof(float) * ((size_t)(2 * d.n + 2) * d.p * (d.p + 1) + 3 * 64);
 }
@@ -1952,6 +1972,19 @@ int rc_launch_emb_final(const StepCtx& c, hipStream_t s) {
   const int nw = (total + ept * RC_BLOCK - 1) / (ept * RC_BLOCK);
   const size_t lds = rc_emb_final_lds(d);
   if (lds > RC_LDS_MAX_FLOATS * sizeof(float)) { rc_set_error("embedder final: LDS budget exceeded"); return REDCLIFF_ELIMIT; }
+  const char* sv = getenv("REDCLIFF_EMB_FINAL_SPLIT");  // read per launch (A/B): 0 one launch, 1 two
+  // default: packed grids with many parameter workgroups per replica -- R = 128 TST (40 per replica)
+  // 119.4 -> 112.1 us, step 1.027 -> 1.001 ms; R = 128 D4IC (11 per replica) 44.0-44.8 -> 48.3-49.1 us,
+  // where the adjacency launch's own time is not won back (profiles/r06_emb_final_split_ab.jsonl)
+  const bool split = sv ? sv[0] == '1' : (c.nrep >= 8 && nw >= RC_EMB_FINAL_SPLIT_NW);
+  if (split && d.p * d.p <= 4 * RC_BLOCK) {
+    int e = rc_lds_optin(k_emb_final_adj<4>, lds, "k_emb_final LDS");
+    if (e) return e;
+    hipLaunchKernelGGL(k_emb_final_adj<4>, dim3(c.nrep), dim3(RC_BLOCK), lds, s, c);
+    if ((e = rc_check(hipGetLastError(), "k_emb_final_adj"))) return e;
+    hipLaunchKernelGGL(k_emb_final_params<4>, dim3(nw, c.nrep), dim3(RC_BLOCK), 0, s, c, ept);
+    return rc_check(hipGetLastError(), "k_emb_final_params");
+  }
   if (d.p * d.p <= 4 * RC_BLOCK) {
     int e = rc_lds_optin(k_emb_final<4>, lds, "k_emb_final LDS");
     if (e) return e;
