@@ -207,6 +207,10 @@ __global__ __launch_bounds__(RC_BLOCK) void k_fac_fwd_mfma(StepCtx c) {
 //   terms, -> ws.dwp), group norms G / G0, adjacency-L1 value and its gradients wrt the
 //   lagged group norms (-> ws.dgs, used by the dW0 epilogue) and A (-> ws.dAadj), and the
 //   output-layer / hidden-bias gradients + Adam (b0, W1, b1).
+// k_fac_mix: predictions staged per thread per round of loads (each with its nUB slot partials)
+#ifndef RC_MIX_STAGE_U
+#define RC_MIX_STAGE_U 2
+#endif
 template <int NT>
 __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
   const RedcliffDims& d = c.d;
@@ -271,7 +275,7 @@ __global__ __launch_bounds__(NT) void k_fac_mix(StepCtx c, int xcd) {
   // the nUB (<= 8) slot partials of every prediction requested together, summed in slot order;
   // element e = kk * B + b (consecutive windows of one network: contiguous in y) -> ybuf[b][kk]
   const RcDiv dB(B);
-  rc_stage<2, NT>(B * K, [&](int e) {
+  rc_stage<RC_MIX_STAGE_U, NT>(B * K, [&](int e) {
     const int kk = dB.div(e), b = e - kk * B;
     const float* yp = ws + c.wo.y + rc_y_idx(d, 0, kk * p + j, b);
     const int64_t ys_ = (int64_t)d.Bmax * K * p;
