@@ -1342,6 +1342,9 @@ struct EmbWbSum {
 // combine runs in the same launch); adj_inplace: the adjacency workgroup sums its dS partials in
 // place (k_emb_tail, where it does not wait for the combine).
 #define EF_EPT_MAX 8  // runs per thread of the batched parameter path (k_emb_final's ept <= this)
+#ifndef RC_EF_PMV_FIRST
+#define RC_EF_PMV_FIRST 1  // batched path: parameters / moments requested with (1) or after (0) the gradients
+#endif
 template <int NR>
 __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, int ept, bool sc1, bool adj_inplace) {
   const RedcliffDims& d = c.d;
@@ -1401,6 +1404,17 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
           ix[run] = c.eo.fc1W + q;
         }
       }
+      float pv[EF_EPT_MAX], mv[EF_EPT_MAX], vv[EF_EPT_MAX];
+#if RC_EF_PMV_FIRST
+      // the parameters and both moments requested with the gradients (one round, not two)
+#pragma unroll
+      for (int run = 0; run < EF_EPT_MAX; ++run) {
+        const int64_t i = ix[run] >= 0 ? ix[run] : 0;
+        pv[run] = E[i];
+        mv[run] = Mm[i];
+        vv[run] = V[i];
+      }
+#endif
       // the one-record gradients of all runs requested together (the other runs read offset 0)
 #pragma unroll
       for (int run = 0; run < EF_EPT_MAX; ++run) {
@@ -1433,7 +1447,7 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
           g[run] = (g4[0] + g4[1]) + (g4[2] + g4[3]);
         }
       }
-      float pv[EF_EPT_MAX], mv[EF_EPT_MAX], vv[EF_EPT_MAX];
+#if !RC_EF_PMV_FIRST
 #pragma unroll
       for (int run = 0; run < EF_EPT_MAX; ++run) {
         const int64_t i = ix[run] >= 0 ? ix[run] : 0;
@@ -1441,6 +1455,7 @@ __device__ __forceinline__ void emb_final_wg(const StepCtx& c, int wx, int wy, i
         mv[run] = Mm[i];
         vv[run] = V[i];
       }
+#endif
 #pragma unroll
       for (int run = 0; run < EF_EPT_MAX; ++run) {
         if (ix[run] < 0) continue;

@@ -82,40 +82,63 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
 // the partials four at a time (clamped indices, no branch per load) and lane k's fc2 row into
 // registers 32 terms at a time; relu(f1[m]) is read with v_readlane.  (The previous form -- a branch per partial and a
 // global load per fc2 term inside the chain -- compiled to 68 serial load round trips per wave.)
+// W windows per wave (grid (ceil(B / (4 W)), R)): a packed grid's one-window waves are too short to
+// cover their dispatch, so each wave takes W windows, their loads requested together and their
+// chains interleaved (every window keeps its own summation order: the same bits for any W).
+template <int W>
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
   rc_critical_priority();
   const RedcliffDims& d = c.d;
-  const int r = rc_rep(c, blockIdx.y), lane = threadIdx.x & 63, b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= c.B) return;
+  const int r = rc_rep(c, blockIdx.y), lane = threadIdx.x & 63;
+  const int bw = (blockIdx.x * 4 + (threadIdx.x >> 6)) * W;  // the wave's first window
+  if (bw >= c.B) return;
   const int M1 = d.M1, K = d.K;
   const float* E = c.emb + r * c.es;
   float* ws = c.ws + r * c.wss;
   const int ml = lane < M1 ? lane : M1 - 1;
-  const float* part = ws + c.wo.f1p + (int64_t)b * M1 + ml;
+  const float* part = ws + c.wo.f1p + ml;
   const int64_t pst = (int64_t)d.Bmax * M1;
+  int bo[W];  // window offsets of the partials (windows past B read the last one and do not store)
+#pragma unroll
+  for (int w = 0; w < W; ++w) bo[w] = min(bw + w, c.B - 1) * M1;
   // lane k's fc2 row (lanes >= K read row 0 and do not store), 32 terms per round of loads
   const float* w2 = E + c.eo.fc2W + (lane < K ? lane : 0) * M1;
   float w2r[32];
 #pragma unroll
   for (int u = 0; u < 32; ++u) w2r[u] = w2[min(u, M1 - 1)];
   const float fb1 = E[c.eo.fc1b + ml];
-  float t4[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int q0 = 0; q0 < nsplit; q0 += 4) {  // nsplit <= 64; t4[q & 3] += partial q, q ascending
-    float v[4];
+  float t4[W][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = part[(int64_t)min(q0 + u, nsplit - 1) * pst];
+  for (int w = 0; w < W; ++w) t4[w][0] = t4[w][1] = t4[w][2] = t4[w][3] = 0.f;
+  for (int q0 = 0; q0 < nsplit; q0 += 4) {  // nsplit <= 64; t4[q & 3] += partial q, q ascending
+    float v[W][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t qo = (int64_t)min(q0 + u, nsplit - 1) * pst;
+#pragma unroll
+      for (int w = 0; w < W; ++w) v[w][u] = part[qo + bo[w]];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (q0 + u < nsplit) t4[u] += v[u];
+      if (q0 + u < nsplit) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) t4[w][u] += v[w][u];
+      }
   }
-  float v = 0.f;
-  if (lane < M1) {
-    v = ((t4[0] + t4[1]) + (t4[2] + t4[3])) + fb1;
-    ws[c.wo.f1 + (int64_t)b * M1 + lane] = v;
+  float rv[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    float v = 0.f;
+    if (lane < M1) {
+      v = ((t4[w][0] + t4[w][1]) + (t4[w][2] + t4[w][3])) + fb1;
+      if (bw + w < c.B) ws[c.wo.f1 + (int64_t)(bw + w) * M1 + lane] = v;
+    }
+    rv[w] = fmaxf(v, 0.f);
   }
-  const float rv = fmaxf(v, 0.f);
   // w[k] = fc2b[k] + sum_m fc2W[k][m] relu(f1[m]), m ascending
-  float a = 0.f;
+  float a[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) a[w] = 0.f;
   for (int m0 = 0; m0 < M1; m0 += 32) {  // M1 <= 64
     if (m0 > 0) {
 #pragma unroll
@@ -123,9 +146,18 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_head(StepCtx c, int nsplit) {
     }
 #pragma unroll
     for (int u = 0; u < 32; ++u)
-      if (m0 + u < M1) a = fmaf(w2r[u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv), m0 + u)), a);
+      if (m0 + u < M1) {
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          a[w] = fmaf(w2r[u], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rv[w]), m0 + u)), a[w]);
+      }
   }
-  if (lane < K) ws[c.wo.w + (int64_t)b * K + lane] = a + E[c.eo.fc2b + lane];
+  if (lane < K) {
+    const float b2 = E[c.eo.fc2b + lane];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (bw + w < c.B) ws[c.wo.w + (int64_t)(bw + w) * K + lane] = a[w] + b2;
+  }
 }
 
 // grid (ceil(B / WPW), R), WPW = 64 / K windows per workgroup: lanes (item = (window, k), g),
@@ -641,7 +673,15 @@ int rc_launch_emb_fwd_gemm(const StepCtx& c, hipStream_t s) {
     e = rc_gemm_launch(g, nsp, s, "emb fc1");
   }
   if (e) return e;
-  hipLaunchKernelGGL(k_lemb_head, dim3((B + 3) / 4, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
+  // windows per wave: 4 for packs of >= 8 replicas (REDCLIFF_HEAD_WPW=1|2|4 overrides), else 1
+  const char* hv = getenv("REDCLIFF_HEAD_WPW");
+  const int hw = hv ? atoi(hv) : (c.nrep >= 8 ? 4 : 1);
+  if (hw == 4)
+    hipLaunchKernelGGL(k_lemb_head<4>, dim3((B + 15) / 16, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
+  else if (hw == 2)
+    hipLaunchKernelGGL(k_lemb_head<2>, dim3((B + 7) / 8, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
+  else
+    hipLaunchKernelGGL(k_lemb_head<1>, dim3((B + 3) / 4, c.nrep), dim3(RC_BLOCK), 0, s, c, nsp);
   return rc_check(hipGetLastError(), "k_lemb_head");
 }
 
