@@ -28,6 +28,10 @@ namespace {
 
 // windows per k_lemb_dhead workgroup: 64 (window, factor) items of 4 lanes each (K <= 16)
 __host__ __device__ inline int lemb_wpw(const RedcliffDims& d) { return 64 / d.K; }
+// k_lemb_dhead: fc2W (via LDS), f1, w and the labels requested before the dL/dw sums (1) or where used (0)
+#ifndef RC_DHEAD_EARLY
+#define RC_DHEAD_EARLY 1
+#endif
 
 // x_bn[b][c][0][f] = X[row0 + b][Lmax - F + f][c] * alpha_f + beta_f    grid (B, R)
 __global__ __launch_bounds__(RC_BLOCK) void k_lemb_prep(StepCtx c) {
@@ -177,6 +181,22 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   const bool ok = item < WPW * K && b < B;
   const bool fac_grad = c.flags & (RC_LOSS_FORECAST | RC_LOSS_ADJ);
   const bool lab_on = (c.flags & RC_LOSS_FACTOR) && d.nsup > 0;
+  const float* f1 = ws + c.wo.f1;
+#if RC_DHEAD_EARLY
+  // everything the workgroup reads that does not depend on dL/dw is requested up front: fc2W
+  // (K x M1 <= 1024 floats) into LDS, the first four dL/df1 elements' f1 values, and the items'
+  // w / label values -- the dL/dw partial sums below then overlap them
+  __shared__ float w2s[1024];
+  for (int e = tid; e < K * M1; e += RC_BLOCK) w2s[e] = E[c.eo.fc2W + e];
+  float f1p[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + u * RC_BLOCK, sw = e / M1, bb = min(b0 + sw, B - 1);
+    f1p[u] = e < WPW * M1 ? f1[(int64_t)bb * M1 + (e - sw * M1)] : 0.f;
+  }
+  const float wv = ok ? ws[c.wo.w + (int64_t)b * K + k] : 0.f;
+  const float yv = (ok && lab_on) ? c.lab[r * c.labr + (c.row0 + b) * K + k] : 0.f;
+#endif
   float t = 0.f;
   if (ok && fac_grad) {
     // four loads in flight at a time (clamped channel indices, no branch per load), added in j order
@@ -194,14 +214,38 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
   t += __shfl_xor(t, 1);
   t += __shfl_xor(t, 2);
   if (ok && g == 0) {
+#if RC_DHEAD_EARLY
+    const float v = rc_emb_draw(c, r, k, wv, t, yv);
+#else
     const float y = lab_on ? c.lab[r * c.labr + (c.row0 + b) * K + k] : 0.f;
     const float v = rc_emb_draw(c, r, k, ws[c.wo.w + (int64_t)b * K + k], t, y);
+#endif
     drs[item] = v;
     ws[c.wo.edr + (int64_t)b * K + k] = v;
   }
   __syncthreads();
-  const float* f1 = ws + c.wo.f1;
   float* df1 = ws + c.wo.edf1;
+#if RC_DHEAD_EARLY
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + u * RC_BLOCK, sw = e / M1, m = e - sw * M1, bb = b0 + sw;
+    if (e >= WPW * M1 || bb >= B) continue;
+    float gg = 0.f;
+    if (f1p[u] > 0.f) {
+      for (int kk = 0; kk < K; ++kk) gg += drs[sw * K + kk] * w2s[kk * M1 + m];
+    }
+    df1[(int64_t)bb * M1 + m] = gg;
+  }
+  for (int e = tid + 4 * RC_BLOCK; e < WPW * M1; e += RC_BLOCK) {
+    const int sw = e / M1, m = e - sw * M1, bb = b0 + sw;
+    if (bb >= B) continue;
+    float gg = 0.f;
+    if (f1[(int64_t)bb * M1 + m] > 0.f) {
+      for (int kk = 0; kk < K; ++kk) gg += drs[sw * K + kk] * w2s[kk * M1 + m];
+    }
+    df1[(int64_t)bb * M1 + m] = gg;
+  }
+#else
   for (int e = tid; e < WPW * M1; e += RC_BLOCK) {
     const int sw = e / M1, m = e - sw * M1, bb = b0 + sw;
     if (bb >= B) continue;
@@ -216,6 +260,7 @@ __global__ __launch_bounds__(RC_BLOCK) void k_lemb_dhead(StepCtx c) {
     }
     df1[(int64_t)bb * M1 + m] = gg;
   }
+#endif
 }
 
 // Workgroups [0, ngfc): fc2 weight / fc2 bias / fc1 bias gradients, 64 outputs per workgroup,
